@@ -1,0 +1,211 @@
+"""Benchmark: periodic 3-D Poisson CG (-ksp_type cg -pc_type jacobi, constant null space) at 512^3
+fp64 per GPU -- BASELINE.json metric "CG iter/s and DoF-updates/s at 512^3; achieved HBM GB/s".
+
+A step = one CG iteration over every DoF of the grid (one pass of the KSPSolve hot path).
+Weak scaling: every GPU owns a 512^3 z-slab worth of DoF; the global grid doubles z, y, x in turn
+(N=1: 512^3, N=2: 512x512x1024, N=4: 512x1024x1024, N=8: 1024^3 = SURVEY config 4).
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
+(one rank per GPU; RCCL unique id broadcast over the gloo process group).
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X spec (MI355X_MICROARCH.md "Chip-level parameters")
+PASS_B_BYTES = 40            # algorithmic bytes/DoF of CG pass B: read p, x, r; write x, r
+PASS_A_BYTES = 24            # pass A: read r, p_old; write p_new
+CG_ITER_BYTES = 64           # per CG iteration (both passes; SURVEY §8d lower bound is 80)
+MATVEC_BYTES = 16            # y = A x: read x, write y
+SEED = 20231015
+
+
+def global_grid(ngpus, base=512):
+    n = [base, base, base]
+    k = ngpus
+    d = 2
+    while k > 1 and k % 2 == 0:
+        n[d] *= 2
+        d = (d - 1) % 3
+        k //= 2
+    n[2] *= k  # non power-of-two remainder goes to z
+    return tuple(n)
+
+
+def cpu_baseline(seconds=12.0):
+    """The oracle (C restatement of PETSc KSPCG + PCJacobi + null space, 7-point, OpenMP) timed
+    on this host on a bounded 256^3 sample."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("PB_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    n = (256, 256, 256)
+    N = 256 ** 3
+    h = (1 / 256,) * 3
+    b = O.stencil(O.fill_random(N, SEED), n, h, nthreads=threads)
+    O.cg_fixed(b, n, h, 1, nthreads=threads)  # warm
+    its, t0 = 0, time.perf_counter()
+    while True:
+        O.cg_fixed(b, n, h, 2, nthreads=threads)
+        its += 2
+        el = time.perf_counter() - t0
+        if el >= seconds or its >= 200:
+            break
+    return {"value": N * its / el, "unit": "DoF-updates/s", "cores": threads, "kind": "port",
+            "iter_per_s": its / el,
+            "sample": f"256^3 grid, {its} CG iterations (+setup) of oracle/pb_oracle.c "
+                      f"(PETSc KSPCG+PCJacobi+MatNullSpace sequence, 7-point, OpenMP {threads} "
+                      f"threads) in {el:.1f} s on the GPU box host"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--base", type=int, default=512, help="per-GPU cube edge (default 512)")
+    ap.add_argument("--matvecs", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            sys.exit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} ranks")
+
+    import poissbox_amd as pb
+
+    dist = None
+    uid = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        obj = [pb.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
+
+    n = global_grid(world, args.base)
+    ctx = pb.Context(local_rank, rank, world, uid)
+    da = pb.initialise_grid(ctx, n)
+    h = da.spacing
+    P, A, x, b = pb.initialise_linear_system(da, h)
+    xt = pb.Vec(da)
+    xt.set_random(SEED)          # synthetic x_true, decomposition independent
+    A.mult(xt, b)                # b = A x_true (src/example.f90:70-72)
+    opts = pb.ksp_options(["-ksp_type", "cg", "-pc_type", "jacobi"], rtol=0.0, atol=0.0,
+                          dtol=1e300, max_it=args.warmup + args.steps + 16, check_every=8)
+    ksp = pb.KSP(A, P, opts)
+    ksp.begin(b, x)
+    ksp.iterate(args.warmup)
+    ctx.barrier()
+    if dist:
+        dist.barrier()
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    ksp.iterate(args.steps)
+    ctx.sync()
+    t1 = time.perf_counter()
+    ctx.barrier()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    ms_a, cnt_a = ctx.timing("cg_pass_a")
+    ms_b, cnt_b = ctx.timing("cg_pass_b")
+    ctx.set_timing(False)
+    reason, its, hist = ksp.end()
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # standalone matvec timing (north-star target kernel), outside the timed CG region
+    y = pb.Vec(da)
+    for _ in range(3):
+        A.mult(x, y)
+    ctx.sync()
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    for _ in range(args.matvecs):
+        A.mult(x, y)
+    ctx.sync()
+    ms_mv, cnt_mv = ctx.timing("stencil")
+    ctx.set_timing(False)
+
+    nloc = da.nlocal
+    N = n[0] * n[1] * n[2]
+    t_b = ms_b / max(cnt_b, 1) / 1e3
+    t_a = ms_a / max(cnt_a, 1) / 1e3
+    t_mv = ms_mv / max(cnt_mv, 1) / 1e3
+    gbs = lambda bytes_per_dof, t: bytes_per_dof * nloc / t / 1e9 if t > 0 else 0.0
+
+    if rank == 0:
+        out = {
+            "metric": "CG iter/s and DoF-updates/s at 512^3; achieved HBM GB/s vs peak",
+            "value": N * args.steps / elapsed,
+            "unit": "DoF-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (x_true = SplitMix64 U[-1,1], b = A x_true, x0 = 0)",
+            "config": {"workload": f"fp64 CG + Jacobi, 7-pt periodic Laplacian, "
+                                   f"{n[0]}x{n[1]}x{n[2]} grid ({args.base}^3 DoF per GPU)",
+                       "grid": list(n), "global_dofs": N, "per_gpu_dofs": nloc,
+                       "parallelism": f"z-slab x{world}" + (" (RCCL halo + allreduce)" if world > 1 else ""),
+                       "ksp": "-ksp_type cg -pc_type jacobi, constant null space, rtol=0 (fixed iterations)"},
+            "iter_per_s": args.steps / elapsed,
+            "achieved_GBps_cg": CG_ITER_BYTES * N / (elapsed / args.steps) / 1e9,
+            "roofline": {"bound": "hbm", "kernel": "cg_pass_b (fused stencil + x/r update + 4 sums)",
+                         "achieved": gbs(PASS_B_BYTES, t_b), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs(PASS_B_BYTES, t_b) / HBM_PEAK_GBS,
+                         "traffic": None, "bytes_per_dof": PASS_B_BYTES,
+                         "avg_launch_ms": t_b * 1e3},
+            "kernels": {
+                "cg_pass_a": {"avg_ms": t_a * 1e3, "GBps": gbs(PASS_A_BYTES, t_a),
+                              "frac": gbs(PASS_A_BYTES, t_a) / HBM_PEAK_GBS, "bytes_per_dof": PASS_A_BYTES},
+                "cg_pass_b": {"avg_ms": t_b * 1e3, "GBps": gbs(PASS_B_BYTES, t_b),
+                              "frac": gbs(PASS_B_BYTES, t_b) / HBM_PEAK_GBS, "bytes_per_dof": PASS_B_BYTES},
+                "matvec_star7": {"avg_ms": t_mv * 1e3, "GBps": gbs(MATVEC_BYTES, t_mv),
+                                 "frac": gbs(MATVEC_BYTES, t_mv) / HBM_PEAK_GBS,
+                                 "dofs_per_s": nloc / t_mv if t_mv > 0 else 0.0,
+                                 "bytes_per_dof": MATVEC_BYTES},
+            },
+            "ksp_state": {"reason": pb.REASONS.get(reason, reason), "its": its,
+                          "rnorm0": float(hist[0]), "rnorm_last": float(hist[-1])},
+        }
+        traffic_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(traffic_file):
+            try:
+                tr = json.load(open(traffic_file))
+                key = f"{n[0]}x{n[1]}x{n[2]}"
+                if key in tr and "cg_pass_b" in tr[key]:
+                    out["roofline"]["traffic"] = tr[key]["cg_pass_b"]["bytes_per_launch"]
+                    out["roofline"]["traffic_source"] = tr[key]["cg_pass_b"].get("source")
+            except Exception:
+                pass
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    for o in (ksp, y, xt, x, b, A, P):
+        o.destroy()
+    da.destroy()
+    ctx.destroy()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

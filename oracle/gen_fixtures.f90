@@ -1,0 +1,122 @@
+!! oracle/gen_fixtures.f90 -- golden-vector generator (TEST INFRASTRUCTURE ONLY).
+!
+! Our own driver program (not reference source). It is linked against the reference's own
+! modules compiled where they lie (/root/reference/src/{constants,tridsol,compact_schemes}.f90,
+! see oracle/Makefile target `ref`) and evaluates them on inputs written by
+! tests/golden/make_golden.py, so the committed fixtures are outputs of the real reference.
+!
+! Manifest (text, one case per line):  op nx ny nz dx dy dz infile outfile
+!   tdma | tdma_periodic | fwd_sweep : in = [a, b, c, d] (4*nx), out = [b', d'] (2*nx)
+!   bwd_sweep                        : in = [b, c, d] (3*nx),    out = d' (nx)
+!   grad_1d | div_1d                 : in = f (nx), out = df (nx), uses dx
+!   interp_1d | interp_1d_div        : in = f (nx), out = fi (nx)
+!   grad                             : in = f (N),  out = df (3N)
+!   div                              : in = f (3N), out = df (N)
+!   interp | interp_div              : in = f (N),  out = fi (N)
+!   lapl                             : in = f (N),  out = d2f (N)
+program gen_fixtures
+
+  use constants
+  use tridsol
+  use compact_schemes
+
+  implicit none
+
+  character(len=512) :: manifest, op, infile, outfile
+  integer :: nx, ny, nz, ios, u
+  real(pb_dp) :: dx, dy, dz
+
+  call get_command_argument(1, manifest)
+  open(newunit=u, file=trim(manifest), status='old', action='read')
+  do
+     read(u, *, iostat=ios) op, nx, ny, nz, dx, dy, dz, infile, outfile
+     if (ios /= 0) exit
+     call run_case(trim(op), nx, ny, nz, [dx, dy, dz], trim(infile), trim(outfile))
+  end do
+  close(u)
+
+contains
+
+  subroutine read_vec(fname, v)
+    character(len=*), intent(in) :: fname
+    real(pb_dp), dimension(:), intent(out) :: v
+    integer :: iu
+    open(newunit=iu, file=fname, access='stream', form='unformatted', status='old', action='read')
+    read(iu) v
+    close(iu)
+  end subroutine read_vec
+
+  subroutine write_vec(fname, v)
+    character(len=*), intent(in) :: fname
+    real(pb_dp), dimension(:), intent(in) :: v
+    integer :: iu
+    open(newunit=iu, file=fname, access='stream', form='unformatted', status='replace', &
+         action='write')
+    write(iu) v
+    close(iu)
+  end subroutine write_vec
+
+  subroutine run_case(op, nx, ny, nz, h, infile, outfile)
+    character(len=*), intent(in) :: op, infile, outfile
+    integer, intent(in) :: nx, ny, nz
+    real(pb_dp), dimension(3), intent(in) :: h
+
+    real(pb_dp), allocatable :: buf(:), a(:), b(:), c(:), d(:)
+    real(pb_dp), allocatable :: f3(:, :, :), g3(:, :, :), v4(:, :, :, :)
+    integer :: n
+
+    n = nx
+    select case (op)
+    case ('tdma', 'tdma_periodic', 'fwd_sweep')
+       allocate(buf(4 * n))
+       call read_vec(infile, buf)
+       a = buf(1:n); b = buf(n+1:2*n); c = buf(2*n+1:3*n); d = buf(3*n+1:4*n)
+       if (op == 'tdma') then
+          call tdma(a, b, c, d)
+       else if (op == 'tdma_periodic') then
+          call tdma_periodic(a, b, c, d)
+       else
+          call fwd_sweep(a, b, c, d)
+       end if
+       call write_vec(outfile, [b, d])
+    case ('bwd_sweep')
+       allocate(buf(3 * n))
+       call read_vec(infile, buf)
+       b = buf(1:n); c = buf(n+1:2*n); d = buf(2*n+1:3*n)
+       call bwd_sweep(b, c, d)
+       call write_vec(outfile, d)
+    case ('grad_1d', 'div_1d', 'interp_1d', 'interp_1d_div')
+       allocate(a(n), d(n))
+       call read_vec(infile, a)
+       if (op == 'grad_1d') call grad_1d(a, h(1), d)
+       if (op == 'div_1d') call div_1d(a, h(1), d)
+       if (op == 'interp_1d') call interp_1d(a, d)
+       if (op == 'interp_1d_div') call interp_1d_div(a, d)
+       call write_vec(outfile, d)
+    case ('grad')
+       allocate(f3(nx, ny, nz), v4(nx, ny, nz, 3), buf(nx * ny * nz))
+       call read_vec(infile, buf)
+       f3 = reshape(buf, [nx, ny, nz])
+       call grad(f3, h, v4)
+       call write_vec(outfile, reshape(v4, [3 * nx * ny * nz]))
+    case ('div')
+       allocate(v4(nx, ny, nz, 3), g3(nx, ny, nz), buf(3 * nx * ny * nz))
+       call read_vec(infile, buf)
+       v4 = reshape(buf, [nx, ny, nz, 3])
+       call div(v4, h, g3)
+       call write_vec(outfile, reshape(g3, [nx * ny * nz]))
+    case ('interp', 'interp_div', 'lapl')
+       allocate(f3(nx, ny, nz), g3(nx, ny, nz), buf(nx * ny * nz))
+       call read_vec(infile, buf)
+       f3 = reshape(buf, [nx, ny, nz])
+       if (op == 'interp') call interp(f3, g3)
+       if (op == 'interp_div') call interp_div(f3, g3)
+       if (op == 'lapl') call lapl(f3, h, g3)
+       call write_vec(outfile, reshape(g3, [nx * ny * nz]))
+    case default
+       print *, "unknown op ", op
+       stop 2
+    end select
+  end subroutine run_case
+
+end program gen_fixtures

@@ -1,0 +1,483 @@
+/* pb_oracle.c -- CPU restatement of the poissbox hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg as the checker / reported CPU baseline. The product (poissbox_amd/,
+ * libpoissbox_gpu.so) never links or calls this file.
+ *
+ * Every function cites the reference (3decomp/poissbox) file:line it restates. Arithmetic is
+ * written in the reference's evaluation order; build with -ffp-contract=off (see Makefile) so
+ * that no multiply-add is fused -- the flang-built reference (oracle/_ref) on x86-64 baseline
+ * has no FMA either, which is what makes the tridiagonal/compact pins bit-exact.
+ */
+#include "pb_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define IDX(i, j, k, nx, ny) ((i) + (nx) * ((j) + (ny) * (k)))
+
+static inline int64_t wrap(int64_t i, int64_t n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+
+/* ---------------------------------------------------------------------------------------------
+ * Coefficients
+ * ------------------------------------------------------------------------------------------- */
+
+/* src/coefficients.f90:22-35 lapl_1d_coeffs: [1, -2, 1] / dx**2 */
+void pbo_lapl_1d_coeffs(double dx, double c[3]) {
+  double invdx2 = 1.0 / (dx * dx);
+  c[0] = invdx2;
+  c[1] = -(2.0 * invdx2);
+  c[2] = invdx2;
+}
+
+/* src/coefficients.f90:38-48 lapl_star_coeffs: zero box, then the three 1-D stencils are
+ * ADDED along the x, y and z lines through the centre (centre accumulates x, then y, then z). */
+void pbo_lapl_star_coeffs(double dx, double dy, double dz, double c[27]) {
+  double cx[3], cy[3], cz[3];
+  pbo_lapl_1d_coeffs(dx, cx);
+  pbo_lapl_1d_coeffs(dy, cy);
+  pbo_lapl_1d_coeffs(dz, cz);
+  for (int m = 0; m < 27; ++m) c[m] = 0.0;
+  /* column-major (ii,jj,kk) -> ii + 3*jj + 9*kk */
+  for (int t = 0; t < 3; ++t) c[t + 3 * 1 + 9 * 1] += cx[t]; /* coeffs(:, 2, 2) */
+  for (int t = 0; t < 3; ++t) c[1 + 3 * t + 9 * 1] += cy[t]; /* coeffs(2, :, 2) */
+  for (int t = 0; t < 3; ++t) c[1 + 3 * 1 + 9 * t] += cz[t]; /* coeffs(2, 2, :) */
+}
+
+/* Jacobi diagonal of P = centre coefficient (src/coefficients.f90:44-46 via :105) */
+double pbo_diag(const double h[3]) {
+  double c[27];
+  pbo_lapl_star_coeffs(h[0], h[1], h[2], c);
+  return c[13];
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * 7-point operator
+ * ------------------------------------------------------------------------------------------- */
+
+/* src/poissbox.f90:84-126 compute_lapl_pointwise + :128-148 evaluate_laplacian_pointwise:
+ * for every owned point, dot_product(reshape(xdof(i-1:i+1, j-1:j+1, k-1:k+1)), reshape(coeffs))
+ * with the coefficients rebuilt per point (:143) and periodic ghosts (DM_BOUNDARY_PERIODIC,
+ * :192). Summation runs over all 27 entries in column-major order, starting from 0. */
+void pbo_stencil_apply27(const int64_t n[3], const double h[3], const double* x, double* y) {
+  const int64_t nx = n[0], ny = n[1], nz = n[2];
+  for (int64_t k = 0; k < nz; ++k)
+    for (int64_t j = 0; j < ny; ++j)
+      for (int64_t i = 0; i < nx; ++i) {
+        double c[27];
+        pbo_lapl_star_coeffs(h[0], h[1], h[2], c); /* recomputed at every point, :143 */
+        double s = 0.0;
+        for (int kk = 0; kk < 3; ++kk)
+          for (int jj = 0; jj < 3; ++jj)
+            for (int ii = 0; ii < 3; ++ii) {
+              double f = x[IDX(wrap(i + ii - 1, nx), wrap(j + jj - 1, ny), wrap(k + kk - 1, nz), nx, ny)];
+              s += f * c[ii + 3 * jj + 9 * kk];
+            }
+        y[IDX(i, j, k, nx, ny)] = s;
+      }
+}
+
+/* Same operator with the 20 zero terms dropped. For finite x, 0*f adds +-0 to a running sum that
+ * is exactly 0 until the first non-zero term, so the result is bit-identical to apply27:
+ * ((((((cz*f[z-] + cy*f[y-]) + cx*f[x-]) + cc*f[c]) + cx*f[x+]) + cy*f[y+]) + cz*f[z+]). */
+void pbo_stencil_apply7(const int64_t n[3], const double h[3], const double* x, double* y,
+                        int nthreads) {
+  const int64_t nx = n[0], ny = n[1], nz = n[2];
+  double c[27];
+  pbo_lapl_star_coeffs(h[0], h[1], h[2], c);
+  const double cx = c[12], cy = c[10], cz = c[4], cc = c[13];
+  (void)nthreads;
+#pragma omp parallel for num_threads(nthreads) schedule(static) collapse(2)
+  for (int64_t k = 0; k < nz; ++k)
+    for (int64_t j = 0; j < ny; ++j) {
+      const double* xm = x + nx * (j + ny * wrap(k - 1, nz));
+      const double* xp = x + nx * (j + ny * wrap(k + 1, nz));
+      const double* ym = x + nx * (wrap(j - 1, ny) + ny * k);
+      const double* yp = x + nx * (wrap(j + 1, ny) + ny * k);
+      const double* xc = x + nx * (j + ny * k);
+      double* out = y + nx * (j + ny * k);
+      for (int64_t i = 0; i < nx; ++i) {
+        int64_t im = i == 0 ? nx - 1 : i - 1, ip = i == nx - 1 ? 0 : i + 1;
+        double s = cz * xm[i];
+        s += cy * ym[i];
+        s += cx * xc[im];
+        s += cc * xc[i];
+        s += cx * xc[ip];
+        s += cy * yp[i];
+        s += cz * xp[i];
+        out[i] = s;
+      }
+    }
+}
+
+static int cmp_i64(const void* a, const void* b) {
+  int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+/* src/coefficients.f90:50-113 assemble_laplacian: one MatSetValuesStencil row of the 27 box
+ * entries (20 explicit zeros) per DoF, INSERT_VALUES; MatMult over an AIJ row sums the stored
+ * entries in ascending global column order (natural ordering on one rank). Requires n >= 3 in
+ * every direction so that the 27 columns are distinct. */
+void pbo_assembled_apply(const int64_t n[3], const double h[3], const double* x, double* y) {
+  const int64_t nx = n[0], ny = n[1], nz = n[2];
+  double c[27];
+  pbo_lapl_star_coeffs(h[0], h[1], h[2], c);
+  for (int64_t k = 0; k < nz; ++k)
+    for (int64_t j = 0; j < ny; ++j)
+      for (int64_t i = 0; i < nx; ++i) {
+        int64_t key[27][2];
+        for (int m = 0; m < 27; ++m) {
+          int ii = m % 3, jj = (m / 3) % 3, kk = m / 9;
+          key[m][0] = IDX(wrap(i + ii - 1, nx), wrap(j + jj - 1, ny), wrap(k + kk - 1, nz), nx, ny);
+          key[m][1] = m;
+        }
+        qsort(key, 27, sizeof(key[0]), cmp_i64);
+        double s = 0.0;
+        for (int m = 0; m < 27; ++m) s += c[key[m][1]] * x[key[m][0]];
+        y[IDX(i, j, k, nx, ny)] = s;
+      }
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Synthetic input (same distribution as src/example.f90:180-181)
+ * ------------------------------------------------------------------------------------------- */
+uint64_t pbo_splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+void pbo_fill_random(int64_t count, uint64_t seed, int64_t g0, double* x) {
+  for (int64_t t = 0; t < count; ++t) {
+    double u = (double)(pbo_splitmix64(seed ^ (uint64_t)(g0 + t)) >> 11) * 0x1.0p-53;
+    x[t] = 2.0 * (0.5 - u); /* src/example.f90:181 */
+  }
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * KSPSolve with -ksp_type cg -pc_type jacobi and the constant null space
+ * (src/poissbox.f90:269-298 -> PETSc KSPSolve_CG; semantics in SURVEY.md Appendix A)
+ * ------------------------------------------------------------------------------------------- */
+enum {
+  KSP_CONVERGED_ITERATING = 0, KSP_CONVERGED_RTOL = 2, KSP_CONVERGED_ATOL = 3,
+  KSP_DIVERGED_ITS = -3, KSP_DIVERGED_DTOL = -4, KSP_DIVERGED_NANORINF = -9,
+  KSP_DIVERGED_INDEFINITE_MAT = -10
+};
+
+static double vdot(int64_t N, const double* a, const double* b, int nt) {
+  double s = 0.0;
+  (void)nt;
+#pragma omp parallel for num_threads(nt) reduction(+ : s) schedule(static) if (nt > 1)
+  for (int64_t t = 0; t < N; ++t) s += b[t] * a[t];
+  return s;
+}
+static double vsum(int64_t N, const double* a, int nt) {
+  double s = 0.0;
+  (void)nt;
+#pragma omp parallel for num_threads(nt) reduction(+ : s) schedule(static) if (nt > 1)
+  for (int64_t t = 0; t < N; ++t) s += a[t];
+  return s;
+}
+
+/* KSP_PCApply = PCApply_Jacobi (z = diag^-1 .* r, PETSc stores the reciprocal) followed by
+ * KSP_RemoveNullSpace -> MatNullSpaceRemove(has_cnst): z += VecSum(z) / (-N). */
+static void pc_apply(int64_t N, const double* r, double* z, double dinv, int pc, int nsp, int nt) {
+  (void)nt;
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+  for (int64_t t = 0; t < N; ++t) z[t] = pc ? dinv * r[t] : r[t];
+  if (nsp) {
+    double shift = vsum(N, z, nt) / (-1.0 * (double)N);
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+    for (int64_t t = 0; t < N; ++t) z[t] += shift;
+  }
+}
+
+static void op_apply(const int64_t n[3], const double h[3], const double* x, double* y, int op27,
+                     int nt) {
+  if (op27)
+    pbo_stencil_apply27(n, h, x, y);
+  else
+    pbo_stencil_apply7(n, h, x, y, nt);
+}
+
+int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, const double* b,
+                 double* x, double* history, int64_t* its_out) {
+  const int64_t N = n[0] * n[1] * n[2];
+  const int nt = o->nthreads > 0 ? o->nthreads : 1;
+  double* R = (double*)malloc(sizeof(double) * N);
+  double* Z = (double*)malloc(sizeof(double) * N);
+  double* P = (double*)malloc(sizeof(double) * N);
+  double* W = (double*)malloc(sizeof(double) * N);
+  const double dinv = 1.0 / pbo_diag(h);
+  int reason = KSP_CONVERGED_ITERATING;
+  int64_t its = 0;
+  double dp, beta, betaold = 0.0, dpi = 0.0, dpiold, ttol, rnorm0;
+
+  memset(x, 0, sizeof(double) * N); /* KSPSolve: guess_zero => X = 0 */
+  memcpy(R, b, sizeof(double) * N); /* r = b */
+  pc_apply(N, R, Z, dinv, o->pc_type, o->nullspace, nt);
+  dp = sqrt(vdot(N, Z, Z, nt)); /* KSP_NORM_PRECONDITIONED */
+  history[0] = dp;
+  /* KSPConvergedDefault at n = 0 */
+  if (dp != dp || isinf(dp)) { reason = KSP_DIVERGED_NANORINF; goto done; }
+  ttol = fmax(o->rtol * dp, o->atol);
+  rnorm0 = dp;
+  if (dp <= ttol) { reason = dp < o->atol ? KSP_CONVERGED_ATOL : KSP_CONVERGED_RTOL; goto done; }
+  beta = vdot(N, Z, R, nt);
+
+  int64_t i = 0;
+  do {
+    its = i + 1;
+    if (beta == 0.0) { reason = KSP_CONVERGED_ATOL; break; }
+    if (i == 0) {
+      memcpy(P, Z, sizeof(double) * N);
+    } else {
+      double bb = beta / betaold;
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+      for (int64_t t = 0; t < N; ++t) P[t] = Z[t] + bb * P[t]; /* VecAYPX */
+    }
+    dpiold = dpi;
+    op_apply(n, h, P, W, o->op27, nt); /* KSP_MatMult -> mfmult */
+    dpi = vdot(N, P, W, nt);
+    betaold = beta;
+    if (dpi == 0.0 || (i > 0 && ((dpi > 0) - (dpi < 0)) * ((dpiold > 0) - (dpiold < 0)) < 0)) {
+      reason = KSP_DIVERGED_INDEFINITE_MAT;
+      break;
+    }
+    double a = beta / dpi;
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+    for (int64_t t = 0; t < N; ++t) {
+      x[t] = x[t] + a * P[t];
+      R[t] = R[t] + (-a) * W[t];
+    }
+    pc_apply(N, R, Z, dinv, o->pc_type, o->nullspace, nt);
+    dp = sqrt(vdot(N, Z, Z, nt));
+    history[i + 1] = dp;
+    if (dp != dp || isinf(dp)) { reason = KSP_DIVERGED_NANORINF; break; }
+    if (dp <= ttol) { reason = dp < o->atol ? KSP_CONVERGED_ATOL : KSP_CONVERGED_RTOL; break; }
+    if (dp >= o->dtol * rnorm0) { reason = KSP_DIVERGED_DTOL; break; }
+    beta = vdot(N, Z, R, nt);
+    i++;
+  } while (i < o->max_it);
+  if (i >= o->max_it) reason = KSP_DIVERGED_ITS;
+done:
+  *its_out = its;
+  free(R); free(Z); free(P); free(W);
+  return reason;
+}
+
+/* The CPU-baseline workload: `iters` CG iterations (same per-iteration work as pbo_cg_solve:
+ * MatMult, 2 dots, 1 norm, 1 sum, AXPY x2, PC, shift, AYPX), no stopping test. */
+double pbo_cg_fixed(const int64_t n[3], const double h[3], int64_t iters, int nthreads,
+                    const double* b, double* x, double* work) {
+  const int64_t N = n[0] * n[1] * n[2];
+  const int nt = nthreads > 0 ? nthreads : 1;
+  double *R = work, *Z = work + N, *P = work + 2 * N, *W = work + 3 * N;
+  const double dinv = 1.0 / pbo_diag(h);
+  memset(x, 0, sizeof(double) * N);
+  memcpy(R, b, sizeof(double) * N);
+  pc_apply(N, R, Z, dinv, 1, 1, nt);
+  double dp = sqrt(vdot(N, Z, Z, nt)), beta = vdot(N, Z, R, nt), betaold = 1.0;
+  for (int64_t i = 0; i < iters; ++i) {
+    double bb = i == 0 ? 0.0 : beta / betaold;
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+    for (int64_t t = 0; t < N; ++t) P[t] = Z[t] + bb * (i == 0 ? 0.0 : P[t]);
+    pbo_stencil_apply7(n, h, P, W, nt);
+    double dpi = vdot(N, P, W, nt);
+    betaold = beta;
+    double a = beta / dpi;
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+    for (int64_t t = 0; t < N; ++t) {
+      x[t] = x[t] + a * P[t];
+      R[t] = R[t] + (-a) * W[t];
+    }
+    pc_apply(N, R, Z, dinv, 1, 1, nt);
+    dp = sqrt(vdot(N, Z, Z, nt));
+    beta = vdot(N, Z, R, nt);
+  }
+  return dp;
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Tridiagonal solvers (src/tridsol.f90)
+ * ------------------------------------------------------------------------------------------- */
+
+/* src/tridsol.f90:76-96 fwd_sweep */
+void pbo_fwd_sweep(int64_t n, const double* a, double* b, const double* c, double* d) {
+  for (int64_t i = 1; i < n; ++i) {
+    double w = a[i] / b[i - 1];
+    b[i] = b[i] - w * c[i - 1];
+    d[i] = d[i] - w * d[i - 1];
+  }
+}
+
+/* src/tridsol.f90:98-115 bwd_sweep */
+void pbo_bwd_sweep(int64_t n, const double* b, const double* c, double* d) {
+  d[n - 1] = d[n - 1] / b[n - 1];
+  for (int64_t i = n - 2; i >= 0; --i) d[i] = (d[i] - c[i] * d[i + 1]) / b[i];
+}
+
+/* src/tridsol.f90:22-32 tdma: b (diagonal) and d (rhs -> solution) are overwritten */
+void pbo_tdma(int64_t n, const double* a, double* b, const double* c, double* d) {
+  pbo_fwd_sweep(n, a, b, c, d);
+  pbo_bwd_sweep(n, b, c, d);
+}
+
+/* src/tridsol.f90:34-74 tdma_periodic (Sherman-Morrison); a(1) couples x(n), c(n) couples x(1).
+ * b is left unchanged (the routine works on copies bmod), d is overwritten with the solution. */
+void pbo_tdma_periodic(int64_t n, const double* a, double* b, const double* c, double* d) {
+  double* bmod = (double*)malloc(sizeof(double) * n);
+  double* u = (double*)malloc(sizeof(double) * n);
+  const double gamma = -b[0];                                   /* :51 */
+  memcpy(bmod, b, sizeof(double) * n);                          /* :54-56 */
+  bmod[0] = bmod[0] - gamma;
+  bmod[n - 1] = bmod[n - 1] - c[n - 1] * a[0] / gamma;
+  pbo_tdma(n, a, bmod, c, d);                                   /* :57 */
+  memcpy(bmod, b, sizeof(double) * n);                          /* :59-61 */
+  bmod[0] = bmod[0] - gamma;
+  bmod[n - 1] = bmod[n - 1] - c[n - 1] * a[0] / gamma;
+  for (int64_t i = 0; i < n; ++i) u[i] = 0.0;                   /* :62-65 */
+  u[0] = gamma;
+  u[n - 1] = c[n - 1];
+  pbo_tdma(n, a, bmod, c, u);                                   /* :66 */
+  const double num = d[0] + (a[0] / gamma) * d[n - 1];          /* :69-70 */
+  const double den = 1.0 + (u[0] + (a[0] / gamma) * u[n - 1]);
+  for (int64_t i = 0; i < n; ++i) d[i] = d[i] - (u[i] * num) / den;
+  free(bmod);
+  free(u);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Compact schemes (src/compact_schemes.f90)
+ * ------------------------------------------------------------------------------------------- */
+
+/* src/compact_schemes.f90:332-372 eval_1d_rhs. The reference special-cases the first/last rows;
+ * every special case is the interior formula with periodic index wrap, restated here as such:
+ *   stagger -1: rhs(i) = a*(f(i)   + s*f(i-1)) + b*(f(i+1) + s*f(i-2))
+ *   stagger +1: rhs(i) = a*(f(i+1) + s*f(i))   + b*(f(i+2) + s*f(i-1))      (needs n >= 3) */
+void pbo_eval_1d_rhs(double a, double b, int opsign, int stagger, int64_t n, const double* f,
+                     double* rhs) {
+  const double s = (double)opsign;
+  const int64_t sh = stagger == -1 ? 0 : 1;
+  for (int64_t i = 0; i < n; ++i) {
+    double f0 = f[wrap(i + sh, n)], fm1 = f[wrap(i - 1 + sh, n)];
+    double f1 = f[wrap(i + 1 + sh, n)], fm2 = f[wrap(i - 2 + sh, n)];
+    rhs[i] = a * (f0 + s * fm1) + b * (f1 + s * fm2);
+  }
+}
+
+/* (alpha, 1, alpha) periodic solve as grad_1d/interp_1d set it up (:200-205 / :315-320) */
+static void solve_alpha(int64_t n, double alpha, double* rhs) {
+  double* ld = (double*)malloc(sizeof(double) * n);
+  double* d = (double*)malloc(sizeof(double) * n);
+  double* ud = (double*)malloc(sizeof(double) * n);
+  for (int64_t i = 0; i < n; ++i) { ld[i] = alpha; d[i] = 1.0; ud[i] = alpha; }
+  pbo_tdma_periodic(n, ld, d, ud, rhs);
+  free(ld); free(d); free(ud);
+}
+
+/* src/compact_schemes.f90:155-204 grad_1d (stagger -1 cell->vertex; +1 = div_1d :260-268) */
+void pbo_grad_1d(int64_t n, const double* f, double dx, double* df, int stagger) {
+  const double a = 63.0 / 62.0 / dx;                 /* :188 */
+  const double b = 17.0 / 62.0 / (3.0 * dx);         /* :189 */
+  const double alpha = 9.0 / 62.0;                   /* :190 */
+  pbo_eval_1d_rhs(a, b, -1, stagger, n, f, df);      /* :194 */
+  solve_alpha(n, alpha, df);                         /* :197 */
+}
+
+/* src/compact_schemes.f90:271-319 interp_1d (stagger +1 = interp_1d_div :322-329) */
+void pbo_interp_1d(int64_t n, const double* f, double* fi, int stagger) {
+  const double a = 0.75, b = 1.0 / 20.0, alpha = 3.0 / 10.0; /* :303-305 */
+  pbo_eval_1d_rhs(a, b, +1, stagger, n, f, fi);               /* :309 */
+  solve_alpha(n, alpha, fi);                                  /* :312 */
+}
+
+/* Apply a 1-D line operator along direction `dir` of an nx*ny*nz field. */
+typedef enum { L_INTERP, L_GRAD } line_kind;
+static void line_op(const int64_t n[3], int dir, line_kind kind, int stagger, double dx,
+                    const double* in, double* out) {
+  const int64_t nx = n[0], ny = n[1], nz = n[2];
+  const int64_t len = n[dir];
+  const int64_t stride = dir == 0 ? 1 : (dir == 1 ? nx : nx * ny);
+  const int64_t nlines = (nx * ny * nz) / len;
+  double* f = (double*)malloc(sizeof(double) * len);
+  double* g = (double*)malloc(sizeof(double) * len);
+  for (int64_t l = 0; l < nlines; ++l) {
+    int64_t base;
+    if (dir == 0) base = l * nx;                                  /* l = j + ny*k */
+    else if (dir == 1) base = (l % nx) + (l / nx) * nx * ny;      /* l = i + nx*k */
+    else base = l;                                                /* l = i + nx*j */
+    for (int64_t t = 0; t < len; ++t) f[t] = in[base + t * stride];
+    if (kind == L_INTERP) pbo_interp_1d(len, f, g, stagger);
+    else pbo_grad_1d(len, f, dx, g, stagger);
+    for (int64_t t = 0; t < len; ++t) out[base + t * stride] = g[t];
+  }
+  free(f);
+  free(g);
+}
+
+/* src/compact_schemes.f90:42-88 grad: Z (interp, copy, grad) -> Y -> X */
+void pbo_grad(const int64_t n[3], const double* f, const double dx[3], double* df) {
+  const int64_t N = n[0] * n[1] * n[2];
+  double* dff = (double*)malloc(sizeof(double) * N * 3);
+  double* dfe = (double*)malloc(sizeof(double) * N * 3);
+  line_op(n, 2, L_INTERP, -1, 0.0, f, dff);                /* :61 */
+  memcpy(dff + N, dff, sizeof(double) * N);                /* :62 */
+  line_op(n, 2, L_GRAD, -1, dx[2], f, dff + 2 * N);        /* :63 */
+  line_op(n, 1, L_INTERP, -1, 0.0, dff, dfe);              /* :71 */
+  line_op(n, 1, L_GRAD, -1, dx[1], dff + N, dfe + N);      /* :72 */
+  line_op(n, 1, L_INTERP, -1, 0.0, dff + 2 * N, dfe + 2 * N); /* :73 */
+  line_op(n, 0, L_GRAD, -1, dx[0], dfe, df);               /* :81 */
+  line_op(n, 0, L_INTERP, -1, 0.0, dfe + N, df + N);       /* :82 */
+  line_op(n, 0, L_INTERP, -1, 0.0, dfe + 2 * N, df + 2 * N); /* :83 */
+  free(dff);
+  free(dfe);
+}
+
+/* src/compact_schemes.f90:93-142 interp (Z -> Y -> X with the given stagger) */
+void pbo_interp(const int64_t n[3], const double* f, double* fi, int stagger) {
+  const int64_t N = n[0] * n[1] * n[2];
+  double* ff = (double*)malloc(sizeof(double) * N);
+  double* fe = (double*)malloc(sizeof(double) * N);
+  line_op(n, 2, L_INTERP, stagger, 0.0, f, ff);
+  line_op(n, 1, L_INTERP, stagger, 0.0, ff, fe);
+  line_op(n, 0, L_INTERP, stagger, 0.0, fe, fi);
+  free(ff);
+  free(fe);
+}
+
+/* src/compact_schemes.f90:207-257 div: X -> Y -> Z, Z step interpolates dff1 + dff2 (:249) */
+void pbo_div(const int64_t n[3], const double* f, const double dx[3], double* df) {
+  const int64_t N = n[0] * n[1] * n[2];
+  double* dfe = (double*)malloc(sizeof(double) * N * 3);
+  double* dff = (double*)malloc(sizeof(double) * N * 3);
+  double* dfc = (double*)malloc(sizeof(double) * N);
+  line_op(n, 0, L_GRAD, +1, dx[0], f, dfe);                  /* :227 */
+  line_op(n, 0, L_INTERP, +1, 0.0, f + N, dfe + N);          /* :228 */
+  line_op(n, 0, L_INTERP, +1, 0.0, f + 2 * N, dfe + 2 * N);  /* :229 */
+  line_op(n, 1, L_INTERP, +1, 0.0, dfe, dff);                /* :237 */
+  line_op(n, 1, L_GRAD, +1, dx[1], dfe + N, dff + N);        /* :238 */
+  line_op(n, 1, L_INTERP, +1, 0.0, dfe + 2 * N, dff + 2 * N); /* :239 */
+  for (int64_t t = 0; t < N; ++t) dfe[t] = dff[t] + dff[N + t];
+  line_op(n, 2, L_INTERP, +1, 0.0, dfe, dfc);                /* :248 */
+  line_op(n, 2, L_GRAD, +1, dx[2], dff + 2 * N, df);         /* :249 */
+  for (int64_t t = 0; t < N; ++t) df[t] = df[t] + dfc[t];    /* :250 */
+  free(dfe);
+  free(dff);
+  free(dfc);
+}
+
+/* src/compact_schemes.f90:17-37 lapl = div(grad f) */
+void pbo_lapl(const int64_t n[3], const double* f, const double dx[3], double* out) {
+  const int64_t N = n[0] * n[1] * n[2];
+  double* df = (double*)malloc(sizeof(double) * N * 3);
+  pbo_grad(n, f, dx, df);
+  pbo_div(n, df, dx, out);
+  free(df);
+}

@@ -1,0 +1,82 @@
+/* pb_oracle.h -- CPU restatement of the poissbox hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * This header declares the oracle: a plain-C restatement of the reference algorithms
+ * (3decomp/poissbox, Fortran + PETSc) used by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py as the CHECKER. Nothing in poissbox_amd/ links or calls it.
+ *
+ * Layout everywhere: Fortran column-major (i,j,k), i fastest == C [k][j][i].
+ * Vector fields of 3 components (grad output): [c][k][j][i], c slowest (Fortran df(nx,ny,nz,3)).
+ *
+ * Parity pins: tridiagonal + compact-scheme functions are pinned bit-for-bit against the
+ * flang-built reference (oracle/_ref, fixtures in tests/golden/). The 7-point operator is pinned
+ * by the reference's own known-answer tests (tests/coefficients/test_star.f90) -- the
+ * PETSc-dependent sources (poissbox.f90, coefficients.f90) cannot be compiled here. The
+ * KSPCG + PCJacobi + MatNullSpace restatement (PETSc is external and absent) is
+ * "parity unpinned" against real PETSc: it follows SURVEY.md Appendix A.
+ */
+#ifndef PB_ORACLE_H
+#define PB_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- coefficients (src/coefficients.f90) ---- */
+void pbo_lapl_1d_coeffs(double dx, double c[3]);
+void pbo_lapl_star_coeffs(double dx, double dy, double dz, double c[27]);
+
+/* ---- 7-point operator (src/poissbox.f90:84-148) ---- */
+/* faithful: 27-term dot product over the 3x3x3 box incl. zero coefficients, column-major order */
+void pbo_stencil_apply27(const int64_t n[3], const double h[3], const double* x, double* y);
+/* fast: the 7 non-zero terms in the same order (z-, y-, x-, c, x+, y+, z+); identical results
+ * for finite inputs */
+void pbo_stencil_apply7(const int64_t n[3], const double h[3], const double* x, double* y,
+                        int nthreads);
+/* assembled P (src/coefficients.f90:50-113) applied as a 27-point BOX SpMV, row-wise sum over
+ * the 27 stored entries in MatSetValuesStencil column order */
+void pbo_assembled_apply(const int64_t n[3], const double h[3], const double* x, double* y);
+double pbo_diag(const double h[3]);
+
+/* ---- synthetic input ---- */
+uint64_t pbo_splitmix64(uint64_t z);
+/* x[g] = 2*(0.5 - U(seed ^ (g0+g))), g = global linear index i + nx*(j + ny*k) */
+void pbo_fill_random(int64_t count, uint64_t seed, int64_t g0, double* x);
+
+/* ---- KSPCG + PCJacobi + constant null space (PETSc cg.c semantics) ---- */
+typedef struct {
+  double rtol, atol, dtol;
+  int64_t max_it;
+  int pc_type;       /* 0 = none, 1 = jacobi */
+  int nullspace;     /* 1 = remove constant mode after every PCApply */
+  int op27;          /* 1 = use the faithful 27-term operator (slow), 0 = 7-term */
+  int nthreads;      /* OpenMP threads for the 7-term operator/vector ops (1 = serial sums) */
+} pbo_ksp_opts;
+
+/* Returns PETSc KSPConvergedReason; history[0..its] = ||z_k||_2 (len max_it+1). */
+int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* opts, const double* b,
+                 double* x, double* history, int64_t* its);
+/* Fixed number of iterations (no stopping test) -- the CPU baseline workload. Returns dp. */
+double pbo_cg_fixed(const int64_t n[3], const double h[3], int64_t iters, int nthreads,
+                    const double* b, double* x, double* work /* 4*N */);
+
+/* ---- tridiagonal (src/tridsol.f90) -- arg order (sub, diag, super, rhs) as the code uses ---- */
+void pbo_fwd_sweep(int64_t n, const double* a, double* b, const double* c, double* d);
+void pbo_bwd_sweep(int64_t n, const double* b, const double* c, double* d);
+void pbo_tdma(int64_t n, const double* a, double* b, const double* c, double* d);
+void pbo_tdma_periodic(int64_t n, const double* a, double* b, const double* c, double* d);
+
+/* ---- compact schemes (src/compact_schemes.f90) ---- */
+void pbo_eval_1d_rhs(double a, double b, int opsign, int stagger, int64_t n, const double* f,
+                     double* rhs);
+void pbo_grad_1d(int64_t n, const double* f, double dx, double* df, int stagger);
+void pbo_interp_1d(int64_t n, const double* f, double* fi, int stagger);
+void pbo_grad(const int64_t n[3], const double* f, const double dx[3], double* df);
+void pbo_div(const int64_t n[3], const double* f, const double dx[3], double* df);
+void pbo_interp(const int64_t n[3], const double* f, double* fi, int stagger);
+void pbo_lapl(const int64_t n[3], const double* f, const double dx[3], double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

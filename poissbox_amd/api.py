@@ -1,0 +1,353 @@
+"""Python host side of the poissbox KSPSolve path, mirroring the reference's Fortran/PETSc interface.
+
+Reference (3decomp/poissbox) -> here:
+  MPI_Init + PetscInitialize (src/example.f90:43-47)        -> Context(device, rank, nranks, uid)
+  initialise_grid(nglobal, da) (src/poissbox.f90:183-204)   -> initialise_grid(ctx, nglobal) -> DA
+  DMDAGetCorners (src/poissbox.f90:107)                     -> DA.get_corners()
+  initialise_linear_system(da, ctx, P, A, x, b) (:206-240)  -> initialise_linear_system(da, deltas)
+  MatCreateShell + MATOP_MULT = mfmult (:242-267, :300-322) -> Mat(kind=STAR7) .mult(x, y)
+  compute_lapl_pointwise(da, grid_deltas, x, b) (:84-126)   -> compute_lapl_pointwise(da, deltas, x, b)
+  solve(P, A, x, b) (:269-298) + KSPSetFromOptions          -> solve(P, A, x, b, options=argv)
+  Vec* (VecAXPY/VecNorm/VecSum/VecDuplicate/...)            -> Vec methods
+  tdma / tdma_periodic (src/tridsol.f90)                    -> tdma_batched(...)
+  grad/div/interp/interp_div/lapl (src/compact_schemes.f90) -> compact_* functions
+
+All compute runs in libpoissbox_gpu.so (HIP kernels for gfx950); there is no CPU fallback.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+STAR7, COMPACT, ASSEMBLED27 = 0, 1, 2
+PC_NONE, PC_JACOBI, PC_SOR, PC_MG = 0, 1, 2, 3
+
+REASONS = {0: "CONVERGED_ITERATING", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",
+           4: "CONVERGED_ITS", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",
+           -9: "DIVERGED_NANORINF", -10: "DIVERGED_INDEFINITE_MAT"}
+
+
+def _i64_3(v):
+    return (C.c_int64 * 3)(*[int(t) for t in v])
+
+
+def _d_3(v):
+    return (C.c_double * 3)(*[float(t) for t in v])
+
+
+def _dptr(a):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(L.P_d)
+
+
+def comm_unique_id():
+    buf = C.create_string_buffer(128)
+    L.call("pb_comm_unique_id", buf)
+    return bytes(buf.raw)
+
+
+def slab_partition(nz, nranks, rank):
+    k0, nk = C.c_int64(), C.c_int64()
+    L.call("pb_slab_partition", int(nz), int(nranks), int(rank), C.byref(k0), C.byref(nk))
+    return k0.value, nk.value
+
+
+class Context:
+    """One GPU, one rank. nranks > 1 needs either an RCCL unique id (uid, from rank 0's
+    comm_unique_id()) or a host transport (set_host_transport) before the grid is created."""
+
+    def __init__(self, device=0, rank=0, nranks=1, uid=None):
+        h = C.c_void_p()
+        L.call("pb_ctx_create", int(device), int(rank), int(nranks), uid, C.byref(h))
+        self.h = h
+        self.rank, self.nranks = rank, nranks
+        self._keep = []
+
+    def set_host_transport(self, sendrecv, allreduce):
+        """sendrecv(send_lo, send_hi) -> (recv_lo, recv_hi) numpy arrays; allreduce(vals) -> vals."""
+
+        def _sr(user, s_lo, s_hi, r_lo, r_hi, count):
+            try:
+                a = np.ctypeslib.as_array(s_lo, shape=(count,)).copy()
+                b = np.ctypeslib.as_array(s_hi, shape=(count,)).copy()
+                lo, hi = sendrecv(a, b)
+                np.ctypeslib.as_array(r_lo, shape=(count,))[:] = lo
+                np.ctypeslib.as_array(r_hi, shape=(count,))[:] = hi
+                return 0
+            except Exception as e:  # pragma: no cover - reported through the C error path
+                print("host sendrecv failed:", e)
+                return 1
+
+        def _ar(user, vals, count):
+            try:
+                v = np.ctypeslib.as_array(vals, shape=(count,))
+                v[:] = allreduce(v.copy())
+                return 0
+            except Exception as e:  # pragma: no cover
+                print("host allreduce failed:", e)
+                return 1
+
+        f1, f2 = L.SENDRECV_FN(_sr), L.ALLREDUCE_FN(_ar)
+        self._keep += [f1, f2]
+        L.call("pb_ctx_set_host_transport", self.h, f1, f2, None)
+
+    def sync(self):
+        L.call("pb_ctx_sync", self.h)
+
+    def barrier(self):
+        L.call("pb_ctx_barrier", self.h)
+
+    def set_timing(self, on=True):
+        L.call("pb_ctx_set_timing", self.h, int(bool(on)))
+
+    def timing(self, name):
+        ms, cnt = C.c_double(), C.c_int64()
+        L.call("pb_ctx_get_timing", self.h, name.encode(), C.byref(ms), C.byref(cnt))
+        return ms.value, cnt.value
+
+    def reset_timing(self):
+        L.call("pb_ctx_reset_timing", self.h)
+
+    def destroy(self):
+        if self.h:
+            L.call("pb_ctx_destroy", self.h)
+            self.h = None
+
+
+class DA:
+    """DMDA analogue: periodic grid, z-slab per rank (src/poissbox.f90:191-202)."""
+
+    def __init__(self, ctx, nglobal, L_=(1.0, 1.0, 1.0)):
+        h = C.c_void_p()
+        L.call("pb_grid_create", ctx.h, _i64_3(nglobal), _d_3(L_), C.byref(h))
+        self.h, self.ctx = h, ctx
+        n, hh, nl = (C.c_int64 * 3)(), (C.c_double * 3)(), C.c_int64()
+        L.call("pb_grid_get_info", h, n, hh, C.byref(nl))
+        self.n = tuple(n)
+        self.spacing = tuple(hh)
+        self.nlocal = nl.value
+
+    def get_corners(self):
+        """0-based (start, size) of the owned block, like DMDAGetCorners."""
+        s, z = (C.c_int64 * 3)(), (C.c_int64 * 3)()
+        L.call("pb_grid_get_corners", self.h, s, z)
+        return tuple(s), tuple(z)
+
+    def create_global_vector(self):
+        return Vec(self)
+
+    def destroy(self):
+        if self.h:
+            L.call("pb_grid_destroy", self.h)
+            self.h = None
+
+
+class Vec:
+    def __init__(self, da, _handle=None):
+        self.da = da
+        if _handle is None:
+            h = C.c_void_p()
+            L.call("pb_vec_create", da.h, C.byref(h))
+            _handle = h
+        self.h = _handle
+
+    def duplicate(self):
+        return Vec(self.da)
+
+    def set(self, a):
+        L.call("pb_vec_set", self.h, float(a))
+        return self
+
+    def copy_to(self, dst):
+        L.call("pb_vec_copy", self.h, dst.h)
+
+    def axpy(self, a, x):  # VecAXPY(self, a, x): self = self + a*x
+        L.call("pb_vec_axpy", self.h, float(a), x.h)
+
+    def aypx(self, b, x):  # VecAYPX(self, b, x): self = x + b*self
+        L.call("pb_vec_aypx", self.h, float(b), x.h)
+
+    def scale(self, a):
+        L.call("pb_vec_scale", self.h, float(a))
+
+    def dot(self, y):
+        out = C.c_double()
+        L.call("pb_vec_dot", self.h, y.h, C.byref(out))
+        return out.value
+
+    def norm(self):
+        out = C.c_double()
+        L.call("pb_vec_norm2", self.h, C.byref(out))
+        return out.value
+
+    def sum(self):
+        out = C.c_double()
+        L.call("pb_vec_sum", self.h, C.byref(out))
+        return out.value
+
+    def set_values(self, owned):
+        a = np.ascontiguousarray(owned, dtype=np.float64).reshape(-1)
+        if a.size != self.da.nlocal:
+            raise ValueError(f"expected {self.da.nlocal} owned values, got {a.size}")
+        L.call("pb_vec_set_values_host", self.h, _dptr(a))
+
+    def get_values(self):
+        a = np.empty(self.da.nlocal)
+        L.call("pb_vec_get_values_host", self.h, _dptr(a))
+        return a
+
+    def set_random(self, seed):
+        L.call("pb_vec_set_random", self.h, C.c_uint64(int(seed)))
+
+    def device_ptr(self):
+        p, n = C.c_void_p(), C.c_int64()
+        L.call("pb_vec_device_ptr", self.h, C.byref(p), C.byref(n))
+        return p.value, n.value
+
+    def destroy(self):
+        if self.h:
+            L.call("pb_vec_destroy", self.h)
+            self.h = None
+
+
+class Mat:
+    """MatShell analogue (kind STAR7 = mfmult's compute_lapl_pointwise) or the assembled P."""
+
+    def __init__(self, da, kind=STAR7, deltas=None):
+        h = C.c_void_p()
+        d = _d_3(deltas) if deltas is not None else None
+        L.call("pb_op_create", da.h, int(kind), d, C.byref(h))
+        self.h, self.da, self.kind = h, da, kind
+
+    def mult(self, x, y):  # MatMult(self, x, y)
+        L.call("pb_op_apply", self.h, x.h, y.h)
+
+    def diagonal(self):
+        d = C.c_double()
+        L.call("pb_op_get_diagonal", self.h, C.byref(d))
+        return d.value
+
+    def destroy(self):
+        if self.h:
+            L.call("pb_op_destroy", self.h)
+            self.h = None
+
+
+def MatMult(A, x, y):
+    A.mult(x, y)
+
+
+def ksp_options(argv=(), **kw):
+    o = L.KspOpts()
+    L.call("pb_ksp_opts_default", C.byref(o))
+    if argv:
+        arr = (C.c_char_p * len(argv))(*[str(a).encode() for a in argv])
+        L.call("pb_ksp_opts_parse", C.byref(o), len(argv), arr)
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+class KSP:
+    """KSPCreate + KSPSetOperators(ksp, A, P) + KSPSetFromOptions (src/poissbox.f90:293-295)."""
+
+    def __init__(self, A, P=None, options=None):
+        self.opts = options if isinstance(options, L.KspOpts) else ksp_options(options or ())
+        h = C.c_void_p()
+        L.call("pb_ksp_create", A.h, (P or A).h, C.byref(self.opts), C.byref(h))
+        self.h = h
+
+    def solve(self, b, x):
+        """Returns (reason, its, history[:its+1])."""
+        res = L.KspResult()
+        hist = np.zeros(int(self.opts.max_it) + 1)
+        L.call("pb_ksp_solve", self.h, b.h, x.h, C.byref(res), _dptr(hist), hist.size)
+        self.result = res
+        return res.reason, res.its, hist[: res.its + 1].copy()
+
+    def begin(self, b, x):
+        L.call("pb_ksp_begin", self.h, b.h, x.h)
+
+    def iterate(self, n):
+        L.call("pb_ksp_iterate", self.h, int(n))
+
+    def end(self):
+        res = L.KspResult()
+        hist = np.zeros(int(self.opts.max_it) + 1)
+        L.call("pb_ksp_end", self.h, C.byref(res), _dptr(hist), hist.size)
+        self.result = res
+        return res.reason, res.its, hist[: res.its + 1].copy()
+
+    def destroy(self):
+        if self.h:
+            L.call("pb_ksp_destroy", self.h)
+            self.h = None
+
+
+# ---- reference-named entry points ----------------------------------------------------------
+def initialise_grid(ctx, nglobal, L_=(1.0, 1.0, 1.0)):
+    """src/poissbox.f90:183-204"""
+    return DA(ctx, nglobal, L_)
+
+
+def initialise_linear_system(da, grid_deltas, matrix_free=True):
+    """src/poissbox.f90:206-240: returns (P, A, x, b); A is the matrix-free operator when
+    matrix_free (src/example.f90:60-65), else A = P."""
+    P = Mat(da, ASSEMBLED27, grid_deltas)
+    A = Mat(da, STAR7, grid_deltas) if matrix_free else P
+    return P, A, Vec(da), Vec(da)
+
+
+def compute_lapl_pointwise(da, grid_deltas, x, b):
+    """src/poissbox.f90:84-126 (one pass of the stencil, same kernel as mfmult)."""
+    op = Mat(da, STAR7, grid_deltas)
+    try:
+        op.mult(x, b)
+    finally:
+        op.destroy()
+
+
+def solve(P, A, x, b, options=("-ksp_type", "cg", "-pc_type", "jacobi")):
+    """src/poissbox.f90:269-298: constant null space on A and P, KSPSolve(b -> x)."""
+    ksp = KSP(A, P, options)
+    try:
+        return ksp.solve(b, x)
+    finally:
+        ksp.destroy()
+
+
+# ---- tridiagonal / compact ------------------------------------------------------------------
+def tdma_batched(ctx, n, nbatch, line_stride, elem_stride, a_ptr, b_ptr, c_ptr, d_ptr,
+                 periodic=False):
+    L.call("pb_tdma_batched", ctx.h, int(n), int(nbatch), int(line_stride), int(elem_stride),
+           a_ptr, b_ptr, c_ptr, d_ptr, int(bool(periodic)))
+
+
+def pcr_alpha_batched(ctx, n, nbatch, line_stride, elem_stride, alpha, d_ptr):
+    L.call("pb_pcr_alpha_batched", ctx.h, int(n), int(nbatch), int(line_stride),
+           int(elem_stride), float(alpha), d_ptr)
+
+
+def compact_1d_batched(ctx, kind, stagger, dx, n, nbatch, line_stride, elem_stride, f_ptr,
+                       out_ptr):
+    L.call("pb_compact_1d_batched", ctx.h, int(kind), int(stagger), float(dx), int(n),
+           int(nbatch), int(line_stride), int(elem_stride), f_ptr, out_ptr)
+
+
+def compact_grad(da, dx, f, df3):
+    arr = (C.c_void_p * 3)(*[v.h.value for v in df3])
+    L.call("pb_compact_grad", da.h, _d_3(dx), f.h, arr)
+
+
+def compact_div(da, dx, f3, df):
+    arr = (C.c_void_p * 3)(*[v.h.value for v in f3])
+    L.call("pb_compact_div", da.h, _d_3(dx), arr, df.h)
+
+
+def compact_interp(da, stagger, f, fi):
+    L.call("pb_compact_interp", da.h, int(stagger), f.h, fi.h)
+
+
+def compact_lapl(da, dx, f, out):
+    L.call("pb_compact_lapl", da.h, _d_3(dx), f.h, out.h)

@@ -1,0 +1,425 @@
+// pb_compact.hip -- batched tridiagonal solvers and the 6th-order staggered compact operators.
+//
+// Replaces src/tridsol.f90 (tdma, tdma_periodic, fwd_sweep, bwd_sweep) and
+// src/compact_schemes.f90 (grad/div/interp/interp_div/lapl and their 1-D forms).
+//
+// * General systems (pb_tdma_batched): one lane per line, Thomas + Sherman-Morrison in the
+//   reference's exact operation order (bit-identical results with -ffp-contract=off).
+// * Compact-scheme systems are constant-coefficient periodic (alpha, 1, alpha): the Thomas
+//   factorisation (multipliers, modified diagonal, Sherman-Morrison vector) is the same for every
+//   line, so it is computed once on the host with the reference's arithmetic and each line only
+//   runs the 3 data-dependent sweeps -- again bit-identical to the reference.
+// * pb_pcr_alpha_batched: parallel cyclic reduction, one line per workgroup held in LDS
+//   (log2(n) steps); results agree with Thomas to rounding, not bit for bit.
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "pb_internal.hpp"
+
+namespace pb {
+
+// ---------------------------------------------------------------------------------------------
+// General batched Thomas / periodic Thomas (src/tridsol.f90:22-115)
+// ---------------------------------------------------------------------------------------------
+struct LineMap {
+  int64_t m1, s1, s2, es;  // base(l) = (l % m1) * s1 + (l / m1) * s2; element e at base + e*es
+  __device__ __forceinline__ int64_t base(int64_t l) const { return (l % m1) * s1 + (l / m1) * s2; }
+};
+
+__global__ __launch_bounds__(64) void tdma_kernel(int64_t n, int64_t nb, LineMap lm,
+                                                  const double* __restrict__ a, double* b,
+                                                  const double* __restrict__ c, double* d) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nb) return;
+  const int64_t o = lm.base(l), es = lm.es;
+  // fwd_sweep :90-94
+  for (int64_t i = 1; i < n; ++i) {
+    const double w = a[o + i * es] / b[o + (i - 1) * es];
+    b[o + i * es] = b[o + i * es] - w * c[o + (i - 1) * es];
+    d[o + i * es] = d[o + i * es] - w * d[o + (i - 1) * es];
+  }
+  // bwd_sweep :110-113
+  d[o + (n - 1) * es] = d[o + (n - 1) * es] / b[o + (n - 1) * es];
+  for (int64_t i = n - 2; i >= 0; --i)
+    d[o + i * es] = (d[o + i * es] - c[o + i * es] * d[o + (i + 1) * es]) / b[o + i * es];
+}
+
+// tdma_periodic :34-74; the two auxiliary Thomas solves share one forward elimination of bmod
+// (the reference recomputes bmod identically for the second solve). scratch: 2*n per line.
+__global__ __launch_bounds__(64) void tdma_periodic_kernel(int64_t n, int64_t nb, LineMap lm,
+                                                           const double* __restrict__ a,
+                                                           const double* __restrict__ b,
+                                                           const double* __restrict__ c,
+                                                           double* d, double* scratch) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nb) return;
+  const int64_t o = lm.base(l), es = lm.es;
+  double* bm = scratch + l;               // bm[i] at bm[i*nb]  (coalesced across lines)
+  double* u = scratch + n * nb + l;
+  const double a0 = a[o], cn = c[o + (n - 1) * es];
+  const double gamma = -b[o];
+  for (int64_t i = 0; i < n; ++i) {
+    bm[i * nb] = b[o + i * es];
+    u[i * nb] = 0.0;
+  }
+  bm[0] = bm[0] - gamma;
+  bm[(n - 1) * nb] = bm[(n - 1) * nb] - cn * a0 / gamma;
+  u[0] = gamma;
+  u[(n - 1) * nb] = cn;
+  for (int64_t i = 1; i < n; ++i) {
+    const double w = a[o + i * es] / bm[(i - 1) * nb];
+    bm[i * nb] = bm[i * nb] - w * c[o + (i - 1) * es];
+    d[o + i * es] = d[o + i * es] - w * d[o + (i - 1) * es];
+    u[i * nb] = u[i * nb] - w * u[(i - 1) * nb];
+  }
+  d[o + (n - 1) * es] = d[o + (n - 1) * es] / bm[(n - 1) * nb];
+  u[(n - 1) * nb] = u[(n - 1) * nb] / bm[(n - 1) * nb];
+  for (int64_t i = n - 2; i >= 0; --i) {
+    d[o + i * es] = (d[o + i * es] - c[o + i * es] * d[o + (i + 1) * es]) / bm[i * nb];
+    u[i * nb] = (u[i * nb] - c[o + i * es] * u[(i + 1) * nb]) / bm[i * nb];
+  }
+  const double num = d[o] + (a0 / gamma) * d[o + (n - 1) * es];
+  const double den = 1.0 + (u[0] + (a0 / gamma) * u[(n - 1) * nb]);
+  for (int64_t i = 0; i < n; ++i) d[o + i * es] = d[o + i * es] - (u[i * nb] * num) / den;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Constant-coefficient (alpha, 1, alpha) periodic factorisation, computed on the host with the
+// reference arithmetic of tdma_periodic (:51-70) applied to ld = ud = alpha, d = 1.
+// W[i] = a_i / bm'_{i-1}, BM[i] = bm'_i, U[i] = Sherman-Morrison vector solution.
+// ---------------------------------------------------------------------------------------------
+struct AlphaFactor {
+  double* dev = nullptr;  // [W | BM | U], 3n doubles
+  double alpha, gamma, a0g, den;
+};
+
+static std::mutex g_fac_mu;
+static std::map<std::pair<int, std::pair<int64_t, double>>, AlphaFactor> g_fac;
+
+static int alpha_factor(pb_ctx* ctx, int64_t n, double alpha, AlphaFactor* out) {
+  std::lock_guard<std::mutex> lk(g_fac_mu);
+  auto key = std::make_pair(ctx->device, std::make_pair(n, alpha));
+  auto it = g_fac.find(key);
+  if (it != g_fac.end()) {
+    *out = it->second;
+    return PB_OK;
+  }
+  std::vector<double> W(n, 0.0), BM(n, 1.0), U(n, 0.0);
+  const double a0 = alpha, cn = alpha;
+  const double gamma = -1.0;  // -b(1), b = 1
+  BM[0] = BM[0] - gamma;
+  BM[n - 1] = BM[n - 1] - cn * a0 / gamma;
+  U[0] = gamma;
+  U[n - 1] = cn;
+  for (int64_t i = 1; i < n; ++i) {
+    W[i] = alpha / BM[i - 1];
+    BM[i] = BM[i] - W[i] * alpha;
+    U[i] = U[i] - W[i] * U[i - 1];
+  }
+  U[n - 1] = U[n - 1] / BM[n - 1];
+  for (int64_t i = n - 2; i >= 0; --i) U[i] = (U[i] - alpha * U[i + 1]) / BM[i];
+  AlphaFactor f;
+  f.alpha = alpha;
+  f.gamma = gamma;
+  f.a0g = a0 / gamma;
+  f.den = 1.0 + (U[0] + f.a0g * U[n - 1]);
+  std::vector<double> all(3 * n);
+  memcpy(all.data(), W.data(), n * sizeof(double));
+  memcpy(all.data() + n, BM.data(), n * sizeof(double));
+  memcpy(all.data() + 2 * n, U.data(), n * sizeof(double));
+  PB_HIP(hipMalloc(&f.dev, 3 * n * sizeof(double)));
+  PB_HIP(hipMemcpy(f.dev, all.data(), 3 * n * sizeof(double), hipMemcpyHostToDevice));
+  g_fac[key] = f;
+  *out = f;
+  return PB_OK;
+}
+
+// Scheme parameters (src/compact_schemes.f90:188-190, :303-305)
+struct Scheme {
+  double a, b, alpha, sign;
+};
+static Scheme scheme(int kind, double dx) {
+  if (kind == 0) return Scheme{63.0 / 62.0 / dx, 17.0 / 62.0 / (3.0 * dx), 9.0 / 62.0, -1.0};
+  return Scheme{0.75, 1.0 / 20.0, 3.0 / 10.0, +1.0};
+}
+
+// One compact 1-D operator per line: RHS (eval_1d_rhs :332-372, periodic formula) fused into
+// the forward sweep, then backward sweep and Sherman-Morrison correction. `in2` (optional) is
+// added to the input first (div's Z step, :249), `addend` (optional) to the output (:250).
+__global__ __launch_bounds__(64) void compact_line_kernel(
+    int64_t n, int64_t nb, LineMap lm, Scheme sc, int shift, const double* __restrict__ in,
+    const double* __restrict__ in2, const double* __restrict__ addend, double* out,
+    const double* __restrict__ fac, double a0g, double den) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nb) return;
+  const int64_t o = lm.base(l), es = lm.es;
+  const double* W = fac;
+  const double* BM = fac + n;
+  const double* U = fac + 2 * n;
+  auto F = [&](int64_t i) -> double {
+    i = i < 0 ? i + n : (i >= n ? i - n : i);
+    double v = in[o + i * es];
+    if (in2) v = v + in2[o + i * es];
+    return v;
+  };
+  auto rhs = [&](int64_t i) -> double {
+    const double f0 = F(i + shift), fm1 = F(i - 1 + shift);
+    const double f1 = F(i + 1 + shift), fm2 = F(i - 2 + shift);
+    return sc.a * (f0 + sc.sign * fm1) + sc.b * (f1 + sc.sign * fm2);
+  };
+  // forward sweep: d[i] = rhs[i] - W[i] * d[i-1]
+  double prev = rhs(0);
+  out[o] = prev;
+  for (int64_t i = 1; i < n; ++i) {
+    const double di = rhs(i) - W[i] * prev;
+    out[o + i * es] = di;
+    prev = di;
+  }
+  // backward sweep
+  double next = out[o + (n - 1) * es] / BM[n - 1];
+  out[o + (n - 1) * es] = next;
+  const double dlast = next;
+  for (int64_t i = n - 2; i >= 0; --i) {
+    const double di = (out[o + i * es] - sc.alpha * next) / BM[i];
+    out[o + i * es] = di;
+    next = di;
+  }
+  // Sherman-Morrison correction (:69-70), then optional addend
+  const double num = next + a0g * dlast;
+  for (int64_t i = 0; i < n; ++i) {
+    double v = out[o + i * es] - (U[i] * num) / den;
+    if (addend) v = v + addend[o + i * es];
+    out[o + i * es] = v;
+  }
+}
+
+static int launch_line(pb_ctx* ctx, int kind, int stagger, double dx, int64_t n, int64_t nb,
+                       LineMap lm, const double* in, const double* in2, const double* addend,
+                       double* out) {
+  Scheme sc = scheme(kind, dx);
+  AlphaFactor f;
+  PB_TRY(alpha_factor(ctx, n, sc.alpha, &f));
+  const int shift = stagger == -1 ? 0 : 1;
+  const int64_t blocks = (nb + 63) / 64;
+  hipLaunchKernelGGL(compact_line_kernel, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, n, nb,
+                     lm, sc, shift, in, in2, addend, out, (const double*)f.dev, f.a0g, f.den);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+// direction d of an nx*ny*nz field
+static LineMap dir_map(const pb_grid* g, int d) {
+  const int64_t nx = g->n[0], ny = g->n[1];
+  if (d == 0) return LineMap{ny, nx, nx * ny, 1};
+  if (d == 1) return LineMap{nx, 1, nx * ny, nx};
+  return LineMap{nx * ny, 1, 0, nx * ny};
+}
+static int64_t nlines(const pb_grid* g, int d) { return g->nlocal / g->n[d]; }
+
+enum { K_GRAD = 0, K_INTERP = 1 };
+
+static int line3(pb_grid* g, int d, int kind, int stagger, double dx, const double* in,
+                 double* out, const double* in2 = nullptr, const double* addend = nullptr) {
+  return launch_line(g->ctx, kind, stagger, dx, g->n[d], nlines(g, d), dir_map(g, d), in, in2,
+                     addend, out);
+}
+
+// src/compact_schemes.f90:42-88 grad; scratch 5N
+static int grad3(pb_grid* g, const double dx[3], const double* f, double* df1, double* df2,
+                 double* df3, double* ws) {
+  const int64_t N = g->nlocal;
+  double *dff1 = ws, *dff3 = ws + N, *dfe1 = ws + 2 * N, *dfe2 = ws + 3 * N, *dfe3 = ws + 4 * N;
+  PB_TRY(line3(g, 2, K_INTERP, -1, 0.0, f, dff1));      // :61
+  PB_TRY(line3(g, 2, K_GRAD, -1, dx[2], f, dff3));      // :63  (dff2 = dff1, :62)
+  PB_TRY(line3(g, 1, K_INTERP, -1, 0.0, dff1, dfe1));   // :71
+  PB_TRY(line3(g, 1, K_GRAD, -1, dx[1], dff1, dfe2));   // :72
+  PB_TRY(line3(g, 1, K_INTERP, -1, 0.0, dff3, dfe3));   // :73
+  PB_TRY(line3(g, 0, K_GRAD, -1, dx[0], dfe1, df1));    // :81
+  PB_TRY(line3(g, 0, K_INTERP, -1, 0.0, dfe2, df2));    // :82
+  PB_TRY(line3(g, 0, K_INTERP, -1, 0.0, dfe3, df3));    // :83
+  return PB_OK;
+}
+
+// src/compact_schemes.f90:207-257 div; scratch 6N
+static int div3(pb_grid* g, const double dx[3], const double* f1, const double* f2,
+                const double* f3, double* out, double* ws) {
+  const int64_t N = g->nlocal;
+  double *dfe1 = ws, *dfe2 = ws + N, *dfe3 = ws + 2 * N;
+  double *dff1 = ws + 3 * N, *dff2 = ws + 4 * N, *dff3 = ws + 5 * N;
+  PB_TRY(line3(g, 0, K_GRAD, +1, dx[0], f1, dfe1));     // :227
+  PB_TRY(line3(g, 0, K_INTERP, +1, 0.0, f2, dfe2));     // :228
+  PB_TRY(line3(g, 0, K_INTERP, +1, 0.0, f3, dfe3));     // :229
+  PB_TRY(line3(g, 1, K_INTERP, +1, 0.0, dfe1, dff1));   // :237
+  PB_TRY(line3(g, 1, K_GRAD, +1, dx[1], dfe2, dff2));   // :238
+  PB_TRY(line3(g, 1, K_INTERP, +1, 0.0, dfe3, dff3));   // :239
+  double* dfc = dfe1;
+  PB_TRY(line3(g, 2, K_INTERP, +1, 0.0, dff1, dfc, dff2));       // :248 interp(dff1 + dff2)
+  PB_TRY(line3(g, 2, K_GRAD, +1, dx[2], dff3, out, nullptr, dfc));  // :249-250
+  return PB_OK;
+}
+
+int64_t compact_work_len(const pb_grid* g) { return 9 * g->nlocal; }
+
+// src/compact_schemes.f90:17-37 lapl = div(grad f); work: 9N
+int compact_lapl(pb_grid* g, const double dx[3], const double* f, double* out, double* work) {
+  ScopedTimer tm(g->ctx, "compact_lapl");
+  const int64_t N = g->nlocal;
+  double *df1 = work, *df2 = work + N, *df3 = work + 2 * N;
+  PB_TRY(grad3(g, dx, f, df1, df2, df3, work + 3 * N));
+  PB_TRY(div3(g, dx, df1, df2, df3, out, work + 3 * N));
+  return PB_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// PCR for (alpha, 1, alpha) periodic lines: one line per workgroup, line in LDS
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pcr_alpha_kernel(int64_t n, LineMap lm, double alpha,
+                                                        double* d) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* A = sm;          // sub
+  double* C = sm + n;      // super
+  double* D = sm + 2 * n;  // rhs
+  double* B = sm + 3 * n;  // diag
+  const int64_t o = lm.base(blockIdx.x), es = lm.es;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    A[i] = alpha;
+    C[i] = alpha;
+    B[i] = 1.0;
+    D[i] = d[o + i * es];
+  }
+  __syncthreads();
+  // periodic PCR: each step eliminates the couplings at distance s, doubling it
+  for (int64_t s = 1; s < n; s <<= 1) {
+    double na[16], nb_[16], nc[16], nd[16];
+    int cnt = 0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x, ++cnt) {
+      const int64_t im = (i - s % n + n) % n, ip = (i + s) % n;
+      const double k1 = A[i] / B[im], k2 = C[i] / B[ip];
+      na[cnt] = -A[im] * k1;
+      nc[cnt] = -C[ip] * k2;
+      nb_[cnt] = B[i] - C[im] * k1 - A[ip] * k2;
+      nd[cnt] = D[i] - D[im] * k1 - D[ip] * k2;
+    }
+    __syncthreads();
+    cnt = 0;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x, ++cnt) {
+      A[i] = na[cnt];
+      C[i] = nc[cnt];
+      B[i] = nb_[cnt];
+      D[i] = nd[cnt];
+    }
+    __syncthreads();
+  }
+  // after log2(n) steps (n a power of two) the remaining couplings are at distance n, i.e. on the
+  // row itself: (B_i + A_i + C_i) x_i = D_i
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) d[o + i * es] = D[i] / (B[i] + A[i] + C[i]);
+}
+
+}  // namespace pb
+
+using namespace pb;
+
+extern "C" {
+
+int pb_tdma_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                    int64_t elem_stride, const double* a, double* b, const double* c, double* d,
+                    int periodic) {
+  PB_CHECK_ARG(ctx && a && b && c && d, "bad tdma args");
+  PB_CHECK_ARG(n >= 2 && nbatch >= 1, "bad tdma sizes");
+  LineMap lm{nbatch, line_stride, 0, elem_stride};
+  const int64_t blocks = (nbatch + 63) / 64;
+  ScopedTimer tm(ctx, "tdma");
+  if (!periodic) {
+    hipLaunchKernelGGL(tdma_kernel, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, n, nbatch, lm,
+                       a, b, c, d);
+    PB_HIP(hipGetLastError());
+    return PB_OK;
+  }
+  double* scratch = nullptr;
+  PB_HIP(hipMallocAsync((void**)&scratch, (size_t)(2 * n * nbatch) * sizeof(double), ctx->stream));
+  hipLaunchKernelGGL(tdma_periodic_kernel, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, n,
+                     nbatch, lm, a, (const double*)b, c, d, scratch);
+  PB_HIP(hipGetLastError());
+  PB_HIP(hipFreeAsync(scratch, ctx->stream));
+  return PB_OK;
+}
+
+int pb_pcr_alpha_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                         int64_t elem_stride, double alpha, double* d) {
+  PB_CHECK_ARG(ctx && d, "bad pcr args");
+  PB_CHECK_ARG(n >= 3 && n <= 4096 && nbatch >= 1, "pcr: 3 <= n <= 4096");
+  PB_CHECK_ARG((n & (n - 1)) == 0, "pcr: n must be a power of two");
+  LineMap lm{nbatch, line_stride, 0, elem_stride};
+  ScopedTimer tm(ctx, "pcr");
+  hipLaunchKernelGGL(pcr_alpha_kernel, dim3((unsigned)nbatch), dim3(256), 4 * n * sizeof(double),
+                     ctx->stream, n, lm, alpha, d);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+int pb_compact_1d_batched(pb_ctx* ctx, int kind, int stagger, double dx, int64_t n,
+                          int64_t nbatch, int64_t line_stride, int64_t elem_stride,
+                          const double* f, double* out) {
+  PB_CHECK_ARG(ctx && f && out && f != out, "bad compact_1d args");
+  PB_CHECK_ARG(kind == 0 || kind == 1, "kind: 0 = derivative, 1 = interpolation");
+  PB_CHECK_ARG(stagger == -1 || stagger == 1, "stagger must be -1 or +1");
+  PB_CHECK_ARG(n >= 3 && nbatch >= 1, "compact_1d: n >= 3");
+  LineMap lm{nbatch, line_stride, 0, elem_stride};
+  return launch_line(ctx, kind == 0 ? K_GRAD : K_INTERP, stagger, dx, n, nbatch, lm, f, nullptr,
+                     nullptr, out);
+}
+
+static int single_rank(const pb_grid* g) {
+  return g->ctx->nranks == 1
+             ? PB_OK
+             : set_error(PB_ERR_UNSUPPORTED, "compact operators on a split grid: not yet");
+}
+
+int pb_compact_grad(pb_grid* g, const double dx[3], const pb_vec* f, pb_vec* const df[3]) {
+  PB_CHECK_ARG(g && dx && f && df && df[0] && df[1] && df[2], "bad grad args");
+  PB_TRY(single_rank(g));
+  double* ws = nullptr;
+  PB_HIP(hipMallocAsync((void**)&ws, (size_t)(5 * g->nlocal) * sizeof(double), g->ctx->stream));
+  int rc = grad3(g, dx, f->d, df[0]->d, df[1]->d, df[2]->d, ws);
+  (void)hipFreeAsync(ws, g->ctx->stream);
+  return rc;
+}
+
+int pb_compact_div(pb_grid* g, const double dx[3], const pb_vec* const f[3], pb_vec* df) {
+  PB_CHECK_ARG(g && dx && f && f[0] && f[1] && f[2] && df, "bad div args");
+  PB_TRY(single_rank(g));
+  double* ws = nullptr;
+  PB_HIP(hipMallocAsync((void**)&ws, (size_t)(6 * g->nlocal) * sizeof(double), g->ctx->stream));
+  int rc = div3(g, dx, f[0]->d, f[1]->d, f[2]->d, df->d, ws);
+  (void)hipFreeAsync(ws, g->ctx->stream);
+  return rc;
+}
+
+int pb_compact_interp(pb_grid* g, int stagger, const pb_vec* f, pb_vec* fi) {
+  PB_CHECK_ARG(g && f && fi && f != fi, "bad interp args");
+  PB_CHECK_ARG(stagger == -1 || stagger == 1, "stagger must be -1 or +1");
+  PB_TRY(single_rank(g));
+  double* ws = nullptr;
+  const int64_t N = g->nlocal;
+  PB_HIP(hipMallocAsync((void**)&ws, (size_t)(2 * N) * sizeof(double), g->ctx->stream));
+  int rc = line3(g, 2, K_INTERP, stagger, 0.0, f->d, ws);           // :238
+  if (!rc) rc = line3(g, 1, K_INTERP, stagger, 0.0, ws, ws + N);    // :246
+  if (!rc) rc = line3(g, 0, K_INTERP, stagger, 0.0, ws + N, fi->d); // :254
+  (void)hipFreeAsync(ws, g->ctx->stream);
+  return rc;
+}
+
+int pb_compact_lapl(pb_grid* g, const double dx[3], const pb_vec* f, pb_vec* out) {
+  PB_CHECK_ARG(g && dx && f && out && f != out, "bad lapl args");
+  PB_TRY(single_rank(g));
+  double* ws = nullptr;
+  PB_HIP(hipMallocAsync((void**)&ws, (size_t)compact_work_len(g) * sizeof(double), g->ctx->stream));
+  int rc = compact_lapl(g, dx, f->d, out->d, ws);
+  (void)hipFreeAsync(ws, g->ctx->stream);
+  return rc;
+}
+
+}  // extern "C"

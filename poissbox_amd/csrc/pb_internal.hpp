@@ -1,0 +1,182 @@
+// pb_internal.hpp -- shared internals of libpoissbox_gpu (host runtime + HIP kernels, gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "poissbox_gpu.h"
+
+namespace pb {
+
+// ---------------------------------------------------------------------------------------------
+// Errors
+// ---------------------------------------------------------------------------------------------
+int set_error(int code, const char* fmt, ...);
+
+#define PB_HIP(call)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return ::pb::set_error(PB_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #call,     \
+                             hipGetErrorString(e_));                                    \
+  } while (0)
+
+#define PB_NCCL(call)                                                                   \
+  do {                                                                                  \
+    ncclResult_t r_ = (call);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      return ::pb::set_error(PB_ERR_COMM, "%s:%d %s: %s", __FILE__, __LINE__, #call,    \
+                             ncclGetErrorString(r_));                                   \
+  } while (0)
+
+#define PB_TRY(call)            \
+  do {                          \
+    int rc_ = (call);           \
+    if (rc_ != PB_OK) return rc_; \
+  } while (0)
+
+#define PB_CHECK_ARG(cond, msg)                                  \
+  do {                                                           \
+    if (!(cond)) return ::pb::set_error(PB_ERR_ARG, "%s", msg);  \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// Kernel timing (HIP events on the context stream)
+// ---------------------------------------------------------------------------------------------
+struct TimerSlot {
+  double total_ms = 0.0;
+  int64_t count = 0;
+};
+
+}  // namespace pb
+
+struct pb_ctx {
+  int device = 0;
+  int rank = 0;
+  int nranks = 1;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  // host transport (tests)
+  pb_sendrecv_fn h_sendrecv = nullptr;
+  pb_allreduce_fn h_allreduce = nullptr;
+  void* h_user = nullptr;
+  // reduction scratch
+  double* d_partials = nullptr;   // [max_blocks * 8]
+  int64_t partials_cap = 0;
+  double* d_scalars = nullptr;    // small device scalars for vector reductions
+  double* h_scalars = nullptr;    // pinned mirror
+  int num_cus = 256;
+  // timing
+  bool timing = false;
+  std::map<std::string, pb::TimerSlot> timers;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<hipEvent_t> event_pool;
+};
+
+struct pb_grid {
+  pb_ctx* ctx = nullptr;
+  int64_t n[3] = {0, 0, 0};
+  double L[3] = {1, 1, 1};
+  double h[3] = {1, 1, 1};
+  int64_t k0 = 0, nzl = 0;   // owned planes [k0, k0 + nzl)
+  int64_t plane = 0;         // n[0] * n[1]
+  int64_t nlocal = 0;        // plane * nzl
+  // ghost planes (received halos) and send staging (CG boundary p planes)
+  double* ghost_lo = nullptr;
+  double* ghost_hi = nullptr;
+  double* bnd_lo = nullptr;
+  double* bnd_hi = nullptr;
+  double* h_stage = nullptr;  // pinned host staging for the host transport (4 planes)
+};
+
+struct pb_vec {
+  pb_grid* grid = nullptr;
+  double* d = nullptr;
+  int64_t nlocal = 0;
+};
+
+struct pb_op {
+  pb_grid* grid = nullptr;
+  int kind = PB_OP_STAR7;
+  double deltas[3] = {1, 1, 1};
+  double cx = 0, cy = 0, cz = 0, cc = 0;  // star coefficients
+  // compact scratch
+  double* work = nullptr;
+  int64_t work_len = 0;
+};
+
+namespace pb {
+
+// ---- coefficient helpers (src/coefficients.f90:22-48) ----
+struct Star {
+  double cx, cy, cz, cc;
+};
+Star star_coeffs(const double h[3]);
+
+// ---- timing ----
+void timer_begin(pb_ctx* ctx, const char* name, hipEvent_t* ev);
+void timer_end(pb_ctx* ctx, const char* name, hipEvent_t ev0);
+void timers_collect(pb_ctx* ctx);
+
+struct ScopedTimer {
+  pb_ctx* ctx;
+  const char* name;
+  hipEvent_t ev0 = nullptr;
+  ScopedTimer(pb_ctx* c, const char* n) : ctx(c), name(n) {
+    if (ctx->timing) timer_begin(ctx, name, &ev0);
+  }
+  ~ScopedTimer() {
+    if (ctx->timing) timer_end(ctx, name, ev0);
+  }
+};
+
+// ---- communication (RCCL or host transport) ----
+// Exchange z-boundary planes: send `lo` (first owned plane data) to rank-1 and `hi` to rank+1,
+// receive into grid->ghost_lo (from rank-1) / grid->ghost_hi (from rank+1). Stream ordered.
+int halo_exchange(pb_grid* g, const double* lo, const double* hi);
+// In-place SUM allreduce of `count` device doubles (stream ordered).
+int allreduce_device(pb_ctx* ctx, double* d_vals, int count);
+
+// ---- kernels (pb_stencil.hip) ----
+struct StencilPlanes {
+  const double* ghost_lo;  // plane at k = -1
+  const double* ghost_hi;  // plane at k = nzl
+};
+int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
+                       const StencilPlanes& gp);
+
+// CG state (device resident; all scalars computed on device, host only polls `done`)
+struct CgState {
+  double beta, betaold, dpi, dpiold, alpha, mu, dp, ttol, rnorm0;
+  double rtol, atol, dtol, dinv, ntot;
+  int64_t it, its, max_it, nhist;
+  int reason, done, pc, nullspace;
+};
+int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p, CgState* st,
+                   double dinv, double* hist, int* h_done);
+int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st);
+int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
+                     double* p_new, const StencilPlanes& gp, CgState* st);
+int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, double* x, double* r,
+                     const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
+                     int64_t host_iter);
+int stencil_blocks(pb_grid* g);  // number of partial-sum slots a stencil pass writes
+
+// ---- vector ops (pb_vecops.hip) ----
+int vec_fill(pb_ctx* ctx, double* d, int64_t n, double a);
+// form 0: VecAXPY y = y + coef*x;  1: VecAYPX y = x + coef*y;  2: VecScale y = coef*y
+int vec_update(pb_ctx* ctx, int form, double* y, const double* x, int64_t n, double coef);
+int vec_random(pb_ctx* ctx, double* d, int64_t n, uint64_t seed, int64_t g0);
+// reduce kind: 0 = sum(x), 1 = dot(x, y); result into *out (global over ranks)
+int vec_reduce(pb_ctx* ctx, int kind, const double* x, const double* y, int64_t n, double* out);
+
+// ---- partial-sum reduction (deterministic, fixed order) ----
+int reduce_partials(pb_ctx* ctx, const double* parts, int nparts, int width, double* out);
+
+}  // namespace pb

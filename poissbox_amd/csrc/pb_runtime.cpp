@@ -1,0 +1,442 @@
+// pb_runtime.cpp -- host runtime of libpoissbox_gpu: errors, context (device, stream, RCCL),
+// slab grid, vectors, halo exchange and allreduce, the operator entry point and kernel timing.
+#include <cstdarg>
+#include <cstdlib>
+#include <cstring>
+
+#include "pb_internal.hpp"
+
+namespace pb {
+
+static thread_local char g_err[1024] = "";
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+// src/coefficients.f90:22-48: [1,-2,1]/dx^2 per direction, centre summed x then y then z
+Star star_coeffs(const double h[3]) {
+  double inv[3];
+  for (int d = 0; d < 3; ++d) inv[d] = 1.0 / (h[d] * h[d]);
+  Star s;
+  s.cx = inv[0];
+  s.cy = inv[1];
+  s.cz = inv[2];
+  double c = 0.0;
+  c = c + -(2.0 * inv[0]);
+  c = c + -(2.0 * inv[1]);
+  c = c + -(2.0 * inv[2]);
+  s.cc = c;
+  return s;
+}
+
+// ---- timing ----
+static hipEvent_t take_event(pb_ctx* ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void timer_begin(pb_ctx* ctx, const char*, hipEvent_t* ev) {
+  *ev = take_event(ctx);
+  (void)hipEventRecord(*ev, ctx->stream);
+}
+
+void timer_end(pb_ctx* ctx, const char* name, hipEvent_t ev0) {
+  hipEvent_t ev1 = take_event(ctx);
+  (void)hipEventRecord(ev1, ctx->stream);
+  ctx->pending.push_back({std::string(name), {ev0, ev1}});
+  if (ctx->pending.size() > 4096) timers_collect(ctx);
+}
+
+void timers_collect(pb_ctx* ctx) {
+  for (auto& p : ctx->pending) {
+    float ms = 0.f;
+    (void)hipEventSynchronize(p.second.second);
+    (void)hipEventElapsedTime(&ms, p.second.first, p.second.second);
+    TimerSlot& t = ctx->timers[p.first];
+    t.total_ms += ms;
+    t.count += 1;
+    ctx->event_pool.push_back(p.second.first);
+    ctx->event_pool.push_back(p.second.second);
+  }
+  ctx->pending.clear();
+}
+
+// ---- communication ----
+int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
+  pb_ctx* ctx = g->ctx;
+  ScopedTimer tm(ctx, "halo");
+  const int64_t cnt = g->plane;
+  if (ctx->nranks == 1) {
+    PB_HIP(hipMemcpyAsync(g->ghost_lo, hi, cnt * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    PB_HIP(hipMemcpyAsync(g->ghost_hi, lo, cnt * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    return PB_OK;
+  }
+  const int down = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
+  const int up = (ctx->rank + 1) % ctx->nranks;
+  if (ctx->h_sendrecv) {
+    double* s_lo = g->h_stage;
+    double* s_hi = g->h_stage + cnt;
+    double* r_lo = g->h_stage + 2 * cnt;
+    double* r_hi = g->h_stage + 3 * cnt;
+    PB_HIP(hipMemcpyAsync(s_lo, lo, cnt * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    PB_HIP(hipMemcpyAsync(s_hi, hi, cnt * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    PB_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->h_sendrecv(ctx->h_user, s_lo, s_hi, r_lo, r_hi, cnt) != 0)
+      return set_error(PB_ERR_COMM, "host sendrecv callback failed");
+    PB_HIP(hipMemcpyAsync(g->ghost_lo, r_lo, cnt * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    PB_HIP(hipMemcpyAsync(g->ghost_hi, r_hi, cnt * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    return PB_OK;
+  }
+  // Two phases whose issue order pairs correctly even when down == up (2 ranks):
+  //   (1) send my lowest plane down, receive the plane above me from up  -> ghost_hi
+  //   (2) send my highest plane up,  receive the plane below me from down -> ghost_lo
+  PB_NCCL(ncclGroupStart());
+  PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->stream));
+  PB_NCCL(ncclRecv(g->ghost_hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->stream));
+  PB_NCCL(ncclSend(hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->stream));
+  PB_NCCL(ncclRecv(g->ghost_lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->stream));
+  PB_NCCL(ncclGroupEnd());
+  return PB_OK;
+}
+
+int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
+  if (ctx->nranks == 1) return PB_OK;
+  ScopedTimer tm(ctx, "allreduce");
+  if (ctx->h_allreduce) {
+    PB_HIP(hipMemcpyAsync(ctx->h_scalars + 16, d_vals, count * sizeof(double), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    PB_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->h_allreduce(ctx->h_user, ctx->h_scalars + 16, count) != 0)
+      return set_error(PB_ERR_COMM, "host allreduce callback failed");
+    PB_HIP(hipMemcpyAsync(d_vals, ctx->h_scalars + 16, count * sizeof(double), hipMemcpyHostToDevice,
+                          ctx->stream));
+    PB_HIP(hipStreamSynchronize(ctx->stream));  // staging buffer is reused by the next call
+    return PB_OK;
+  }
+  PB_NCCL(ncclAllReduce(d_vals, d_vals, (size_t)count, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+  return PB_OK;
+}
+
+}  // namespace pb
+
+using namespace pb;
+
+extern "C" {
+
+const char* pb_last_error(void) { return g_err; }
+
+int pb_version(int* major, int* minor) {
+  if (major) *major = PB_VERSION_MAJOR;
+  if (minor) *minor = PB_VERSION_MINOR;
+  return PB_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Context
+// ---------------------------------------------------------------------------------------------
+int pb_comm_unique_id(unsigned char uid[128]) {
+  PB_CHECK_ARG(uid, "uid is NULL");
+  ncclUniqueId id;
+  PB_NCCL(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  memcpy(uid, &id, 128);
+  return PB_OK;
+}
+
+int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb_ctx** out) {
+  PB_CHECK_ARG(out, "ctx out is NULL");
+  PB_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
+  int ndev = 0;
+  PB_HIP(hipGetDeviceCount(&ndev));
+  PB_CHECK_ARG(device >= 0 && device < ndev, "device index out of range");
+  PB_HIP(hipSetDevice(device));
+  pb_ctx* ctx = new pb_ctx();
+  ctx->device = device;
+  ctx->rank = rank;
+  ctx->nranks = nranks;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+      cus > 0)
+    ctx->num_cus = cus;
+  PB_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  ctx->partials_cap = (int64_t)1 << 20;  // doubles: room for 131072 blocks x 8 sums
+  PB_HIP(hipMalloc(&ctx->d_partials, ctx->partials_cap * sizeof(double)));
+  PB_HIP(hipMalloc(&ctx->d_scalars, 64 * sizeof(double)));
+  PB_HIP(hipMemset(ctx->d_scalars, 0, 64 * sizeof(double)));
+  PB_HIP(hipHostMalloc(&ctx->h_scalars, 64 * sizeof(double), hipHostMallocDefault));
+  if (nranks > 1 && uid) {
+    ncclUniqueId id;
+    memcpy(&id, uid, 128);
+    PB_NCCL(ncclCommInitRank(&ctx->comm, nranks, id, rank));
+  }
+  *out = ctx;
+  return PB_OK;
+}
+
+int pb_ctx_set_host_transport(pb_ctx* ctx, pb_sendrecv_fn sr, pb_allreduce_fn ar, void* user) {
+  PB_CHECK_ARG(ctx && sr && ar, "bad host transport");
+  ctx->h_sendrecv = sr;
+  ctx->h_allreduce = ar;
+  ctx->h_user = user;
+  return PB_OK;
+}
+
+int pb_ctx_get_rank(const pb_ctx* ctx, int* rank, int* nranks) {
+  PB_CHECK_ARG(ctx, "ctx is NULL");
+  if (rank) *rank = ctx->rank;
+  if (nranks) *nranks = ctx->nranks;
+  return PB_OK;
+}
+
+int pb_ctx_sync(pb_ctx* ctx) {
+  PB_CHECK_ARG(ctx, "ctx is NULL");
+  PB_HIP(hipStreamSynchronize(ctx->stream));
+  return PB_OK;
+}
+
+int pb_ctx_barrier(pb_ctx* ctx) {
+  PB_CHECK_ARG(ctx, "ctx is NULL");
+  PB_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->nranks > 1) {
+    PB_TRY(allreduce_device(ctx, ctx->d_scalars + 32, 1));
+    PB_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  return PB_OK;
+}
+
+int pb_ctx_destroy(pb_ctx* ctx) {
+  if (!ctx) return PB_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  timers_collect(ctx);
+  for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  (void)hipFree(ctx->d_partials);
+  (void)hipFree(ctx->d_scalars);
+  (void)hipHostFree(ctx->h_scalars);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return PB_OK;
+}
+
+int pb_ctx_set_timing(pb_ctx* ctx, int enable) {
+  PB_CHECK_ARG(ctx, "ctx is NULL");
+  ctx->timing = enable != 0;
+  return PB_OK;
+}
+
+int pb_ctx_get_timing(pb_ctx* ctx, const char* name, double* total_ms, int64_t* count) {
+  PB_CHECK_ARG(ctx && name, "bad args");
+  timers_collect(ctx);
+  auto it = ctx->timers.find(name);
+  if (total_ms) *total_ms = it == ctx->timers.end() ? 0.0 : it->second.total_ms;
+  if (count) *count = it == ctx->timers.end() ? 0 : it->second.count;
+  return PB_OK;
+}
+
+int pb_ctx_reset_timing(pb_ctx* ctx) {
+  PB_CHECK_ARG(ctx, "ctx is NULL");
+  timers_collect(ctx);
+  ctx->timers.clear();
+  return PB_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Grid
+// ---------------------------------------------------------------------------------------------
+int pb_slab_partition(int64_t nz, int nranks, int rank, int64_t* kstart, int64_t* nk) {
+  PB_CHECK_ARG(nz >= 1 && nranks >= 1 && rank >= 0 && rank < nranks, "bad partition args");
+  const int64_t q = nz / nranks, r = nz % nranks;
+  const int64_t mine = q + (rank < r ? 1 : 0);
+  const int64_t start = rank * q + (rank < r ? rank : r);
+  if (kstart) *kstart = start;
+  if (nk) *nk = mine;
+  return PB_OK;
+}
+
+int pb_grid_create(pb_ctx* ctx, const int64_t n[3], const double L[3], pb_grid** out) {
+  PB_CHECK_ARG(ctx && n && out, "bad grid args");
+  for (int d = 0; d < 3; ++d) PB_CHECK_ARG(n[d] >= 3, "grid needs n >= 3 in every direction");
+  PB_CHECK_ARG(n[0] < (1 << 30) && n[1] < (1 << 30), "nx, ny must fit in int32");
+  PB_CHECK_ARG(n[2] >= ctx->nranks, "fewer z-planes than ranks");
+  PB_CHECK_ARG(ctx->nranks == 1 || ctx->comm || ctx->h_sendrecv,
+               "multi-rank context has neither RCCL nor a host transport");
+  PB_HIP(hipSetDevice(ctx->device));
+  pb_grid* g = new pb_grid();
+  g->ctx = ctx;
+  for (int d = 0; d < 3; ++d) {
+    g->n[d] = n[d];
+    g->L[d] = L ? L[d] : 1.0;
+    g->h[d] = g->L[d] / (double)n[d];  // src/example.f90:33-35
+  }
+  PB_TRY(pb_slab_partition(n[2], ctx->nranks, ctx->rank, &g->k0, &g->nzl));
+  g->plane = n[0] * n[1];
+  g->nlocal = g->plane * g->nzl;
+  const size_t pb = (size_t)g->plane * sizeof(double);
+  double* ghosts = nullptr;
+  if (hipMalloc(&ghosts, 4 * pb) != hipSuccess) {
+    delete g;
+    return set_error(PB_ERR_ALLOC, "ghost planes: out of device memory");
+  }
+  g->ghost_lo = ghosts;
+  g->ghost_hi = ghosts + g->plane;
+  g->bnd_lo = ghosts + 2 * g->plane;
+  g->bnd_hi = ghosts + 3 * g->plane;
+  if (ctx->h_sendrecv) PB_HIP(hipHostMalloc(&g->h_stage, 4 * pb, hipHostMallocDefault));
+  *out = g;
+  return PB_OK;
+}
+
+int pb_grid_get_corners(const pb_grid* g, int64_t start[3], int64_t size[3]) {
+  PB_CHECK_ARG(g, "grid is NULL");
+  if (start) {
+    start[0] = 0;
+    start[1] = 0;
+    start[2] = g->k0;
+  }
+  if (size) {
+    size[0] = g->n[0];
+    size[1] = g->n[1];
+    size[2] = g->nzl;
+  }
+  return PB_OK;
+}
+
+int pb_grid_get_info(const pb_grid* g, int64_t n[3], double h[3], int64_t* nlocal) {
+  PB_CHECK_ARG(g, "grid is NULL");
+  for (int d = 0; d < 3; ++d) {
+    if (n) n[d] = g->n[d];
+    if (h) h[d] = g->h[d];
+  }
+  if (nlocal) *nlocal = g->nlocal;
+  return PB_OK;
+}
+
+int pb_grid_destroy(pb_grid* g) {
+  if (!g) return PB_OK;
+  (void)hipStreamSynchronize(g->ctx->stream);
+  (void)hipFree(g->ghost_lo);
+  if (g->h_stage) (void)hipHostFree(g->h_stage);
+  delete g;
+  return PB_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Vectors
+// ---------------------------------------------------------------------------------------------
+int pb_vec_create(pb_grid* g, pb_vec** out) {
+  PB_CHECK_ARG(g && out, "bad vec args");
+  pb_vec* v = new pb_vec();
+  v->grid = g;
+  v->nlocal = g->nlocal;
+  if (hipMalloc(&v->d, (size_t)v->nlocal * sizeof(double)) != hipSuccess) {
+    delete v;
+    return set_error(PB_ERR_ALLOC, "vector of %lld doubles: out of device memory",
+                     (long long)g->nlocal);
+  }
+  int rc = vec_fill(g->ctx, v->d, v->nlocal, 0.0);  // PETSc vectors start zeroed
+  if (rc) return rc;
+  *out = v;
+  return PB_OK;
+}
+
+int pb_vec_duplicate(const pb_vec* v, pb_vec** out) {
+  PB_CHECK_ARG(v, "vec is NULL");
+  return pb_vec_create(v->grid, out);
+}
+
+int pb_vec_destroy(pb_vec* v) {
+  if (!v) return PB_OK;
+  (void)hipStreamSynchronize(v->grid->ctx->stream);
+  (void)hipFree(v->d);
+  delete v;
+  return PB_OK;
+}
+
+int pb_vec_set(pb_vec* v, double a) {
+  PB_CHECK_ARG(v, "vec is NULL");
+  return vec_fill(v->grid->ctx, v->d, v->nlocal, a);
+}
+
+static int same_layout(const pb_vec* a, const pb_vec* b) {
+  return a && b && a->grid == b->grid;
+}
+
+int pb_vec_copy(const pb_vec* src, pb_vec* dst) {
+  PB_CHECK_ARG(same_layout(src, dst), "vectors of different grids");
+  if (src == dst) return PB_OK;
+  PB_HIP(hipMemcpyAsync(dst->d, src->d, (size_t)src->nlocal * sizeof(double),
+                        hipMemcpyDeviceToDevice, src->grid->ctx->stream));
+  return PB_OK;
+}
+
+int pb_vec_axpy(pb_vec* y, double a, const pb_vec* x) {
+  PB_CHECK_ARG(same_layout(x, y), "vectors of different grids");
+  return vec_update(y->grid->ctx, 0, y->d, x->d, y->nlocal, a);
+}
+
+int pb_vec_aypx(pb_vec* y, double b, const pb_vec* x) {
+  PB_CHECK_ARG(same_layout(x, y), "vectors of different grids");
+  return vec_update(y->grid->ctx, 1, y->d, x->d, y->nlocal, b);
+}
+
+int pb_vec_scale(pb_vec* v, double a) {
+  PB_CHECK_ARG(v, "vec is NULL");
+  return vec_update(v->grid->ctx, 2, v->d, nullptr, v->nlocal, a);
+}
+
+int pb_vec_dot(const pb_vec* x, const pb_vec* y, double* out) {
+  PB_CHECK_ARG(same_layout(x, y) && out, "bad dot args");
+  return vec_reduce(x->grid->ctx, 1, x->d, y->d, x->nlocal, out);
+}
+
+int pb_vec_norm2(const pb_vec* v, double* out) {
+  PB_CHECK_ARG(v && out, "bad norm args");
+  double s = 0.0;
+  PB_TRY(vec_reduce(v->grid->ctx, 1, v->d, v->d, v->nlocal, &s));
+  *out = sqrt(s);
+  return PB_OK;
+}
+
+int pb_vec_sum(const pb_vec* v, double* out) {
+  PB_CHECK_ARG(v && out, "bad sum args");
+  return vec_reduce(v->grid->ctx, 0, v->d, nullptr, v->nlocal, out);
+}
+
+int pb_vec_set_values_host(pb_vec* v, const double* owned) {
+  PB_CHECK_ARG(v && owned, "bad set_values args");
+  PB_HIP(hipMemcpy(v->d, owned, (size_t)v->nlocal * sizeof(double), hipMemcpyHostToDevice));
+  return PB_OK;
+}
+
+int pb_vec_get_values_host(const pb_vec* v, double* owned) {
+  PB_CHECK_ARG(v && owned, "bad get_values args");
+  PB_HIP(hipStreamSynchronize(v->grid->ctx->stream));
+  PB_HIP(hipMemcpy(owned, v->d, (size_t)v->nlocal * sizeof(double), hipMemcpyDeviceToHost));
+  return PB_OK;
+}
+
+int pb_vec_set_random(pb_vec* v, uint64_t seed) {
+  PB_CHECK_ARG(v, "vec is NULL");
+  return vec_random(v->grid->ctx, v->d, v->nlocal, seed, v->grid->k0 * v->grid->plane);
+}
+
+int pb_vec_device_ptr(pb_vec* v, double** dptr, int64_t* nlocal) {
+  PB_CHECK_ARG(v, "vec is NULL");
+  if (dptr) *dptr = v->d;
+  if (nlocal) *nlocal = v->nlocal;
+  return PB_OK;
+}
+
+}  // extern "C"

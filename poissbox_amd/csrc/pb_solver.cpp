@@ -1,0 +1,394 @@
+// pb_solver.cpp -- operator (MatShell analogue) and KSP (KSPSolve_CG analogue) host logic.
+//
+// The CG iteration runs as 2 fused stencil passes + 2 one-block finalize kernels per iteration
+// (plus a plane-sized boundary kernel and, on several ranks, one halo exchange and two scalar
+// allreduces). All CG scalars live on the device; the host never waits inside an iteration and
+// polls a per-iteration "done" flag (host-mapped) every `check_every` iterations, lagged by one
+// poll interval so that every rank stops after the same number of enqueued iterations.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "pb_internal.hpp"
+
+using namespace pb;
+
+namespace pb {
+int compact_lapl(pb_grid* g, const double dx[3], const double* f, double* out, double* work);
+int64_t compact_work_len(const pb_grid* g);
+}
+
+struct pb_ksp {
+  pb_op* A = nullptr;
+  pb_op* P = nullptr;
+  pb_ksp_opts opts;
+  double* r = nullptr;
+  double* p0 = nullptr;
+  double* p1 = nullptr;
+  double* w = nullptr;   // generic (unfused) path only
+  double* z = nullptr;   // generic path only
+  CgState* d_st = nullptr;
+  double* d_hist = nullptr;
+  int64_t nhist = 0;
+  int* h_done = nullptr;      // host-mapped, one flag per host iteration (+1)
+  int* h_done_dev = nullptr;  // its device alias
+  int64_t done_cap = 0;
+  std::vector<hipEvent_t> ring;
+  // solve state
+  const pb_vec* b = nullptr;
+  pb_vec* x = nullptr;
+  int64_t host_iter = 0;
+  bool stopped = false;
+  bool begun = false;
+};
+
+extern "C" {
+
+// ---------------------------------------------------------------------------------------------
+// Operator (src/poissbox.f90:242-267 initialise_matrix_free; :300-322 mfmult)
+// ---------------------------------------------------------------------------------------------
+int pb_op_create(pb_grid* g, int kind, const double deltas[3], pb_op** out) {
+  PB_CHECK_ARG(g && out, "bad op args");
+  PB_CHECK_ARG(kind == PB_OP_STAR7 || kind == PB_OP_COMPACT || kind == PB_OP_ASSEMBLED27,
+               "unknown operator kind");
+  pb_op* op = new pb_op();
+  op->grid = g;
+  op->kind = kind;
+  for (int d = 0; d < 3; ++d) op->deltas[d] = deltas ? deltas[d] : g->h[d];
+  Star s = star_coeffs(op->deltas);
+  op->cx = s.cx;
+  op->cy = s.cy;
+  op->cz = s.cz;
+  op->cc = s.cc;
+  if (kind == PB_OP_COMPACT) {
+    if (g->ctx->nranks != 1) {
+      delete op;
+      return set_error(PB_ERR_UNSUPPORTED, "compact operator on a split grid is not supported yet");
+    }
+    op->work_len = compact_work_len(g);
+    if (hipMalloc(&op->work, (size_t)op->work_len * sizeof(double)) != hipSuccess) {
+      delete op;
+      return set_error(PB_ERR_ALLOC, "compact operator workspace: out of device memory");
+    }
+  }
+  *out = op;
+  return PB_OK;
+}
+
+static int op_apply_raw(pb_op* op, const double* x, double* y) {
+  pb_grid* g = op->grid;
+  Star s{op->cx, op->cy, op->cz, op->cc};
+  if (op->kind == PB_OP_COMPACT) return compact_lapl(g, op->deltas, x, y, op->work);
+  // STAR7 and ASSEMBLED27 (the assembled BOX matrix has the same 7 non-zeros per row)
+  StencilPlanes gp;
+  if (g->ctx->nranks == 1) {
+    gp.ghost_lo = x + (g->nzl - 1) * g->plane;  // periodic wrap: no copy
+    gp.ghost_hi = x;
+  } else {
+    PB_TRY(halo_exchange(g, x, x + (g->nzl - 1) * g->plane));
+    gp.ghost_lo = g->ghost_lo;
+    gp.ghost_hi = g->ghost_hi;
+  }
+  return launch_star7_apply(g, s, x, y, gp);
+}
+
+int pb_op_apply(pb_op* op, const pb_vec* x, pb_vec* y) {
+  PB_CHECK_ARG(op && x && y, "bad apply args");
+  PB_CHECK_ARG(x->grid == op->grid && y->grid == op->grid, "vector/operator grid mismatch");
+  PB_CHECK_ARG(x != y, "MatMult requires distinct input and output vectors");
+  return op_apply_raw(op, x->d, y->d);
+}
+
+int pb_op_get_diagonal(const pb_op* op, double* diag) {
+  PB_CHECK_ARG(op && diag, "bad args");
+  *diag = op->cc;
+  return PB_OK;
+}
+
+int pb_op_destroy(pb_op* op) {
+  if (!op) return PB_OK;
+  if (op->work) {
+    (void)hipStreamSynchronize(op->grid->ctx->stream);
+    (void)hipFree(op->work);
+  }
+  delete op;
+  return PB_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Options (PETSc options database names, src/poissbox.f90:295 KSPSetFromOptions)
+// ---------------------------------------------------------------------------------------------
+int pb_ksp_opts_default(pb_ksp_opts* o) {
+  PB_CHECK_ARG(o, "opts is NULL");
+  o->rtol = 1e-5;
+  o->atol = 1e-50;
+  o->dtol = 1e5;
+  o->max_it = 10000;
+  o->ksp_type = PB_KSP_CG;
+  o->pc_type = PB_PC_JACOBI;
+  o->nullspace = 1;
+  o->monitor = 0;
+  o->converged_reason = 0;
+  o->check_every = 8;
+  return PB_OK;
+}
+
+int pb_ksp_opts_parse(pb_ksp_opts* o, int argc, const char* const* argv) {
+  PB_CHECK_ARG(o, "opts is NULL");
+  for (int i = 0; i < argc; ++i) {
+    const char* a = argv[i];
+    const char* v = i + 1 < argc ? argv[i + 1] : nullptr;
+    if (!strcmp(a, "-ksp_type") && v) {
+      if (strcmp(v, "cg")) return set_error(PB_ERR_UNSUPPORTED, "-ksp_type %s: only cg", v);
+      o->ksp_type = PB_KSP_CG;
+      ++i;
+    } else if (!strcmp(a, "-pc_type") && v) {
+      if (!strcmp(v, "none")) o->pc_type = PB_PC_NONE;
+      else if (!strcmp(v, "jacobi")) o->pc_type = PB_PC_JACOBI;
+      else if (!strcmp(v, "sor")) o->pc_type = PB_PC_SOR;
+      else if (!strcmp(v, "mg") || !strcmp(v, "gamg")) o->pc_type = PB_PC_MG;
+      else return set_error(PB_ERR_UNSUPPORTED, "-pc_type %s", v);
+      ++i;
+    } else if (!strcmp(a, "-ksp_rtol") && v) {
+      o->rtol = atof(v);
+      ++i;
+    } else if (!strcmp(a, "-ksp_atol") && v) {
+      o->atol = atof(v);
+      ++i;
+    } else if (!strcmp(a, "-ksp_divtol") && v) {
+      o->dtol = atof(v);
+      ++i;
+    } else if (!strcmp(a, "-ksp_max_it") && v) {
+      o->max_it = atoll(v);
+      ++i;
+    } else if (!strcmp(a, "-ksp_monitor")) {
+      o->monitor = 1;
+    } else if (!strcmp(a, "-ksp_converged_reason")) {
+      o->converged_reason = 1;
+    }
+  }
+  return PB_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// KSP
+// ---------------------------------------------------------------------------------------------
+int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
+  PB_CHECK_ARG(A && out, "bad ksp args");
+  if (!P) P = A;
+  PB_CHECK_ARG(A->grid == P->grid, "A and P on different grids");
+  pb_ksp* k = new pb_ksp();
+  k->A = A;
+  k->P = P;
+  if (opts) k->opts = *opts;
+  else pb_ksp_opts_default(&k->opts);
+  if (k->opts.check_every < 1) k->opts.check_every = 8;
+  if (k->opts.pc_type != PB_PC_NONE && k->opts.pc_type != PB_PC_JACOBI) {
+    delete k;
+    return set_error(PB_ERR_UNSUPPORTED, "pc_type %d not available in this build", opts->pc_type);
+  }
+  pb_grid* g = A->grid;
+  const size_t vb = (size_t)g->nlocal * sizeof(double);
+  if (hipMalloc(&k->r, vb) != hipSuccess || hipMalloc(&k->p0, vb) != hipSuccess ||
+      hipMalloc(&k->p1, vb) != hipSuccess) {
+    delete k;
+    return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
+  }
+  if (A->kind != PB_OP_STAR7 && A->kind != PB_OP_ASSEMBLED27) {
+    if (hipMalloc(&k->w, vb) != hipSuccess || hipMalloc(&k->z, vb) != hipSuccess) {
+      delete k;
+      return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
+    }
+  }
+  PB_HIP(hipMalloc(&k->d_st, sizeof(CgState)));
+  *out = k;
+  return PB_OK;
+}
+
+static int ensure_done_cap(pb_ksp* k, int64_t need) {
+  if (need <= k->done_cap) return PB_OK;
+  int64_t cap = need < 1024 ? 1024 : need * 2;
+  int* h = nullptr;
+  PB_HIP(hipHostMalloc(&h, (size_t)cap * sizeof(int), hipHostMallocMapped));
+  memset(h, 0, (size_t)cap * sizeof(int));
+  if (k->h_done) {
+    PB_HIP(hipStreamSynchronize(k->A->grid->ctx->stream));
+    memcpy(h, k->h_done, (size_t)k->done_cap * sizeof(int));
+    (void)hipHostFree(k->h_done);
+  }
+  k->h_done = h;
+  PB_HIP(hipHostGetDevicePointer((void**)&k->h_done_dev, h, 0));
+  k->done_cap = cap;
+  return PB_OK;
+}
+
+int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
+  PB_CHECK_ARG(k && b && x, "bad begin args");
+  pb_grid* g = k->A->grid;
+  PB_CHECK_ARG(b->grid == g && x->grid == g, "vector/operator grid mismatch");
+  pb_ctx* ctx = g->ctx;
+  PB_CHECK_ARG(k->A->kind == PB_OP_STAR7 || k->A->kind == PB_OP_ASSEMBLED27,
+               "fused CG path requires the 7-point operator");
+  // history buffer: max_it + 1 entries
+  const int64_t nh = k->opts.max_it + 1;
+  if (nh > k->nhist) {
+    if (k->d_hist) (void)hipFree(k->d_hist);
+    PB_HIP(hipMalloc(&k->d_hist, (size_t)nh * sizeof(double)));
+    k->nhist = nh;
+  }
+  PB_TRY(ensure_done_cap(k, 1024));
+  memset(k->h_done, 0, (size_t)k->done_cap * sizeof(int));
+  CgState st;
+  memset(&st, 0, sizeof(st));
+  st.rtol = k->opts.rtol;
+  st.atol = k->opts.atol;
+  st.dtol = k->opts.dtol;
+  st.max_it = k->opts.max_it;
+  st.nhist = k->nhist;
+  st.pc = k->opts.pc_type;
+  st.nullspace = k->opts.nullspace;
+  // PCJacobi stores the reciprocal of diag(P) (src/coefficients.f90:44-46 centre coefficient)
+  st.dinv = k->opts.pc_type == PB_PC_JACOBI ? 1.0 / k->P->cc : 1.0;
+  st.ntot = (double)(g->n[0] * g->n[1] * g->n[2]);
+  PB_HIP(hipMemcpyAsync(k->d_st, &st, sizeof(st), hipMemcpyHostToDevice, ctx->stream));
+  PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->p0, k->d_st, st.dinv, k->d_hist, k->h_done_dev));
+  PB_HIP(hipStreamSynchronize(ctx->stream));
+  k->b = b;
+  k->x = x;
+  k->host_iter = 0;
+  k->stopped = k->h_done[0] != 0;
+  k->begun = true;
+  return PB_OK;
+}
+
+static int enqueue_iteration(pb_ksp* k) {
+  pb_grid* g = k->A->grid;
+  pb_ctx* ctx = g->ctx;
+  Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};
+  PB_TRY(launch_cg_boundary(g, k->r, k->p0, k->d_st));
+  StencilPlanes gp;
+  if (ctx->nranks == 1) {
+    gp.ghost_lo = g->bnd_hi;  // p_new of plane nzl-1 wraps below plane 0
+    gp.ghost_hi = g->bnd_lo;
+  } else {
+    PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
+    gp.ghost_lo = g->ghost_lo;
+    gp.ghost_hi = g->ghost_hi;
+  }
+  PB_TRY(launch_cg_pass_a(g, s, k->r, k->p0, k->p1, gp, k->d_st));
+  PB_TRY(launch_cg_pass_b(g, s, k->p1, k->x->d, k->r, gp, k->d_st, k->d_hist, k->h_done_dev,
+                          k->host_iter));
+  std::swap(k->p0, k->p1);
+  return PB_OK;
+}
+
+int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
+  PB_CHECK_ARG(k, "ksp is NULL");
+  if (!k->begun) return set_error(PB_ERR_STATE, "pb_ksp_iterate before pb_ksp_begin");
+  pb_ctx* ctx = k->A->grid->ctx;
+  const int C = k->opts.check_every;
+  const int R = 4 * C;
+  if ((int)k->ring.size() < R) {
+    for (int i = (int)k->ring.size(); i < R; ++i) {
+      hipEvent_t e;
+      PB_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      k->ring.push_back(e);
+    }
+  }
+  PB_TRY(ensure_done_cap(k, k->host_iter + iters + 2));
+  for (int64_t n = 0; n < iters && !k->stopped; ++n) {
+    PB_TRY(enqueue_iteration(k));
+    const int64_t hi = k->host_iter++;
+    PB_HIP(hipEventRecord(k->ring[hi % R], ctx->stream));
+    // lagged, rank-consistent poll: decide on the flag of iteration hi + 1 - C only
+    if ((hi + 1) % C == 0 && hi + 1 >= C) {
+      const int64_t j = hi + 1 - C;
+      PB_HIP(hipEventSynchronize(k->ring[j % R]));
+      if (k->h_done[j + 1]) k->stopped = true;
+    }
+  }
+  return PB_OK;
+}
+
+static const char* reason_name(int r) {
+  switch (r) {
+    case PB_KSP_CONVERGED_RTOL: return "CONVERGED_RTOL";
+    case PB_KSP_CONVERGED_ATOL: return "CONVERGED_ATOL";
+    case PB_KSP_CONVERGED_ITS: return "CONVERGED_ITS";
+    case PB_KSP_DIVERGED_ITS: return "DIVERGED_ITS";
+    case PB_KSP_DIVERGED_DTOL: return "DIVERGED_DTOL";
+    case PB_KSP_DIVERGED_NANORINF: return "DIVERGED_NANORINF";
+    case PB_KSP_DIVERGED_INDEFINITE_MAT: return "DIVERGED_INDEFINITE_MAT";
+    default: return "CONVERGED_ITERATING";
+  }
+}
+
+int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
+  PB_CHECK_ARG(k, "ksp is NULL");
+  if (!k->begun) return set_error(PB_ERR_STATE, "pb_ksp_end before pb_ksp_begin");
+  pb_ctx* ctx = k->A->grid->ctx;
+  PB_HIP(hipStreamSynchronize(ctx->stream));
+  CgState st;
+  PB_HIP(hipMemcpy(&st, k->d_st, sizeof(st), hipMemcpyDeviceToHost));
+  if (res) {
+    res->reason = st.reason;
+    res->its = st.its;
+    res->rnorm = st.dp;
+    res->rnorm0 = st.rnorm0;
+  }
+  const int64_t nh = std::min<int64_t>(st.its + 1, k->nhist);
+  std::vector<double> hist((size_t)std::max<int64_t>(nh, 1));
+  if (nh > 0) PB_HIP(hipMemcpy(hist.data(), k->d_hist, (size_t)nh * sizeof(double), hipMemcpyDeviceToHost));
+  if (history && cap > 0) memcpy(history, hist.data(), (size_t)std::min(nh, cap) * sizeof(double));
+  if (ctx->rank == 0) {
+    if (k->opts.monitor)
+      for (int64_t i = 0; i < nh; ++i)
+        printf("  %3lld KSP Residual norm %14.12e \n", (long long)i, hist[i]);
+    if (k->opts.converged_reason) {
+      if (st.reason > 0)
+        printf("Linear solve converged due to %s iterations %lld\n", reason_name(st.reason),
+               (long long)st.its);
+      else
+        printf("Linear solve did not converge due to %s iterations %lld\n",
+               reason_name(st.reason), (long long)st.its);
+    }
+    fflush(stdout);
+  }
+  k->begun = false;
+  return PB_OK;
+}
+
+int pb_ksp_solve(pb_ksp* k, const pb_vec* b, pb_vec* x, pb_ksp_result* res, double* history,
+                 int64_t cap) {
+  PB_TRY(pb_ksp_begin(k, b, x));
+  PB_TRY(pb_ksp_iterate(k, k->opts.max_it + 2 * (int64_t)k->opts.check_every));
+  return pb_ksp_end(k, res, history, cap);
+}
+
+int pb_ksp_destroy(pb_ksp* k) {
+  if (!k) return PB_OK;
+  (void)hipStreamSynchronize(k->A->grid->ctx->stream);
+  (void)hipFree(k->r);
+  (void)hipFree(k->p0);
+  (void)hipFree(k->p1);
+  if (k->w) (void)hipFree(k->w);
+  if (k->z) (void)hipFree(k->z);
+  (void)hipFree(k->d_st);
+  if (k->d_hist) (void)hipFree(k->d_hist);
+  if (k->h_done) (void)hipHostFree(k->h_done);
+  for (hipEvent_t e : k->ring) (void)hipEventDestroy(e);
+  delete k;
+  return PB_OK;
+}
+
+int pb_solve(pb_op* A, pb_op* P, const pb_ksp_opts* opts, const pb_vec* b, pb_vec* x,
+             pb_ksp_result* res, double* history, int64_t cap) {
+  pb_ksp* k = nullptr;
+  PB_TRY(pb_ksp_create(A, P, opts, &k));
+  int rc = pb_ksp_solve(k, b, x, res, history, cap);
+  pb_ksp_destroy(k);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,660 @@
+// pb_stencil.hip -- 7-point periodic Laplacian engine for gfx950 (MI355X) and the fused CG passes.
+//
+// Replaces the reference hot loop src/poissbox.f90:112-119 (compute_lapl_pointwise ->
+// evaluate_laplacian_pointwise, :128-148) and the PETSc KSPSolve_CG vector kernels around it
+// (SURVEY.md Appendix A).
+//
+// Work decomposition (HBM-bound, AI ~ 0.8 flop/B, MFMA unused):
+//   * a wave owns an x-segment of 64*V points (V = 2 -> one 16-B load per lane, 1 KiB per
+//     wave-instruction) of TY consecutive y-rows, and marches in z over a chunk of planes, keeping
+//     planes k-1, k, k+1 of its rows in registers (each plane is read from HBM once per chunk);
+//   * x-neighbours come from the neighbouring lane (cross-lane shuffle), the two segment-end
+//     values from a masked load (L1/L2 hit); y-neighbours come from the wave's own rows in
+//     registers, the tile's top/bottom rows from the neighbouring tile (cache hit);
+//   * 4 waves per workgroup stack in y so their halo rows are shared through the CU's L1;
+//   * z ghosts (periodic wrap or the neighbouring rank's plane) are read from plane pointers
+//     chosen per plane, so no ghost copy is made on one rank.
+// Summation order per point matches the reference dot product with its zero terms dropped:
+// z-, y-, x-, centre, x+, y+, z+ (built with -ffp-contract=off => bit-identical to the oracle).
+#include "pb_internal.hpp"
+
+namespace pb {
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
+static constexpr int kWaves = 4;
+static constexpr int kThreads = 64 * kWaves;
+
+struct Geo {
+  int nx, ny, nzl;
+  int64_t plane;
+  int nsegx, ntile, nchunk, kc, ty;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Loaders: value of the field at an owned linear index (plane*k + nx*j + i)
+// ---------------------------------------------------------------------------------------------
+struct PlainLoad {
+  const double* __restrict__ x;
+  __device__ __forceinline__ void prepare() {}
+  template <int V>
+  __device__ __forceinline__ void row(int64_t idx, double (&v)[V]) const {
+    if constexpr (V == 2) {
+      dv2 t = *reinterpret_cast<const dv2*>(x + idx);
+      v[0] = t.x;
+      v[1] = t.y;
+    } else {
+      v[0] = x[idx];
+    }
+  }
+  __device__ __forceinline__ double one(int64_t idx) const { return x[idx]; }
+};
+
+// p_new = (dinv*r + shift) + bb*p_old  -- PCApply_Jacobi + MatNullSpaceRemove + VecAYPX fused
+struct CgState;
+__device__ __forceinline__ double cg_bb(const CgState* st);
+struct CombineLoad {
+  const double* __restrict__ r;
+  const double* __restrict__ p;
+  const CgState* st;
+  double dinv, shift, bb;
+  __device__ __forceinline__ void prepare() {
+    dinv = st->dinv;
+    shift = -st->mu;
+    bb = cg_bb(st);
+  }
+  __device__ __forceinline__ double f(double rv, double pv) const {
+    double z = dinv * rv;
+    z = z + shift;
+    return z + bb * pv;
+  }
+  template <int V>
+  __device__ __forceinline__ void row(int64_t idx, double (&v)[V]) const {
+    if constexpr (V == 2) {
+      dv2 a = *reinterpret_cast<const dv2*>(r + idx);
+      dv2 b = *reinterpret_cast<const dv2*>(p + idx);
+      v[0] = f(a.x, b.x);
+      v[1] = f(a.y, b.y);
+    } else {
+      v[0] = f(r[idx], p[idx]);
+    }
+  }
+  __device__ __forceinline__ double one(int64_t idx) const { return f(r[idx], p[idx]); }
+};
+
+template <int V>
+__device__ __forceinline__ void ghost_row(const double* __restrict__ g, int64_t idx,
+                                          double (&v)[V]) {
+  if constexpr (V == 2) {
+    dv2 t = *reinterpret_cast<const dv2*>(g + idx);
+    v[0] = t.x;
+    v[1] = t.y;
+  } else {
+    v[0] = g[idx];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Epilogues: consume centre value c and Laplacian w at owned index idx
+// ---------------------------------------------------------------------------------------------
+struct StoreY {
+  static constexpr int NS = 0;
+  double* __restrict__ y;
+  __device__ __forceinline__ void prepare() {}
+  template <int V>
+  __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
+                                      double*) const {
+    if constexpr (V == 2) {
+      dv2 t;
+      t.x = w[0];
+      t.y = w[1];
+      __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(y + idx));
+    } else {
+      __builtin_nontemporal_store(w[0], y + idx);
+    }
+    (void)c;
+  }
+};
+
+// CG pass A: store p_new, accumulate p.w (VecXDot(P, W))
+struct PassA {
+  static constexpr int NS = 1;
+  double* __restrict__ p_new;
+  __device__ __forceinline__ void prepare() {}
+  template <int V>
+  __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
+                                      double* acc) const {
+    if constexpr (V == 2) {
+      dv2 t;
+      t.x = c[0];
+      t.y = c[1];
+      __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p_new + idx));
+    } else {
+      __builtin_nontemporal_store(c[0], p_new + idx);
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[0] += w[e] * c[e];
+  }
+};
+
+// CG pass B: x += a p; r += (-a) w; then the PC/null-space sums of the new residual:
+//   s = dinv*r, t = s - mu_old:  sum t, sum t^2, sum t*r, sum r
+struct PassB {
+  static constexpr int NS = 4;
+  double* __restrict__ x;
+  double* __restrict__ r;
+  const CgState* st;
+  double alpha, dinv, mu;
+  __device__ __forceinline__ void prepare() {
+    alpha = st->alpha;
+    dinv = st->dinv;
+    mu = st->mu;
+  }
+  template <int V>
+  __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
+                                      double* acc) const {
+    double xv[V], rv[V];
+    if constexpr (V == 2) {
+      dv2 a = *reinterpret_cast<const dv2*>(x + idx);
+      dv2 b = *reinterpret_cast<const dv2*>(r + idx);
+      xv[0] = a.x; xv[1] = a.y;
+      rv[0] = b.x; rv[1] = b.y;
+    } else {
+      xv[0] = x[idx];
+      rv[0] = r[idx];
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      xv[e] = xv[e] + alpha * c[e];
+      rv[e] = rv[e] + (-alpha) * w[e];
+      double s = dinv * rv[e];
+      double t = s - mu;
+      acc[0] += t;
+      acc[1] += t * t;
+      acc[2] += t * rv[e];
+      acc[3] += rv[e];
+    }
+    if constexpr (V == 2) {
+      dv2 a, b;
+      a.x = xv[0]; a.y = xv[1];
+      b.x = rv[0]; b.y = rv[1];
+      __builtin_nontemporal_store(a, reinterpret_cast<dv2*>(x + idx));
+      __builtin_nontemporal_store(b, reinterpret_cast<dv2*>(r + idx));
+    } else {
+      __builtin_nontemporal_store(xv[0], x + idx);
+      __builtin_nontemporal_store(rv[0], r + idx);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Block-level deterministic reduction of NS partial sums -> parts[block*NS + s]
+// ---------------------------------------------------------------------------------------------
+template <int NS>
+__device__ __forceinline__ void block_partials(double* acc, double* parts) {
+  if constexpr (NS > 0) {
+    __shared__ double red[kWaves][NS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      double v = acc[s];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+      acc[s] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) red[wid][s] = acc[s];
+    }
+    __syncthreads();
+    if (threadIdx.x < NS) {
+      double v = 0.0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) v += red[w][threadIdx.x];
+      parts[(int64_t)blockIdx.x * NS + threadIdx.x] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The stencil engine
+// ---------------------------------------------------------------------------------------------
+template <int V, int TY, class Load, class Epi>
+__global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, double cy, double cz,
+                                                         double cc, Load ld0,
+                                                         const double* __restrict__ ghost_lo,
+                                                         const double* __restrict__ ghost_hi,
+                                                         Epi ep0, double* parts,
+                                                         const int* __restrict__ skip) {
+  if (skip && *skip) return;  // device-side convergence flag (uniform)
+  Load ld = ld0;
+  ld.prepare();
+  Epi ep = ep0;
+  ep.prepare();
+  constexpr int NS = Epi::NS;
+  double acc[NS > 0 ? NS : 1];
+#pragma unroll
+  for (int s = 0; s < (NS > 0 ? NS : 1); ++s) acc[s] = 0.0;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int b = blockIdx.x;
+  const int seg = b % g.nsegx;
+  b /= g.nsegx;
+  const int tile = b % g.ntile;
+  const int chunk = b / g.ntile;
+  const int j0 = (tile * kWaves + wid) * TY;
+  const int kb = chunk * g.kc;
+  const int ke = min(kb + g.kc, g.nzl);
+  const int i0 = seg * 64 * V + lane * V;
+  const bool active = i0 < g.nx;
+  const bool wave_on = j0 < g.ny && kb < g.nzl;
+  const int nx = g.nx;
+  const int ic = active ? i0 : 0;  // clamp addresses of idle lanes
+  // x-edge sources: lane 0 needs x[i0-1]; the last active lane needs x[i0+V]
+  const bool needL = lane == 0;
+  const bool needR = active && (lane == 63 || i0 + V >= nx);
+  const int iL = i0 == 0 ? nx - 1 : i0 - 1;
+  const int iR = (i0 + V >= nx) ? 0 : i0 + V;
+  const int jdn = j0 == 0 ? g.ny - 1 : j0 - 1;
+  const int jup = (j0 + TY >= g.ny) ? 0 : j0 + TY;
+
+  if (wave_on) {
+    double q0[TY][V], q1[TY][V], q2[TY][V];
+    // plane loader for the z-queue: kk in [-1, nzl]
+    auto load_plane = [&](int kk, double (&q)[TY][V]) {
+      if (kk < 0 || kk >= g.nzl) {
+        const double* gp = kk < 0 ? ghost_lo : ghost_hi;
+#pragma unroll
+        for (int t = 0; t < TY; ++t) ghost_row<V>(gp, (int64_t)(j0 + t) * nx + ic, q[t]);
+      } else {
+        const int64_t base = (int64_t)kk * g.plane;
+#pragma unroll
+        for (int t = 0; t < TY; ++t) ld.template row<V>(base + (int64_t)(j0 + t) * nx + ic, q[t]);
+      }
+    };
+    load_plane(kb - 1, q0);
+    load_plane(kb, q1);
+    for (int k = kb; k < ke; ++k) {
+      load_plane(k + 1, q2);
+      const int64_t base = (int64_t)k * g.plane;
+      double hdn[V], hup[V];
+      ld.template row<V>(base + (int64_t)jdn * nx + ic, hdn);
+      ld.template row<V>(base + (int64_t)jup * nx + ic, hup);
+#pragma unroll
+      for (int t = 0; t < TY; ++t) {
+        const int64_t rowb = base + (int64_t)(j0 + t) * nx;
+        double eL = 0.0, eR = 0.0;
+        if (needL) eL = ld.one(rowb + iL);
+        if (needR) eR = ld.one(rowb + iR);
+        const double fromL = __shfl(q1[t][V - 1], (lane + 63) & 63, 64);
+        const double fromR = __shfl(q1[t][0], (lane + 1) & 63, 64);
+        const double xl0 = needL ? eL : fromL;
+        const double xrl = needR ? eR : fromR;
+        double w[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const double xm = e == 0 ? xl0 : q1[t][e - 1];
+          const double xp = e == V - 1 ? xrl : q1[t][e + 1];
+          const double ym = t == 0 ? hdn[e] : q1[t - 1][e];
+          const double yp = t == TY - 1 ? hup[e] : q1[t + 1][e];
+          double s = cz * q0[t][e];
+          s = s + cy * ym;
+          s = s + cx * xm;
+          s = s + cc * q1[t][e];
+          s = s + cx * xp;
+          s = s + cy * yp;
+          s = s + cz * q2[t][e];
+          w[e] = s;
+        }
+        if (active) ep.template put<V>(rowb + i0, q1[t], w, acc);
+      }
+#pragma unroll
+      for (int t = 0; t < TY; ++t)
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          q0[t][e] = q1[t][e];
+          q1[t][e] = q2[t][e];
+        }
+    }
+  }
+  block_partials<NS>(acc, parts);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Launch configuration
+// ---------------------------------------------------------------------------------------------
+static int env_int(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return s ? atoi(s) : dflt;
+}
+
+static Geo make_geo(pb_grid* g, int V, int TY) {
+  Geo geo;
+  geo.nx = (int)g->n[0];
+  geo.ny = (int)g->n[1];
+  geo.nzl = (int)g->nzl;
+  geo.plane = g->plane;
+  geo.ty = TY;
+  geo.nsegx = (geo.nx + 64 * V - 1) / (64 * V);
+  geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
+  const int columns = geo.nsegx * geo.ntile;
+  int target = env_int("PB_STENCIL_BLOCKS", 4 * g->ctx->num_cus);
+  int nchunk = (target + columns - 1) / columns;
+  if (nchunk > geo.nzl) nchunk = geo.nzl;
+  if (nchunk < 1) nchunk = 1;
+  geo.kc = (geo.nzl + nchunk - 1) / nchunk;
+  geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
+  return geo;
+}
+
+static int pick_ty(int ny) {
+  int forced = env_int("PB_STENCIL_TY", 0);
+  if (forced > 0 && ny % forced == 0) return forced;
+  if (ny % 4 == 0) return 4;
+  if (ny % 2 == 0) return 2;
+  return 1;
+}
+
+template <int V, int TY, class Load, class Epi>
+static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
+                    const Epi& ep, const int* skip) {
+  Geo geo = make_geo(g, V, TY);
+  const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
+  if (nblocks > g->ctx->partials_cap / 8)
+    return set_error(PB_ERR_UNSUPPORTED, "stencil grid of %lld blocks exceeds partials capacity",
+                     (long long)nblocks);
+  hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+                     g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
+                     g->ctx->d_partials, skip);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+template <class Load, class Epi>
+static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
+                      const Epi& ep, const int* skip) {
+  const bool vec2 = (g->n[0] % 2) == 0;
+  const int ty = pick_ty((int)g->n[1]);
+  if (vec2) {
+    switch (ty) {
+      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip);
+      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip);
+      case 8: return launch_t<2, 8>(g, s, ld, gp, ep, skip);
+      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip);
+    }
+  }
+  switch (ty) {
+    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip);
+    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip);
+    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip);
+  }
+}
+
+int stencil_blocks(pb_grid* g) {
+  const bool vec2 = (g->n[0] % 2) == 0;
+  Geo geo = make_geo(g, vec2 ? 2 : 1, pick_ty((int)g->n[1]));
+  return geo.nsegx * geo.ntile * geo.nchunk;
+}
+
+int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
+                       const StencilPlanes& gp) {
+  ScopedTimer tm(g->ctx, "stencil");
+  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, nullptr);
+}
+
+// ---------------------------------------------------------------------------------------------
+// CG (PETSc KSPSolve_CG + PCJacobi + MatNullSpace), device-resident state
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double cg_bb(const CgState* st) {
+  return st->it == 0 ? 0.0 : st->beta / st->betaold;
+}
+
+// r = b, x = 0, p = 0 and the sums of s = dinv*r (t = s - 0)
+__global__ __launch_bounds__(256) void cg_init_kernel(const double* __restrict__ b,
+                                                      double* __restrict__ x,
+                                                      double* __restrict__ r,
+                                                      double* __restrict__ p, int64_t n,
+                                                      double dinv, double* parts) {
+  double acc[4] = {0, 0, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    double rv = b[i];
+    r[i] = rv;
+    x[i] = 0.0;
+    p[i] = 0.0;
+    double s = dinv * rv;
+    acc[0] += s;
+    acc[1] += s * s;
+    acc[2] += s * rv;
+    acc[3] += rv;
+  }
+  block_partials<4>(acc, parts);
+}
+
+// boundary planes of p_new (for the halo exchange / periodic self-wrap)
+__global__ __launch_bounds__(256) void cg_boundary_kernel(const double* __restrict__ r,
+                                                          const double* __restrict__ p,
+                                                          int64_t plane, int64_t last_off,
+                                                          double* __restrict__ lo,
+                                                          double* __restrict__ hi,
+                                                          const CgState* st) {
+  if (st->done) return;
+  CombineLoad c{r, p, st, 0.0, 0.0, 0.0};
+  c.prepare();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < plane;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    lo[i] = c.one(i);
+    hi[i] = c.one(last_off + i);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Finalize: deterministic fixed-order reduction of the per-block partials, then the PETSc CG
+// scalar logic (KSPSolve_CG + KSPConvergedDefault) on the device. mode bit 1 = reduce partials
+// into sums[], bit 2 = update the state from sums[] (split around the RCCL allreduce).
+// stage 0 = after init, 1 = after pass A (p.w), 2 = after pass B (residual sums).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool finite(double v) { return v == v && v - v == 0.0; }
+
+__global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restrict__ parts,
+                                                          int nparts, int width, double* sums,
+                                                          int mode, int stage, CgState* st,
+                                                          double* hist, int* h_done,
+                                                          int64_t host_iter) {
+  __shared__ double red[256][4];
+  if (mode & 1) {
+    for (int s = 0; s < width; ++s) {
+      double v = 0.0;
+      for (int b = threadIdx.x; b < nparts; b += 256) v += parts[(int64_t)b * width + s];
+      red[threadIdx.x][s] = v;
+    }
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+      if ((int)threadIdx.x < off)
+        for (int s = 0; s < width; ++s) red[threadIdx.x][s] += red[threadIdx.x + off][s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0)
+      for (int s = 0; s < width; ++s) sums[s] = red[0][s];
+  }
+  if (!(mode & 2) || threadIdx.x != 0) return;
+  double S[4];
+  for (int s = 0; s < 4; ++s) S[s] = s < width ? sums[s] : 0.0;
+  const double N = st->ntot;
+  if (stage == 0) {
+    double mu = 0.0, zz = S[1], zr = S[2];
+    if (st->nullspace) {
+      const double delta = S[0] / N;
+      mu = delta;
+      zz = S[1] - N * delta * delta;
+      zr = S[2] - delta * S[3];
+    }
+    const double dp = sqrt(zz > 0.0 ? zz : 0.0);
+    st->mu = mu;
+    st->dp = dp;
+    st->rnorm0 = dp;
+    st->it = 0;
+    st->its = 0;
+    st->dpi = 0.0;
+    st->reason = 0;
+    st->done = 0;
+    if (st->nhist > 0) hist[0] = dp;
+    if (!finite(dp)) {
+      st->reason = PB_KSP_DIVERGED_NANORINF;
+      st->done = 1;
+    } else {
+      st->ttol = fmax(st->rtol * dp, st->atol);
+      if (dp <= st->ttol) {
+        st->reason = dp < st->atol ? PB_KSP_CONVERGED_ATOL : PB_KSP_CONVERGED_RTOL;
+        st->done = 1;
+      } else {
+        st->beta = zr;
+        if (!finite(zr)) {
+          st->reason = PB_KSP_DIVERGED_NANORINF;
+          st->done = 1;
+        } else if (zr == 0.0) {
+          st->its = 1;
+          st->reason = PB_KSP_CONVERGED_ATOL;
+          st->done = 1;
+        } else if (st->max_it <= 0) {
+          st->reason = PB_KSP_DIVERGED_ITS;
+          st->done = 1;
+        }
+      }
+    }
+    if (h_done) h_done[0] = st->done;
+    return;
+  }
+  if (stage == 1) {
+    if (st->done) return;
+    const int64_t i = st->it;
+    const double dpi = S[0];
+    const double sp = (double)((dpi > 0) - (dpi < 0)), so = (double)((st->dpi > 0) - (st->dpi < 0));
+    if (!finite(dpi)) {
+      st->its = i + 1;
+      st->reason = PB_KSP_DIVERGED_NANORINF;
+      st->done = 1;
+    } else if (dpi == 0.0 || (i > 0 && sp * so < 0.0)) {
+      st->its = i + 1;
+      st->reason = PB_KSP_DIVERGED_INDEFINITE_MAT;
+      st->done = 1;
+    } else {
+      st->dpiold = st->dpi;
+      st->dpi = dpi;
+      st->betaold = st->beta;
+      st->alpha = st->beta / dpi;
+    }
+    return;
+  }
+  // stage 2
+  if (!st->done) {
+    const int64_t i = st->it;
+    double mu = st->mu, zz = S[1], zr = S[2];
+    if (st->nullspace) {
+      const double delta = S[0] / N;
+      mu = st->mu + delta;
+      zz = S[1] - N * delta * delta;
+      zr = S[2] - delta * S[3];
+    }
+    const double dp = sqrt(zz > 0.0 ? zz : 0.0);
+    st->dp = dp;
+    st->its = i + 1;
+    if (i + 1 < st->nhist) hist[i + 1] = dp;
+    if (!finite(dp)) {
+      st->reason = PB_KSP_DIVERGED_NANORINF;
+      st->done = 1;
+    } else if (dp <= st->ttol) {
+      st->reason = dp < st->atol ? PB_KSP_CONVERGED_ATOL : PB_KSP_CONVERGED_RTOL;
+      st->done = 1;
+    } else if (dp >= st->dtol * st->rnorm0) {
+      st->reason = PB_KSP_DIVERGED_DTOL;
+      st->done = 1;
+    } else {
+      st->beta = zr;
+      st->mu = mu;
+      st->it = i + 1;
+      if (!finite(zr)) {
+        st->reason = PB_KSP_DIVERGED_NANORINF;
+        st->done = 1;
+      } else if (st->it >= st->max_it) {
+        st->reason = PB_KSP_DIVERGED_ITS;
+        st->done = 1;
+      } else if (zr == 0.0) {
+        st->its = st->it + 1;
+        st->reason = PB_KSP_CONVERGED_ATOL;
+        st->done = 1;
+      }
+    }
+  }
+  if (h_done) h_done[host_iter + 1] = st->done;
+}
+
+static int cg_reduce_update(pb_ctx* ctx, int stage, int nparts, int width, CgState* st,
+                            double* hist, int* h_done, int64_t host_iter) {
+  double* sums = ctx->d_scalars;
+  if (ctx->nranks == 1) {
+    hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+                       nparts, width, sums, 3, stage, st, hist, h_done, host_iter);
+    PB_HIP(hipGetLastError());
+    return PB_OK;
+  }
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+                     nparts, width, sums, 1, stage, st, hist, h_done, host_iter);
+  PB_HIP(hipGetLastError());
+  PB_TRY(allreduce_device(ctx, sums, width));
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+                     nparts, width, sums, 2, stage, st, hist, h_done, host_iter);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+static int elementwise_blocks(pb_ctx* ctx, int64_t n) {
+  int64_t b = (n + 255) / 256;
+  int64_t cap = (int64_t)ctx->num_cus * 8;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p, CgState* st,
+                   double dinv, double* hist, int* h_done) {
+  pb_ctx* ctx = g->ctx;
+  ScopedTimer tm(ctx, "cg_init");
+  const int nb = elementwise_blocks(ctx, g->nlocal);
+  hipLaunchKernelGGL(cg_init_kernel, dim3(nb), dim3(256), 0, ctx->stream, b, x, r, p, g->nlocal,
+                     dinv, ctx->d_partials);
+  PB_HIP(hipGetLastError());
+  return cg_reduce_update(ctx, 0, nb, 4, st, hist, h_done, -1);
+}
+
+int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st) {
+  pb_ctx* ctx = g->ctx;
+  ScopedTimer tm(ctx, "cg_boundary");
+  const int nb = elementwise_blocks(ctx, g->plane);
+  hipLaunchKernelGGL(cg_boundary_kernel, dim3(nb), dim3(256), 0, ctx->stream, r, p_old, g->plane,
+                     (g->nzl - 1) * g->plane, g->bnd_lo, g->bnd_hi, (const CgState*)st);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
+                     double* p_new, const StencilPlanes& gp, CgState* st) {
+  {
+    ScopedTimer tm(g->ctx, "cg_pass_a");
+    PB_TRY(launch_any(g, s, CombineLoad{r, p_old, st, 0.0, 0.0, 0.0}, gp, PassA{p_new},
+                      &st->done));
+  }
+  return cg_reduce_update(g->ctx, 1, stencil_blocks(g), 1, st, nullptr, nullptr, 0);
+}
+
+int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, double* x, double* r,
+                     const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
+                     int64_t host_iter) {
+  {
+    ScopedTimer tm(g->ctx, "cg_pass_b");
+    PB_TRY(launch_any(g, s, PlainLoad{p}, gp, PassB{x, r, st, 0.0, 0.0, 0.0}, &st->done));
+  }
+  return cg_reduce_update(g->ctx, 2, stencil_blocks(g), 4, st, hist, h_done, host_iter);
+}
+
+}  // namespace pb

@@ -1,0 +1,67 @@
+"""CPU tier: the C-ABI library loads and exports every entry point include/poissbox_gpu.h declares;
+host-only logic (slab partition) is checked without a GPU."""
+import os
+import re
+
+import pytest
+
+import poissbox_amd as pb
+from poissbox_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "poissbox_gpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pb_[a-z0-9_]+)\s*\(", src)) - {"pb_sendrecv_fn", "pb_allreduce_fn"})
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 40
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # the Python binding declares a signature for each of them
+    assert set(names) <= set(_lib.EXPORTED), set(names) - set(_lib.EXPORTED)
+
+
+def test_version_and_error_string():
+    lib = _lib.load()
+    assert isinstance(lib.pb_last_error(), bytes)
+    import ctypes as C
+    a, b = C.c_int(), C.c_int()
+    assert lib.pb_version(C.byref(a), C.byref(b)) == 0 and (a.value, b.value) == (0, 1)
+
+
+@pytest.mark.parametrize("nz,nranks", [(64, 3), (7, 3), (1024, 8), (5, 5), (512, 1), (13, 4)])
+def test_slab_partition(nz, nranks):
+    parts = [pb.slab_partition(nz, nranks, r) for r in range(nranks)]
+    assert parts[0][0] == 0
+    for (k0, nk), (k1, _) in zip(parts, parts[1:]):
+        assert k0 + nk == k1
+    assert sum(nk for _, nk in parts) == nz
+    sizes = [nk for _, nk in parts]
+    assert max(sizes) - min(sizes) <= 1 and sizes == sorted(sizes, reverse=True)
+
+
+def test_readme_dof_split():
+    """README.md:30-32: 64^3 on 3 ranks -> 90112 / 86016 / 86016 DoF (22/21/21 planes)."""
+    assert [pb.slab_partition(64, 3, r)[1] * 64 * 64 for r in range(3)] == [90112, 86016, 86016]
+
+
+def test_bad_partition_raises():
+    with pytest.raises(pb.PbError):
+        pb.slab_partition(4, 2, 5)
+
+
+def test_options_parse_petsc_names():
+    o = pb.ksp_options(["-ksp_type", "cg", "-pc_type", "none", "-ksp_rtol", "1e-10",
+                        "-ksp_max_it", "77", "-ksp_monitor", "-ksp_converged_reason", "-foo"])
+    assert o.pc_type == pb.PC_NONE and o.rtol == 1e-10 and o.max_it == 77
+    assert o.monitor == 1 and o.converged_reason == 1 and o.nullspace == 1
+    d = pb.ksp_options()
+    assert (d.rtol, d.atol, d.dtol, d.max_it, d.pc_type) == (1e-5, 1e-50, 1e5, 10000, pb.PC_JACOBI)
+    with pytest.raises(pb.PbError):
+        pb.ksp_options(["-ksp_type", "gmres"])

@@ -1,0 +1,398 @@
+"""GPU tier: the HIP path (through the C ABI) against the oracle and the reference fixtures.
+
+Bars (stated per test): bit-exact for the 7-point operator, the vector updates, the synthetic
+input, the tridiagonal solvers and the compact operators (same operation order, no FMA
+contraction); CG residual history within a stated relative tolerance of the PETSc-semantics
+restatement (reduction order differs), same iteration count and stopping reason.
+"""
+import ctypes as C
+import queue
+import threading
+
+import numpy as np
+import pytest
+
+import poissbox_amd as pb
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20231015
+
+
+# ---------------------------------------------------------------------------------------------
+# helpers
+# ---------------------------------------------------------------------------------------------
+class Dev:
+    """Raw device buffer through the HIP runtime (ctypes, no torch needed)."""
+
+    _hip = None
+
+    def __init__(self, arr):
+        if Dev._hip is None:
+            Dev._hip = C.CDLL("libamdhip64.so")
+        arr = np.ascontiguousarray(arr, dtype=np.float64)
+        self.n = arr.size
+        self.p = C.c_void_p()
+        assert Dev._hip.hipMalloc(C.byref(self.p), C.c_size_t(max(8, 8 * self.n))) == 0
+        assert Dev._hip.hipMemcpy(self.p, arr.ctypes.data_as(C.c_void_p), C.c_size_t(8 * self.n), 1) == 0
+
+    def get(self):
+        out = np.empty(self.n)
+        assert Dev._hip.hipDeviceSynchronize() == 0
+        assert Dev._hip.hipMemcpy(out.ctypes.data_as(C.c_void_p), self.p, C.c_size_t(8 * self.n), 2) == 0
+        return out
+
+    def free(self):
+        Dev._hip.hipFree(self.p)
+
+
+def grid_vec(ctx, n, values=None, L=(1.0, 1.0, 1.0)):
+    da = pb.DA(ctx, n, L)
+    v = pb.Vec(da)
+    if values is not None:
+        v.set_values(values)
+    return da, v
+
+
+# ---------------------------------------------------------------------------------------------
+# 7-point operator (mfmult / compute_lapl_pointwise)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [(3, 3, 3), (16, 16, 16), (17, 12, 9), (130, 18, 7), (64, 64, 64),
+                               (256, 8, 5), (20, 36, 11), (128, 128, 4)])
+def test_stencil_bit_exact(ctx, n):
+    N = int(np.prod(n))
+    x = O.fill_random(N, SEED + N)
+    h = tuple(1.0 / m for m in n)
+    da, xv = grid_vec(ctx, n, x)
+    yv = pb.Vec(da)
+    A = pb.Mat(da, pb.STAR7)
+    A.mult(xv, yv)
+    y = yv.get_values()
+    ref = O.stencil(x, n, h, faithful=N <= 40000)
+    assert np.array_equal(y, ref), np.max(np.abs(y - ref))
+    # assembled-P kind applies the same 7 non-zeros
+    P = pb.Mat(da, pb.ASSEMBLED27)
+    P.mult(xv, yv)
+    assert np.array_equal(yv.get_values(), ref)
+    for o in (A, P, xv, yv):
+        o.destroy()
+    da.destroy()
+
+
+def test_stencil_nonuniform_spacing(ctx):
+    n = (24, 20, 10)
+    L = (1.0, 2.5, 0.3)
+    da = pb.DA(ctx, n, L)
+    h = da.spacing
+    assert np.allclose(h, [L[i] / n[i] for i in range(3)])
+    x = O.fill_random(int(np.prod(n)), 11)
+    xv, yv = pb.Vec(da), pb.Vec(da)
+    xv.set_values(x)
+    pb.compute_lapl_pointwise(da, h, xv, yv)
+    assert np.array_equal(yv.get_values(), O.stencil(x, n, h, faithful=True))
+
+
+def test_stencil_polynomial_known_answer(ctx):
+    """Quadratic field a*(x^2+y^2+z^2) -> 3*2a away from the periodic seam
+    (tests/coefficients/test_star.f90:108-116)."""
+    n = (16, 16, 16)
+    a = 2.718
+    h = 0.155
+    i = np.arange(16) * h
+    f = a * (i[None, None, :] ** 2 + i[None, :, None] ** 2 + i[:, None, None] ** 2)
+    da = pb.DA(ctx, n, (16 * h,) * 3)
+    xv, yv = pb.Vec(da), pb.Vec(da)
+    xv.set_values(f.reshape(-1))
+    pb.Mat(da, pb.STAR7, (h, h, h)).mult(xv, yv)
+    y = yv.get_values().reshape(16, 16, 16)[1:-1, 1:-1, 1:-1]
+    assert np.allclose(y, 6 * a, rtol=0, atol=1e-9 * 6 * a / h ** 2 * h ** 2 + 1e-9)
+
+
+# ---------------------------------------------------------------------------------------------
+# vectors
+# ---------------------------------------------------------------------------------------------
+def test_vector_ops(ctx):
+    n = (40, 30, 20)
+    N = 40 * 30 * 20
+    a, b = O.fill_random(N, 1), O.fill_random(N, 2)
+    da = pb.DA(ctx, n)
+    va, vb = pb.Vec(da), pb.Vec(da)
+    va.set_values(a)
+    vb.set_values(b)
+    assert np.isclose(va.dot(vb), np.dot(a, b), rtol=1e-13)
+    assert np.isclose(va.norm(), np.linalg.norm(a), rtol=1e-13)
+    assert np.isclose(va.sum(), a.sum(), rtol=1e-12, atol=1e-12)
+    vc = va.duplicate()
+    va.copy_to(vc)
+    vc.axpy(-0.37, vb)
+    assert np.array_equal(vc.get_values(), a + (-0.37) * b)
+    vc.aypx(1.5, vb)
+    assert np.array_equal(vc.get_values(), b + 1.5 * (a + (-0.37) * b))
+    vc.scale(-2.0)
+    vc.set(3.25)
+    assert np.all(vc.get_values() == 3.25)
+
+
+def test_random_fill_matches_oracle(ctx):
+    n = (33, 17, 9)
+    da = pb.DA(ctx, n)
+    v = pb.Vec(da)
+    v.set_random(SEED)
+    assert np.array_equal(v.get_values(), O.fill_random(33 * 17 * 9, SEED))
+
+
+# ---------------------------------------------------------------------------------------------
+# CG (KSPSolve -ksp_type cg -pc_type jacobi, constant null space)
+# ---------------------------------------------------------------------------------------------
+HIST_RTOL = 1e-7  # relative tolerance on every ||z_k|| of the history (reduction order differs)
+
+
+@pytest.mark.parametrize("n,rtol", [(16, 1e-5), (32, 1e-5), (32, 1e-10), (64, 1e-10),
+                                    ((24, 20, 12), 1e-8)])
+def test_cg_matches_petsc_semantics(ctx, n, rtol):
+    n3 = (n, n, n) if isinstance(n, int) else n
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    xt = O.fill_random(N, SEED)
+    b = O.stencil(xt, n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=rtol)
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(P, A, x, bv, ["-ksp_type", "cg", "-pc_type", "jacobi",
+                                               "-ksp_rtol", str(rtol)])
+    assert reason == ro == 2
+    assert its == itso
+    rel = np.abs(hist - ho) / ho
+    assert np.max(rel) < HIST_RTOL, np.max(rel)
+    xs = x.get_values()
+    assert np.max(np.abs(xs - xo)) <= 1e-6 * np.max(np.abs(xo))
+    # residual ||A x - b|| like src/example.f90:79-84
+    r = pb.Vec(da)
+    A.mult(x, r)
+    r.axpy(-1.0, bv)
+    assert r.norm() <= 1e3 * rtol * np.linalg.norm(b) + 1e-9
+
+
+def test_cg_pc_none_and_max_it(ctx):
+    n3 = (16, 16, 16)
+    h = (1 / 16,) * 3
+    xt = O.fill_random(4096, 5)
+    b = O.stencil(xt, n3, h)
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    bv.set_values(b)
+    _, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-8, pc="none")
+    reason, its, hist = pb.solve(P, A, x, bv, ["-pc_type", "none", "-ksp_rtol", "1e-8"])
+    assert (reason, its) == (ro, itso)
+    assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
+    # DIVERGED_ITS at max_it
+    _, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-12, max_it=7)
+    reason, its, hist = pb.solve(P, A, x, bv, ["-ksp_rtol", "1e-12", "-ksp_max_it", "7"])
+    assert (reason, its) == (ro, itso) == (-3, 7)
+    assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
+
+
+def test_cg_zero_rhs_converges_immediately(ctx):
+    n3 = (8, 8, 8)
+    da = pb.DA(ctx, n3)
+    P, A, x, b = pb.initialise_linear_system(da, (1 / 8,) * 3)
+    reason, its, hist = pb.solve(P, A, x, b)
+    # ||z0|| = 0 <= max(rtol*0, atol) -> CONVERGED_ATOL at iteration 0
+    assert reason == 3 and its == 0 and hist[0] == 0.0
+
+
+def test_cg_split_iterate_equals_solve(ctx):
+    """pb_ksp_begin / iterate / end (the benchmark form) gives the same iterates as KSPSolve."""
+    n3 = (32, 16, 8)
+    N = 32 * 16 * 8
+    h = (1 / 32, 1 / 16, 1 / 8)
+    b = O.stencil(O.fill_random(N, 9), n3, h)
+    da = pb.DA(ctx, n3)
+    P, A, x1, bv = pb.initialise_linear_system(da, h)
+    bv.set_values(b)
+    x2 = pb.Vec(da)
+    opts = pb.ksp_options(["-ksp_rtol", "0", "-ksp_max_it", "40"], atol=0.0)
+    k = pb.KSP(A, P, opts)
+    k.begin(bv, x1)
+    k.iterate(15)
+    k.iterate(25)
+    r1, its1, h1 = k.end()
+    r2, its2, h2 = pb.KSP(A, P, opts).solve(bv, x2)
+    assert its1 == its2 == 40 and np.array_equal(h1, h2)
+    assert np.array_equal(x1.get_values(), x2.get_values())
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-rank (host transport: N contexts on one GPU, one thread per rank)
+# ---------------------------------------------------------------------------------------------
+def run_ranks(nranks, body):
+    """Run body(ctx, rank) on nranks contexts (same GPU, one thread each) connected by an
+    in-process host transport: keyed mailboxes for the halo planes, a barrier allreduce."""
+    box = [{"from_up": queue.Queue(), "from_down": queue.Queue()} for _ in range(nranks)]
+    barrier = threading.Barrier(nranks)
+    red = [None] * nranks
+    results, errors = [None] * nranks, []
+
+    def worker(rank):
+        try:
+            ctx = pb.Context(0, rank, nranks)
+            down, up = (rank - 1) % nranks, (rank + 1) % nranks
+
+            def sendrecv(lo, hi):
+                box[down]["from_up"].put(lo)    # my first plane sits above rank-1's last
+                box[up]["from_down"].put(hi)    # my last plane sits below rank+1's first
+                return box[rank]["from_down"].get(timeout=120), box[rank]["from_up"].get(timeout=120)
+
+            def allreduce(vals):
+                red[rank] = vals.copy()
+                barrier.wait(timeout=120)
+                total = red[0].copy()
+                for r in range(1, nranks):
+                    total = total + red[r]
+                barrier.wait(timeout=120)
+                return total
+
+            ctx.set_host_transport(sendrecv, allreduce)
+            results[rank] = body(ctx, rank)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+            barrier.abort()
+
+    ts = [threading.Thread(target=worker, args=(r,)) for r in range(nranks)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=600)
+    if errors:
+        raise errors[0]
+    return results
+
+
+@pytest.mark.parametrize("nranks,n", [(2, (16, 12, 10)), (3, (20, 16, 7)), (4, (32, 32, 8))])
+def test_multirank_stencil_bit_exact(nranks, n):
+    N = int(np.prod(n))
+    x = O.fill_random(N, SEED)
+    h = tuple(1.0 / m for m in n)
+    ref = O.stencil(x, n, h).reshape(n[2], n[1] * n[0])
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        xv, yv = pb.Vec(da), pb.Vec(da)
+        xv.set_values(x.reshape(n[2], -1)[k0:k0 + nk])
+        pb.Mat(da, pb.STAR7).mult(xv, yv)
+        return k0, nk, yv.get_values()
+
+    for k0, nk, y in run_ranks(nranks, body):
+        assert np.array_equal(y, ref[k0:k0 + nk].reshape(-1))
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_multirank_cg(nranks):
+    n = (16, 16, 12)
+    N = int(np.prod(n))
+    h = tuple(1.0 / m for m in n)
+    b = O.stencil(O.fill_random(N, SEED), n, h)
+    xo, ro, itso, ho = O.cg_solve(b, n, h, rtol=1e-8)
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        P, A, x, bv = pb.initialise_linear_system(da, h)
+        xt = pb.Vec(da)  # decomposition-independent synthetic input ...
+        xt.set_random(SEED)
+        A.mult(xt, bv)        # ... b = A x_true, as src/example.f90:70-72
+        reason, its, hist = pb.solve(P, A, x, bv, ["-ksp_rtol", "1e-8"])
+        return reason, its, hist, k0, nk, x.get_values()
+
+    out = run_ranks(nranks, body)
+    for reason, its, hist, k0, nk, xs in out:
+        assert (reason, its) == (ro, itso)
+        assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
+        assert np.max(np.abs(xs - xo.reshape(n[2], -1)[k0:k0 + nk].reshape(-1))) <= 1e-6
+
+
+# ---------------------------------------------------------------------------------------------
+# tridiagonal + compact schemes against the reference fixtures (bit-exact)
+# ---------------------------------------------------------------------------------------------
+def _cases(golden, prefix):
+    names = sorted({k.rsplit("__", 1)[0] for k in golden.files})
+    return [n for n in names if n.split("__")[0] == prefix]
+
+
+@pytest.mark.parametrize("op", ["tdma", "tdma_periodic"])
+def test_tdma_batched_bit_exact(ctx, golden, op):
+    for name in _cases(golden, op):
+        n = int(golden[name + "__meta"][0])
+        inp, out = golden[name + "__in"], golden[name + "__out"]
+        # batch of 3 copies, interleaved layout (line stride 1, element stride 3)
+        rep = lambda v: np.repeat(v[:, None], 3, axis=1).reshape(-1)
+        bufs = [Dev(rep(inp[i * n:(i + 1) * n])) for i in range(4)]
+        pb.tdma_batched(ctx, n, 3, 1, 3, *[d.p for d in bufs], periodic=(op == "tdma_periodic"))
+        d = bufs[3].get().reshape(n, 3)
+        for j in range(3):
+            assert np.array_equal(d[:, j], out[n:]), name
+        for bb in bufs:
+            bb.free()
+
+
+@pytest.mark.parametrize("op,kind,stagger", [("grad_1d", 0, -1), ("div_1d", 0, 1),
+                                              ("interp_1d", 1, -1), ("interp_1d_div", 1, 1)])
+def test_compact_1d_bit_exact(ctx, golden, op, kind, stagger):
+    for name in _cases(golden, op):
+        m = golden[name + "__meta"]
+        n, dx = int(m[0]), float(m[3])
+        f = Dev(golden[name + "__in"])
+        o = Dev(np.zeros(n))
+        pb.compact_1d_batched(ctx, kind, stagger, dx, n, 1, n, 1, f.p, o.p)
+        assert np.array_equal(o.get(), golden[name + "__out"]), name
+        f.free()
+        o.free()
+
+
+@pytest.mark.parametrize("op", ["grad", "div", "interp", "interp_div", "lapl"])
+def test_compact_3d_bit_exact(ctx, golden, op):
+    for name in _cases(golden, op):
+        m = golden[name + "__meta"]
+        n3, h3 = tuple(int(v) for v in m[:3]), tuple(float(v) for v in m[3:])
+        N = int(np.prod(n3))
+        da = pb.DA(ctx, n3)
+        inp = golden[name + "__in"]
+        if op == "div":
+            fs = [pb.Vec(da) for _ in range(3)]
+            for c in range(3):
+                fs[c].set_values(inp[c * N:(c + 1) * N])
+            out = pb.Vec(da)
+            pb.compact_div(da, h3, fs, out)
+            got = out.get_values()
+        elif op == "grad":
+            f = pb.Vec(da)
+            f.set_values(inp)
+            dfs = [pb.Vec(da) for _ in range(3)]
+            pb.compact_grad(da, h3, f, dfs)
+            got = np.concatenate([v.get_values() for v in dfs])
+        else:
+            f, out = pb.Vec(da), pb.Vec(da)
+            f.set_values(inp)
+            if op == "lapl":
+                pb.compact_lapl(da, h3, f, out)
+            else:
+                pb.compact_interp(da, -1 if op == "interp" else 1, f, out)
+            got = out.get_values()
+        assert np.array_equal(got, golden[name + "__out"]), name
+
+
+def test_pcr_alpha_matches_thomas(ctx):
+    for n, alpha in ((64, 3 / 10), (512, 9 / 62), (8, 3 / 10)):
+        rng = np.random.default_rng(n)
+        nb = 5
+        d = rng.random((nb, n)) * 2 - 1
+        ref = np.stack([O.tdma(np.full(n, alpha), np.ones(n), np.full(n, alpha), row,
+                               periodic=True)[1] for row in d])
+        buf = Dev(d.reshape(-1))
+        pb.pcr_alpha_batched(ctx, n, nb, n, 1, alpha, buf.p)
+        got = buf.get().reshape(nb, n)
+        assert np.max(np.abs(got - ref)) <= 1e-14 * np.max(np.abs(ref)) * 10
+        buf.free()
