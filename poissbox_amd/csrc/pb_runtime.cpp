@@ -416,14 +416,18 @@ int pb_vec_sum(const pb_vec* v, double* out) {
 
 int pb_vec_set_values_host(pb_vec* v, const double* owned) {
   PB_CHECK_ARG(v && owned, "bad set_values args");
-  PB_HIP(hipMemcpy(v->d, owned, (size_t)v->nlocal * sizeof(double), hipMemcpyHostToDevice));
+  // stream-ordered after any pending work on the vector (e.g. the zero fill at creation)
+  hipStream_t s = v->grid->ctx->stream;
+  PB_HIP(hipMemcpyAsync(v->d, owned, (size_t)v->nlocal * sizeof(double), hipMemcpyHostToDevice, s));
+  PB_HIP(hipStreamSynchronize(s));
   return PB_OK;
 }
 
 int pb_vec_get_values_host(const pb_vec* v, double* owned) {
   PB_CHECK_ARG(v && owned, "bad get_values args");
-  PB_HIP(hipStreamSynchronize(v->grid->ctx->stream));
-  PB_HIP(hipMemcpy(owned, v->d, (size_t)v->nlocal * sizeof(double), hipMemcpyDeviceToHost));
+  hipStream_t s = v->grid->ctx->stream;
+  PB_HIP(hipMemcpyAsync(owned, v->d, (size_t)v->nlocal * sizeof(double), hipMemcpyDeviceToHost, s));
+  PB_HIP(hipStreamSynchronize(s));
   return PB_OK;
 }
 

@@ -330,7 +330,8 @@ int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
   pb_ctx* ctx = k->A->grid->ctx;
   PB_HIP(hipStreamSynchronize(ctx->stream));
   CgState st;
-  PB_HIP(hipMemcpy(&st, k->d_st, sizeof(st), hipMemcpyDeviceToHost));
+  PB_HIP(hipMemcpyAsync(&st, k->d_st, sizeof(st), hipMemcpyDeviceToHost, ctx->stream));
+  PB_HIP(hipStreamSynchronize(ctx->stream));
   if (res) {
     res->reason = st.reason;
     res->its = st.its;
@@ -339,7 +340,11 @@ int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
   }
   const int64_t nh = std::min<int64_t>(st.its + 1, k->nhist);
   std::vector<double> hist((size_t)std::max<int64_t>(nh, 1));
-  if (nh > 0) PB_HIP(hipMemcpy(hist.data(), k->d_hist, (size_t)nh * sizeof(double), hipMemcpyDeviceToHost));
+  if (nh > 0) {
+    PB_HIP(hipMemcpyAsync(hist.data(), k->d_hist, (size_t)nh * sizeof(double), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    PB_HIP(hipStreamSynchronize(ctx->stream));
+  }
   if (history && cap > 0) memcpy(history, hist.data(), (size_t)std::min(nh, cap) * sizeof(double));
   if (ctx->rank == 0) {
     if (k->opts.monitor)

@@ -188,6 +188,28 @@ struct PassB {
 };
 
 // ---------------------------------------------------------------------------------------------
+// Cross-lane helpers (DPP wave shifts: VALU only, no LDS traffic)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double dpp_from_lower(double v) {  // lane l <- lane l-1 (wave_shr:1)
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_from_upper(double v) {  // lane l <- lane l+1 (wave_shl:1)
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Block-level deterministic reduction of NS partial sums -> parts[block*NS + s]
 // ---------------------------------------------------------------------------------------------
 template <int NS>
@@ -250,11 +272,16 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   const bool wave_on = j0 < g.ny && kb < g.nzl;
   const int nx = g.nx;
   const int ic = active ? i0 : 0;  // clamp addresses of idle lanes
-  // x-edge sources: lane 0 needs x[i0-1]; the last active lane needs x[i0+V]
+  // x-edges: lane 0 needs x[seg0-1]; the last active lane needs x[seg_end] (periodic wrap).
+  // One masked load per plane fetches them for all TY rows: lane t < TY the left edge of row t,
+  // lane 32 + t the right edge; they are broadcast with readlane.
+  const int seg0 = seg * 64 * V;
+  const int seg_end = min(seg0 + 64 * V, nx);
   const bool needL = lane == 0;
   const bool needR = active && (lane == 63 || i0 + V >= nx);
-  const int iL = i0 == 0 ? nx - 1 : i0 - 1;
-  const int iR = (i0 + V >= nx) ? 0 : i0 + V;
+  const int edge_row = lane < 32 ? lane : lane - 32;
+  const bool edge_lane = edge_row < TY;
+  const int edge_i = lane < 32 ? (seg0 == 0 ? nx - 1 : seg0 - 1) : (seg_end >= nx ? 0 : seg_end);
   const int jdn = j0 == 0 ? g.ny - 1 : j0 - 1;
   const int jup = (j0 + TY >= g.ny) ? 0 : j0 + TY;
 
@@ -280,14 +307,15 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
       double hdn[V], hup[V];
       ld.template row<V>(base + (int64_t)jdn * nx + ic, hdn);
       ld.template row<V>(base + (int64_t)jup * nx + ic, hup);
+      double edge = 0.0;
+      if (edge_lane) edge = ld.one(base + (int64_t)(j0 + edge_row) * nx + edge_i);
 #pragma unroll
       for (int t = 0; t < TY; ++t) {
         const int64_t rowb = base + (int64_t)(j0 + t) * nx;
-        double eL = 0.0, eR = 0.0;
-        if (needL) eL = ld.one(rowb + iL);
-        if (needR) eR = ld.one(rowb + iR);
-        const double fromL = __shfl(q1[t][V - 1], (lane + 63) & 63, 64);
-        const double fromR = __shfl(q1[t][0], (lane + 1) & 63, 64);
+        const double eL = readlane_d(edge, t);
+        const double eR = readlane_d(edge, 32 + t);
+        const double fromL = dpp_from_lower(q1[t][V - 1]);
+        const double fromR = dpp_from_upper(q1[t][0]);
         const double xl0 = needL ? eL : fromL;
         const double xrl = needR ? eR : fromR;
         double w[V];
@@ -338,7 +366,7 @@ static Geo make_geo(pb_grid* g, int V, int TY) {
   geo.nsegx = (geo.nx + 64 * V - 1) / (64 * V);
   geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
   const int columns = geo.nsegx * geo.ntile;
-  int target = env_int("PB_STENCIL_BLOCKS", 4 * g->ctx->num_cus);
+  int target = env_int("PB_STENCIL_BLOCKS", 2 * g->ctx->num_cus);
   int nchunk = (target + columns - 1) / columns;
   if (nchunk > geo.nzl) nchunk = geo.nzl;
   if (nchunk < 1) nchunk = 1;
