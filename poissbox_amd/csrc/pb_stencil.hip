@@ -29,7 +29,24 @@ struct Geo {
   int nx, ny, nzl;
   int64_t plane;
   int nsegx, ntile, nchunk, kc, ty;
+  int remap;   // XCD-aware block remap on/off (PB_XCD_REMAP, default on)
+  int nt;      // non-temporal output stores (PB_STENCIL_NT, default on)
+  int ablate;  // timing-only ablation: skip halo/edge loads (PB_STENCIL_ABLATE, wrong results)
+  int xspan;   // 1: the block's waves span consecutive x-segments; 0: they stack in y
+  int nsegb;   // x-segment groups per row (xspan) or x-segments (stacked)
 };
+
+__device__ __forceinline__ void store2(double* p, double a, double b, int nt) {
+  dv2 t;
+  t.x = a;
+  t.y = b;
+  if (nt) __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p));
+  else *reinterpret_cast<dv2*>(p) = t;
+}
+__device__ __forceinline__ void store1(double* p, double a, int nt) {
+  if (nt) __builtin_nontemporal_store(a, p);
+  else *p = a;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Loaders: value of the field at an owned linear index (plane*k + nx*j + i)
@@ -103,15 +120,9 @@ struct StoreY {
   __device__ __forceinline__ void prepare() {}
   template <int V>
   __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
-                                      double*) const {
-    if constexpr (V == 2) {
-      dv2 t;
-      t.x = w[0];
-      t.y = w[1];
-      __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(y + idx));
-    } else {
-      __builtin_nontemporal_store(w[0], y + idx);
-    }
+                                      double*, int nt) const {
+    if constexpr (V == 2) store2(y + idx, w[0], w[1], nt);
+    else store1(y + idx, w[0], nt);
     (void)c;
   }
 };
@@ -123,15 +134,9 @@ struct PassA {
   __device__ __forceinline__ void prepare() {}
   template <int V>
   __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
-                                      double* acc) const {
-    if constexpr (V == 2) {
-      dv2 t;
-      t.x = c[0];
-      t.y = c[1];
-      __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p_new + idx));
-    } else {
-      __builtin_nontemporal_store(c[0], p_new + idx);
-    }
+                                      double* acc, int nt) const {
+    if constexpr (V == 2) store2(p_new + idx, c[0], c[1], nt);
+    else store1(p_new + idx, c[0], nt);
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[0] += w[e] * c[e];
   }
@@ -152,7 +157,7 @@ struct PassB {
   }
   template <int V>
   __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
-                                      double* acc) const {
+                                      double* acc, int nt) const {
     double xv[V], rv[V];
     if constexpr (V == 2) {
       dv2 a = *reinterpret_cast<const dv2*>(x + idx);
@@ -175,14 +180,11 @@ struct PassB {
       acc[3] += rv[e];
     }
     if constexpr (V == 2) {
-      dv2 a, b;
-      a.x = xv[0]; a.y = xv[1];
-      b.x = rv[0]; b.y = rv[1];
-      __builtin_nontemporal_store(a, reinterpret_cast<dv2*>(x + idx));
-      __builtin_nontemporal_store(b, reinterpret_cast<dv2*>(r + idx));
+      store2(x + idx, xv[0], xv[1], nt);
+      store2(r + idx, rv[0], rv[1], nt);
     } else {
-      __builtin_nontemporal_store(xv[0], x + idx);
-      __builtin_nontemporal_store(rv[0], r + idx);
+      store1(x + idx, xv[0], nt);
+      store1(r + idx, rv[0], nt);
     }
   }
 };
@@ -241,7 +243,7 @@ __device__ __forceinline__ void block_partials(double* acc, double* parts) {
 // ---------------------------------------------------------------------------------------------
 // The stencil engine
 // ---------------------------------------------------------------------------------------------
-template <int V, int TY, class Load, class Epi>
+template <int V, int TY, int PF, class Load, class Epi>
 __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, double cy, double cz,
                                                          double cc, Load ld0,
                                                          const double* __restrict__ ghost_lo,
@@ -259,17 +261,26 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   for (int s = 0; s < (NS > 0 ? NS : 1); ++s) acc[s] = 0.0;
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // XCD-aware remap (speed only): the dispatcher deals blocks round-robin over the 8 XCDs, so
+  // give each XCD a contiguous range of logical tiles -- y/x-neighbouring tiles then share the
+  // XCD's L2 and their halo rows hit there. Bijective for any grid size.
   int b = blockIdx.x;
-  const int seg = b % g.nsegx;
-  b /= g.nsegx;
+  if (g.remap) {
+    const int nb = gridDim.x, q = nb / 8, r = nb % 8;
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int segb = b % g.nsegb;
+  b /= g.nsegb;
   const int tile = b % g.ntile;
   const int chunk = b / g.ntile;
-  const int j0 = (tile * kWaves + wid) * TY;
+  const int seg = g.xspan ? segb * kWaves + wid : segb;
+  const int j0 = g.xspan ? tile * TY : (tile * kWaves + wid) * TY;
   const int kb = chunk * g.kc;
   const int ke = min(kb + g.kc, g.nzl);
   const int i0 = seg * 64 * V + lane * V;
   const bool active = i0 < g.nx;
-  const bool wave_on = j0 < g.ny && kb < g.nzl;
+  const bool wave_on = j0 < g.ny && kb < g.nzl && seg < g.nsegx;
   const int nx = g.nx;
   const int ic = active ? i0 : 0;  // clamp addresses of idle lanes
   // x-edges: lane 0 needs x[seg0-1]; the last active lane needs x[seg_end] (periodic wrap).
@@ -286,7 +297,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   const int jup = (j0 + TY >= g.ny) ? 0 : j0 + TY;
 
   if (wave_on) {
-    double q0[TY][V], q1[TY][V], q2[TY][V];
+    double q0[TY][V], q1[TY][V], q2[TY][V], q3[TY][V];
     // plane loader for the z-queue: kk in [-1, nzl]
     auto load_plane = [&](int kk, double (&q)[TY][V]) {
       if (kk < 0 || kk >= g.nzl) {
@@ -301,14 +312,28 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
     };
     load_plane(kb - 1, q0);
     load_plane(kb, q1);
+    if constexpr (PF == 2) load_plane(kb + 1, q2);
     for (int k = kb; k < ke; ++k) {
-      load_plane(k + 1, q2);
+      // z-queue: PF = 1 loads plane k+1 now; PF = 2 keeps plane k+2 in flight one step ahead
+      if constexpr (PF == 2) {
+        if (k + 2 <= ke) load_plane(k + 2, q3);
+      } else {
+        load_plane(k + 1, q2);
+      }
       const int64_t base = (int64_t)k * g.plane;
       double hdn[V], hup[V];
-      ld.template row<V>(base + (int64_t)jdn * nx + ic, hdn);
-      ld.template row<V>(base + (int64_t)jup * nx + ic, hup);
       double edge = 0.0;
-      if (edge_lane) edge = ld.one(base + (int64_t)(j0 + edge_row) * nx + edge_i);
+      if (!g.ablate) {
+        ld.template row<V>(base + (int64_t)jdn * nx + ic, hdn);
+        ld.template row<V>(base + (int64_t)jup * nx + ic, hup);
+        if (edge_lane) edge = ld.one(base + (int64_t)(j0 + edge_row) * nx + edge_i);
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          hdn[e] = q1[0][e];
+          hup[e] = q1[TY - 1][e];
+        }
+      }
 #pragma unroll
       for (int t = 0; t < TY; ++t) {
         const int64_t rowb = base + (int64_t)(j0 + t) * nx;
@@ -334,7 +359,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
           s = s + cz * q2[t][e];
           w[e] = s;
         }
-        if (active) ep.template put<V>(rowb + i0, q1[t], w, acc);
+        if (active) ep.template put<V>(rowb + i0, q1[t], w, acc, g.nt);
       }
 #pragma unroll
       for (int t = 0; t < TY; ++t)
@@ -342,6 +367,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         for (int e = 0; e < V; ++e) {
           q0[t][e] = q1[t][e];
           q1[t][e] = q2[t][e];
+          if constexpr (PF == 2) q2[t][e] = q3[t][e];
         }
     }
   }
@@ -363,9 +389,19 @@ static Geo make_geo(pb_grid* g, int V, int TY) {
   geo.nzl = (int)g->nzl;
   geo.plane = g->plane;
   geo.ty = TY;
+  geo.remap = env_int("PB_XCD_REMAP", 1);
+  geo.nt = env_int("PB_STENCIL_NT", 1);
+  geo.ablate = env_int("PB_STENCIL_ABLATE", 0);
   geo.nsegx = (geo.nx + 64 * V - 1) / (64 * V);
-  geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
-  const int columns = geo.nsegx * geo.ntile;
+  geo.xspan = env_int("PB_STENCIL_XSPAN", 0) && geo.nsegx >= kWaves;
+  if (geo.xspan) {
+    geo.nsegb = (geo.nsegx + kWaves - 1) / kWaves;
+    geo.ntile = (geo.ny + TY - 1) / TY;
+  } else {
+    geo.nsegb = geo.nsegx;
+    geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
+  }
+  const int columns = geo.nsegb * geo.ntile;
   int target = env_int("PB_STENCIL_BLOCKS", 2 * g->ctx->num_cus);
   int nchunk = (target + columns - 1) / columns;
   if (nchunk > geo.nzl) nchunk = geo.nzl;
@@ -375,53 +411,59 @@ static Geo make_geo(pb_grid* g, int V, int TY) {
   return geo;
 }
 
-static int pick_ty(int ny) {
+static int pick_ty(int ny, bool) {
   int forced = env_int("PB_STENCIL_TY", 0);
-  if (forced > 0 && ny % forced == 0) return forced;
+  if ((forced == 1 || forced == 2 || forced == 4) && ny % forced == 0) return forced;
   if (ny % 4 == 0) return 4;
   if (ny % 2 == 0) return 2;
   return 1;
 }
 
-template <int V, int TY, class Load, class Epi>
+template <int V, int TY, int PF, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                     const Epi& ep, const int* skip) {
   Geo geo = make_geo(g, V, TY);
-  const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
+  const int64_t nblocks = (int64_t)geo.nsegb * geo.ntile * geo.nchunk;
   if (nblocks > g->ctx->partials_cap / 8)
     return set_error(PB_ERR_UNSUPPORTED, "stencil grid of %lld blocks exceeds partials capacity",
                      (long long)nblocks);
-  hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+  hipLaunchKernelGGL((star7_kernel<V, TY, PF, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                      g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
                      g->ctx->d_partials, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
 
+template <int V, int TY, class Load, class Epi>
+static int launch_pf(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
+                     const Epi& ep, const int* skip) {
+  if (env_int("PB_STENCIL_PF", 1) == 2) return launch_t<V, TY, 2>(g, s, ld, gp, ep, skip);
+  return launch_t<V, TY, 1>(g, s, ld, gp, ep, skip);
+}
+
 template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                       const Epi& ep, const int* skip) {
   const bool vec2 = (g->n[0] % 2) == 0;
-  const int ty = pick_ty((int)g->n[1]);
+  const int ty = pick_ty((int)g->n[1], vec2);
   if (vec2) {
     switch (ty) {
-      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip);
-      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip);
-      case 8: return launch_t<2, 8>(g, s, ld, gp, ep, skip);
-      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip);
+      case 4: return launch_pf<2, 4>(g, s, ld, gp, ep, skip);
+      case 2: return launch_pf<2, 2>(g, s, ld, gp, ep, skip);
+      default: return launch_pf<2, 1>(g, s, ld, gp, ep, skip);
     }
   }
   switch (ty) {
-    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip);
-    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip);
-    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip);
+    case 4: return launch_t<1, 4, 1>(g, s, ld, gp, ep, skip);
+    case 2: return launch_t<1, 2, 1>(g, s, ld, gp, ep, skip);
+    default: return launch_t<1, 1, 1>(g, s, ld, gp, ep, skip);
   }
 }
 
 int stencil_blocks(pb_grid* g) {
   const bool vec2 = (g->n[0] % 2) == 0;
-  Geo geo = make_geo(g, vec2 ? 2 : 1, pick_ty((int)g->n[1]));
-  return geo.nsegx * geo.ntile * geo.nchunk;
+  Geo geo = make_geo(g, vec2 ? 2 : 1, pick_ty((int)g->n[1], vec2));
+  return geo.nsegb * geo.ntile * geo.nchunk;
 }
 
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,

@@ -1,7 +1,8 @@
 import json, sys
-rows = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")]
-last = max(r["round"] for r in rows)
-for r in rows:
-    if r["round"] == last:
-        print(f"TY={r['ty']} blocks={r['blocks']:5d}  mv {r['mv_ms']:.3f} ms {r['mv_GBps']:5.0f}  "
-              f"A {r['a_ms']:.3f} {r['a_GBps']:5.0f}  B {r['b_ms']:.3f} {r['b_GBps']:5.0f}")
+for l in open(sys.argv[1]):
+    if not l.startswith("{"):
+        continue
+    r = json.loads(l)
+    print(f"{json.dumps(r['cfg']):60s} mv {r['mv_min_ms']:.3f}/{r['mv_med_ms']:.3f} ({r['mv_GBps_med']:4.0f})  "
+          f"A {r['a_min_ms']:.3f}/{r['a_med_ms']:.3f} ({r['a_GBps_med']:4.0f})  "
+          f"B {r['b_min_ms']:.3f}/{r['b_med_ms']:.3f} ({r['b_GBps_med']:4.0f})")
