@@ -1,0 +1,126 @@
+!! poissbox_demo.f90 -- the reference demo flow (src/example.f90) on one MI355X.
+!
+! Same sequence of steps as poissbox_example (src/example.f90:55-84): grid + check_grid, linear
+! system, x = random in [-1,1], b = A x, check_lapl (A x vs pointwise stencil), check_matrices
+! (A x vs P x), KSP solve from PETSc-style options, final residual ||A x - b||_2.
+! Usage: poissbox_demo [-n N] [-ksp_rtol 1e-10] [-ksp_monitor] [-ksp_converged_reason] ...
+program poissbox_demo
+
+  use iso_c_binding, only: c_int64_t
+  use poissbox_gpu
+
+  implicit none
+
+  integer :: ierr, n1, its, reason
+  integer, dimension(3) :: n
+  real(pb_dp), dimension(3) :: h
+  real(pb_dp) :: error, xsum, rnorm
+  type(tDM) :: da
+  type(tMat) :: P, A
+  type(tVec) :: x, b, x2
+  type(mat_ctx) :: ctx
+
+  n1 = arg_int("-n", 64)
+  n = [n1, n1, n1]
+  h = 1.0_pb_dp / real(n, pb_dp)  ! src/example.f90:33-35, L = 1
+
+  call PoissboxInitialize(0, ierr)
+  if (ierr /= 0) stop 1
+  print *, "Running poissbox on ", 1, " GPU"
+
+  call initialise_grid(n, da, ierr)
+  call check_grid(n, da)
+
+  ctx%da = da
+  ctx%grid_deltas = h
+  call initialise_linear_system(da, ctx, P, A, x, b, ierr)
+  if (ierr /= 0) stop 1
+
+  ! set_solution (src/example.f90:154-199): x = 2(0.5 - U)
+  call VecSetRandom(x, 20231015_c_int64_t, ierr)
+  call VecSum(x, xsum, ierr)
+  print *, "Rank ", 0, "XSUM of the specified solution: ", xsum
+  print *, "Calling MatMult"
+  call MatMult(A, x, b, ierr)
+  call check_lapl(da, x, b)
+  call check_matrices(A, P, x)
+
+  call solve(P, A, x, b, ierr, its, reason, rnorm)
+  if (ierr /= 0) stop 1
+  call VecDuplicate(x, x2, ierr)
+  print *, "Calling MatMult"
+  call MatMult(A, x, x2, ierr)
+  call VecAXPY(x2, -1.0_pb_dp, b, ierr)
+  call VecNorm(x2, error, ierr)
+  print *, "KSP iterations: ", its, " reason: ", reason, " ||z||: ", rnorm
+  print *, "Solution residual (L2 norm): ", error
+
+  call VecDestroy(x2, ierr)
+  call VecDestroy(x, ierr)
+  call VecDestroy(b, ierr)
+  call PoissboxFinalize(ierr)
+
+contains
+
+  integer function arg_int(name, dflt)
+    character(len=*), intent(in) :: name
+    integer, intent(in) :: dflt
+    character(len=64) :: a
+    integer :: i
+    arg_int = dflt
+    do i = 1, command_argument_count() - 1
+       call get_command_argument(i, a)
+       if (trim(a) == name) then
+          call get_command_argument(i + 1, a)
+          read(a, *) arg_int
+       end if
+    end do
+  end function arg_int
+
+  !! src/example.f90:92-116: owned DoF vs global DoF
+  subroutine check_grid(nglobal, da)
+    integer, dimension(3), intent(in) :: nglobal
+    type(tDM), intent(in) :: da
+    integer :: istart, jstart, kstart, ni, nj, nk, ierr
+    call DMDAGetCorners(da, istart, jstart, kstart, ni, nj, nk, ierr)
+    print *, "(DMDA): Rank ", 0, " has ", ni * nj * nk, " of ", ni * nj * nk, &
+         " expected: ", product(nglobal)
+  end subroutine check_grid
+
+  !! src/example.f90:201-233: ||A x - pointwise(x)||_2 (identical kernels -> 0)
+  subroutine check_lapl(da, x, b)
+    type(tDM), intent(in) :: da
+    type(tVec), intent(in) :: x, b
+    type(tVec) :: b2, c
+    real(pb_dp) :: residual
+    integer :: ierr
+    call VecDuplicate(b, b2, ierr)
+    call VecCopy(b, b2, ierr)
+    call VecDuplicate(b, c, ierr)
+    call compute_lapl_pointwise(da, h, x, c, ierr)
+    call VecAXPY(b2, -1.0_pb_dp, c, ierr)
+    call VecNorm(b2, residual, ierr)
+    print *, "Rank ", 0, "Delta between b=Mx and pointwise calculation: ", residual
+    call VecDestroy(b2, ierr)
+    call VecDestroy(c, ierr)
+  end subroutine check_lapl
+
+  !! src/example.f90:235-261: ||A x - P x||_2
+  subroutine check_matrices(A, P, x)
+    type(tMat), intent(in) :: A, P
+    type(tVec), intent(in) :: x
+    type(tVec) :: bP, bA
+    real(pb_dp) :: delta
+    integer :: ierr
+    call VecDuplicate(x, bP, ierr)
+    call VecDuplicate(x, bA, ierr)
+    call MatMult(P, x, bP, ierr)
+    call MatMult(A, x, bA, ierr)
+    call VecAXPY(bA, -1.0_pb_dp, bP, ierr)
+    call VecNorm(bA, delta, ierr)
+    print *, "Ax - Px = ", delta
+    call VecDestroy(bP, ierr)
+    call VecDestroy(bA, ierr)
+  end subroutine check_matrices
+
+end program poissbox_demo

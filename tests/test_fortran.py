@@ -1,0 +1,44 @@
+"""The Fortran host side (iso_c_binding module + demo mirroring src/example.f90)."""
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FDIR = os.path.join(REPO, "poissbox_amd", "fortran")
+DEMO = os.path.join(FDIR, "build", "poissbox_demo")
+FLANG = "/opt/rocm/lib/llvm/bin/flang"
+
+
+@pytest.mark.skipif(not os.path.exists(FLANG), reason="flang not in this image")
+def test_fortran_module_compiles(tmp_path):
+    out = subprocess.run([FLANG, "-c", os.path.join(FDIR, "poissbox_gpu.f90")], cwd=tmp_path,
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert (tmp_path / "poissbox_gpu.mod").exists()
+
+
+@pytest.mark.gpu
+def test_fortran_demo_matches_oracle():
+    from oracle import oracle as O
+    if not os.path.exists(DEMO):
+        subprocess.run(["make", "-s", "-C", FDIR], check=True)
+    out = subprocess.run([DEMO, "-n", "32", "-ksp_type", "cg", "-pc_type", "jacobi",
+                          "-ksp_rtol", "1e-8", "-ksp_converged_reason"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    txt = out.stdout
+    assert re.search(r"has\s+32768\s+of\s+32768\s+expected:\s+32768", txt)
+    assert re.search(r"pointwise calculation:\s+0\.0", txt)          # same kernel: exact
+    assert re.search(r"Ax - Px =\s+0\.0", txt)                        # same 7 non-zeros
+    m = re.search(r"converged due to CONVERGED_RTOL iterations (\d+)", txt)
+    n = (32, 32, 32)
+    h = (1 / 32,) * 3
+    b = O.stencil(O.fill_random(32 ** 3, 20231015), n, h)
+    _, reason, its, _ = O.cg_solve(b, n, h, rtol=1e-8)
+    assert m and int(m.group(1)) == its
+    res = float(re.search(r"Solution residual \(L2 norm\):\s+(\S+)", txt).group(1))
+    assert res < 1e-4 * np.linalg.norm(b)
