@@ -131,7 +131,11 @@ static int alpha_factor(pb_ctx* ctx, int64_t n, double alpha, AlphaFactor* out) 
   memcpy(all.data() + n, BM.data(), n * sizeof(double));
   memcpy(all.data() + 2 * n, U.data(), n * sizeof(double));
   PB_HIP(hipMalloc(&f.dev, 3 * n * sizeof(double)));
-  PB_HIP(hipMemcpy(f.dev, all.data(), 3 * n * sizeof(double), hipMemcpyHostToDevice));
+  // stream-ordered upload, completed before any kernel can use the cached factors (a blocking
+  // hipMemcpy from pageable memory may return before the DMA lands)
+  PB_HIP(hipMemcpyAsync(f.dev, all.data(), 3 * n * sizeof(double), hipMemcpyHostToDevice,
+                        ctx->stream));
+  PB_HIP(hipStreamSynchronize(ctx->stream));
   g_fac[key] = f;
   *out = f;
   return PB_OK;

@@ -153,19 +153,20 @@ int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
 
 // CG state (device resident; all scalars computed on device, host only polls `done`)
 struct CgState {
-  double beta, betaold, dpi, dpiold, alpha, mu, dp, ttol, rnorm0;
+  double beta, betaold, dpi, dpiold, alpha, alpha_prev, pend_alpha, mu, dp, ttol, rnorm0;
   double rtol, atol, dtol, dinv, ntot;
-  int64_t it, its, max_it, nhist;
-  int reason, done, pc, nullspace;
+  int64_t it, its, max_it, nhist, pend_iter;
+  int reason, done, pc, nullspace, defer_x;
 };
 int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p, CgState* st,
                    double dinv, double* hist, int* h_done);
 int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st);
 int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
                      double* p_new, const StencilPlanes& gp, CgState* st);
-int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, double* x, double* r,
-                     const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
-                     int64_t host_iter);
+int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
+                     double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
+                     int64_t host_iter, bool defer_x);
+int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
 int stencil_blocks(pb_grid* g);  // number of partial-sum slots a stencil pass writes
 
 // ---- vector ops (pb_vecops.hip) ----

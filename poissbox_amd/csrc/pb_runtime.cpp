@@ -173,7 +173,7 @@ int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb
   ctx->partials_cap = (int64_t)1 << 20;  // doubles: room for 131072 blocks x 8 sums
   PB_HIP(hipMalloc(&ctx->d_partials, ctx->partials_cap * sizeof(double)));
   PB_HIP(hipMalloc(&ctx->d_scalars, 64 * sizeof(double)));
-  PB_HIP(hipMemset(ctx->d_scalars, 0, 64 * sizeof(double)));
+  PB_HIP(hipMemsetAsync(ctx->d_scalars, 0, 64 * sizeof(double), ctx->stream));
   PB_HIP(hipHostMalloc(&ctx->h_scalars, 64 * sizeof(double), hipHostMallocDefault));
   if (nranks > 1 && uid) {
     ncclUniqueId id;

@@ -24,8 +24,7 @@ struct pb_ksp {
   pb_op* P = nullptr;
   pb_ksp_opts opts;
   double* r = nullptr;
-  double* p0 = nullptr;
-  double* p1 = nullptr;
+  double* pb[2] = {nullptr, nullptr};  // iteration i: p_old = pb[i%2], p_new = pb[(i+1)%2]
   double* w = nullptr;   // generic (unfused) path only
   double* z = nullptr;   // generic path only
   CgState* d_st = nullptr;
@@ -41,6 +40,7 @@ struct pb_ksp {
   int64_t host_iter = 0;
   bool stopped = false;
   bool begun = false;
+  bool defer_x = true;  // x update every second iteration (PB_CG_DEFER_X=0 disables)
 };
 
 extern "C" {
@@ -190,8 +190,8 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   }
   pb_grid* g = A->grid;
   const size_t vb = (size_t)g->nlocal * sizeof(double);
-  if (hipMalloc(&k->r, vb) != hipSuccess || hipMalloc(&k->p0, vb) != hipSuccess ||
-      hipMalloc(&k->p1, vb) != hipSuccess) {
+  if (hipMalloc(&k->r, vb) != hipSuccess || hipMalloc(&k->pb[0], vb) != hipSuccess ||
+      hipMalloc(&k->pb[1], vb) != hipSuccess) {
     delete k;
     return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
   }
@@ -251,8 +251,11 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   // PCJacobi stores the reciprocal of diag(P) (src/coefficients.f90:44-46 centre coefficient)
   st.dinv = k->opts.pc_type == PB_PC_JACOBI ? 1.0 / k->P->cc : 1.0;
   st.ntot = (double)(g->n[0] * g->n[1] * g->n[2]);
+  const char* dx = getenv("PB_CG_DEFER_X");
+  k->defer_x = !(dx && atoi(dx) == 0);
+  st.defer_x = k->defer_x ? 1 : 0;
   PB_HIP(hipMemcpyAsync(k->d_st, &st, sizeof(st), hipMemcpyHostToDevice, ctx->stream));
-  PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->p0, k->d_st, st.dinv, k->d_hist, k->h_done_dev));
+  PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->pb[0], k->d_st, st.dinv, k->d_hist, k->h_done_dev));
   PB_HIP(hipStreamSynchronize(ctx->stream));
   k->b = b;
   k->x = x;
@@ -266,7 +269,10 @@ static int enqueue_iteration(pb_ksp* k) {
   pb_grid* g = k->A->grid;
   pb_ctx* ctx = g->ctx;
   Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};
-  PB_TRY(launch_cg_boundary(g, k->r, k->p0, k->d_st));
+  const int64_t i = k->host_iter;  // == device iteration index until convergence
+  double* p_old = k->pb[i % 2];
+  double* p_new = k->pb[(i + 1) % 2];
+  PB_TRY(launch_cg_boundary(g, k->r, p_old, k->d_st));
   StencilPlanes gp;
   if (ctx->nranks == 1) {
     gp.ghost_lo = g->bnd_hi;  // p_new of plane nzl-1 wraps below plane 0
@@ -276,10 +282,9 @@ static int enqueue_iteration(pb_ksp* k) {
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
   }
-  PB_TRY(launch_cg_pass_a(g, s, k->r, k->p0, k->p1, gp, k->d_st));
-  PB_TRY(launch_cg_pass_b(g, s, k->p1, k->x->d, k->r, gp, k->d_st, k->d_hist, k->h_done_dev,
-                          k->host_iter));
-  std::swap(k->p0, k->p1);
+  PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st));
+  PB_TRY(launch_cg_pass_b(g, s, p_new, p_old, k->x->d, k->r, gp, k->d_st, k->d_hist,
+                          k->h_done_dev, i, k->defer_x));
   return PB_OK;
 }
 
@@ -332,6 +337,10 @@ int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
   CgState st;
   PB_HIP(hipMemcpyAsync(&st, k->d_st, sizeof(st), hipMemcpyDeviceToHost, ctx->stream));
   PB_HIP(hipStreamSynchronize(ctx->stream));
+  if (st.pend_iter >= 0) {  // apply the deferred alpha_i p_i of the last even iteration
+    PB_TRY(launch_cg_flush(k->A->grid, k->x->d, k->pb[(st.pend_iter + 1) % 2], st.pend_alpha));
+    PB_HIP(hipStreamSynchronize(ctx->stream));
+  }
   if (res) {
     res->reason = st.reason;
     res->its = st.its;
@@ -375,8 +384,8 @@ int pb_ksp_destroy(pb_ksp* k) {
   if (!k) return PB_OK;
   (void)hipStreamSynchronize(k->A->grid->ctx->stream);
   (void)hipFree(k->r);
-  (void)hipFree(k->p0);
-  (void)hipFree(k->p1);
+  (void)hipFree(k->pb[0]);
+  (void)hipFree(k->pb[1]);
   if (k->w) (void)hipFree(k->w);
   if (k->z) (void)hipFree(k->z);
   (void)hipFree(k->d_st);

@@ -6,13 +6,16 @@
 //
 // Work decomposition (HBM-bound, AI ~ 0.8 flop/B, MFMA unused):
 //   * a wave owns an x-segment of 64*V points (V = 2 -> one 16-B load per lane, 1 KiB per
-//     wave-instruction) of TY consecutive y-rows, and marches in z over a chunk of planes, keeping
+//     wave-instruction) of TY consecutive y-rows and marches in z over a chunk of planes, keeping
 //     planes k-1, k, k+1 of its rows in registers (each plane is read from HBM once per chunk);
-//   * x-neighbours come from the neighbouring lane (cross-lane shuffle), the two segment-end
-//     values from a masked load (L1/L2 hit); y-neighbours come from the wave's own rows in
-//     registers, the tile's top/bottom rows from the neighbouring tile (cache hit);
-//   * 4 waves per workgroup stack in y so their halo rows are shared through the CU's L1;
-//   * z ghosts (periodic wrap or the neighbouring rank's plane) are read from plane pointers
+//   * software pipeline: while plane k is computed, plane k+2 of the z-queue and the halo rows,
+//     segment edges and epilogue operands (x, r in CG pass B) of plane k+1 are in flight -- the
+//     grid is sized to 2 workgroups per CU, so registers, not occupancy, buy the latency hiding;
+//   * x-neighbours come from the neighbouring lane (DPP wave shift); the two segment-end values
+//     of all TY rows come from ONE masked load, broadcast with readlane; y-neighbours come from
+//     the wave's own rows, the tile's top/bottom rows from the neighbouring tile (L2 hit: tiles
+//     are remapped so neighbours share an XCD);
+//   * z ghosts (periodic wrap or the neighbouring rank's plane) are read through plane pointers
 //     chosen per plane, so no ghost copy is made on one rank.
 // Summation order per point matches the reference dot product with its zero terms dropped:
 // z-, y-, x-, centre, x+, y+, z+ (built with -ffp-contract=off => bit-identical to the oracle).
@@ -29,48 +32,50 @@ struct Geo {
   int nx, ny, nzl;
   int64_t plane;
   int nsegx, ntile, nchunk, kc, ty;
-  int remap;   // XCD-aware block remap on/off (PB_XCD_REMAP, default on)
-  int nt;      // non-temporal output stores (PB_STENCIL_NT, default on)
-  int ablate;  // timing-only ablation: skip halo/edge loads (PB_STENCIL_ABLATE, wrong results)
-  int xspan;   // 1: the block's waves span consecutive x-segments; 0: they stack in y
-  int nsegb;   // x-segment groups per row (xspan) or x-segments (stacked)
+  int remap;  // XCD-aware block remap on/off (PB_XCD_REMAP, default on)
+  int nt;     // non-temporal output stores (PB_STENCIL_NT, default on)
 };
 
-__device__ __forceinline__ void store2(double* p, double a, double b, int nt) {
-  dv2 t;
-  t.x = a;
-  t.y = b;
-  if (nt) __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p));
-  else *reinterpret_cast<dv2*>(p) = t;
+template <int V>
+__device__ __forceinline__ void load_row(const double* __restrict__ p, int64_t idx, double (&v)[V]) {
+  if constexpr (V == 2) {
+    const dv2 t = *reinterpret_cast<const dv2*>(p + idx);
+    v[0] = t.x;
+    v[1] = t.y;
+  } else {
+    v[0] = p[idx];
+  }
 }
-__device__ __forceinline__ void store1(double* p, double a, int nt) {
-  if (nt) __builtin_nontemporal_store(a, p);
-  else *p = a;
+template <int V>
+__device__ __forceinline__ void store_row(double* p, int64_t idx, const double (&v)[V], int nt) {
+  if constexpr (V == 2) {
+    dv2 t;
+    t.x = v[0];
+    t.y = v[1];
+    if (nt) __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p + idx));
+    else *reinterpret_cast<dv2*>(p + idx) = t;
+  } else {
+    if (nt) __builtin_nontemporal_store(v[0], p + idx);
+    else p[idx] = v[0];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Loaders: value of the field at an owned linear index (plane*k + nx*j + i)
+// Loaders: NR raw arrays per point, combined into the field value by value().
 // ---------------------------------------------------------------------------------------------
 struct PlainLoad {
+  static constexpr int NR = 1;
   const double* __restrict__ x;
   __device__ __forceinline__ void prepare() {}
-  template <int V>
-  __device__ __forceinline__ void row(int64_t idx, double (&v)[V]) const {
-    if constexpr (V == 2) {
-      dv2 t = *reinterpret_cast<const dv2*>(x + idx);
-      v[0] = t.x;
-      v[1] = t.y;
-    } else {
-      v[0] = x[idx];
-    }
-  }
-  __device__ __forceinline__ double one(int64_t idx) const { return x[idx]; }
+  __device__ __forceinline__ const double* src(int) const { return x; }
+  __device__ __forceinline__ double value(const double* raw) const { return raw[0]; }
 };
 
 // p_new = (dinv*r + shift) + bb*p_old  -- PCApply_Jacobi + MatNullSpaceRemove + VecAYPX fused
 struct CgState;
 __device__ __forceinline__ double cg_bb(const CgState* st);
 struct CombineLoad {
+  static constexpr int NR = 2;
   const double* __restrict__ r;
   const double* __restrict__ p;
   const CgState* st;
@@ -80,111 +85,97 @@ struct CombineLoad {
     shift = -st->mu;
     bb = cg_bb(st);
   }
+  __device__ __forceinline__ const double* src(int a) const { return a == 0 ? r : p; }
   __device__ __forceinline__ double f(double rv, double pv) const {
     double z = dinv * rv;
     z = z + shift;
     return z + bb * pv;
   }
-  template <int V>
-  __device__ __forceinline__ void row(int64_t idx, double (&v)[V]) const {
-    if constexpr (V == 2) {
-      dv2 a = *reinterpret_cast<const dv2*>(r + idx);
-      dv2 b = *reinterpret_cast<const dv2*>(p + idx);
-      v[0] = f(a.x, b.x);
-      v[1] = f(a.y, b.y);
-    } else {
-      v[0] = f(r[idx], p[idx]);
-    }
-  }
+  __device__ __forceinline__ double value(const double* raw) const { return f(raw[0], raw[1]); }
   __device__ __forceinline__ double one(int64_t idx) const { return f(r[idx], p[idx]); }
 };
 
-template <int V>
-__device__ __forceinline__ void ghost_row(const double* __restrict__ g, int64_t idx,
-                                          double (&v)[V]) {
-  if constexpr (V == 2) {
-    dv2 t = *reinterpret_cast<const dv2*>(g + idx);
-    v[0] = t.x;
-    v[1] = t.y;
-  } else {
-    v[0] = g[idx];
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
-// Epilogues: consume centre value c and Laplacian w at owned index idx
+// Epilogues: NE operand arrays prefetched one plane ahead; put() consumes centre value c,
+// Laplacian w and the operands at owned index idx.
 // ---------------------------------------------------------------------------------------------
 struct StoreY {
-  static constexpr int NS = 0;
+  static constexpr int NS = 0, NE = 0;
+  static constexpr bool PREFETCH = true;
   double* __restrict__ y;
   __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ const double* src(int) const { return nullptr; }
   template <int V>
   __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
-                                      double*, int nt) const {
-    if constexpr (V == 2) store2(y + idx, w[0], w[1], nt);
-    else store1(y + idx, w[0], nt);
+                                      double (&)[1][V], double*, int nt) const {
+    store_row<V>(y, idx, w, nt);
     (void)c;
   }
 };
 
 // CG pass A: store p_new, accumulate p.w (VecXDot(P, W))
 struct PassA {
-  static constexpr int NS = 1;
+  static constexpr int NS = 1, NE = 0;
+  static constexpr bool PREFETCH = true;
   double* __restrict__ p_new;
   __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ const double* src(int) const { return nullptr; }
   template <int V>
   __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
-                                      double* acc, int nt) const {
-    if constexpr (V == 2) store2(p_new + idx, c[0], c[1], nt);
-    else store1(p_new + idx, c[0], nt);
+                                      double (&)[1][V], double* acc, int nt) const {
+    store_row<V>(p_new, idx, c, nt);
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[0] += w[e] * c[e];
   }
 };
 
-// CG pass B: x += a p; r += (-a) w; then the PC/null-space sums of the new residual:
-//   s = dinv*r, t = s - mu_old:  sum t, sum t^2, sum t*r, sum r
+// CG pass B: r += (-a) w with w = A p recomputed; then the PC/null-space sums of the new
+// residual: s = dinv*r, t = s - mu_old:  sum t, sum t^2, sum t*r, sum r.
+// The solution update is deferred to every second iteration (x is not part of the recurrence):
+//   XU = 0 (even iteration i): no x traffic, alpha_i p_i stays pending;
+//   XU = 1 (odd iteration i):  x += (alpha_{i-1} p_{i-1} + alpha_i p_i), p_{i-1} is still
+//                              resident in the other p buffer;
+//   XU = 2 (no deferral):      x += alpha_i p_i every iteration.
+// Operands are prefetched one plane ahead except for XU = 1, whose 3 operand rows would push
+// the kernel past 256 VGPRs (1 wave per SIMD, half the workgroups resident).
+template <int XU>
 struct PassB {
-  static constexpr int NS = 4;
+  static constexpr int NS = 4, NE = XU == 1 ? 3 : (XU == 2 ? 2 : 1);
+  static constexpr bool PREFETCH = XU != 1;
   double* __restrict__ x;
   double* __restrict__ r;
+  const double* __restrict__ p_prev;
   const CgState* st;
-  double alpha, dinv, mu;
-  __device__ __forceinline__ void prepare() {
-    alpha = st->alpha;
-    dinv = st->dinv;
-    mu = st->mu;
+  double alpha, alpha_prev, dinv, mu;
+  __device__ __forceinline__ void prepare();
+  __device__ __forceinline__ const double* src(int a) const {
+    return a == 0 ? r : (a == 1 ? x : p_prev);
   }
   template <int V>
   __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
-                                      double* acc, int nt) const {
-    double xv[V], rv[V];
-    if constexpr (V == 2) {
-      dv2 a = *reinterpret_cast<const dv2*>(x + idx);
-      dv2 b = *reinterpret_cast<const dv2*>(r + idx);
-      xv[0] = a.x; xv[1] = a.y;
-      rv[0] = b.x; rv[1] = b.y;
-    } else {
-      xv[0] = x[idx];
-      rv[0] = r[idx];
-    }
+                                      double (&op)[NE][V], double* acc, int nt) const {
+    double rv[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      xv[e] = xv[e] + alpha * c[e];
-      rv[e] = rv[e] + (-alpha) * w[e];
-      double s = dinv * rv[e];
-      double t = s - mu;
+      rv[e] = op[0][e] + (-alpha) * w[e];
+      const double s = dinv * rv[e];
+      const double t = s - mu;
       acc[0] += t;
       acc[1] += t * t;
       acc[2] += t * rv[e];
       acc[3] += rv[e];
     }
-    if constexpr (V == 2) {
-      store2(x + idx, xv[0], xv[1], nt);
-      store2(r + idx, rv[0], rv[1], nt);
-    } else {
-      store1(x + idx, xv[0], nt);
-      store1(r + idx, rv[0], nt);
+    store_row<V>(r, idx, rv, nt);
+    if constexpr (XU == 1) {
+      double xv[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) xv[e] = op[1][e] + (alpha_prev * op[2][e] + alpha * c[e]);
+      store_row<V>(x, idx, xv, nt);
+    } else if constexpr (XU == 2) {
+      double xv[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) xv[e] = op[1][e] + alpha * c[e];
+      store_row<V>(x, idx, xv, nt);
     }
   }
 };
@@ -243,7 +234,7 @@ __device__ __forceinline__ void block_partials(double* acc, double* parts) {
 // ---------------------------------------------------------------------------------------------
 // The stencil engine
 // ---------------------------------------------------------------------------------------------
-template <int V, int TY, int PF, class Load, class Epi>
+template <int V, int TY, class Load, class Epi>
 __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, double cy, double cz,
                                                          double cc, Load ld0,
                                                          const double* __restrict__ ghost_lo,
@@ -255,7 +246,8 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   ld.prepare();
   Epi ep = ep0;
   ep.prepare();
-  constexpr int NS = Epi::NS;
+  constexpr int NS = Epi::NS, NR = Load::NR;
+  constexpr int NE = Epi::NE > 0 ? Epi::NE : 1;
   double acc[NS > 0 ? NS : 1];
 #pragma unroll
   for (int s = 0; s < (NS > 0 ? NS : 1); ++s) acc[s] = 0.0;
@@ -270,22 +262,21 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
     const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
     b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
-  const int segb = b % g.nsegb;
-  b /= g.nsegb;
+  const int seg = b % g.nsegx;
+  b /= g.nsegx;
   const int tile = b % g.ntile;
   const int chunk = b / g.ntile;
-  const int seg = g.xspan ? segb * kWaves + wid : segb;
-  const int j0 = g.xspan ? tile * TY : (tile * kWaves + wid) * TY;
+  const int j0 = (tile * kWaves + wid) * TY;
   const int kb = chunk * g.kc;
   const int ke = min(kb + g.kc, g.nzl);
-  const int i0 = seg * 64 * V + lane * V;
-  const bool active = i0 < g.nx;
-  const bool wave_on = j0 < g.ny && kb < g.nzl && seg < g.nsegx;
   const int nx = g.nx;
+  const int i0 = seg * 64 * V + lane * V;
+  const bool active = i0 < nx;
+  const bool wave_on = j0 < g.ny && kb < g.nzl;
   const int ic = active ? i0 : 0;  // clamp addresses of idle lanes
   // x-edges: lane 0 needs x[seg0-1]; the last active lane needs x[seg_end] (periodic wrap).
-  // One masked load per plane fetches them for all TY rows: lane t < TY the left edge of row t,
-  // lane 32 + t the right edge; they are broadcast with readlane.
+  // One masked load per plane and array fetches them for all TY rows: lane t < TY the left edge
+  // of row t, lane 32 + t the right edge; they are broadcast with readlane.
   const int seg0 = seg * 64 * V;
   const int seg_end = min(seg0 + 64 * V, nx);
   const bool needL = lane == 0;
@@ -293,50 +284,112 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   const int edge_row = lane < 32 ? lane : lane - 32;
   const bool edge_lane = edge_row < TY;
   const int edge_i = lane < 32 ? (seg0 == 0 ? nx - 1 : seg0 - 1) : (seg_end >= nx ? 0 : seg_end);
-  const int jdn = j0 == 0 ? g.ny - 1 : j0 - 1;
-  const int jup = (j0 + TY >= g.ny) ? 0 : j0 + TY;
+  const int64_t edge_off = (int64_t)(j0 + (edge_lane ? edge_row : 0)) * nx + edge_i;
+  const int64_t off_dn = (int64_t)(j0 == 0 ? g.ny - 1 : j0 - 1) * nx + ic;
+  const int64_t off_up = (int64_t)((j0 + TY >= g.ny) ? 0 : j0 + TY) * nx + ic;
 
   if (wave_on) {
-    double q0[TY][V], q1[TY][V], q2[TY][V], q3[TY][V];
-    // plane loader for the z-queue: kk in [-1, nzl]
-    auto load_plane = [&](int kk, double (&q)[TY][V]) {
-      if (kk < 0 || kk >= g.nzl) {
+    // combined z-queue (planes k-1, k, k+1) and raw prefetch of plane k+2
+    double q0[TY][V], q1[TY][V], q2[TY][V];
+    double zr[NR][TY][V];
+    bool zr_ghost = false;
+    // plane-k operands (combined) and their plane-(k+1) prefetch (raw)
+    double hdn[V], hup[V], edge = 0.0;
+    double hdn_r[NR][V], hup_r[NR][V], edge_r[NR];
+    double opc[TY][NE][V], opn[Epi::PREFETCH ? TY : 1][NE][V];
+
+    auto issue_zrow = [&](int kk) {  // raw rows of plane kk in [-1, nzl] -> zr
+      zr_ghost = kk < 0 || kk >= g.nzl;
+      if (zr_ghost) {
         const double* gp = kk < 0 ? ghost_lo : ghost_hi;
 #pragma unroll
-        for (int t = 0; t < TY; ++t) ghost_row<V>(gp, (int64_t)(j0 + t) * nx + ic, q[t]);
+        for (int t = 0; t < TY; ++t) load_row<V>(gp, (int64_t)(j0 + t) * nx + ic, zr[0][t]);
       } else {
         const int64_t base = (int64_t)kk * g.plane;
 #pragma unroll
-        for (int t = 0; t < TY; ++t) ld.template row<V>(base + (int64_t)(j0 + t) * nx + ic, q[t]);
+        for (int a = 0; a < NR; ++a)
+#pragma unroll
+          for (int t = 0; t < TY; ++t)
+            load_row<V>(ld.src(a), base + (int64_t)(j0 + t) * nx + ic, zr[a][t]);
       }
     };
-    load_plane(kb - 1, q0);
-    load_plane(kb, q1);
-    if constexpr (PF == 2) load_plane(kb + 1, q2);
-    for (int k = kb; k < ke; ++k) {
-      // z-queue: PF = 1 loads plane k+1 now; PF = 2 keeps plane k+2 in flight one step ahead
-      if constexpr (PF == 2) {
-        if (k + 2 <= ke) load_plane(k + 2, q3);
-      } else {
-        load_plane(k + 1, q2);
-      }
-      const int64_t base = (int64_t)k * g.plane;
-      double hdn[V], hup[V];
-      double edge = 0.0;
-      if (!g.ablate) {
-        ld.template row<V>(base + (int64_t)jdn * nx + ic, hdn);
-        ld.template row<V>(base + (int64_t)jup * nx + ic, hup);
-        if (edge_lane) edge = ld.one(base + (int64_t)(j0 + edge_row) * nx + edge_i);
-      } else {
+    auto take_zrow = [&](double (&q)[TY][V]) {  // combine zr into q
+#pragma unroll
+      for (int t = 0; t < TY; ++t)
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          hdn[e] = q1[0][e];
-          hup[e] = q1[TY - 1][e];
+          double raw[NR];
+#pragma unroll
+          for (int a = 0; a < NR; ++a) raw[a] = zr[a][t][e];
+          q[t][e] = zr_ghost ? zr[0][t][e] : ld.value(raw);
         }
+    };
+    auto issue_plane_ops = [&](int kk) {  // halo rows, edges, epilogue operands of own plane kk
+      const int64_t base = (int64_t)kk * g.plane;
+#pragma unroll
+      for (int a = 0; a < NR; ++a) {
+        load_row<V>(ld.src(a), base + off_dn, hdn_r[a]);
+        load_row<V>(ld.src(a), base + off_up, hup_r[a]);
+        edge_r[a] = 0.0;
+        if (edge_lane) edge_r[a] = ld.src(a)[base + edge_off];
       }
+      if constexpr (Epi::NE > 0 && Epi::PREFETCH) {
+#pragma unroll
+        for (int t = 0; t < TY; ++t)
+#pragma unroll
+          for (int a = 0; a < Epi::NE; ++a)
+            load_row<V>(ep.src(a), base + (int64_t)(j0 + t) * nx + ic, opn[t][a]);
+      }
+    };
+    auto issue_ops_now = [&](int kk) {  // operands without prefetch: plane kk straight to opc
+      if constexpr (Epi::NE > 0 && !Epi::PREFETCH) {
+        const int64_t base = (int64_t)kk * g.plane;
+#pragma unroll
+        for (int t = 0; t < TY; ++t)
+#pragma unroll
+          for (int a = 0; a < Epi::NE; ++a)
+            load_row<V>(ep.src(a), base + (int64_t)(j0 + t) * nx + ic, opc[t][a]);
+      }
+    };
+    auto take_plane_ops = [&]() {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        double rd[NR], ru[NR];
+#pragma unroll
+        for (int a = 0; a < NR; ++a) {
+          rd[a] = hdn_r[a][e];
+          ru[a] = hup_r[a][e];
+        }
+        hdn[e] = ld.value(rd);
+        hup[e] = ld.value(ru);
+      }
+      edge = ld.value(edge_r);
+      if constexpr (Epi::NE > 0 && Epi::PREFETCH) {
+#pragma unroll
+        for (int t = 0; t < TY; ++t)
+#pragma unroll
+          for (int a = 0; a < Epi::NE; ++a)
+#pragma unroll
+            for (int e = 0; e < V; ++e) opc[t][a][e] = opn[t][a][e];
+      }
+    };
+
+    // prologue: planes kb-1, kb combined; raw plane kb+1 and plane kb's operands in flight
+    issue_zrow(kb - 1);
+    take_zrow(q0);
+    issue_zrow(kb);
+    take_zrow(q1);
+    issue_plane_ops(kb);
+    issue_zrow(kb + 1);
+    for (int k = kb; k < ke; ++k) {
+      take_zrow(q2);                    // plane k+1 (in flight since the previous step)
+      take_plane_ops();                 // halo/edges/operands of plane k
+      issue_ops_now(k);
+      if (k + 2 <= ke) issue_zrow(k + 2);
+      if (k + 1 < ke) issue_plane_ops(k + 1);
+      const int64_t base = (int64_t)k * g.plane;
 #pragma unroll
       for (int t = 0; t < TY; ++t) {
-        const int64_t rowb = base + (int64_t)(j0 + t) * nx;
         const double eL = readlane_d(edge, t);
         const double eR = readlane_d(edge, 32 + t);
         const double fromL = dpp_from_lower(q1[t][V - 1]);
@@ -359,7 +412,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
           s = s + cz * q2[t][e];
           w[e] = s;
         }
-        if (active) ep.template put<V>(rowb + i0, q1[t], w, acc, g.nt);
+        if (active) ep.template put<V>(base + (int64_t)(j0 + t) * nx + i0, q1[t], w, opc[t], acc, g.nt);
       }
 #pragma unroll
       for (int t = 0; t < TY; ++t)
@@ -367,7 +420,6 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         for (int e = 0; e < V; ++e) {
           q0[t][e] = q1[t][e];
           q1[t][e] = q2[t][e];
-          if constexpr (PF == 2) q2[t][e] = q3[t][e];
         }
     }
   }
@@ -391,18 +443,11 @@ static Geo make_geo(pb_grid* g, int V, int TY) {
   geo.ty = TY;
   geo.remap = env_int("PB_XCD_REMAP", 1);
   geo.nt = env_int("PB_STENCIL_NT", 1);
-  geo.ablate = env_int("PB_STENCIL_ABLATE", 0);
   geo.nsegx = (geo.nx + 64 * V - 1) / (64 * V);
-  geo.xspan = env_int("PB_STENCIL_XSPAN", 0) && geo.nsegx >= kWaves;
-  if (geo.xspan) {
-    geo.nsegb = (geo.nsegx + kWaves - 1) / kWaves;
-    geo.ntile = (geo.ny + TY - 1) / TY;
-  } else {
-    geo.nsegb = geo.nsegx;
-    geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
-  }
-  const int columns = geo.nsegb * geo.ntile;
-  int target = env_int("PB_STENCIL_BLOCKS", 2 * g->ctx->num_cus);
+  geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
+  const int columns = geo.nsegx * geo.ntile;
+  // 3 workgroups per CU: long z-chunks (few chunk-boundary re-reads), all blocks resident
+  int target = env_int("PB_STENCIL_BLOCKS", 3 * g->ctx->num_cus);
   int nchunk = (target + columns - 1) / columns;
   if (nchunk > geo.nzl) nchunk = geo.nzl;
   if (nchunk < 1) nchunk = 1;
@@ -411,7 +456,7 @@ static Geo make_geo(pb_grid* g, int V, int TY) {
   return geo;
 }
 
-static int pick_ty(int ny, bool) {
+static int pick_ty(int ny) {
   int forced = env_int("PB_STENCIL_TY", 0);
   if ((forced == 1 || forced == 2 || forced == 4) && ny % forced == 0) return forced;
   if (ny % 4 == 0) return 4;
@@ -419,51 +464,44 @@ static int pick_ty(int ny, bool) {
   return 1;
 }
 
-template <int V, int TY, int PF, class Load, class Epi>
+template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                     const Epi& ep, const int* skip) {
   Geo geo = make_geo(g, V, TY);
-  const int64_t nblocks = (int64_t)geo.nsegb * geo.ntile * geo.nchunk;
+  const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
   if (nblocks > g->ctx->partials_cap / 8)
     return set_error(PB_ERR_UNSUPPORTED, "stencil grid of %lld blocks exceeds partials capacity",
                      (long long)nblocks);
-  hipLaunchKernelGGL((star7_kernel<V, TY, PF, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+  hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                      g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
                      g->ctx->d_partials, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
 
-template <int V, int TY, class Load, class Epi>
-static int launch_pf(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
-                     const Epi& ep, const int* skip) {
-  if (env_int("PB_STENCIL_PF", 1) == 2) return launch_t<V, TY, 2>(g, s, ld, gp, ep, skip);
-  return launch_t<V, TY, 1>(g, s, ld, gp, ep, skip);
-}
-
 template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                       const Epi& ep, const int* skip) {
   const bool vec2 = (g->n[0] % 2) == 0;
-  const int ty = pick_ty((int)g->n[1], vec2);
+  const int ty = pick_ty((int)g->n[1]);
   if (vec2) {
     switch (ty) {
-      case 4: return launch_pf<2, 4>(g, s, ld, gp, ep, skip);
-      case 2: return launch_pf<2, 2>(g, s, ld, gp, ep, skip);
-      default: return launch_pf<2, 1>(g, s, ld, gp, ep, skip);
+      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip);
+      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip);
+      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip);
     }
   }
   switch (ty) {
-    case 4: return launch_t<1, 4, 1>(g, s, ld, gp, ep, skip);
-    case 2: return launch_t<1, 2, 1>(g, s, ld, gp, ep, skip);
-    default: return launch_t<1, 1, 1>(g, s, ld, gp, ep, skip);
+    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip);
+    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip);
+    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip);
   }
 }
 
 int stencil_blocks(pb_grid* g) {
   const bool vec2 = (g->n[0] % 2) == 0;
-  Geo geo = make_geo(g, vec2 ? 2 : 1, pick_ty((int)g->n[1], vec2));
-  return geo.nsegb * geo.ntile * geo.nchunk;
+  Geo geo = make_geo(g, vec2 ? 2 : 1, pick_ty((int)g->n[1]));
+  return geo.nsegx * geo.ntile * geo.nchunk;
 }
 
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
@@ -477,6 +515,14 @@ int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ double cg_bb(const CgState* st) {
   return st->it == 0 ? 0.0 : st->beta / st->betaold;
+}
+
+template <int XU>
+__device__ __forceinline__ void PassB<XU>::prepare() {
+  alpha = st->alpha;
+  alpha_prev = st->alpha_prev;
+  dinv = st->dinv;
+  mu = st->mu;
 }
 
 // r = b, x = 0, p = 0 and the sums of s = dinv*r (t = s - 0)
@@ -566,6 +612,9 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
     st->it = 0;
     st->its = 0;
     st->dpi = 0.0;
+    st->alpha = 0.0;
+    st->alpha_prev = 0.0;
+    st->pend_iter = -1;
     st->reason = 0;
     st->done = 0;
     if (st->nhist > 0) hist[0] = dp;
@@ -612,6 +661,7 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
       st->dpiold = st->dpi;
       st->dpi = dpi;
       st->betaold = st->beta;
+      st->alpha_prev = st->alpha;
       st->alpha = st->beta / dpi;
     }
     return;
@@ -627,6 +677,13 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
       zr = S[2] - delta * S[3];
     }
     const double dp = sqrt(zz > 0.0 ? zz : 0.0);
+    // even iterations leave alpha_i p_i pending in x; odd ones applied both (PassB<XU>)
+    if (st->defer_x && i % 2 == 0) {
+      st->pend_iter = i;
+      st->pend_alpha = st->alpha;
+    } else {
+      st->pend_iter = -1;
+    }
     st->dp = dp;
     st->its = i + 1;
     if (i + 1 < st->nhist) hist[i + 1] = dp;
@@ -717,14 +774,41 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
   return cg_reduce_update(g->ctx, 1, stencil_blocks(g), 1, st, nullptr, nullptr, 0);
 }
 
-int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, double* x, double* r,
-                     const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
-                     int64_t host_iter) {
+int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
+                     double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
+                     int64_t host_iter, bool defer_x) {
   {
-    ScopedTimer tm(g->ctx, "cg_pass_b");
-    PB_TRY(launch_any(g, s, PlainLoad{p}, gp, PassB{x, r, st, 0.0, 0.0, 0.0}, &st->done));
+    if (!defer_x) {
+      ScopedTimer tm(g->ctx, "cg_pass_b");
+      PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
+                        PassB<2>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done));
+    } else if (host_iter % 2 == 0) {
+      ScopedTimer tm(g->ctx, "cg_pass_b_even");
+      PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
+                        PassB<0>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done));
+    } else {
+      ScopedTimer tm(g->ctx, "cg_pass_b_odd");
+      PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
+                        PassB<1>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done));
+    }
   }
   return cg_reduce_update(g->ctx, 2, stencil_blocks(g), 4, st, hist, h_done, host_iter);
+}
+
+// x += alpha * p (the pending half of the deferred solution update)
+__global__ __launch_bounds__(256) void cg_flush_kernel(double* __restrict__ x,
+                                                       const double* __restrict__ p, int64_t n,
+                                                       double alpha) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = x[i] + alpha * p[i];
+}
+
+int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha) {
+  const int nb = elementwise_blocks(g->ctx, g->nlocal);
+  hipLaunchKernelGGL(cg_flush_kernel, dim3(nb), dim3(256), 0, g->ctx->stream, x, p, g->nlocal, alpha);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
 }
 
 }  // namespace pb

@@ -2,7 +2,7 @@
 set -u
 mkdir -p gpurun_out
 timeout -k 10 900 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -6 gpurun_out/pytest_gpu.log
+rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-timeout -k 10 600 python scripts/tune_stencil.py > gpurun_out/tune.log 2>&1
+timeout -k 10 900 python scripts/tune_stencil.py > gpurun_out/tune.log 2>&1
 rc=$?; echo "tune rc=$rc"; exit $rc

@@ -8,6 +8,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import poissbox_amd as pb  # noqa: E402
@@ -23,11 +24,11 @@ xt.set_random(1)
 A.mult(xt, b)
 y = pb.Vec(da)
 N = da.nlocal
-acc = {i: {"mv": [], "a": [], "b": []} for i in range(len(configs))}
+acc = {i: {"mv": [], "a": [], "b": [], "be": [], "it": []} for i in range(len(configs))}
 base_env = dict(os.environ)
 for rnd in range(rounds):
     for i, cfg in enumerate(configs):
-        for k in ("PB_STENCIL_TY", "PB_STENCIL_BLOCKS", "PB_XCD_REMAP"):
+        for k in ("PB_STENCIL_TY", "PB_STENCIL_BLOCKS", "PB_XCD_REMAP", "PB_CG_DEFER_X"):
             if k in base_env:
                 os.environ[k] = base_env[k]
             else:
@@ -40,22 +41,32 @@ for rnd in range(rounds):
         ctx.reset_timing()
         for _ in range(20):
             A.mult(xt, y)
-        k = pb.KSP(A, P, pb.ksp_options(rtol=0.0, atol=0.0, dtol=1e300, max_it=40))
+        k = pb.KSP(A, P, pb.ksp_options(rtol=0.0, atol=0.0, dtol=1e300, max_it=80))
         k.begin(b, x)
-        k.iterate(16)
+        k.iterate(4)
         ctx.sync()
-        mv, pa, pbb = ctx.timing("stencil"), ctx.timing("cg_pass_a"), ctx.timing("cg_pass_b")
+        t0 = time.perf_counter()
+        k.iterate(32)
+        ctx.sync()
+        it_ms = (time.perf_counter() - t0) / 32 * 1e3
+        mv, pa = ctx.timing("stencil"), ctx.timing("cg_pass_a")
+        pbb = ctx.timing("cg_pass_b_odd")
+        if pbb[1] == 0:
+            pbb = ctx.timing("cg_pass_b")
+        pbe = ctx.timing("cg_pass_b_even")
         ctx.set_timing(False)
         k.end()
         k.destroy()
         acc[i]["mv"].append(mv[0] / mv[1])
         acc[i]["a"].append(pa[0] / pa[1])
         acc[i]["b"].append(pbb[0] / pbb[1])
+        acc[i]["be"].append(pbe[0] / pbe[1] if pbe[1] else 0.0)
+        acc[i]["it"].append(it_ms)
 for i, cfg in enumerate(configs):
     out = {"cfg": cfg}
-    for key, nbytes in (("mv", 16), ("a", 24), ("b", 40)):
+    for key, nbytes in (("mv", 16), ("a", 24), ("b", 48), ("be", 24), ("it", 60)):
         v = acc[i][key]
         out[key + "_min_ms"] = min(v)
         out[key + "_med_ms"] = statistics.median(v)
-        out[key + "_GBps_med"] = nbytes * N / statistics.median(v) / 1e6
+        out[key + "_GBps_med"] = nbytes * N / max(statistics.median(v), 1e-9) / 1e6
     print(json.dumps(out), flush=True)

@@ -36,6 +36,7 @@ class Dev:
         self.p = C.c_void_p()
         assert Dev._hip.hipMalloc(C.byref(self.p), C.c_size_t(max(8, 8 * self.n))) == 0
         assert Dev._hip.hipMemcpy(self.p, arr.ctypes.data_as(C.c_void_p), C.c_size_t(8 * self.n), 1) == 0
+        assert Dev._hip.hipDeviceSynchronize() == 0  # pageable H2D may return before the DMA lands
 
     def get(self):
         out = np.empty(self.n)
