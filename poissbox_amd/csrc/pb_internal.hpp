@@ -61,6 +61,8 @@ struct pb_ctx {
   int rank = 0;
   int nranks = 1;
   hipStream_t stream = nullptr;
+  hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with interior planes
+  hipEvent_t ev_ready = nullptr, ev_done = nullptr;
   ncclComm_t comm = nullptr;
   // host transport (tests)
   pb_sendrecv_fn h_sendrecv = nullptr;
@@ -140,6 +142,10 @@ struct ScopedTimer {
 // Exchange z-boundary planes: send `lo` (first owned plane data) to rank-1 and `hi` to rank+1,
 // receive into grid->ghost_lo (from rank-1) / grid->ghost_hi (from rank+1). Stream ordered.
 int halo_exchange(pb_grid* g, const double* lo, const double* hi);
+// Split form: begin (RCCL on the context's comm stream after an event on the compute stream;
+// host transport: synchronous), end (compute stream waits for the exchange).
+int halo_begin(pb_grid* g, const double* lo, const double* hi);
+int halo_end(pb_grid* g);
 // In-place SUM allreduce of `count` device doubles (stream ordered).
 int allreduce_device(pb_ctx* ctx, double* d_vals, int count);
 
@@ -148,8 +154,9 @@ struct StencilPlanes {
   const double* ghost_lo;  // plane at k = -1
   const double* ghost_hi;  // plane at k = nzl
 };
+enum { PLANES_ALL = 0, PLANES_INTERIOR = 1, PLANES_BOUNDARY = 2 };
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
-                       const StencilPlanes& gp);
+                       const StencilPlanes& gp, int mode);
 
 // CG state (device resident; all scalars computed on device, host only polls `done`)
 struct CgState {
@@ -162,12 +169,14 @@ int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p,
                    double dinv, double* hist, int* h_done);
 int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st);
 int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                     double* p_new, const StencilPlanes& gp, CgState* st);
+                     double* p_new, const StencilPlanes& gp, CgState* st, int mode, int part_off,
+                     int* nblocks);
+int cg_finalize_pass_a(pb_ctx* ctx, int nparts, CgState* st);
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
                      double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
                      int64_t host_iter, bool defer_x);
 int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
-int stencil_blocks(pb_grid* g);  // number of partial-sum slots a stencil pass writes
+int stencil_blocks(pb_grid* g, int mode);  // partial-sum slots a stencil pass writes
 
 // ---- vector ops (pb_vecops.hip) ----
 int vec_fill(pb_ctx* ctx, double* d, int64_t n, double a);

@@ -110,6 +110,31 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
   return PB_OK;
 }
 
+int halo_begin(pb_grid* g, const double* lo, const double* hi) {
+  pb_ctx* ctx = g->ctx;
+  if (ctx->nranks == 1 || !ctx->comm) return halo_exchange(g, lo, hi);
+  const int64_t cnt = g->plane;
+  const int down = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
+  const int up = (ctx->rank + 1) % ctx->nranks;
+  PB_HIP(hipEventRecord(ctx->ev_ready, ctx->stream));
+  PB_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->ev_ready, 0));
+  PB_NCCL(ncclGroupStart());
+  PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
+  PB_NCCL(ncclRecv(g->ghost_hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
+  PB_NCCL(ncclSend(hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
+  PB_NCCL(ncclRecv(g->ghost_lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
+  PB_NCCL(ncclGroupEnd());
+  PB_HIP(hipEventRecord(ctx->ev_done, ctx->comm_stream));
+  return PB_OK;
+}
+
+int halo_end(pb_grid* g) {
+  pb_ctx* ctx = g->ctx;
+  if (ctx->nranks == 1 || !ctx->comm) return PB_OK;
+  PB_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_done, 0));
+  return PB_OK;
+}
+
 int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
   if (ctx->nranks == 1) return PB_OK;
   ScopedTimer tm(ctx, "allreduce");
@@ -170,6 +195,9 @@ int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb
       cus > 0)
     ctx->num_cus = cus;
   PB_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  PB_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+  PB_HIP(hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming));
+  PB_HIP(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
   ctx->partials_cap = (int64_t)1 << 20;  // doubles: room for 131072 blocks x 8 sums
   PB_HIP(hipMalloc(&ctx->d_partials, ctx->partials_cap * sizeof(double)));
   PB_HIP(hipMalloc(&ctx->d_scalars, 64 * sizeof(double)));
@@ -225,6 +253,10 @@ int pb_ctx_destroy(pb_ctx* ctx) {
   (void)hipFree(ctx->d_partials);
   (void)hipFree(ctx->d_scalars);
   (void)hipHostFree(ctx->h_scalars);
+  (void)hipStreamSynchronize(ctx->comm_stream);
+  (void)hipEventDestroy(ctx->ev_ready);
+  (void)hipEventDestroy(ctx->ev_done);
+  (void)hipStreamDestroy(ctx->comm_stream);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return PB_OK;

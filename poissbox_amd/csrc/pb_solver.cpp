@@ -85,12 +85,19 @@ static int op_apply_raw(pb_op* op, const double* x, double* y) {
   if (g->ctx->nranks == 1) {
     gp.ghost_lo = x + (g->nzl - 1) * g->plane;  // periodic wrap: no copy
     gp.ghost_hi = x;
-  } else {
-    PB_TRY(halo_exchange(g, x, x + (g->nzl - 1) * g->plane));
-    gp.ghost_lo = g->ghost_lo;
-    gp.ghost_hi = g->ghost_hi;
+    return launch_star7_apply(g, s, x, y, gp, PLANES_ALL);
   }
-  return launch_star7_apply(g, s, x, y, gp);
+  gp.ghost_lo = g->ghost_lo;
+  gp.ghost_hi = g->ghost_hi;
+  if (g->nzl < 3) {
+    PB_TRY(halo_exchange(g, x, x + (g->nzl - 1) * g->plane));
+    return launch_star7_apply(g, s, x, y, gp, PLANES_ALL);
+  }
+  // interior planes overlap the halo exchange; the two boundary planes follow it
+  PB_TRY(halo_begin(g, x, x + (g->nzl - 1) * g->plane));
+  PB_TRY(launch_star7_apply(g, s, x, y, gp, PLANES_INTERIOR));
+  PB_TRY(halo_end(g));
+  return launch_star7_apply(g, s, x, y, gp, PLANES_BOUNDARY);
 }
 
 int pb_op_apply(pb_op* op, const pb_vec* x, pb_vec* y) {
@@ -274,15 +281,28 @@ static int enqueue_iteration(pb_ksp* k) {
   double* p_new = k->pb[(i + 1) % 2];
   PB_TRY(launch_cg_boundary(g, k->r, p_old, k->d_st));
   StencilPlanes gp;
+  int nparts = 0;
   if (ctx->nranks == 1) {
     gp.ghost_lo = g->bnd_hi;  // p_new of plane nzl-1 wraps below plane 0
     gp.ghost_hi = g->bnd_lo;
-  } else {
+    PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
+  } else if (g->nzl < 3) {
     PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
+    PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
+  } else {
+    // the p-plane halo exchange (RCCL, comm stream) overlaps pass A's interior planes
+    gp.ghost_lo = g->ghost_lo;
+    gp.ghost_hi = g->ghost_hi;
+    int nb1 = 0, nb2 = 0;
+    PB_TRY(halo_begin(g, g->bnd_lo, g->bnd_hi));
+    PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1));
+    PB_TRY(halo_end(g));
+    PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1, &nb2));
+    nparts = nb1 + nb2;
   }
-  PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st));
+  PB_TRY(cg_finalize_pass_a(ctx, nparts, k->d_st));
   PB_TRY(launch_cg_pass_b(g, s, p_new, p_old, k->x->d, k->r, gp, k->d_st, k->d_hist,
                           k->h_done_dev, i, k->defer_x));
   return PB_OK;

@@ -32,6 +32,7 @@ struct Geo {
   int nx, ny, nzl;
   int64_t plane;
   int nsegx, ntile, nchunk, kc, ty;
+  int k_lo, k_hi, kstride;  // chunk c covers planes [k_lo + c*kstride, min(+kc, k_hi))
   int remap;  // XCD-aware block remap on/off (PB_XCD_REMAP, default on)
   int nt;     // non-temporal output stores (PB_STENCIL_NT, default on)
 };
@@ -267,12 +268,12 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   const int tile = b % g.ntile;
   const int chunk = b / g.ntile;
   const int j0 = (tile * kWaves + wid) * TY;
-  const int kb = chunk * g.kc;
-  const int ke = min(kb + g.kc, g.nzl);
+  const int kb = g.k_lo + chunk * g.kstride;
+  const int ke = min(kb + g.kc, g.k_hi);
   const int nx = g.nx;
   const int i0 = seg * 64 * V + lane * V;
   const bool active = i0 < nx;
-  const bool wave_on = j0 < g.ny && kb < g.nzl;
+  const bool wave_on = j0 < g.ny && kb < g.k_hi;
   const int ic = active ? i0 : 0;  // clamp addresses of idle lanes
   // x-edges: lane 0 needs x[seg0-1]; the last active lane needs x[seg_end] (periodic wrap).
   // One masked load per plane and array fetches them for all TY rows: lane t < TY the left edge
@@ -434,7 +435,10 @@ static int env_int(const char* name, int dflt) {
   return s ? atoi(s) : dflt;
 }
 
-static Geo make_geo(pb_grid* g, int V, int TY) {
+// Plane sets: PLANES_ALL = [0, nzl); PLANES_INTERIOR = [1, nzl-1) (no ghost plane is read);
+// PLANES_BOUNDARY = {0, nzl-1} (the two planes that read ghosts) -- the split lets the halo
+// exchange of a multi-rank step overlap the interior.
+static Geo make_geo(pb_grid* g, int V, int TY, int mode) {
   Geo geo;
   geo.nx = (int)g->n[0];
   geo.ny = (int)g->n[1];
@@ -445,14 +449,26 @@ static Geo make_geo(pb_grid* g, int V, int TY) {
   geo.nt = env_int("PB_STENCIL_NT", 1);
   geo.nsegx = (geo.nx + 64 * V - 1) / (64 * V);
   geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
+  if (mode == PLANES_BOUNDARY) {
+    geo.k_lo = 0;
+    geo.k_hi = geo.nzl;
+    geo.kc = 1;
+    geo.kstride = geo.nzl - 1;
+    geo.nchunk = 2;
+    return geo;
+  }
+  geo.k_lo = mode == PLANES_INTERIOR ? 1 : 0;
+  geo.k_hi = mode == PLANES_INTERIOR ? geo.nzl - 1 : geo.nzl;
+  const int nk = geo.k_hi - geo.k_lo;
   const int columns = geo.nsegx * geo.ntile;
-  // 3 workgroups per CU: long z-chunks (few chunk-boundary re-reads), all blocks resident
+  // 3 workgroups per CU: long z-chunks (few chunk-boundary re-reads)
   int target = env_int("PB_STENCIL_BLOCKS", 3 * g->ctx->num_cus);
   int nchunk = (target + columns - 1) / columns;
-  if (nchunk > geo.nzl) nchunk = geo.nzl;
+  if (nchunk > nk) nchunk = nk;
   if (nchunk < 1) nchunk = 1;
-  geo.kc = (geo.nzl + nchunk - 1) / nchunk;
-  geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
+  geo.kc = (nk + nchunk - 1) / nchunk;
+  geo.kstride = geo.kc;
+  geo.nchunk = (nk + geo.kc - 1) / geo.kc;
   return geo;
 }
 
@@ -466,48 +482,51 @@ static int pick_ty(int ny) {
 
 template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
-                    const Epi& ep, const int* skip) {
-  Geo geo = make_geo(g, V, TY);
+                    const Epi& ep, const int* skip, int mode, int part_off, int* nb_out) {
+  Geo geo = make_geo(g, V, TY, mode);
   const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
-  if (nblocks > g->ctx->partials_cap / 8)
+  constexpr int NS = Epi::NS > 0 ? Epi::NS : 1;
+  if ((part_off + nblocks) * NS > g->ctx->partials_cap)
     return set_error(PB_ERR_UNSUPPORTED, "stencil grid of %lld blocks exceeds partials capacity",
                      (long long)nblocks);
   hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                      g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
-                     g->ctx->d_partials, skip);
+                     g->ctx->d_partials + (int64_t)part_off * NS, skip);
   PB_HIP(hipGetLastError());
+  if (nb_out) *nb_out = (int)nblocks;
   return PB_OK;
 }
 
 template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
-                      const Epi& ep, const int* skip) {
+                      const Epi& ep, const int* skip, int mode = PLANES_ALL, int part_off = 0,
+                      int* nb_out = nullptr) {
   const bool vec2 = (g->n[0] % 2) == 0;
   const int ty = pick_ty((int)g->n[1]);
   if (vec2) {
     switch (ty) {
-      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip);
-      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip);
-      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip);
+      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
+      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
+      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
     }
   }
   switch (ty) {
-    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip);
-    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip);
-    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip);
+    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
+    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
+    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
   }
 }
 
-int stencil_blocks(pb_grid* g) {
+int stencil_blocks(pb_grid* g, int mode) {
   const bool vec2 = (g->n[0] % 2) == 0;
-  Geo geo = make_geo(g, vec2 ? 2 : 1, pick_ty((int)g->n[1]));
+  Geo geo = make_geo(g, vec2 ? 2 : 1, pick_ty((int)g->n[1]), mode);
   return geo.nsegx * geo.ntile * geo.nchunk;
 }
 
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
-                       const StencilPlanes& gp) {
+                       const StencilPlanes& gp, int mode) {
   ScopedTimer tm(g->ctx, "stencil");
-  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, nullptr);
+  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, nullptr, mode);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -765,13 +784,15 @@ int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState
 }
 
 int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                     double* p_new, const StencilPlanes& gp, CgState* st) {
-  {
-    ScopedTimer tm(g->ctx, "cg_pass_a");
-    PB_TRY(launch_any(g, s, CombineLoad{r, p_old, st, 0.0, 0.0, 0.0}, gp, PassA{p_new},
-                      &st->done));
-  }
-  return cg_reduce_update(g->ctx, 1, stencil_blocks(g), 1, st, nullptr, nullptr, 0);
+                     double* p_new, const StencilPlanes& gp, CgState* st, int mode, int part_off,
+                     int* nblocks) {
+  ScopedTimer tm(g->ctx, "cg_pass_a");
+  return launch_any(g, s, CombineLoad{r, p_old, st, 0.0, 0.0, 0.0}, gp, PassA{p_new}, &st->done,
+                    mode, part_off, nblocks);
+}
+
+int cg_finalize_pass_a(pb_ctx* ctx, int nparts, CgState* st) {
+  return cg_reduce_update(ctx, 1, nparts, 1, st, nullptr, nullptr, 0);
 }
 
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
@@ -792,7 +813,7 @@ int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p
                         PassB<1>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done));
     }
   }
-  return cg_reduce_update(g->ctx, 2, stencil_blocks(g), 4, st, hist, h_done, host_iter);
+  return cg_reduce_update(g->ctx, 2, stencil_blocks(g, PLANES_ALL), 4, st, hist, h_done, host_iter);
 }
 
 // x += alpha * p (the pending half of the deferred solution update)
