@@ -72,6 +72,9 @@ def main():
     ap.add_argument("--base", type=int, default=512, help="per-GPU cube edge (default 512)")
     ap.add_argument("--matvecs", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
+                    help="multi-rank transport: RCCL (default) or the gloo host transport "
+                         "(lets several ranks share one GPU for testing)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -82,18 +85,22 @@ def main():
             sys.exit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} ranks")
 
     import poissbox_amd as pb
+    from poissbox_amd.dist import GlooTransport, broadcast_uid, init_from_env
 
-    dist = None
+    rank, world, local_rank, dist = init_from_env("gloo")   # control plane only
     uid = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-        obj = [pb.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
+    device = local_rank
+    if dist and args.transport == "rccl":
+        uid = broadcast_uid(dist, rank, pb.comm_unique_id)
+    elif dist:
+        import torch
+        device = local_rank % max(1, torch.cuda.device_count())
 
     n = global_grid(world, args.base)
-    ctx = pb.Context(local_rank, rank, world, uid)
+    ctx = pb.Context(device, rank, world, uid)
+    if dist and args.transport == "host":
+        tr = GlooTransport(dist)
+        ctx.set_host_transport(tr.sendrecv, tr.allreduce)
     da = pb.initialise_grid(ctx, n)
     h = da.spacing
     P, A, x, b = pb.initialise_linear_system(da, h)
@@ -167,7 +174,9 @@ def main():
             "config": {"workload": f"fp64 CG + Jacobi, 7-pt periodic Laplacian, "
                                    f"{n[0]}x{n[1]}x{n[2]} grid ({args.base}^3 DoF per GPU)",
                        "grid": list(n), "global_dofs": N, "per_gpu_dofs": nloc,
-                       "parallelism": f"z-slab x{world}" + (" (RCCL halo + allreduce)" if world > 1 else ""),
+                       "parallelism": f"z-slab x{world}" + (
+                           f" ({'RCCL' if args.transport == 'rccl' else 'gloo host'} halo + allreduce)"
+                           if world > 1 else ""),
                        "ksp": "-ksp_type cg -pc_type jacobi, constant null space, rtol=0 (fixed iterations)"},
             "iter_per_s": args.steps / elapsed,
             "achieved_GBps_cg": CG_ITER_BYTES * N / (elapsed / args.steps) / 1e9,

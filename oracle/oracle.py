@@ -75,6 +75,15 @@ def stencil(x, n, h, faithful=False, nthreads=1):
     return y
 
 
+def stencil_slab(x, n_local, h, ghost_lo, ghost_hi):
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    glo = np.ascontiguousarray(ghost_lo, dtype=np.float64).reshape(-1)
+    ghi = np.ascontiguousarray(ghost_hi, dtype=np.float64).reshape(-1)
+    y = np.empty_like(x)
+    lib().pbo_stencil_slab(_n3(n_local), _h3(h), _p(x), _p(glo), _p(ghi), _p(y))
+    return y
+
+
 def assembled(x, n, h):
     x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
     y = np.empty_like(x)

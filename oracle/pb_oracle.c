@@ -114,6 +114,36 @@ void pbo_stencil_apply7(const int64_t n[3], const double h[3], const double* x, 
     }
 }
 
+/* One z-slab of nzl planes with explicit ghost planes below (glo) and above (ghi): the per-rank
+ * view of compute_lapl_pointwise after DMGlobalToLocal (src/poissbox.f90:104-119). x/y periodic. */
+void pbo_stencil_slab(const int64_t n[3], const double h[3], const double* x, const double* glo,
+                      const double* ghi, double* y) {
+  const int64_t nx = n[0], ny = n[1], nz = n[2];
+  double c[27];
+  pbo_lapl_star_coeffs(h[0], h[1], h[2], c);
+  const double cx = c[12], cy = c[10], cz = c[4], cc = c[13];
+  for (int64_t k = 0; k < nz; ++k)
+    for (int64_t j = 0; j < ny; ++j) {
+      const double* xm = k == 0 ? glo + nx * j : x + nx * (j + ny * (k - 1));
+      const double* xp = k == nz - 1 ? ghi + nx * j : x + nx * (j + ny * (k + 1));
+      const double* ym = x + nx * (wrap(j - 1, ny) + ny * k);
+      const double* yp = x + nx * (wrap(j + 1, ny) + ny * k);
+      const double* xc = x + nx * (j + ny * k);
+      double* out = y + nx * (j + ny * k);
+      for (int64_t i = 0; i < nx; ++i) {
+        int64_t im = i == 0 ? nx - 1 : i - 1, ip = i == nx - 1 ? 0 : i + 1;
+        double s = cz * xm[i];
+        s += cy * ym[i];
+        s += cx * xc[im];
+        s += cc * xc[i];
+        s += cx * xc[ip];
+        s += cy * yp[i];
+        s += cz * xp[i];
+        out[i] = s;
+      }
+    }
+}
+
 static int cmp_i64(const void* a, const void* b) {
   int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
   return x < y ? -1 : x > y;

@@ -33,6 +33,9 @@ void pbo_stencil_apply27(const int64_t n[3], const double h[3], const double* x,
  * for finite inputs */
 void pbo_stencil_apply7(const int64_t n[3], const double h[3], const double* x, double* y,
                         int nthreads);
+/* one z-slab (n[2] = owned planes) with explicit ghost planes below/above */
+void pbo_stencil_slab(const int64_t n[3], const double h[3], const double* x, const double* glo,
+                      const double* ghi, double* y);
 /* assembled P (src/coefficients.f90:50-113) applied as a 27-point BOX SpMV, row-wise sum over
  * the 27 stored entries in MatSetValuesStencil column order */
 void pbo_assembled_apply(const int64_t n[3], const double h[3], const double* x, double* y);

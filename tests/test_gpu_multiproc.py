@@ -1,0 +1,65 @@
+"""GPU tier, N processes on the one GPU: each rank is a separate process with its own context,
+connected through the gloo host transport (RCCL refuses two ranks on one device). Exercises
+the library's multi-rank path end to end (slab split, interior/boundary overlap split, halo,
+allreduce, lagged rank-consistent stopping) against the single-rank oracle."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from test_dist_cpu import REPO, SEED, _run
+
+pytestmark = pytest.mark.gpu
+
+N3 = (24, 20, 13)
+
+
+def _gpu_rank(rank, world, tr):
+    import poissbox_amd as pb
+    ctx = pb.Context(0, rank, world)
+    ctx.set_host_transport(tr.sendrecv, tr.allreduce)
+    da = pb.DA(ctx, N3)
+    (_, _, k0), (_, _, nk) = da.get_corners()
+    h = da.spacing
+    P, A, x, b = pb.initialise_linear_system(da, h)
+    xt = pb.Vec(da)
+    xt.set_random(SEED)
+    A.mult(xt, b)
+    bl = b.get_values()
+    reason, its, hist = pb.solve(P, A, x, b, ["-ksp_rtol", "1e-9"])
+    out = (k0, nk, bl, reason, its, hist, x.get_values())
+    ctx.destroy()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multiprocess_cg_on_one_gpu(world):
+    from oracle import oracle as O
+    h = tuple(1.0 / m for m in N3)
+    b = O.stencil(O.fill_random(int(np.prod(N3)), SEED), N3, h)
+    xo, ro, itso, ho = O.cg_solve(b, N3, h, rtol=1e-9)
+    bz, xz = b.reshape(N3[2], -1), xo.reshape(N3[2], -1)
+    for k0, nk, bl, reason, its, hist, xs in _run(world, _gpu_rank):
+        assert np.array_equal(bl, bz[k0:k0 + nk].reshape(-1))      # bit-exact distributed A x
+        assert (reason, its) == (ro, itso)
+        assert np.max(np.abs(hist - ho) / ho) < 1e-7
+        assert np.max(np.abs(xs - xz[k0:k0 + nk].reshape(-1))) <= 1e-6 * np.max(np.abs(xo))
+
+
+def test_bench_two_ranks_host_transport():
+    """bench.py's multi-rank orchestration (torch.distributed.run, barrier, max-over-ranks,
+    weak-scaling grid) on one GPU through the host transport, at a small per-GPU size."""
+    env = dict(os.environ, PYTHONPATH=REPO)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29531", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "6", "--warmup", "2", "--base", "48", "--matvecs", "2",
+           "--transport", "host"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    import json
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["config"]["grid"] == [48, 48, 96] and d["value"] > 0
