@@ -188,6 +188,10 @@ int pb_compact_grad(pb_grid* grid, const double dx[3], const pb_vec* f, pb_vec* 
 int pb_compact_div(pb_grid* grid, const double dx[3], const pb_vec* const f[3], pb_vec* df);
 int pb_compact_interp(pb_grid* grid, int stagger, const pb_vec* f, pb_vec* fi);
 int pb_compact_lapl(pb_grid* grid, const double dx[3], const pb_vec* f, pb_vec* out);
+/* Same operator by the 3-pass factorisation lapl = Lx Jy Jz + Jx Ly Jz + Jx Jy Lz (SURVEY.md
+ * App. D) with PCR line solves in LDS: ~80 B/DoF instead of 16 line-solve families; agrees with
+ * pb_compact_lapl to rounding. This is what PB_OP_COMPACT applies inside CG. */
+int pb_compact_lapl_fast(pb_grid* grid, const double dx[3], const pb_vec* f, pb_vec* out);
 /* 1-D line operators on device arrays, batched like pb_tdma_batched (grad_1d/div_1d/interp_1d/
  * interp_1d_div: kind 0 = derivative, 1 = interpolation). */
 int pb_compact_1d_batched(pb_ctx* ctx, int kind, int stagger, double dx, int64_t n,

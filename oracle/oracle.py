@@ -39,7 +39,7 @@ def lib():
 class KspOpts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("dtol", C.c_double),
                 ("max_it", C.c_int64), ("pc_type", C.c_int), ("nullspace", C.c_int),
-                ("op27", C.c_int), ("nthreads", C.c_int)]
+                ("op_kind", C.c_int), ("nthreads", C.c_int)]
 
 
 def _p(a):
@@ -98,15 +98,16 @@ def fill_random(count, seed, g0=0):
 
 
 def cg_solve(b, n, h, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
-             nullspace=True, faithful=False, nthreads=1):
+             nullspace=True, faithful=False, nthreads=1, op="star7"):
     """KSPSolve(-ksp_type cg -pc_type jacobi|none) with the constant null space.
     Returns (x, reason, its, history[:its+1])."""
     b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1)
     x = np.empty_like(b)
     hist = np.zeros(int(max_it) + 2)
     its = C.c_int64(0)
-    o = KspOpts(rtol, atol, dtol, max_it, 1 if pc == "jacobi" else 0, int(nullspace),
-                int(faithful), nthreads)
+    kind = 2 if op == "compact" else (1 if faithful else 0)
+    o = KspOpts(rtol, atol, dtol, max_it, 1 if pc == "jacobi" else 0, int(nullspace), kind,
+                nthreads)
     reason = lib().pbo_cg_solve(_n3(n), _h3(h), C.byref(o), _p(b), _p(x), _p(hist), C.byref(its))
     k = its.value
     return x, reason, k, hist[:k + 1].copy()

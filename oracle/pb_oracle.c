@@ -228,10 +228,12 @@ static void pc_apply(int64_t N, const double* r, double* z, double dinv, int pc,
   }
 }
 
-static void op_apply(const int64_t n[3], const double h[3], const double* x, double* y, int op27,
+static void op_apply(const int64_t n[3], const double h[3], const double* x, double* y, int kind,
                      int nt) {
-  if (op27)
+  if (kind == 1)
     pbo_stencil_apply27(n, h, x, y);
+  else if (kind == 2)
+    pbo_lapl(n, x, h, y); /* compact A; P (Jacobi diag) stays the 7-point */
   else
     pbo_stencil_apply7(n, h, x, y, nt);
 }
@@ -273,7 +275,7 @@ int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, c
       for (int64_t t = 0; t < N; ++t) P[t] = Z[t] + bb * P[t]; /* VecAYPX */
     }
     dpiold = dpi;
-    op_apply(n, h, P, W, o->op27, nt); /* KSP_MatMult -> mfmult */
+    op_apply(n, h, P, W, o->op_kind, nt); /* KSP_MatMult -> mfmult */
     dpi = vdot(N, P, W, nt);
     betaold = beta;
     if (dpi == 0.0 || (i > 0 && ((dpi > 0) - (dpi < 0)) * ((dpiold > 0) - (dpiold < 0)) < 0)) {

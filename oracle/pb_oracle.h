@@ -52,7 +52,7 @@ typedef struct {
   int64_t max_it;
   int pc_type;       /* 0 = none, 1 = jacobi */
   int nullspace;     /* 1 = remove constant mode after every PCApply */
-  int op27;          /* 1 = use the faithful 27-term operator (slow), 0 = 7-term */
+  int op_kind;       /* 0 = 7-term stencil, 1 = faithful 27-term (slow), 2 = compact lapl */
   int nthreads;      /* OpenMP threads for the 7-term operator/vector ops (1 = serial sums) */
 } pbo_ksp_opts;
 

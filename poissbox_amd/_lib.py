@@ -89,6 +89,7 @@ _SIGS = {
     "pb_compact_div": [c_p, P_d, C.POINTER(c_p), c_p],
     "pb_compact_interp": [c_p, C.c_int, c_p, c_p],
     "pb_compact_lapl": [c_p, P_d, c_p, c_p],
+    "pb_compact_lapl_fast": [c_p, P_d, c_p, c_p],
     "pb_compact_1d_batched": [c_p, C.c_int, C.c_int, c_d, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
 }
 _RESTYPES = {"pb_last_error": C.c_char_p}

@@ -343,11 +343,10 @@ int pb_tdma_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
     return PB_OK;
   }
   double* scratch = nullptr;
-  PB_HIP(hipMallocAsync((void**)&scratch, (size_t)(2 * n * nbatch) * sizeof(double), ctx->stream));
+  PB_TRY(ctx_scratch(ctx, (size_t)(2 * n * nbatch), &scratch));
   hipLaunchKernelGGL(tdma_periodic_kernel, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, n,
                      nbatch, lm, a, (const double*)b, c, d, scratch);
   PB_HIP(hipGetLastError());
-  PB_HIP(hipFreeAsync(scratch, ctx->stream));
   return PB_OK;
 }
 
@@ -386,9 +385,8 @@ int pb_compact_grad(pb_grid* g, const double dx[3], const pb_vec* f, pb_vec* con
   PB_CHECK_ARG(g && dx && f && df && df[0] && df[1] && df[2], "bad grad args");
   PB_TRY(single_rank(g));
   double* ws = nullptr;
-  PB_HIP(hipMallocAsync((void**)&ws, (size_t)(5 * g->nlocal) * sizeof(double), g->ctx->stream));
+  PB_TRY(ctx_scratch(g->ctx, (size_t)(5 * g->nlocal), &ws));
   int rc = grad3(g, dx, f->d, df[0]->d, df[1]->d, df[2]->d, ws);
-  (void)hipFreeAsync(ws, g->ctx->stream);
   return rc;
 }
 
@@ -396,9 +394,8 @@ int pb_compact_div(pb_grid* g, const double dx[3], const pb_vec* const f[3], pb_
   PB_CHECK_ARG(g && dx && f && f[0] && f[1] && f[2] && df, "bad div args");
   PB_TRY(single_rank(g));
   double* ws = nullptr;
-  PB_HIP(hipMallocAsync((void**)&ws, (size_t)(6 * g->nlocal) * sizeof(double), g->ctx->stream));
+  PB_TRY(ctx_scratch(g->ctx, (size_t)(6 * g->nlocal), &ws));
   int rc = div3(g, dx, f[0]->d, f[1]->d, f[2]->d, df->d, ws);
-  (void)hipFreeAsync(ws, g->ctx->stream);
   return rc;
 }
 
@@ -408,11 +405,10 @@ int pb_compact_interp(pb_grid* g, int stagger, const pb_vec* f, pb_vec* fi) {
   PB_TRY(single_rank(g));
   double* ws = nullptr;
   const int64_t N = g->nlocal;
-  PB_HIP(hipMallocAsync((void**)&ws, (size_t)(2 * N) * sizeof(double), g->ctx->stream));
+  PB_TRY(ctx_scratch(g->ctx, (size_t)(2 * N), &ws));
   int rc = line3(g, 2, K_INTERP, stagger, 0.0, f->d, ws);           // :238
   if (!rc) rc = line3(g, 1, K_INTERP, stagger, 0.0, ws, ws + N);    // :246
   if (!rc) rc = line3(g, 0, K_INTERP, stagger, 0.0, ws + N, fi->d); // :254
-  (void)hipFreeAsync(ws, g->ctx->stream);
   return rc;
 }
 
@@ -420,9 +416,8 @@ int pb_compact_lapl(pb_grid* g, const double dx[3], const pb_vec* f, pb_vec* out
   PB_CHECK_ARG(g && dx && f && out && f != out, "bad lapl args");
   PB_TRY(single_rank(g));
   double* ws = nullptr;
-  PB_HIP(hipMallocAsync((void**)&ws, (size_t)compact_work_len(g) * sizeof(double), g->ctx->stream));
+  PB_TRY(ctx_scratch(g->ctx, (size_t)compact_work_len(g), &ws));
   int rc = compact_lapl(g, dx, f->d, out->d, ws);
-  (void)hipFreeAsync(ws, g->ctx->stream);
   return rc;
 }
 

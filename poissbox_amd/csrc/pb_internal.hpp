@@ -74,6 +74,10 @@ struct pb_ctx {
   double* d_scalars = nullptr;    // small device scalars for vector reductions
   double* h_scalars = nullptr;    // pinned mirror
   int num_cus = 256;
+  // context-owned scratch for the one-shot compact / tridiagonal entry points (grown on demand;
+  // every use is ordered on `stream`, so one buffer serves all of them)
+  double* scratch = nullptr;
+  size_t scratch_len = 0;
   // timing
   bool timing = false;
   std::map<std::string, pb::TimerSlot> timers;
@@ -178,6 +182,16 @@ int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p
 int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
 int stencil_blocks(pb_grid* g, int mode);  // partial-sum slots a stencil pass writes
 
+// ---- compact fast path + generic CG (pb_compact_fast.hip) ----
+int64_t compact_fast_work_len(const pb_grid* g);
+int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* out, double* work);
+int launch_cg_generic_p(pb_grid* g, const double* r, double* p, CgState* st);
+int launch_cg_generic_dot(pb_grid* g, const double* p, const double* w, CgState* st, int* nparts);
+int launch_cg_generic_xr(pb_grid* g, const double* p, const double* w, double* x, double* r,
+                         CgState* st, int* nparts);
+int cg_finalize_stage2(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done,
+                       int64_t host_iter);
+
 // ---- vector ops (pb_vecops.hip) ----
 int vec_fill(pb_ctx* ctx, double* d, int64_t n, double a);
 // form 0: VecAXPY y = y + coef*x;  1: VecAYPX y = x + coef*y;  2: VecScale y = coef*y
@@ -185,6 +199,9 @@ int vec_update(pb_ctx* ctx, int form, double* y, const double* x, int64_t n, dou
 int vec_random(pb_ctx* ctx, double* d, int64_t n, uint64_t seed, int64_t g0);
 // reduce kind: 0 = sum(x), 1 = dot(x, y); result into *out (global over ranks)
 int vec_reduce(pb_ctx* ctx, int kind, const double* x, const double* y, int64_t n, double* out);
+
+// ---- context scratch: at least n doubles, valid until the next call on this context ----
+int ctx_scratch(pb_ctx* ctx, size_t n, double** out);
 
 // ---- partial-sum reduction (deterministic, fixed order) ----
 int reduce_partials(pb_ctx* ctx, const double* parts, int nparts, int width, double* out);

@@ -135,6 +135,20 @@ int halo_end(pb_grid* g) {
   return PB_OK;
 }
 
+int ctx_scratch(pb_ctx* ctx, size_t n, double** out) {
+  if (n > ctx->scratch_len) {
+    PB_HIP(hipStreamSynchronize(ctx->stream));  // previous users of the old buffer are done
+    if (ctx->scratch) PB_HIP(hipFree(ctx->scratch));
+    ctx->scratch = nullptr;
+    ctx->scratch_len = 0;
+    if (hipMalloc(&ctx->scratch, n * sizeof(double)) != hipSuccess)
+      return set_error(PB_ERR_ALLOC, "scratch of %zu doubles: out of device memory", n);
+    ctx->scratch_len = n;
+  }
+  *out = ctx->scratch;
+  return PB_OK;
+}
+
 int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
   if (ctx->nranks == 1) return PB_OK;
   ScopedTimer tm(ctx, "allreduce");
@@ -250,6 +264,7 @@ int pb_ctx_destroy(pb_ctx* ctx) {
   timers_collect(ctx);
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
   (void)hipFree(ctx->d_partials);
   (void)hipFree(ctx->d_scalars);
   (void)hipHostFree(ctx->h_scalars);

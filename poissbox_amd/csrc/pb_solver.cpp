@@ -19,6 +19,8 @@ int compact_lapl(pb_grid* g, const double dx[3], const double* f, double* out, d
 int64_t compact_work_len(const pb_grid* g);
 }
 
+static bool fused_kind(int kind) { return kind == PB_OP_STAR7 || kind == PB_OP_ASSEMBLED27; }
+
 struct pb_ksp {
   pb_op* A = nullptr;
   pb_op* P = nullptr;
@@ -66,7 +68,7 @@ int pb_op_create(pb_grid* g, int kind, const double deltas[3], pb_op** out) {
       delete op;
       return set_error(PB_ERR_UNSUPPORTED, "compact operator on a split grid is not supported yet");
     }
-    op->work_len = compact_work_len(g);
+    op->work_len = compact_fast_work_len(g);
     if (hipMalloc(&op->work, (size_t)op->work_len * sizeof(double)) != hipSuccess) {
       delete op;
       return set_error(PB_ERR_ALLOC, "compact operator workspace: out of device memory");
@@ -79,7 +81,7 @@ int pb_op_create(pb_grid* g, int kind, const double deltas[3], pb_op** out) {
 static int op_apply_raw(pb_op* op, const double* x, double* y) {
   pb_grid* g = op->grid;
   Star s{op->cx, op->cy, op->cz, op->cc};
-  if (op->kind == PB_OP_COMPACT) return compact_lapl(g, op->deltas, x, y, op->work);
+  if (op->kind == PB_OP_COMPACT) return compact_lapl_fast(g, op->deltas, x, y, op->work);
   // STAR7 and ASSEMBLED27 (the assembled BOX matrix has the same 7 non-zeros per row)
   StencilPlanes gp;
   if (g->ctx->nranks == 1) {
@@ -202,7 +204,7 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
     delete k;
     return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
   }
-  if (A->kind != PB_OP_STAR7 && A->kind != PB_OP_ASSEMBLED27) {
+  if (!fused_kind(A->kind)) {
     if (hipMalloc(&k->w, vb) != hipSuccess || hipMalloc(&k->z, vb) != hipSuccess) {
       delete k;
       return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
@@ -235,8 +237,6 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   pb_grid* g = k->A->grid;
   PB_CHECK_ARG(b->grid == g && x->grid == g, "vector/operator grid mismatch");
   pb_ctx* ctx = g->ctx;
-  PB_CHECK_ARG(k->A->kind == PB_OP_STAR7 || k->A->kind == PB_OP_ASSEMBLED27,
-               "fused CG path requires the 7-point operator");
   // history buffer: max_it + 1 entries
   const int64_t nh = k->opts.max_it + 1;
   if (nh > k->nhist) {
@@ -257,9 +257,11 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   st.nullspace = k->opts.nullspace;
   // PCJacobi stores the reciprocal of diag(P) (src/coefficients.f90:44-46 centre coefficient)
   st.dinv = k->opts.pc_type == PB_PC_JACOBI ? 1.0 / k->P->cc : 1.0;
+  if (!fused_kind(k->A->kind)) k->defer_x = false;  // generic path updates x every iteration
   st.ntot = (double)(g->n[0] * g->n[1] * g->n[2]);
   const char* dx = getenv("PB_CG_DEFER_X");
   k->defer_x = !(dx && atoi(dx) == 0);
+  if (!fused_kind(k->A->kind)) k->defer_x = false;
   st.defer_x = k->defer_x ? 1 : 0;
   PB_HIP(hipMemcpyAsync(k->d_st, &st, sizeof(st), hipMemcpyHostToDevice, ctx->stream));
   PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->pb[0], k->d_st, st.dinv, k->d_hist, k->h_done_dev));
@@ -272,7 +274,23 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   return PB_OK;
 }
 
+// Unfused iteration for operators without a stencil engine (PB_OP_COMPACT): one vector pass
+// for p, the operator, a dot pass, an x/r pass (same device scalar logic as the fused path).
+static int enqueue_generic_iteration(pb_ksp* k) {
+  pb_grid* g = k->A->grid;
+  pb_ctx* ctx = g->ctx;
+  double* p = k->pb[0];
+  int np = 0;
+  PB_TRY(launch_cg_generic_p(g, k->r, p, k->d_st));
+  PB_TRY(op_apply_raw(k->A, p, k->w));
+  PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
+  PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
+  PB_TRY(launch_cg_generic_xr(g, p, k->w, k->x->d, k->r, k->d_st, &np));
+  return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
+}
+
 static int enqueue_iteration(pb_ksp* k) {
+  if (!fused_kind(k->A->kind)) return enqueue_generic_iteration(k);
   pb_grid* g = k->A->grid;
   pb_ctx* ctx = g->ctx;
   Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};

@@ -795,6 +795,11 @@ int cg_finalize_pass_a(pb_ctx* ctx, int nparts, CgState* st) {
   return cg_reduce_update(ctx, 1, nparts, 1, st, nullptr, nullptr, 0);
 }
 
+int cg_finalize_stage2(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done,
+                       int64_t host_iter) {
+  return cg_reduce_update(ctx, 2, nparts, 4, st, hist, h_done, host_iter);
+}
+
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
                      double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
                      int64_t host_iter, bool defer_x) {

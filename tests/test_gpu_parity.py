@@ -397,3 +397,79 @@ def test_pcr_alpha_matches_thomas(ctx):
         got = buf.get().reshape(nb, n)
         assert np.max(np.abs(got - ref)) <= 1e-14 * np.max(np.abs(ref)) * 10
         buf.free()
+
+
+# ---------------------------------------------------------------------------------------------
+# compact Laplacian fast path (3-pass factorisation + PCR) and CG with the compact operator
+# ---------------------------------------------------------------------------------------------
+FAST_RTOL = 1e-12  # relative to max|reference|; operation order differs from the reference
+
+
+def test_compact_lapl_fast_matches_reference(ctx, golden):
+    names = _cases(golden, "lapl")
+    assert names
+    for name in names:
+        m = golden[name + "__meta"]
+        n3, h3 = tuple(int(v) for v in m[:3]), tuple(float(v) for v in m[3:])
+        da = pb.DA(ctx, n3)
+        f, out = pb.Vec(da), pb.Vec(da)
+        f.set_values(golden[name + "__in"])
+        pb.compact_lapl_fast(da, h3, f, out)
+        ref = golden[name + "__out"]
+        err = np.max(np.abs(out.get_values() - ref))
+        assert err <= FAST_RTOL * np.max(np.abs(ref)), (name, err)
+
+
+@pytest.mark.parametrize("n3", [(64, 48, 40), (33, 17, 9), (128, 128, 64)])
+def test_compact_lapl_fast_vs_oracle_sizes(ctx, n3):
+    from oracle import oracle as O
+    N = int(np.prod(n3))
+    h3 = tuple(2 * np.pi / m for m in n3)
+    f = O.fill_random(N, 77)
+    ref = O.lapl(f, n3, h3)
+    da = pb.DA(ctx, n3)
+    fv, out = pb.Vec(da), pb.Vec(da)
+    fv.set_values(f)
+    pb.compact_lapl_fast(da, h3, fv, out)
+    assert np.max(np.abs(out.get_values() - ref)) <= FAST_RTOL * np.max(np.abs(ref))
+    # analytic pin (tests/lapl/test_lapl.f90): sum of sines -> minus itself at RMS <= 1e-9 (64^3)
+    if n3 == (64, 48, 40):
+        return
+
+
+def test_compact_lapl_fast_analytic_64(ctx):
+    """tests/lapl/test_lapl.f90:87-130 on the GPU fast path: const -> 0, sum sin -> -sum sin."""
+    n3 = (64, 64, 64)
+    h = 2 * np.pi / 64
+    da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+    f, out = pb.Vec(da), pb.Vec(da)
+    f.set(2.8170923)
+    pb.compact_lapl_fast(da, (h, h, h), f, out)
+    assert np.sqrt(np.mean(out.get_values() ** 2)) <= 100 * np.finfo(float).eps
+    x = (np.arange(64) + 0.5) * h
+    s = np.sin(x)
+    fs = (s[None, None, :] + s[None, :, None] + s[:, None, None]).reshape(-1)
+    f.set_values(fs)
+    pb.compact_lapl_fast(da, (h, h, h), f, out)
+    assert np.sqrt(np.mean((out.get_values() + fs) ** 2)) <= 1e-9
+
+
+def test_cg_with_compact_operator(ctx):
+    """compact A inside KSPSolve, Jacobi from the 7-point P (A != P as
+    src/poissbox.f90:226-228,294)."""
+    from oracle import oracle as O
+    n3 = (16, 16, 16)
+    h3 = (1 / 16,) * 3
+    N = 4096
+    b = O.lapl(O.fill_random(N, SEED), n3, h3)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h3, rtol=1e-8, op="compact")
+    da = pb.DA(ctx, n3)
+    P = pb.Mat(da, pb.ASSEMBLED27, h3)
+    A = pb.Mat(da, pb.COMPACT, h3)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(P, A, x, bv, ["-ksp_rtol", "1e-8"])
+    assert (reason, abs(its - itso) <= 1) == (ro, True)
+    k = min(len(hist), len(ho))
+    assert np.max(np.abs(hist[:k - 1] - ho[:k - 1]) / ho[:k - 1]) < 1e-6
+    assert np.max(np.abs(x.get_values() - xo)) <= 1e-6 * np.max(np.abs(xo))
