@@ -335,6 +335,8 @@ int pb_tdma_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
   PB_CHECK_ARG(n >= 2 && nbatch >= 1, "bad tdma sizes");
   LineMap lm{nbatch, line_stride, 0, elem_stride};
   const int64_t blocks = (nbatch + 63) / 64;
+  double* scratch = nullptr;
+  if (periodic) PB_TRY(ctx_scratch(ctx, (size_t)(2 * n * nbatch), &scratch));
   ScopedTimer tm(ctx, "tdma");
   if (!periodic) {
     hipLaunchKernelGGL(tdma_kernel, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, n, nbatch, lm,
@@ -342,8 +344,6 @@ int pb_tdma_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
     PB_HIP(hipGetLastError());
     return PB_OK;
   }
-  double* scratch = nullptr;
-  PB_TRY(ctx_scratch(ctx, (size_t)(2 * n * nbatch), &scratch));
   hipLaunchKernelGGL(tdma_periodic_kernel, dim3((unsigned)blocks), dim3(64), 0, ctx->stream, n,
                      nbatch, lm, a, (const double*)b, c, d, scratch);
   PB_HIP(hipGetLastError());
@@ -371,6 +371,9 @@ int pb_compact_1d_batched(pb_ctx* ctx, int kind, int stagger, double dx, int64_t
   PB_CHECK_ARG(stagger == -1 || stagger == 1, "stagger must be -1 or +1");
   PB_CHECK_ARG(n >= 3 && nbatch >= 1, "compact_1d: n >= 3");
   LineMap lm{nbatch, line_stride, 0, elem_stride};
+  AlphaFactor fac;
+  PB_TRY(alpha_factor(ctx, n, scheme(kind == 0 ? K_GRAD : K_INTERP, dx).alpha, &fac));  // warm cache
+  ScopedTimer tm(ctx, "compact_1d");
   return launch_line(ctx, kind == 0 ? K_GRAD : K_INTERP, stagger, dx, n, nbatch, lm, f, nullptr,
                      nullptr, out);
 }
