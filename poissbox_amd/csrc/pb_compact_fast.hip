@@ -233,7 +233,11 @@ int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* o
   double *u = work, *v = work + N, *s = work + 2 * N, *t = work + 3 * N;
   for (int d = 0; d < 3; ++d)
     if (g->n[d] > kTile) return set_error(PB_ERR_UNSUPPORTED, "compact fast path: n > %d", kTile);
-  {  // Z: lines along k; tile = consecutive i for fixed j
+  static const bool lines_ok = env_int("PB_COMPACT_LINES", 1) != 0;
+  auto reg = [&](int64_t n) { return lines_ok && compact_lines_supported(n); };
+  if (reg(nz)) {
+    PB_TRY(compact_lines_pass(g, 2, dx[2], f, nullptr, u, v));
+  } else {  // Z: lines along k; tile = consecutive i for fixed j
     FastPass p{};
     p.n = (int)nz;
     p.layout = 0;
@@ -253,7 +257,9 @@ int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* o
     p.nout = 2;
     PB_TRY(launch_pass(g->ctx, p));
   }
-  {  // Y: lines along j; tile = consecutive i for fixed k
+  if (reg(ny)) {
+    PB_TRY(compact_lines_pass(g, 1, dx[1], u, v, s, t));
+  } else {  // Y: lines along j; tile = consecutive i for fixed k
     FastPass p{};
     p.n = (int)ny;
     p.layout = 0;
@@ -275,7 +281,9 @@ int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* o
     p.nout = 2;
     PB_TRY(launch_pass(g->ctx, p));
   }
-  {  // X: lines along i (contiguous); tile = consecutive j for fixed k
+  if (reg(nx)) {
+    PB_TRY(compact_lines_pass(g, 0, dx[0], s, t, out, nullptr));
+  } else {  // X: lines along i (contiguous); tile = consecutive j for fixed k
     FastPass p{};
     p.n = (int)nx;
     p.layout = 1;

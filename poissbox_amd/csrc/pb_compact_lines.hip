@@ -1,0 +1,575 @@
+// pb_compact_lines.hip -- register-resident line solves for the 3-pass compact Laplacian.
+//
+// Same factorisation as pb_compact_fast.hip (lapl = Lx Jy Jz + Jx Ly Jz + Jx Jy Lz, SURVEY.md
+// Appendix D; reference src/compact_schemes.f90:17-37), but each 1-D line of n = 64*C points is
+// owned by ONE wave with C consecutive points per lane, so both the explicit RHS and the periodic
+// (alpha, 1, alpha) solve run in registers:
+//
+//   (alpha,1,alpha) = kappa (1 + q S^-1)(1 + q S),  q = 2 alpha / (1 + sqrt(1 - 4 alpha^2)),
+//                                                   kappa = alpha / q
+// so the solve is a causal first-order recursion y_i = d_i - q y_{i-1} followed by the
+// anti-causal z_i = y_i - q z_{i+1}, each periodic. A lane runs its chunk with zero initial state,
+// then the chunk-end values are combined across lanes by a cyclic Kogge-Stone scan with
+// multiplier G = (-q)^C (truncated once G^(2^s) < 1e-24, or the exact periodic factor
+// 1/(1 - G^64) when the scan covers the whole line), and each point is corrected by
+// (-q)^(m+1) * carry. Nothing touches LDS except the tile transpose that gives coalesced HBM
+// rows for the strided (Y, Z) passes. HBM traffic is the 80 B/DoF of the factorisation.
+//
+// Line sets: Z pass (lines along k, tile = TL consecutive i at fixed j), Y pass (along j, tile =
+// TL consecutive i at fixed k), X pass (along i, tile = TL consecutive contiguous lines).
+// The results match the reference to rounding (operation order differs from Thomas + Sherman-
+// Morrison in src/tridsol.f90:34-74); the bit-exact reference-order path stays in pb_compact.hip.
+#include <cmath>
+
+#include "pb_internal.hpp"
+
+#pragma clang fp contract(fast)
+
+namespace pb {
+
+
+struct LineOp {
+  double a, b, sign;  // explicit 4-point RHS (src/compact_schemes.f90:332-372)
+  double mq;          // -q
+  double inv_kappa;
+  double corr;        // 1 / (1 - G^64) if the scan wraps the whole line, else 1
+  double gs[6];       // G^(2^s)
+  double pw[16];      // (-q)^(m+1)
+  int nsteps;
+};
+
+struct LinePass {
+  const double* in0;
+  const double* in1;
+  double* out0;
+  double* out1;
+  int64_t li, lo, es;  // address of (outer, inner line, element e) = outer*lo + inner*li + e*es
+  int ninner, ntiles_inner, nouter, TL, P;
+  int ablate;  // tuning only (PB_LINES_ABLATE=1): copy lines through, no solves
+  LineOp J, L;
+};
+
+static LineOp make_line_op(int kind, int C, double h) {
+  LineOp o{};
+  double alpha;
+  if (kind == 0) {  // J: interp (:303-305)
+    o.a = 0.75;
+    o.b = 1.0 / 20.0;
+    o.sign = 1.0;
+    alpha = 3.0 / 10.0;
+  } else {  // L: grad / div (:188-190)
+    o.a = 63.0 / 62.0 / h;
+    o.b = 17.0 / 62.0 / (3.0 * h);
+    o.sign = -1.0;
+    alpha = 9.0 / 62.0;
+  }
+  const double q = 2.0 * alpha / (1.0 + std::sqrt(1.0 - 4.0 * alpha * alpha));
+  o.mq = -q;
+  o.inv_kappa = q / alpha;
+  double p = 1.0;
+  for (int m = 0; m < C; ++m) {
+    p *= -q;
+    o.pw[m] = p;
+  }
+  const double G = p;  // (-q)^C
+  double g = G;
+  int s = 0;
+  for (; s < 6; ++s) {
+    if (std::fabs(g) < 1e-24) break;
+    o.gs[s] = g;
+    g = g * g;
+  }
+  o.nsteps = s;
+  o.corr = s == 6 ? 1.0 / (1.0 - g) : 1.0;  // g = G^64 here
+  return o;
+}
+
+__device__ __forceinline__ double lane_shfl(double v, int src) { return __shfl(v, src & 63, 64); }
+
+// d <- explicit RHS of x (stagger -1: cell -> vertex, +1: vertex -> cell), eval_1d_rhs order
+template <int C>
+__device__ __forceinline__ void line_rhs(const double (&x)[C], double (&d)[C], const LineOp& o,
+                                         int stagger, int lane) {
+  double xm2, xm1, xp0, xp1;  // x at local offsets -2, -1, C, C+1
+  xm1 = lane_shfl(x[C - 1], lane - 1);
+  xp0 = lane_shfl(x[0], lane + 1);
+  if constexpr (C >= 2) {
+    if (stagger < 0) {
+      xm2 = lane_shfl(x[C - 2], lane - 1);
+      xp1 = 0.0;
+    } else {
+      xp1 = lane_shfl(x[1], lane + 1);
+      xm2 = 0.0;
+    }
+  } else {
+    if (stagger < 0) {
+      xm2 = lane_shfl(x[0], lane - 2);
+      xp1 = 0.0;
+    } else {
+      xp1 = lane_shfl(x[0], lane + 2);
+      xm2 = 0.0;
+    }
+  }
+  auto at = [&](int o2) -> double {  // o2 is a compile-time constant after unrolling
+    if (o2 == -2) return xm2;
+    if (o2 == -1) return xm1;
+    if (o2 == C) return xp0;
+    if (o2 == C + 1) return xp1;
+    return x[o2];
+  };
+  const double a = o.a, b = o.b, s = o.sign;
+#pragma unroll
+  for (int m = 0; m < C; ++m) {
+    if (stagger < 0)
+      d[m] = a * (at(m) + s * at(m - 1)) + b * (at(m + 1) + s * at(m - 2));
+    else
+      d[m] = a * (at(m + 1) + s * at(m)) + b * (at(m + 2) + s * at(m - 1));
+  }
+}
+
+// d <- (alpha, 1, alpha)^-1 d on the periodic line (64 lanes x C points)
+template <int C>
+__device__ __forceinline__ void line_solve(double (&d)[C], const LineOp& o, int lane) {
+  const double mq = o.mq;
+  // causal sweep y_i = d_i - q y_{i-1}
+#pragma unroll
+  for (int m = 1; m < C; ++m) d[m] = d[m] + mq * d[m - 1];
+  double T = d[C - 1];
+  for (int s = 0; s < o.nsteps; ++s) T = T + o.gs[s] * lane_shfl(T, lane - (1 << s));
+  T *= o.corr;
+  double cin = lane_shfl(T, lane - 1);
+#pragma unroll
+  for (int m = 0; m < C; ++m) d[m] = d[m] + o.pw[m] * cin;
+  // anti-causal sweep z_i = y_i - q z_{i+1}
+#pragma unroll
+  for (int m = C - 2; m >= 0; --m) d[m] = d[m] + mq * d[m + 1];
+  T = d[0];
+  for (int s = 0; s < o.nsteps; ++s) T = T + o.gs[s] * lane_shfl(T, lane + (1 << s));
+  T *= o.corr;
+  cin = lane_shfl(T, lane + 1);
+#pragma unroll
+  for (int m = 0; m < C; ++m) d[m] = (d[m] + o.pw[C - 1 - m] * cin) * o.inv_kappa;
+}
+
+// r <- (I+ I-) x  (J or L: cell -> vertex half, then vertex -> cell half)
+template <int C>
+__device__ __forceinline__ void line_op(const double (&x)[C], double (&r)[C], const LineOp& o,
+                                        int lane, int ablate) {
+  if (ablate) {
+#pragma unroll
+    for (int m = 0; m < C; ++m) r[m] = x[m];
+    return;
+  }
+  double t[C];
+  line_rhs<C>(x, t, o, -1, lane);
+  line_solve<C>(t, o, lane);
+  line_rhs<C>(t, r, o, +1, lane);
+  line_solve<C>(r, o, lane);
+}
+
+// LDS word of (line l, element e): lanes own C consecutive points; chunk pitch odd -> no conflicts
+template <int C>
+struct Lds {
+  static constexpr int CP = (C % 2 == 0) ? C + 1 : C;
+  static constexpr int LP = 64 * CP + 4;  // line pitch (doubles)
+  __device__ static __forceinline__ int word(int l, int e) { return l * LP + (e / C) * CP + (e % C); }
+};
+
+// global <-> LDS tile copies, fully unrolled so every load of the tile is in flight at once.
+// LAYOUT 0: lines run across rows (li == 1, coalesced along l); LAYOUT 1: lines contiguous
+// (es == 1, li == n). V = 2 moves 16-byte pairs along the contiguous direction (needs an even
+// row length); the pair (l, l+1) of LAYOUT 0 sits in two different LDS lines.
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
+template <int C, int LAYOUT, int TL, int V>
+__device__ __forceinline__ void tile_coord(int f, int& l, int& e) {
+  constexpr int n = 64 * C;
+  if (LAYOUT == 0) {
+    l = (f % (TL / V)) * V;
+    e = f / (TL / V);
+  } else {
+    l = (f * V) / n;
+    e = (f * V) % n;
+  }
+}
+
+template <int C, int LAYOUT, int TL, int V, int NT>
+struct TileRegs {
+  static constexpr int NF = TL * 64 * C / V;  // pairs (or singles) in the tile
+  static constexpr int R = (NF + NT - 1) / NT;
+  double v[R][V];
+};
+
+// issue every global load of the tile (no wait: the registers are consumed by tile_put later)
+template <int C, int LAYOUT, int TL, int V, int NT>
+__device__ __forceinline__ void tile_fetch(const LinePass& p, const double* __restrict__ src,
+                                           int64_t base, int nl, TileRegs<C, LAYOUT, TL, V, NT>& t) {
+  using T = TileRegs<C, LAYOUT, TL, V, NT>;
+#pragma unroll
+  for (int r = 0; r < T::R; ++r) {
+    int l, e;
+    const int f = threadIdx.x + NT * r;
+    tile_coord<C, LAYOUT, TL, V>(f, l, e);
+    const double* a = src + base + l * p.li + e * p.es;
+    if ((T::NF % NT == 0 || f < T::NF) && l < nl) {
+      if (V == 2) {
+        const dv2 w = __builtin_nontemporal_load((const dv2*)a);
+        t.v[r][0] = w.x;
+        t.v[r][V - 1] = w.y;
+      } else {
+        t.v[r][0] = __builtin_nontemporal_load(a);
+      }
+    }
+  }
+}
+
+template <int C, int LAYOUT, int TL, int V, int NT>
+__device__ __forceinline__ void tile_put(double* lds, int nl, const TileRegs<C, LAYOUT, TL, V, NT>& t) {
+  using T = TileRegs<C, LAYOUT, TL, V, NT>;
+  constexpr int dl = LAYOUT == 0 ? 1 : 0, de = LAYOUT == 0 ? 0 : 1;  // step of the pair partner
+#pragma unroll
+  for (int r = 0; r < T::R; ++r) {
+    int l, e;
+    const int f = threadIdx.x + NT * r;
+    tile_coord<C, LAYOUT, TL, V>(f, l, e);
+    if ((T::NF % NT == 0 || f < T::NF) && l < nl) {
+      lds[Lds<C>::word(l, e)] = t.v[r][0];
+      if (V == 2) lds[Lds<C>::word(l + dl, e + de)] = t.v[r][V - 1];
+    }
+  }
+}
+
+template <int C, int LAYOUT, int TL, int V, int NT>
+__device__ __forceinline__ void tile_store(const LinePass& p, double* __restrict__ dst,
+                                           const double* lds, int64_t base, int nl) {
+  constexpr int NF = TL * 64 * C / V;
+  constexpr int R = (NF + NT - 1) / NT;
+  constexpr int dl = LAYOUT == 0 ? 1 : 0, de = LAYOUT == 0 ? 0 : 1;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    int l, e;
+    const int f = threadIdx.x + NT * r;
+    tile_coord<C, LAYOUT, TL, V>(f, l, e);
+    if ((NF % NT == 0 || f < NF) && l < nl) {
+      double* a = dst + base + l * p.li + e * p.es;
+      if (V == 2) {
+        dv2 w;
+        w.x = lds[Lds<C>::word(l, e)];
+        w.y = lds[Lds<C>::word(l + dl, e + de)];
+        __builtin_nontemporal_store(w, (dv2*)a);
+      } else {
+        __builtin_nontemporal_store(lds[Lds<C>::word(l, e)], a);
+      }
+    }
+  }
+}
+
+template <int C>
+__device__ __forceinline__ void chunk_read(const double* lds, int l, int lane, double (&x)[C]) {
+  const int w0 = l * Lds<C>::LP + lane * Lds<C>::CP;
+#pragma unroll
+  for (int m = 0; m < C; ++m) x[m] = lds[w0 + m];
+}
+template <int C>
+__device__ __forceinline__ void chunk_write(double* lds, int l, int lane, const double (&x)[C]) {
+  const int w0 = l * Lds<C>::LP + lane * Lds<C>::CP;
+#pragma unroll
+  for (int m = 0; m < C; ++m) lds[w0 + m] = x[m];
+}
+
+// PASS 0 (Z): out0 = J in0, out1 = L in0.   PASS 1 (Y): out0 = J in0, out1 = L in0 + J in1.
+// PASS 2 (X): out0 = L in0 + J in1.
+// K = launch shape: TL lines per tile, NW waves per block (NW divides TL), PF = 1 for persistent
+// blocks that fetch the next input tile into registers while the current one is solved and
+// stored (HBM reads overlap the line solves and the write-back), PF = 0 for one tile per block.
+template <int TL_, int NW_, int PF_>
+struct LineCfg {
+  static constexpr int TL = TL_, NW = NW_, PF = PF_, NT = 64 * NW_, LPW = TL_ / NW_;
+};
+
+template <int C, int LAYOUT, int PASS, class K, int V>
+__global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  constexpr int TL = K::TL, LPW = K::LPW, NT = K::NT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ntiles = p.ntiles_inner * p.nouter;
+  auto tile_of = [&](int t, int64_t& base, int& nl) {
+    const int outer = t / p.ntiles_inner;
+    const int inner0 = (t % p.ntiles_inner) * TL;
+    nl = min(TL, p.ninner - inner0);
+    base = (int64_t)outer * p.lo + (int64_t)inner0 * p.li;
+  };
+  TileRegs<C, LAYOUT, TL, V, NT> pre;
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  int64_t base;
+  int nl;
+  tile_of(t, base, nl);
+  if (K::PF) tile_fetch(p, p.in0, base, nl, pre);
+  double keep[LPW][C];
+  for (; t < ntiles; t += gridDim.x) {
+    tile_of(t, base, nl);
+    const int tn = t + gridDim.x;
+    int64_t base_n = 0;
+    int nl_n = 0;
+    if (K::PF && tn < ntiles) tile_of(tn, base_n, nl_n);
+    __syncthreads();  // previous tile's LDS reads are done
+    if (!K::PF) tile_fetch(p, p.in0, base, nl, pre);
+    tile_put(lds, nl, pre);
+    __syncthreads();
+    if (K::PF) {
+      if (PASS == 0) {
+        if (tn < ntiles) tile_fetch(p, p.in0, base_n, nl_n, pre);
+      } else {
+        tile_fetch(p, p.in1, base, nl, pre);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      const int l = wave * LPW + j;
+      if (l >= nl) continue;
+      double x[C], r[C];
+      chunk_read<C>(lds, l, lane, x);
+      if (PASS != 2) {
+        line_op<C>(x, r, p.J, lane, p.ablate);
+        chunk_write<C>(lds, l, lane, r);
+      }
+      line_op<C>(x, keep[j], p.L, lane, p.ablate);
+    }
+    __syncthreads();
+    if (PASS == 0) {
+      tile_store<C, LAYOUT, TL, V, NT>(p, p.out0, lds, base, nl);
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < LPW; ++j) {
+        const int l = wave * LPW + j;
+        if (l < nl) chunk_write<C>(lds, l, lane, keep[j]);
+      }
+      __syncthreads();
+      tile_store<C, LAYOUT, TL, V, NT>(p, p.out1, lds, base, nl);
+      continue;
+    }
+    if (PASS == 1) {
+      tile_store<C, LAYOUT, TL, V, NT>(p, p.out0, lds, base, nl);
+      __syncthreads();
+    }
+    if (!K::PF) tile_fetch(p, p.in1, base, nl, pre);
+    tile_put(lds, nl, pre);
+    __syncthreads();
+    if (K::PF && tn < ntiles) tile_fetch(p, p.in0, base_n, nl_n, pre);
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      const int l = wave * LPW + j;
+      if (l >= nl) continue;
+      double x[C], r[C];
+      chunk_read<C>(lds, l, lane, x);
+      line_op<C>(x, r, p.J, lane, p.ablate);
+#pragma unroll
+      for (int m = 0; m < C; ++m) r[m] = keep[j][m] + r[m];
+      chunk_write<C>(lds, l, lane, r);
+    }
+    __syncthreads();
+    tile_store<C, LAYOUT, TL, V, NT>(p, PASS == 1 ? p.out1 : p.out0, lds, base, nl);
+  }
+}
+
+// X pass without block barriers: the lines are contiguous, so each wave owns whole lines and
+// re-distributes them through a wave-private LDS strip (coalesced 16-byte loads -> C consecutive
+// points per lane -> coalesced stores). One wave per line: out = L in0 + J in1.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void compact_lines_x_direct(LinePass p, int64_t nlines) {
+  constexpr int LP = Lds<C>::LP, CP = Lds<C>::CP;
+  __shared__ double strip[4][2 * LP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t line = (int64_t)blockIdx.x * 4 + wave;
+  if (line >= nlines) return;
+  double* sl = strip[wave];
+  const int64_t off = line * (64 * C);
+  constexpr int NP = 32 * C;  // 16-byte pieces per line
+  constexpr int R = (NP + 63) / 64;
+  dv2 a[R], b[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = lane + 64 * r;
+    if (NP % 64 == 0 || q < NP) {
+      a[r] = __builtin_nontemporal_load((const dv2*)(p.in0 + off) + q);
+      b[r] = __builtin_nontemporal_load((const dv2*)(p.in1 + off) + q);
+    }
+  }
+  auto w = [&](int e) { return (e / C) * CP + (e % C); };
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = lane + 64 * r;
+    if (NP % 64 == 0 || q < NP) {
+      sl[w(2 * q)] = a[r].x;
+      sl[w(2 * q + 1)] = a[r].y;
+      sl[LP + w(2 * q)] = b[r].x;
+      sl[LP + w(2 * q + 1)] = b[r].y;
+    }
+  }
+  wave_sync();
+  double x[C], y[C], r1[C], r2[C];
+#pragma unroll
+  for (int m = 0; m < C; ++m) {
+    x[m] = sl[lane * CP + m];
+    y[m] = sl[LP + lane * CP + m];
+  }
+  line_op<C>(x, r1, p.L, lane, p.ablate);
+  line_op<C>(y, r2, p.J, lane, p.ablate);
+  wave_sync();
+#pragma unroll
+  for (int m = 0; m < C; ++m) sl[lane * CP + m] = r1[m] + r2[m];
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = lane + 64 * r;
+    if (NP % 64 == 0 || q < NP) {
+      dv2 o;
+      o.x = sl[w(2 * q)];
+      o.y = sl[w(2 * q + 1)];
+      __builtin_nontemporal_store(o, (dv2*)(p.out0 + off) + q);
+    }
+  }
+}
+
+template <int C>
+static int launch_x_direct(pb_ctx* ctx, LinePass& p, int64_t nlines) {
+  hipLaunchKernelGGL(compact_lines_x_direct<C>, dim3((unsigned)((nlines + 3) / 4)), dim3(256), 0,
+                     ctx->stream, p, nlines);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+bool compact_lines_supported(int64_t n) {
+  if (n % 64) return false;
+  const int64_t C = n / 64;
+  return C == 1 || C == 2 || C == 3 || C == 4 || C == 6 || C == 8 || C == 12 || C == 16;
+}
+
+template <int C, int LAYOUT, int PASS, class K, int V>
+static int launch_lines_v(pb_ctx* ctx, LinePass& p, int64_t nouter) {
+  p.TL = K::TL;
+  p.P = Lds<C>::LP;
+  p.ntiles_inner = (p.ninner + K::TL - 1) / K::TL;
+  p.nouter = (int)nouter;
+  const int64_t ntiles = (int64_t)p.ntiles_inner * nouter;
+  const size_t lds = (size_t)K::TL * Lds<C>::LP * sizeof(double);
+  auto kern = compact_lines_kernel<C, LAYOUT, PASS, K, V>;
+  static int occ = 0;
+  if (!occ) {
+    PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    PB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, K::NT, lds));
+    if (occ < 1) occ = 1;
+  }
+  int64_t nblocks = K::PF ? (int64_t)occ * ctx->num_cus : ntiles;
+  if (nblocks > ntiles) nblocks = ntiles;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(K::NT), lds, ctx->stream, p);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+// 16-byte pairs when the contiguous direction has even length (always for LAYOUT 1, n = 64*C)
+template <int C, int LAYOUT, int PASS, class K>
+static int launch_lines_k(pb_ctx* ctx, LinePass& p, int64_t nouter) {
+  if (LAYOUT == 1 || (p.ninner % 2 == 0 && p.li == 1 && p.lo % 2 == 0 && p.es % 2 == 0))
+    return launch_lines_v<C, LAYOUT, PASS, K, 2>(ctx, p, nouter);
+  return launch_lines_v<C, LAYOUT, PASS, K, 1>(ctx, p, nouter);
+}
+
+// Launch shapes (measured at 512^3, profiles/r01/tune_compact.jsonl): strided passes use 16-line
+// tiles (128-B row segments, two blocks per CU), the contiguous X pass 8-line tiles. C > 8 keeps
+// 8-line tiles for LDS. PB_LINES_CFG = 1..6 selects an alternative shape (tuning, C = 4 and 8).
+template <int C, int LAYOUT, int PASS>
+static int launch_lines_c(pb_ctx* ctx, LinePass& p, int64_t nouter) {
+  static const int cfg = env_int("PB_LINES_CFG", 0);
+  if constexpr (C == 4 || C == 8) {
+    switch (cfg) {
+      case 1: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 1>>(ctx, p, nouter);
+      case 2: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 8, 1>>(ctx, p, nouter);
+      case 3: return launch_lines_k<C, LAYOUT, PASS, LineCfg<8, 8, 1>>(ctx, p, nouter);
+      case 4: return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 0>>(ctx, p, nouter);
+      case 5: return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 1>>(ctx, p, nouter);
+      case 6: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 0>>(ctx, p, nouter);
+      default: break;
+    }
+  }
+  if constexpr (LAYOUT == 0 && C <= 8)
+    return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 1>>(ctx, p, nouter);
+  else
+    return launch_lines_k<C, LAYOUT, PASS, LineCfg<8, 8, 0>>(ctx, p, nouter);
+}
+
+template <int LAYOUT, int PASS>
+static int launch_lines(pb_ctx* ctx, LinePass& p, int64_t n, int64_t nouter) {
+  switch (n / 64) {
+    case 1: return launch_lines_c<1, LAYOUT, PASS>(ctx, p, nouter);
+    case 2: return launch_lines_c<2, LAYOUT, PASS>(ctx, p, nouter);
+    case 3: return launch_lines_c<3, LAYOUT, PASS>(ctx, p, nouter);
+    case 4: return launch_lines_c<4, LAYOUT, PASS>(ctx, p, nouter);
+    case 6: return launch_lines_c<6, LAYOUT, PASS>(ctx, p, nouter);
+    case 8: return launch_lines_c<8, LAYOUT, PASS>(ctx, p, nouter);
+    case 12: return launch_lines_c<12, LAYOUT, PASS>(ctx, p, nouter);
+    case 16: return launch_lines_c<16, LAYOUT, PASS>(ctx, p, nouter);
+  }
+  return set_error(PB_ERR_UNSUPPORTED, "compact line solver: n = %lld", (long long)n);
+}
+
+// One pass of the factorised Laplacian with register line solves. axis: 2 = Z, 1 = Y, 0 = X.
+int compact_lines_pass(pb_grid* g, int axis, double h, const double* in0, const double* in1,
+                       double* out0, double* out1) {
+  const int64_t nx = g->n[0], ny = g->n[1], nz = g->nzl;
+  const int64_t n = axis == 2 ? nz : (axis == 1 ? ny : nx);
+  const int C = (int)(n / 64);
+  static const char* names[3] = {"compact_lines_x", "compact_lines_y", "compact_lines_z"};
+  ScopedTimer tm(g->ctx, names[axis]);
+  LinePass p{};
+  static const int ablate = env_int("PB_LINES_ABLATE", 0);
+  p.ablate = ablate;
+  p.in0 = in0;
+  p.in1 = in1;
+  p.out0 = out0;
+  p.out1 = out1;
+  p.J = make_line_op(0, C, h);
+  p.L = make_line_op(1, C, h);
+  if (axis == 2) {
+    p.li = 1;
+    p.lo = nx;
+    p.es = nx * ny;
+    p.ninner = (int)nx;
+    return launch_lines<0, 0>(g->ctx, p, n, ny);
+  }
+  if (axis == 1) {
+    p.li = 1;
+    p.lo = nx * ny;
+    p.es = nx;
+    p.ninner = (int)nx;
+    return launch_lines<0, 1>(g->ctx, p, n, nz);
+  }
+  p.li = nx;
+  p.lo = nx * ny;
+  p.es = 1;
+  p.ninner = (int)ny;
+  static const int xdirect = env_int("PB_LINES_XDIRECT", 1);
+  if (xdirect) {
+    switch (C) {
+      case 1: return launch_x_direct<1>(g->ctx, p, ny * nz);
+      case 2: return launch_x_direct<2>(g->ctx, p, ny * nz);
+      case 3: return launch_x_direct<3>(g->ctx, p, ny * nz);
+      case 4: return launch_x_direct<4>(g->ctx, p, ny * nz);
+      case 6: return launch_x_direct<6>(g->ctx, p, ny * nz);
+      case 8: return launch_x_direct<8>(g->ctx, p, ny * nz);
+      case 12: return launch_x_direct<12>(g->ctx, p, ny * nz);
+      case 16: return launch_x_direct<16>(g->ctx, p, ny * nz);
+    }
+  }
+  return launch_lines<1, 2>(g->ctx, p, n, nz);
+}
+
+}  // namespace pb

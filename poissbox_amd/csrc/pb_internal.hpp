@@ -185,6 +185,16 @@ int stencil_blocks(pb_grid* g, int mode);  // partial-sum slots a stencil pass w
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----
 int64_t compact_fast_work_len(const pb_grid* g);
 int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* out, double* work);
+// integer tuning knob from the environment (PB_*), dflt when unset
+inline int env_int(const char* name, int dflt) {
+  const char* s = getenv(name);
+  return s ? atoi(s) : dflt;
+}
+
+// ---- register-resident line solves (pb_compact_lines.hip) ----
+bool compact_lines_supported(int64_t n);
+int compact_lines_pass(pb_grid* g, int axis, double h, const double* in0, const double* in1,
+                       double* out0, double* out1);
 int launch_cg_generic_p(pb_grid* g, const double* r, double* p, CgState* st);
 int launch_cg_generic_dot(pb_grid* g, const double* p, const double* w, CgState* st, int* nparts);
 int launch_cg_generic_xr(pb_grid* g, const double* p, const double* w, double* x, double* r,

@@ -430,11 +430,6 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 // ---------------------------------------------------------------------------------------------
 // Launch configuration
 // ---------------------------------------------------------------------------------------------
-static int env_int(const char* name, int dflt) {
-  const char* s = getenv(name);
-  return s ? atoi(s) : dflt;
-}
-
 // Plane sets: PLANES_ALL = [0, nzl); PLANES_INTERIOR = [1, nzl-1) (no ghost plane is read);
 // PLANES_BOUNDARY = {0, nzl-1} (the two planes that read ghosts) -- the split lets the halo
 // exchange of a multi-rank step overlap the interior.

@@ -420,7 +420,8 @@ def test_compact_lapl_fast_matches_reference(ctx, golden):
         assert err <= FAST_RTOL * np.max(np.abs(ref)), (name, err)
 
 
-@pytest.mark.parametrize("n3", [(64, 48, 40), (33, 17, 9), (128, 128, 64)])
+@pytest.mark.parametrize("n3", [(64, 48, 40), (33, 17, 9), (128, 128, 64), (256, 192, 64),
+                                (1024, 64, 64), (64, 768, 64), (128, 64, 384)])
 def test_compact_lapl_fast_vs_oracle_sizes(ctx, n3):
     from oracle import oracle as O
     N = int(np.prod(n3))
