@@ -211,6 +211,9 @@ def main():
                 if key in tr and "cg_pass_b_odd" in tr[key]:
                     out["roofline"]["traffic"] = tr[key]["cg_pass_b_odd"]["bytes_per_launch"]
                     out["roofline"]["traffic_source"] = tr[key]["cg_pass_b_odd"].get("source")
+                for role, kv in out["kernels"].items():
+                    if role in tr.get(key, {}):
+                        kv["traffic"] = tr[key][role]["bytes_per_launch"]
             except Exception:
                 pass
         if world == 1 and not args.no_cpu_baseline:

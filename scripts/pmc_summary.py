@@ -1,0 +1,67 @@
+"""Summarise rocprofv3 --pmc CSVs (one counter group per run) into per-kernel means, and write
+profiles/pmc_traffic.json: corrected HBM bytes per launch for the bench kernels.
+
+Correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE/WRITE_SIZE are KiB; on gfx950
+FETCH_SIZE counts exactly half the bytes of wide (16 B/lane) coalesced streaming reads, so
+traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 bytes per launch.
+
+usage: python scripts/pmc_summary.py <gpurun_out dir> <profiles out dir> <grid key, e.g. 512x512x512>
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+# bench.py kernel roles -> kernel-name pattern (template arguments of pb::star7_kernel)
+ROLES = {
+    "matvec_star7": r"star7_kernel<.*PlainLoad, pb::StoreY>",
+    "cg_pass_a": r"star7_kernel<.*CombineLoad, pb::PassA",
+    "cg_pass_b_even": r"star7_kernel<.*PassB<0>",
+    "cg_pass_b_odd": r"star7_kernel<.*PassB<1>",
+}
+
+
+def load(path):
+    acc = defaultdict(lambda: defaultdict(list))
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            name = re.sub(r"\(.*$", "", row["Kernel_Name"])
+            acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return acc
+
+
+def main():
+    src, dst, key = sys.argv[1], sys.argv[2], sys.argv[3]
+    os.makedirs(dst, exist_ok=True)
+    means = defaultdict(dict)
+    for f in glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
+        acc = load(f)
+        tag = os.path.relpath(f, src).split(os.sep)[0]
+        summ = {}
+        for k, ctr in acc.items():
+            for c, vals in ctr.items():
+                summ[f"{k} | {c}"] = {"launches": len(vals), "mean": sum(vals) / len(vals)}
+                means[k][c] = sum(vals) / len(vals)
+        json.dump(summ, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1)
+    traffic = {}
+    for role, pat in ROLES.items():
+        for k, ctr in means.items():
+            if re.search(pat, k) and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
+                rd = 2 * ctr["FETCH_SIZE"] * 1024
+                wr = ctr["WRITE_SIZE"] * 1024
+                traffic[role] = {"bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
+                                 "kernel": k,
+                                 "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                                           "2x FETCH_SIZE (gfx950 half-count), KiB->B"}
+    out = os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json")
+    allt = json.load(open(out)) if os.path.exists(out) else {}
+    allt[key] = traffic
+    json.dump(allt, open(out, "w"), indent=1)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()
