@@ -139,6 +139,9 @@ typedef struct {
   int monitor;       /* -ksp_monitor: print ||z_k|| per iteration after the solve (rank 0) */
   int converged_reason; /* -ksp_converged_reason */
   int check_every;   /* host polls the device convergence flag every N iterations (default 8) */
+  int mg_levels;     /* -pc_mg_levels: multigrid levels (0 = as many as the grid allows)      */
+  int mg_coarse_its; /* -pc_mg_coarse_its: symmetric red-black sweeps on the coarsest level (8) */
+  double sor_omega;  /* -pc_sor_omega: SOR relaxation factor (1.0 = Gauss-Seidel)              */
 } pb_ksp_opts;
 typedef struct {
   int reason;
@@ -148,7 +151,11 @@ typedef struct {
 } pb_ksp_result;
 int pb_ksp_opts_default(pb_ksp_opts* opts);
 /* Parses PETSc-style options (-ksp_type, -pc_type, -ksp_rtol, -ksp_atol, -ksp_divtol,
- * -ksp_max_it, -ksp_monitor, -ksp_converged_reason); unknown options are ignored. */
+ * -ksp_max_it, -ksp_monitor, -ksp_converged_reason, -pc_mg_levels, -pc_mg_coarse_its,
+ * -pc_sor_omega); unknown options are ignored.
+ * -pc_type sor: one symmetric red-black SOR sweep (PETSc PCSOR default: 1 local symmetric sweep,
+ * here in red-black order). -pc_type mg (or gamg): geometric V(1,1) multigrid with red-black SOR
+ * smoothing on the 7-point P (README.md:40-45 recommends GAMG + SOR). Both need even extents. */
 int pb_ksp_opts_parse(pb_ksp_opts* opts, int argc, const char* const* argv);
 
 /* KSPCreate + KSPSetOperators(ksp, A, P) + options. P supplies the Jacobi diagonal. */
@@ -163,6 +170,11 @@ int pb_ksp_begin(pb_ksp* ksp, const pb_vec* b, pb_vec* x);
 int pb_ksp_iterate(pb_ksp* ksp, int64_t iters);
 int pb_ksp_end(pb_ksp* ksp, pb_ksp_result* res, double* history, int64_t history_cap);
 int pb_ksp_destroy(pb_ksp* ksp);
+/* PCApply(KSPGetPC(ksp), r, z): z = M^-1 r of the configured preconditioner (Jacobi: D^-1 r;
+ * SOR / MG: from a zero initial guess), without the null-space removal KSP adds. */
+int pb_ksp_pc_apply(pb_ksp* ksp, const pb_vec* r, pb_vec* z);
+/* number of multigrid levels in use (1 for SOR, 0 for Jacobi / none) */
+int pb_ksp_pc_levels(const pb_ksp* ksp, int* levels);
 /* One-shot convenience: ≙ solve(P, A, x, b). */
 int pb_solve(pb_op* A, pb_op* P, const pb_ksp_opts* opts, const pb_vec* b, pb_vec* x,
              pb_ksp_result* res, double* history, int64_t history_cap);

@@ -39,7 +39,10 @@ def lib():
 class KspOpts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("dtol", C.c_double),
                 ("max_it", C.c_int64), ("pc_type", C.c_int), ("nullspace", C.c_int),
-                ("op_kind", C.c_int), ("nthreads", C.c_int)]
+                ("op_kind", C.c_int), ("nthreads", C.c_int), ("mg_levels", C.c_int),
+                ("mg_coarse_its", C.c_int), ("omega", C.c_double), ("nranks", C.c_int)]
+
+PC_CODES = {"none": 0, "jacobi": 1, "sor": 2, "mg": 3}
 
 
 def _p(a):
@@ -98,19 +101,33 @@ def fill_random(count, seed, g0=0):
 
 
 def cg_solve(b, n, h, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
-             nullspace=True, faithful=False, nthreads=1, op="star7"):
-    """KSPSolve(-ksp_type cg -pc_type jacobi|none) with the constant null space.
+             nullspace=True, faithful=False, nthreads=1, op="star7", mg_levels=0,
+             mg_coarse_its=8, omega=1.0, nranks=1):
+    """KSPSolve(-ksp_type cg -pc_type jacobi|none|sor|mg) with the constant null space.
     Returns (x, reason, its, history[:its+1])."""
     b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1)
     x = np.empty_like(b)
     hist = np.zeros(int(max_it) + 2)
     its = C.c_int64(0)
     kind = 2 if op == "compact" else (1 if faithful else 0)
-    o = KspOpts(rtol, atol, dtol, max_it, 1 if pc == "jacobi" else 0, int(nullspace), kind,
-                nthreads)
+    o = KspOpts(rtol, atol, dtol, max_it, PC_CODES[pc], int(nullspace), kind, nthreads,
+                mg_levels, mg_coarse_its, omega, nranks)
     reason = lib().pbo_cg_solve(_n3(n), _h3(h), C.byref(o), _p(b), _p(x), _p(hist), C.byref(its))
     k = its.value
     return x, reason, k, hist[:k + 1].copy()
+
+
+def mg_plan_levels(n, nranks=1, levels=0):
+    return lib().pbo_mg_plan_levels(_n3(n), C.c_int(nranks), C.c_int(levels))
+
+
+def mg_apply(r, n, h, pc="mg", levels=0, coarse_its=8, omega=1.0, nranks=1):
+    """z = M^-1 r for the red-black SOR / geometric MG preconditioner (pb_mg.hip restatement)."""
+    r = np.ascontiguousarray(r, dtype=np.float64).reshape(-1)
+    z = np.empty_like(r)
+    lib().pbo_mg_apply(_n3(n), _h3(h), C.c_int(PC_CODES[pc]), C.c_int(levels),
+                       C.c_int(coarse_its), C.c_double(omega), C.c_int(nranks), _p(r), _p(z))
+    return z
 
 
 def cg_fixed(b, n, h, iters, nthreads=1):

@@ -215,6 +215,189 @@ static double vsum(int64_t N, const double* a, int nt) {
   return s;
 }
 
+/* ---------------------------------------------------------------------------------------------
+ * Red-black SOR / geometric V(1,1) multigrid preconditioner -- restatement of the GPU design in
+ * poissbox_amd/csrc/pb_mg.hip with the same arithmetic order (tests compare bit for bit).
+ * Periodic cell-centred grid, 7-point operator per level with h_l = 2^l h (lapl_star_coeffs),
+ * trilinear prolongation, restriction = P^T / 8, red = (i + j + k) even.
+ * ------------------------------------------------------------------------------------------- */
+static void slab_part(int64_t n, int nranks, int r, int64_t* k0, int64_t* nz) {
+  const int64_t q = n / nranks, m = n % nranks; /* README.md:30-32: remainder on low ranks */
+  *nz = q + (r < m ? 1 : 0);
+  *k0 = r * q + (r < m ? r : m);
+}
+
+int pbo_mg_plan_levels(const int64_t n[3], int nranks, int levels_req) {
+  int64_t cur[3] = {n[0], n[1], n[2]};
+  int64_t* k0 = (int64_t*)malloc(sizeof(int64_t) * nranks);
+  int64_t* nz = (int64_t*)malloc(sizeof(int64_t) * nranks);
+  for (int r = 0; r < nranks; ++r) slab_part(n[2], nranks, r, &k0[r], &nz[r]);
+  int L = 1;
+  const int cap = levels_req > 0 ? levels_req : 64;
+  while (L < cap) {
+    int ok = cur[0] % 4 == 0 && cur[1] % 4 == 0 && cur[2] % 4 == 0;
+    if (levels_req <= 0) {
+      int64_t mn = cur[0] < cur[1] ? cur[0] : cur[1];
+      mn = mn < cur[2] ? mn : cur[2];
+      ok = ok && mn > 4;
+    }
+    for (int r = 0; r < nranks; ++r) ok = ok && k0[r] % 2 == 0 && nz[r] % 2 == 0;
+    if (!ok) break;
+    for (int d = 0; d < 3; ++d) cur[d] /= 2;
+    for (int r = 0; r < nranks; ++r) {
+      k0[r] /= 2;
+      nz[r] /= 2;
+    }
+    ++L;
+  }
+  free(k0);
+  free(nz);
+  return L;
+}
+
+typedef struct {
+  int64_t n[3];
+  double cx, cy, cz, cc;
+  double *x, *b, *res;
+} mg_level;
+
+static int64_t wrap64(int64_t v, int64_t n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
+
+static void mg_smooth(const mg_level* L, int color, int zero_init, double omega) {
+  const int64_t nx = L->n[0], ny = L->n[1], nz = L->n[2];
+  for (int64_t k = 0; k < nz; ++k)
+    for (int64_t j = 0; j < ny; ++j)
+      for (int64_t i = 0; i < nx; ++i) {
+        const int64_t id = i + nx * (j + ny * k);
+        if (((i + j + k) & 1) != color) {
+          if (zero_init) L->x[id] = 0.0;
+          continue;
+        }
+        double nb = 0.0, xo = 0.0;
+        if (!zero_init) {
+          const double* x = L->x;
+          nb = L->cz * x[i + nx * (j + ny * wrap64(k - 1, nz))];
+          nb = nb + L->cy * x[i + nx * (wrap64(j - 1, ny) + ny * k)];
+          nb = nb + L->cx * x[wrap64(i - 1, nx) + nx * (j + ny * k)];
+          nb = nb + L->cx * x[wrap64(i + 1, nx) + nx * (j + ny * k)];
+          nb = nb + L->cy * x[i + nx * (wrap64(j + 1, ny) + ny * k)];
+          nb = nb + L->cz * x[i + nx * (j + ny * wrap64(k + 1, nz))];
+          xo = x[id];
+        }
+        const double t = (L->b[id] - nb) / L->cc;
+        L->x[id] = (1.0 - omega) * xo + omega * t;
+      }
+}
+
+static void mg_residual(const mg_level* L) {
+  const int64_t nx = L->n[0], ny = L->n[1], nz = L->n[2];
+  const double* x = L->x;
+  for (int64_t k = 0; k < nz; ++k)
+    for (int64_t j = 0; j < ny; ++j)
+      for (int64_t i = 0; i < nx; ++i) {
+        const int64_t id = i + nx * (j + ny * k);
+        double ax = L->cz * x[i + nx * (j + ny * wrap64(k - 1, nz))];
+        ax = ax + L->cy * x[i + nx * (wrap64(j - 1, ny) + ny * k)];
+        ax = ax + L->cx * x[wrap64(i - 1, nx) + nx * (j + ny * k)];
+        ax = ax + L->cc * x[id];
+        ax = ax + L->cx * x[wrap64(i + 1, nx) + nx * (j + ny * k)];
+        ax = ax + L->cy * x[i + nx * (wrap64(j + 1, ny) + ny * k)];
+        ax = ax + L->cz * x[i + nx * (j + ny * wrap64(k + 1, nz))];
+        L->res[id] = L->b[id] - ax;
+      }
+}
+
+static void mg_restrict(const mg_level* F, const mg_level* Cl) {
+  static const double w[4] = {0.125, 0.375, 0.375, 0.125};
+  const int64_t fx = F->n[0], fy = F->n[1], fz = F->n[2];
+  for (int64_t K = 0; K < Cl->n[2]; ++K)
+    for (int64_t J = 0; J < Cl->n[1]; ++J)
+      for (int64_t I = 0; I < Cl->n[0]; ++I) {
+        double sz = 0.0;
+        for (int c = 0; c < 4; ++c) {
+          const int64_t kf = wrap64(2 * K - 1 + c, fz);
+          double sy = 0.0;
+          for (int bb = 0; bb < 4; ++bb) {
+            const int64_t jf = wrap64(2 * J - 1 + bb, fy);
+            double sx = 0.0;
+            for (int a = 0; a < 4; ++a)
+              sx = sx + w[a] * F->res[wrap64(2 * I - 1 + a, fx) + fx * (jf + fy * kf)];
+            sy = sy + w[bb] * sx;
+          }
+          sz = sz + w[c] * sy;
+        }
+        Cl->b[I + Cl->n[0] * (J + Cl->n[1] * K)] = sz;
+      }
+}
+
+static void mg_prolong(const mg_level* F, const mg_level* Cl) {
+  const int64_t cx = Cl->n[0], cy = Cl->n[1], cz = Cl->n[2];
+  const double* c = Cl->x;
+  for (int64_t k = 0; k < F->n[2]; ++k)
+    for (int64_t j = 0; j < F->n[1]; ++j)
+      for (int64_t i = 0; i < F->n[0]; ++i) {
+        const int64_t I = i >> 1, J = j >> 1, K = k >> 1;
+        const int64_t fI = wrap64((i & 1) ? I + 1 : I - 1, cx);
+        const int64_t fJ = wrap64((j & 1) ? J + 1 : J - 1, cy);
+        const int64_t fK = wrap64((k & 1) ? K + 1 : K - 1, cz);
+#define C3(a, b, d) c[(a) + cx * ((b) + cy * (d))]
+        const double vn = 0.75 * (0.75 * C3(I, J, K) + 0.25 * C3(fI, J, K)) +
+                          0.25 * (0.75 * C3(I, fJ, K) + 0.25 * C3(fI, fJ, K));
+        const double vf = 0.75 * (0.75 * C3(I, J, fK) + 0.25 * C3(fI, J, fK)) +
+                          0.25 * (0.75 * C3(I, fJ, fK) + 0.25 * C3(fI, fJ, fK));
+#undef C3
+        const int64_t id = i + F->n[0] * (j + F->n[1] * k);
+        F->x[id] = F->x[id] + (0.75 * vn + 0.25 * vf);
+      }
+}
+
+void pbo_mg_apply(const int64_t n[3], const double h[3], int pc_type, int levels, int coarse_its,
+                  double omega, int nranks, const double* r, double* z) {
+  const int L = pc_type == 3 ? pbo_mg_plan_levels(n, nranks, levels) : 1;
+  const int cits = pc_type == 3 ? (coarse_its > 1 ? coarse_its : 1) : 1;
+  mg_level* lv = (mg_level*)calloc((size_t)L, sizeof(mg_level));
+  for (int l = 0; l < L; ++l) {
+    double hl[3], c27[27];
+    for (int d = 0; d < 3; ++d) {
+      lv[l].n[d] = n[d] >> l;
+      hl[d] = h[d] * (double)(1 << l);
+    }
+    pbo_lapl_star_coeffs(hl[0], hl[1], hl[2], c27);
+    lv[l].cx = c27[12];
+    lv[l].cy = c27[10];
+    lv[l].cz = c27[4];
+    lv[l].cc = c27[13];
+    const int64_t m = lv[l].n[0] * lv[l].n[1] * lv[l].n[2];
+    lv[l].x = l ? (double*)malloc(sizeof(double) * m) : z;
+    lv[l].b = l ? (double*)malloc(sizeof(double) * m) : (double*)r;
+    lv[l].res = (double*)malloc(sizeof(double) * m);
+  }
+  for (int l = 0; l < L - 1; ++l) {
+    mg_smooth(&lv[l], 0, 1, omega);
+    mg_smooth(&lv[l], 1, 0, omega);
+    mg_residual(&lv[l]);
+    mg_restrict(&lv[l], &lv[l + 1]);
+  }
+  mg_smooth(&lv[L - 1], 0, 1, omega);
+  for (int it = 0; it < cits; ++it) {
+    mg_smooth(&lv[L - 1], 1, 0, omega);
+    mg_smooth(&lv[L - 1], 0, 0, omega);
+  }
+  for (int l = L - 2; l >= 0; --l) {
+    mg_prolong(&lv[l], &lv[l + 1]);
+    mg_smooth(&lv[l], 1, 0, omega);
+    mg_smooth(&lv[l], 0, 0, omega);
+  }
+  for (int l = 0; l < L; ++l) {
+    if (l) {
+      free(lv[l].x);
+      free(lv[l].b);
+    }
+    free(lv[l].res);
+  }
+  free(lv);
+}
+
 /* KSP_PCApply = PCApply_Jacobi (z = diag^-1 .* r, PETSc stores the reciprocal) followed by
  * KSP_RemoveNullSpace -> MatNullSpaceRemove(has_cnst): z += VecSum(z) / (-N). */
 static void pc_apply(int64_t N, const double* r, double* z, double dinv, int pc, int nsp, int nt) {
@@ -238,6 +421,23 @@ static void op_apply(const int64_t n[3], const double h[3], const double* x, dou
     pbo_stencil_apply7(n, h, x, y, nt);
 }
 
+/* PCApply for every pc_type: Jacobi / none as above; SOR (2) and MG (3) through pbo_mg_apply,
+ * followed by the same null-space removal */
+static void pc_apply_any(const int64_t n[3], const double h[3], const pbo_ksp_opts* o,
+                         const double* r, double* z, double dinv, int nt) {
+  const int64_t N = n[0] * n[1] * n[2];
+  if (o->pc_type == 2 || o->pc_type == 3) {
+    pbo_mg_apply(n, h, o->pc_type, o->mg_levels, o->mg_coarse_its, o->omega,
+                 o->nranks > 0 ? o->nranks : 1, r, z);
+    if (o->nullspace) {
+      double shift = vsum(N, z, nt) / (-1.0 * (double)N);
+      for (int64_t t = 0; t < N; ++t) z[t] += shift;
+    }
+    return;
+  }
+  pc_apply(N, r, z, dinv, o->pc_type, o->nullspace, nt);
+}
+
 int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, const double* b,
                  double* x, double* history, int64_t* its_out) {
   const int64_t N = n[0] * n[1] * n[2];
@@ -253,7 +453,7 @@ int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, c
 
   memset(x, 0, sizeof(double) * N); /* KSPSolve: guess_zero => X = 0 */
   memcpy(R, b, sizeof(double) * N); /* r = b */
-  pc_apply(N, R, Z, dinv, o->pc_type, o->nullspace, nt);
+  pc_apply_any(n, h, o, R, Z, dinv, nt);
   dp = sqrt(vdot(N, Z, Z, nt)); /* KSP_NORM_PRECONDITIONED */
   history[0] = dp;
   /* KSPConvergedDefault at n = 0 */
@@ -288,7 +488,7 @@ int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, c
       x[t] = x[t] + a * P[t];
       R[t] = R[t] + (-a) * W[t];
     }
-    pc_apply(N, R, Z, dinv, o->pc_type, o->nullspace, nt);
+    pc_apply_any(n, h, o, R, Z, dinv, nt);
     dp = sqrt(vdot(N, Z, Z, nt));
     history[i + 1] = dp;
     if (dp != dp || isinf(dp)) { reason = KSP_DIVERGED_NANORINF; break; }

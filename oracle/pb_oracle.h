@@ -54,7 +54,19 @@ typedef struct {
   int nullspace;     /* 1 = remove constant mode after every PCApply */
   int op_kind;       /* 0 = 7-term stencil, 1 = faithful 27-term (slow), 2 = compact lapl */
   int nthreads;      /* OpenMP threads for the 7-term operator/vector ops (1 = serial sums) */
+  int mg_levels;     /* pc 3: multigrid levels (0 = automatic), pc 2 = one symmetric RB-SOR sweep */
+  int mg_coarse_its; /* symmetric red-black sweeps on the coarsest level */
+  double omega;      /* SOR relaxation */
+  int nranks;        /* slab count the GPU run uses (only changes the automatic level count) */
 } pbo_ksp_opts;
+
+/* ---- red-black SOR / geometric multigrid preconditioner (our GPU design, poissbox_amd/csrc/
+ * pb_mg.hip; the reference's README.md:40-45 recommends PETSc GAMG + SOR, which is absent:
+ * parity for this PC is against this restatement, unpinned against PETSc) ---- */
+int pbo_mg_plan_levels(const int64_t n[3], int nranks, int levels_req);
+/* z = M^-1 r from a zero initial guess; pc_type 2 (SOR) or 3 (MG) */
+void pbo_mg_apply(const int64_t n[3], const double h[3], int pc_type, int levels, int coarse_its,
+                  double omega, int nranks, const double* r, double* z);
 
 /* Returns PETSc KSPConvergedReason; history[0..its] = ||z_k||_2 (len max_it+1). */
 int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* opts, const double* b,

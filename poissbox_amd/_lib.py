@@ -26,7 +26,8 @@ class PbError(RuntimeError):
 class KspOpts(C.Structure):
     _fields_ = [("rtol", c_d), ("atol", c_d), ("dtol", c_d), ("max_it", c_i64),
                 ("ksp_type", C.c_int), ("pc_type", C.c_int), ("nullspace", C.c_int),
-                ("monitor", C.c_int), ("converged_reason", C.c_int), ("check_every", C.c_int)]
+                ("monitor", C.c_int), ("converged_reason", C.c_int), ("check_every", C.c_int),
+                ("mg_levels", C.c_int), ("mg_coarse_its", C.c_int), ("sor_omega", c_d)]
 
 
 class KspResult(C.Structure):
@@ -82,6 +83,8 @@ _SIGS = {
     "pb_ksp_iterate": [c_p, c_i64],
     "pb_ksp_end": [c_p, C.POINTER(KspResult), P_d, c_i64],
     "pb_ksp_destroy": [c_p],
+    "pb_ksp_pc_apply": [c_p, c_p, c_p],
+    "pb_ksp_pc_levels": [c_p, C.POINTER(C.c_int)],
     "pb_solve": [c_p, c_p, C.POINTER(KspOpts), c_p, c_p, C.POINTER(KspResult), P_d, c_i64],
     "pb_tdma_batched": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, C.c_int],
     "pb_pcr_alpha_batched": [c_p, c_i64, c_i64, c_i64, c_i64, c_d, c_p],

@@ -279,6 +279,16 @@ class KSP:
         self.result = res
         return res.reason, res.its, hist[: res.its + 1].copy()
 
+    def pc_apply(self, r, z):
+        """PCApply: z = M^-1 r (no null-space removal)."""
+        L.call("pb_ksp_pc_apply", self.h, r.h, z.h)
+
+    @property
+    def pc_levels(self):
+        v = C.c_int(0)
+        L.call("pb_ksp_pc_levels", self.h, C.byref(v))
+        return v.value
+
     def destroy(self):
         if self.h:
             L.call("pb_ksp_destroy", self.h)

@@ -210,6 +210,27 @@ int vec_random(pb_ctx* ctx, double* d, int64_t n, uint64_t seed, int64_t g0);
 // reduce kind: 0 = sum(x), 1 = dot(x, y); result into *out (global over ranks)
 int vec_reduce(pb_ctx* ctx, int kind, const double* x, const double* y, int64_t n, double* out);
 
+// ---- grid with an explicit slab (multigrid levels) ----
+int grid_create_part(pb_ctx* ctx, const int64_t n[3], const double L[3], int64_t k0, int64_t nzl,
+                     pb_grid** out);
+
+// ---- preconditioned CG pieces (pb_cg_generic.hip) ----
+int launch_cg_pc_xr(pb_grid* g, const double* p, const double* w, double* x, double* r,
+                    CgState* st);
+int launch_cg_pc_sums(pb_grid* g, const double* z, const double* r, CgState* st, int* nparts);
+int cg_finalize_init(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done);
+
+// ---- geometric multigrid / red-black SOR preconditioner (pb_mg.hip) ----
+struct Mg;
+// levels_req: 0 = automatic; pc_type PB_PC_SOR (one symmetric red-black sweep) or PB_PC_MG
+int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, int coarse_its,
+              double omega, Mg** out);
+int mg_apply(Mg* mg, const double* r, double* z);  // z = M^-1 r (zero initial guess)
+int mg_levels(const Mg* mg);
+void mg_destroy(Mg* mg);
+// deterministic level count for a global grid split over nranks z-slabs (every rank agrees)
+int mg_plan_levels(const int64_t n[3], int nranks, int levels_req);
+
 // ---- context scratch: at least n doubles, valid until the next call on this context ----
 int ctx_scratch(pb_ctx* ctx, size_t n, double** out);
 

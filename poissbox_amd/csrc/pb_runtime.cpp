@@ -171,6 +171,38 @@ int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
 
 using namespace pb;
 
+namespace pb {
+// grid with an explicit slab [k0, k0 + nzl) (multigrid levels: the fine partition halved)
+int grid_create_part(pb_ctx* ctx, const int64_t n[3], const double L[3], int64_t k0, int64_t nzl,
+                     pb_grid** out) {
+  PB_HIP(hipSetDevice(ctx->device));
+  pb_grid* g = new pb_grid();
+  g->ctx = ctx;
+  for (int d = 0; d < 3; ++d) {
+    g->n[d] = n[d];
+    g->L[d] = L ? L[d] : 1.0;
+    g->h[d] = g->L[d] / (double)n[d];  // src/example.f90:33-35
+  }
+  g->k0 = k0;
+  g->nzl = nzl;
+  g->plane = n[0] * n[1];
+  g->nlocal = g->plane * g->nzl;
+  const size_t pb = (size_t)g->plane * sizeof(double);
+  double* ghosts = nullptr;
+  if (hipMalloc(&ghosts, 4 * pb) != hipSuccess) {
+    delete g;
+    return set_error(PB_ERR_ALLOC, "ghost planes: out of device memory");
+  }
+  g->ghost_lo = ghosts;
+  g->ghost_hi = ghosts + g->plane;
+  g->bnd_lo = ghosts + 2 * g->plane;
+  g->bnd_hi = ghosts + 3 * g->plane;
+  if (ctx->h_sendrecv) PB_HIP(hipHostMalloc(&g->h_stage, 4 * pb, hipHostMallocDefault));
+  *out = g;
+  return PB_OK;
+}
+}  // namespace pb
+
 extern "C" {
 
 const char* pb_last_error(void) { return g_err; }
@@ -319,30 +351,9 @@ int pb_grid_create(pb_ctx* ctx, const int64_t n[3], const double L[3], pb_grid**
   PB_CHECK_ARG(n[2] >= ctx->nranks, "fewer z-planes than ranks");
   PB_CHECK_ARG(ctx->nranks == 1 || ctx->comm || ctx->h_sendrecv,
                "multi-rank context has neither RCCL nor a host transport");
-  PB_HIP(hipSetDevice(ctx->device));
-  pb_grid* g = new pb_grid();
-  g->ctx = ctx;
-  for (int d = 0; d < 3; ++d) {
-    g->n[d] = n[d];
-    g->L[d] = L ? L[d] : 1.0;
-    g->h[d] = g->L[d] / (double)n[d];  // src/example.f90:33-35
-  }
-  PB_TRY(pb_slab_partition(n[2], ctx->nranks, ctx->rank, &g->k0, &g->nzl));
-  g->plane = n[0] * n[1];
-  g->nlocal = g->plane * g->nzl;
-  const size_t pb = (size_t)g->plane * sizeof(double);
-  double* ghosts = nullptr;
-  if (hipMalloc(&ghosts, 4 * pb) != hipSuccess) {
-    delete g;
-    return set_error(PB_ERR_ALLOC, "ghost planes: out of device memory");
-  }
-  g->ghost_lo = ghosts;
-  g->ghost_hi = ghosts + g->plane;
-  g->bnd_lo = ghosts + 2 * g->plane;
-  g->bnd_hi = ghosts + 3 * g->plane;
-  if (ctx->h_sendrecv) PB_HIP(hipHostMalloc(&g->h_stage, 4 * pb, hipHostMallocDefault));
-  *out = g;
-  return PB_OK;
+  int64_t k0 = 0, nzl = 0;
+  PB_TRY(pb_slab_partition(n[2], ctx->nranks, ctx->rank, &k0, &nzl));
+  return pb::grid_create_part(ctx, n, L, k0, nzl, out);
 }
 
 int pb_grid_get_corners(const pb_grid* g, int64_t start[3], int64_t size[3]) {

@@ -29,6 +29,7 @@ struct pb_ksp {
   double* pb[2] = {nullptr, nullptr};  // iteration i: p_old = pb[i%2], p_new = pb[(i+1)%2]
   double* w = nullptr;   // generic (unfused) path only
   double* z = nullptr;   // generic path only
+  pb::Mg* mg = nullptr;  // SOR / multigrid preconditioner (PB_PC_SOR, PB_PC_MG)
   CgState* d_st = nullptr;
   double* d_hist = nullptr;
   int64_t nhist = 0;
@@ -140,6 +141,9 @@ int pb_ksp_opts_default(pb_ksp_opts* o) {
   o->monitor = 0;
   o->converged_reason = 0;
   o->check_every = 8;
+  o->mg_levels = 0;
+  o->mg_coarse_its = 8;
+  o->sor_omega = 1.0;
   return PB_OK;
 }
 
@@ -171,6 +175,15 @@ int pb_ksp_opts_parse(pb_ksp_opts* o, int argc, const char* const* argv) {
     } else if (!strcmp(a, "-ksp_max_it") && v) {
       o->max_it = atoll(v);
       ++i;
+    } else if (!strcmp(a, "-pc_mg_levels") && v) {
+      o->mg_levels = atoi(v);
+      ++i;
+    } else if ((!strcmp(a, "-pc_mg_coarse_its") || !strcmp(a, "-mg_coarse_ksp_max_it")) && v) {
+      o->mg_coarse_its = atoi(v);
+      ++i;
+    } else if (!strcmp(a, "-pc_sor_omega") && v) {
+      o->sor_omega = atof(v);
+      ++i;
     } else if (!strcmp(a, "-ksp_monitor")) {
       o->monitor = 1;
     } else if (!strcmp(a, "-ksp_converged_reason")) {
@@ -193,19 +206,34 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   if (opts) k->opts = *opts;
   else pb_ksp_opts_default(&k->opts);
   if (k->opts.check_every < 1) k->opts.check_every = 8;
-  if (k->opts.pc_type != PB_PC_NONE && k->opts.pc_type != PB_PC_JACOBI) {
+  const int pc = k->opts.pc_type;
+  if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG) {
     delete k;
-    return set_error(PB_ERR_UNSUPPORTED, "pc_type %d not available in this build", opts->pc_type);
+    return set_error(PB_ERR_UNSUPPORTED, "unknown pc_type %d", pc);
   }
   pb_grid* g = A->grid;
   const size_t vb = (size_t)g->nlocal * sizeof(double);
+  if (pc == PB_PC_SOR || pc == PB_PC_MG) {
+    // the smoother / coarse operators are the 7-point P (src/coefficients.f90 star)
+    if (P->kind == PB_OP_COMPACT) {
+      delete k;
+      return set_error(PB_ERR_UNSUPPORTED, "SOR / MG preconditioning needs a 7-point P");
+    }
+    const int rc = mg_create(g, P->deltas, pc, k->opts.mg_levels, k->opts.mg_coarse_its,
+                             k->opts.sor_omega, &k->mg);
+    if (rc != PB_OK) {
+      delete k;
+      return rc;
+    }
+  }
   if (hipMalloc(&k->r, vb) != hipSuccess || hipMalloc(&k->pb[0], vb) != hipSuccess ||
       hipMalloc(&k->pb[1], vb) != hipSuccess) {
     delete k;
     return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
   }
-  if (!fused_kind(A->kind)) {
+  if (!fused_kind(A->kind) || k->mg) {
     if (hipMalloc(&k->w, vb) != hipSuccess || hipMalloc(&k->z, vb) != hipSuccess) {
+      if (k->mg) mg_destroy(k->mg);
       delete k;
       return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
     }
@@ -255,16 +283,29 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   st.nhist = k->nhist;
   st.pc = k->opts.pc_type;
   st.nullspace = k->opts.nullspace;
-  // PCJacobi stores the reciprocal of diag(P) (src/coefficients.f90:44-46 centre coefficient)
+  // PCJacobi stores the reciprocal of diag(P) (src/coefficients.f90:44-46 centre coefficient);
+  // with SOR / MG the sums are taken over z = M^-1 r itself (dinv = 1)
   st.dinv = k->opts.pc_type == PB_PC_JACOBI ? 1.0 / k->P->cc : 1.0;
-  if (!fused_kind(k->A->kind)) k->defer_x = false;  // generic path updates x every iteration
   st.ntot = (double)(g->n[0] * g->n[1] * g->n[2]);
   const char* dx = getenv("PB_CG_DEFER_X");
   k->defer_x = !(dx && atoi(dx) == 0);
-  if (!fused_kind(k->A->kind)) k->defer_x = false;
+  if (!fused_kind(k->A->kind) || k->mg) k->defer_x = false;  // generic path: x every iteration
   st.defer_x = k->defer_x ? 1 : 0;
   PB_HIP(hipMemcpyAsync(k->d_st, &st, sizeof(st), hipMemcpyHostToDevice, ctx->stream));
-  PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->pb[0], k->d_st, st.dinv, k->d_hist, k->h_done_dev));
+  if (k->mg) {
+    // r = b, x = 0, p = 0; z = M^-1 r; sums of z (KSPSolve_CG setup, PC_LEFT)
+    const size_t vb = (size_t)g->nlocal * sizeof(double);
+    PB_HIP(hipMemcpyAsync(k->r, b->d, vb, hipMemcpyDeviceToDevice, ctx->stream));
+    PB_HIP(hipMemsetAsync(x->d, 0, vb, ctx->stream));
+    PB_HIP(hipMemsetAsync(k->pb[0], 0, vb, ctx->stream));
+    PB_TRY(mg_apply(k->mg, k->r, k->z));
+    int np = 0;
+    PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
+    PB_TRY(cg_finalize_init(ctx, np, k->d_st, k->d_hist, k->h_done_dev));
+  } else {
+    PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->pb[0], k->d_st, st.dinv, k->d_hist,
+                          k->h_done_dev));
+  }
   PB_HIP(hipStreamSynchronize(ctx->stream));
   k->b = b;
   k->x = x;
@@ -289,7 +330,25 @@ static int enqueue_generic_iteration(pb_ksp* k) {
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
 }
 
+// Preconditioned iteration (SOR / MG): p = (z - mu) + b/b0 p, w = A p, p.w, x/r update,
+// z = M^-1 r, sums of z -- PETSc KSPSolve_CG order with PC_LEFT and the null-space shift.
+static int enqueue_pc_iteration(pb_ksp* k) {
+  pb_grid* g = k->A->grid;
+  pb_ctx* ctx = g->ctx;
+  double* p = k->pb[0];
+  int np = 0;
+  PB_TRY(launch_cg_generic_p(g, k->z, p, k->d_st));  // dinv = 1: z - mu
+  PB_TRY(op_apply_raw(k->A, p, k->w));
+  PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
+  PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
+  PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, k->r, k->d_st));
+  PB_TRY(mg_apply(k->mg, k->r, k->z));
+  PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
+  return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
+}
+
 static int enqueue_iteration(pb_ksp* k) {
+  if (k->mg) return enqueue_pc_iteration(k);
   if (!fused_kind(k->A->kind)) return enqueue_generic_iteration(k);
   pb_grid* g = k->A->grid;
   pb_ctx* ctx = g->ctx;
@@ -426,11 +485,35 @@ int pb_ksp_destroy(pb_ksp* k) {
   (void)hipFree(k->pb[1]);
   if (k->w) (void)hipFree(k->w);
   if (k->z) (void)hipFree(k->z);
+  if (k->mg) mg_destroy(k->mg);
   (void)hipFree(k->d_st);
   if (k->d_hist) (void)hipFree(k->d_hist);
   if (k->h_done) (void)hipHostFree(k->h_done);
   for (hipEvent_t e : k->ring) (void)hipEventDestroy(e);
   delete k;
+  return PB_OK;
+}
+
+int pb_ksp_pc_apply(pb_ksp* k, const pb_vec* r, pb_vec* z) {
+  PB_CHECK_ARG(k && r && z && r != z, "bad pc apply args");
+  pb_grid* g = k->A->grid;
+  PB_CHECK_ARG(r->grid == g && z->grid == g, "vector/operator grid mismatch");
+  pb_ctx* ctx = g->ctx;
+  if (k->mg) {
+    PB_TRY(mg_apply(k->mg, r->d, z->d));
+  } else {
+    PB_HIP(hipMemcpyAsync(z->d, r->d, (size_t)g->nlocal * sizeof(double),
+                          hipMemcpyDeviceToDevice, ctx->stream));
+    if (k->opts.pc_type == PB_PC_JACOBI)
+      PB_TRY(vec_update(ctx, 2, z->d, nullptr, g->nlocal, 1.0 / k->P->cc));
+  }
+  PB_HIP(hipStreamSynchronize(ctx->stream));
+  return PB_OK;
+}
+
+int pb_ksp_pc_levels(const pb_ksp* k, int* levels) {
+  PB_CHECK_ARG(k && levels, "bad args");
+  *levels = k->mg ? mg_levels(k->mg) : 0;
   return PB_OK;
 }
 

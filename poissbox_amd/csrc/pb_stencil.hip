@@ -786,6 +786,10 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
                     mode, part_off, nblocks);
 }
 
+int cg_finalize_init(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done) {
+  return cg_reduce_update(ctx, 0, nparts, 4, st, hist, h_done, -1);
+}
+
 int cg_finalize_pass_a(pb_ctx* ctx, int nparts, CgState* st) {
   return cg_reduce_update(ctx, 1, nparts, 1, st, nullptr, nullptr, 0);
 }

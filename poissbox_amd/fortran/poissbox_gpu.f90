@@ -45,6 +45,8 @@ module poissbox_gpu
      real(c_double) :: rtol, atol, dtol
      integer(c_int64_t) :: max_it
      integer(c_int) :: ksp_type, pc_type, nullspace, monitor, converged_reason, check_every
+     integer(c_int) :: mg_levels, mg_coarse_its
+     real(c_double) :: sor_omega
   end type pb_ksp_opts
 
   type, bind(C), public :: pb_ksp_result

@@ -474,3 +474,100 @@ def test_cg_with_compact_operator(ctx):
     k = min(len(hist), len(ho))
     assert np.max(np.abs(hist[:k - 1] - ho[:k - 1]) / ho[:k - 1]) < 1e-6
     assert np.max(np.abs(x.get_values() - xo)) <= 1e-6 * np.max(np.abs(xo))
+
+
+# ---------------------------------------------------------------------------------------------
+# SOR / geometric multigrid preconditioners -- parity against the oracle's
+# restatement of the same V-cycle (bit-exact PC apply), CG histories within HIST_RTOL
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("pc,n3,levels", [("sor", (16, 12, 8), 0), ("mg", (32, 32, 32), 0),
+                                          ("mg", (64, 48, 32), 0), ("mg", (32, 16, 24), 2),
+                                          ("mg", (8, 8, 8), 0)])
+def test_pc_apply_bit_exact(ctx, pc, n3, levels):
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    r = O.fill_random(N, 11)
+    ref = O.mg_apply(r, n3, h, pc=pc, levels=levels)
+    da = pb.DA(ctx, n3)
+    P, A, _, _ = pb.initialise_linear_system(da, h)
+    k = pb.KSP(A, P, pb.ksp_options(["-pc_type", pc, "-pc_mg_levels", str(levels)]))
+    assert k.pc_levels == (O.mg_plan_levels(n3, 1, levels) if pc == "mg" else 1)
+    rv, zv = pb.Vec(da), pb.Vec(da)
+    rv.set_values(r)
+    k.pc_apply(rv, zv)
+    assert np.array_equal(zv.get_values(), ref)
+    k.destroy()
+
+
+@pytest.mark.parametrize("pc,n", [("sor", 32), ("mg", 32), ("mg", 64)])
+def test_cg_sor_mg_matches_oracle(ctx, pc, n):
+    n3 = (n, n, n)
+    N = n ** 3
+    h = (1.0 / n,) * 3
+    b = O.stencil(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-10, pc=pc)
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(P, A, x, bv, ["-pc_type", pc, "-ksp_rtol", "1e-10"])
+    assert reason == ro == 2 and its == itso
+    assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
+    assert np.max(np.abs(x.get_values() - xo)) <= 1e-6 * np.max(np.abs(xo))
+    if pc == "mg":
+        assert its <= 16  # h-independent V-cycle preconditioning
+
+
+def test_cg_compact_operator_mg_pc(ctx):
+    """Config 5 shape: compact A inside CG, MG-SOR preconditioner on the 7-point P."""
+    n3 = (32, 32, 32)
+    h = (2 * np.pi / 32,) * 3
+    N = 32 ** 3
+    b = O.lapl(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-8, op="compact", pc="mg")
+    da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+    P = pb.Mat(da, pb.ASSEMBLED27, h)
+    A = pb.Mat(da, pb.COMPACT, h)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(P, A, x, bv, ["-pc_type", "mg", "-ksp_rtol", "1e-8"])
+    assert reason == ro == 2 and abs(its - itso) <= 1
+    k = min(len(hist), len(ho))
+    assert np.max(np.abs(hist[:k - 1] - ho[:k - 1]) / ho[:k - 1]) < 1e-6
+    assert np.max(np.abs(x.get_values() - xo)) <= 1e-6 * np.max(np.abs(xo))
+
+
+def test_mg_rejects_odd_extents(ctx):
+    da = pb.DA(ctx, (17, 16, 16))
+    P, A, _, _ = pb.initialise_linear_system(da, (1 / 17, 1 / 16, 1 / 16))
+    with pytest.raises(pb.PbError):
+        pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
+
+
+@pytest.mark.parametrize("nranks,n", [(2, (16, 16, 32)), (4, (16, 16, 32)), (3, (16, 16, 12))])
+def test_multirank_mg_bit_exact_and_cg(nranks, n):
+    """Slab-decomposed V-cycle (halo exchanges per level) equals the single-grid restatement."""
+    N = int(np.prod(n))
+    h = tuple(1.0 / m for m in n)
+    r = O.fill_random(N, 3)
+    ref = O.mg_apply(r, n, h, pc="mg", nranks=nranks).reshape(n[2], -1)
+    b = O.stencil(O.fill_random(N, SEED), n, h)
+    xo, ro, itso, ho = O.cg_solve(b, n, h, rtol=1e-8, pc="mg", nranks=nranks)
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        P, A, x, bv = pb.initialise_linear_system(da, h)
+        k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg", "-ksp_rtol", "1e-8"]))
+        rv, zv = pb.Vec(da), pb.Vec(da)
+        rv.set_values(r.reshape(n[2], -1)[k0:k0 + nk])
+        k.pc_apply(rv, zv)
+        bv.set_values(b.reshape(n[2], -1)[k0:k0 + nk])
+        reason, its, hist = k.solve(bv, x)
+        return k0, nk, zv.get_values(), reason, its, hist, x.get_values(), k.pc_levels
+
+    for k0, nk, z, reason, its, hist, xs, lv in run_ranks(nranks, body):
+        assert lv == O.mg_plan_levels(n, nranks)
+        assert np.array_equal(z, ref[k0:k0 + nk].reshape(-1))
+        assert (reason, its) == (ro, itso)
+        assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
+        assert np.max(np.abs(xs - xo.reshape(n[2], -1)[k0:k0 + nk].reshape(-1))) <= 1e-6

@@ -153,3 +153,42 @@ def test_fill_random_distribution():
     x = O.fill_random(1 << 16, 20231015)
     assert x.min() >= -1.0 and x.max() <= 1.0 and abs(x.mean()) < 0.01
     assert np.array_equal(O.fill_random(10, 5, g0=100), O.fill_random(110, 5)[100:])
+
+
+# ---- SOR / multigrid preconditioner restatement (pb_mg.hip design) ----
+@pytest.mark.parametrize("pc,n3", [("sor", (16, 12, 8)), ("mg", (32, 32, 32)), ("mg", (32, 16, 24))])
+def test_mg_preconditioner_is_symmetric(pc, n3):
+    """CG needs a symmetric M^-1: <M^-1 a, b> == <a, M^-1 b> to rounding."""
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    a, b = O.fill_random(N, 1), O.fill_random(N, 2)
+    ma, mb = O.mg_apply(a, n3, h, pc=pc), O.mg_apply(b, n3, h, pc=pc)
+    lhs, rhs = ma @ b, a @ mb
+    assert abs(lhs - rhs) <= 1e-12 * max(abs(lhs), np.linalg.norm(ma) * np.linalg.norm(b))
+    # negative definite on mean-free vectors like A^-1 (A is NSD, diag < 0)
+    a0 = a - a.mean()
+    assert O.mg_apply(a0, n3, h, pc=pc) @ a0 < 0
+
+
+def test_mg_level_plan():
+    assert O.mg_plan_levels((512, 512, 512)) == 8      # 512 -> 4
+    assert O.mg_plan_levels((64, 48, 32)) == 4         # 8 x 6 x 4 coarsest
+    assert O.mg_plan_levels((16, 16, 32), 4) == 3
+    assert O.mg_plan_levels((16, 16, 12), 3) == 2      # slabs of 4 -> 2 planes
+    assert O.mg_plan_levels((16, 16, 14), 2) == 1      # odd slabs: no coarsening
+    assert O.mg_plan_levels((64, 64, 64), 1, 2) == 2   # explicit -pc_mg_levels
+
+
+def test_cg_mg_iterations_grid_independent():
+    """V-cycle PCG: the iteration count does not grow with n (Jacobi-PCG's doubles)."""
+    its = {}
+    for n in (16, 32, 64):
+        n3 = (n, n, n)
+        h = (1.0 / n,) * 3
+        b = O.stencil(O.fill_random(n ** 3, 20231015), n3, h)
+        x, reason, k, hist = O.cg_solve(b, n3, h, rtol=1e-10, pc="mg")
+        assert reason == 2
+        r = O.stencil(x, n3, h) - b
+        assert np.linalg.norm(r) <= 1e-8 * np.linalg.norm(b)
+        its[n] = k
+    assert max(its.values()) <= 16 and its[64] <= its[16] + 3, its
