@@ -178,7 +178,7 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
 int cg_finalize_pass_a(pb_ctx* ctx, int nparts, CgState* st);
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
                      double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
-                     int64_t host_iter, bool defer_x);
+                     int64_t host_iter, bool defer_x, bool finalize = true);
 int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
 int stencil_blocks(pb_grid* g, int mode);  // partial-sum slots a stencil pass writes
 
@@ -225,7 +225,9 @@ struct Mg;
 // levels_req: 0 = automatic; pc_type PB_PC_SOR (one symmetric red-black sweep) or PB_PC_MG
 int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, int coarse_its,
               double omega, Mg** out);
-int mg_apply(Mg* mg, const double* r, double* z);  // z = M^-1 r (zero initial guess)
+// z = M^-1 r (zero initial guess); skip: optional device flag (CG's `done`) -- when set, the
+// kernels exit at entry (halo exchanges still run, so ranks stay matched)
+int mg_apply(Mg* mg, const double* r, double* z, const int* skip = nullptr);
 int mg_levels(const Mg* mg);
 void mg_destroy(Mg* mg);
 // deterministic level count for a global grid split over nranks z-slabs (every rank agrees)

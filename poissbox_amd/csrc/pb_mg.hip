@@ -53,95 +53,181 @@ struct Mg {
   double omega = 1.0;
   int coarse_its = 1;
   double* mem = nullptr;
+  const int* skip = nullptr;  // device flag: when set, the kernels of this apply exit at entry
 };
 
 // ---------------------------------------------------------------------------------------------
-// kernels (grid-stride over the owned points of one level; i fastest)
+// kernels. Every level has an even x extent, so one thread owns an (i even, i + 1) pair: 16-byte
+// loads and full-line 16-byte stores; the pair holds one red and one black point.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void mg_ijk(const MgGeo& G, int64_t idx, int& i, int& j, int& k) {
-  k = (int)(idx / G.plane);
-  const int rem = (int)(idx - (int64_t)k * G.plane);
-  j = rem / G.nx;
-  i = rem - j * G.nx;
-}
+typedef double dv2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int wrapm(int v, int n) { return v < 0 ? v + n : (v >= n ? v - n : v); }
 
-// one red-black SOR half-sweep over colour `color`; zero_init: x starts at 0 (the other colour is
-// zeroed, the neighbour sum of this colour is exactly 0)
+struct PairPos {
+  int i0, j, k;       // pair origin (i0 even), row j, local plane k
+  int64_t idx;        // linear index of (i0, j, k)
+};
+
+// 32-bit index arithmetic (a level never holds 2^32 pairs on one GPU)
+__device__ __forceinline__ PairPos pair_pos(const MgGeo& G, int64_t q64) {
+  const uint32_t q = (uint32_t)q64, hx = (uint32_t)G.nx >> 1;
+  const uint32_t row = q / hx;
+  PairPos p;
+  p.i0 = (int)(q - row * hx) * 2;
+  p.k = (int)(row / (uint32_t)G.ny);
+  p.j = (int)(row - (uint32_t)p.k * (uint32_t)G.ny);
+  p.idx = (int64_t)row * G.nx + p.i0;
+  return p;
+}
+
+// value of v at (i, j +- 1) and (i, j, k +- 1) for the point at linear index id (plane offset
+// pid = id - k*plane); lo / hi are the planes below / above the slab
+struct Nb4 {
+  double zm, ym, yp, zp;
+};
+__device__ __forceinline__ Nb4 nb4(const MgGeo& G, const double* v, const double* lo,
+                                   const double* hi, int64_t id, int i, int j, int k) {
+  const int64_t pid = id - (int64_t)k * G.plane;
+  Nb4 r;
+  r.zm = k > 0 ? v[id - G.plane] : lo[pid];
+  r.zp = k < G.nzl - 1 ? v[id + G.plane] : hi[pid];
+  r.ym = v[id + (int64_t)(wrapm(j - 1, G.ny) - j) * G.nx];
+  r.yp = v[id + (int64_t)(wrapm(j + 1, G.ny) - j) * G.nx];
+  (void)i;
+  return r;
+}
+
+// red value after the zero-initialised first half-sweep: (1 - w) * 0 + w * ((b - 0) / c)
+__device__ __forceinline__ double red0(double b, const Star& s, double omega) {
+  const double t = (b - 0.0) / s.cc;
+  return (1.0 - omega) * 0.0 + omega * t;
+}
+
+// mode 0: one red-black SOR half-sweep over `color` (x holds the current iterate).
+// mode 1: the first two half-sweeps from x = 0 fused: red = w D^-1 b, then black from those red
+//         values, computed from b directly (lo / hi are then b's ghost planes).
 __global__ __launch_bounds__(256) void mg_smooth_kernel(MgGeo G, double* x,
                                                         const double* __restrict__ b,
                                                         const double* lo, const double* hi, Star s,
-                                                        double omega, int color, int zero_init) {
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < G.nlocal;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int i, j, k;
-    mg_ijk(G, idx, i, j, k);
-    const int col = (int)((i + j + G.k0 + k) & 1);
-    if (col != color) {
-      if (zero_init) x[idx] = 0.0;
+                                                        double omega, int color, int mode,
+                                                        const int* skip) {
+  if (skip && *skip) return;
+  const int64_t npairs = G.nlocal >> 1;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npairs;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const PairPos P = pair_pos(G, q);
+    const int64_t row = P.idx - P.i0;
+    if (mode == 1) {
+      const dv2 bp = *(const dv2*)(b + P.idx);
+      const int dr = (int)((P.j + G.k0 + P.k) & 1);  // red offset in the pair
+      const int ib = P.i0 + (dr ^ 1);
+      const int64_t idb = row + ib;
+      const double bb = dr ? bp.x : bp.y;               // black point's b
+      const double br = dr ? bp.y : bp.x;
+      const Nb4 n4 = nb4(G, b, lo, hi, idb, ib, P.j, P.k);
+      const double bxm = ib == P.i0 + 1 ? bp.x : b[row + wrapm(ib - 1, G.nx)];
+      const double bxp = ib == P.i0 ? bp.y : b[row + wrapm(ib + 1, G.nx)];
+      double nb = s.cz * red0(n4.zm, s, omega);
+      nb = nb + s.cy * red0(n4.ym, s, omega);
+      nb = nb + s.cx * red0(bxm, s, omega);
+      nb = nb + s.cx * red0(bxp, s, omega);
+      nb = nb + s.cy * red0(n4.yp, s, omega);
+      nb = nb + s.cz * red0(n4.zp, s, omega);
+      const double t = (bb - nb) / s.cc;
+      const double xb = (1.0 - omega) * 0.0 + omega * t;
+      const double xr = red0(br, s, omega);
+      dv2 o;
+      o.x = dr ? xb : xr;
+      o.y = dr ? xr : xb;
+      *(dv2*)(x + P.idx) = o;
       continue;
     }
-    double nb = 0.0, xo = 0.0;
-    if (!zero_init) {
-      const int64_t row = idx - i;
-      const double zm = k > 0 ? x[idx - G.plane] : lo[idx];
-      const double zp = k < G.nzl - 1 ? x[idx + G.plane] : hi[idx - (int64_t)k * G.plane];
-      const double ym = x[idx + (int64_t)(wrapm(j - 1, G.ny) - j) * G.nx];
-      const double yp = x[idx + (int64_t)(wrapm(j + 1, G.ny) - j) * G.nx];
-      const double xm = x[row + wrapm(i - 1, G.nx)];
-      const double xp = x[row + wrapm(i + 1, G.nx)];
-      nb = s.cz * zm;
-      nb = nb + s.cy * ym;
-      nb = nb + s.cx * xm;
-      nb = nb + s.cx * xp;
-      nb = nb + s.cy * yp;
-      nb = nb + s.cz * zp;
-      xo = x[idx];
-    }
-    const double t = (b[idx] - nb) / s.cc;
-    x[idx] = (1.0 - omega) * xo + omega * t;
+    const dv2 xp = *(const dv2*)(x + P.idx);
+    const int d = (int)((color + P.j + G.k0 + P.k) & 1);  // offset of the updated point
+    const int ic = P.i0 + d;
+    const int64_t id = row + ic;
+    const Nb4 n4 = nb4(G, x, lo, hi, id, ic, P.j, P.k);
+    const double xm = d ? xp.x : x[row + wrapm(P.i0 - 1, G.nx)];
+    const double xq = d ? x[row + wrapm(P.i0 + 2, G.nx)] : xp.y;
+    double nb = s.cz * n4.zm;
+    nb = nb + s.cy * n4.ym;
+    nb = nb + s.cx * xm;
+    nb = nb + s.cx * xq;
+    nb = nb + s.cy * n4.yp;
+    nb = nb + s.cz * n4.zp;
+    const double xo = d ? xp.y : xp.x;
+    const double t = (b[id] - nb) / s.cc;
+    const double xn = (1.0 - omega) * xo + omega * t;
+    dv2 o = xp;
+    if (d) o.y = xn;
+    else o.x = xn;
+    *(dv2*)(x + P.idx) = o;
   }
 }
 
-// res = b - A x (7-point, the reference operator's summation order)
+// res = b - A x for both points of the pair (the reference operator's summation order)
 __global__ __launch_bounds__(256) void mg_residual_kernel(MgGeo G, const double* __restrict__ x,
                                                           const double* __restrict__ b,
                                                           const double* __restrict__ lo,
                                                           const double* __restrict__ hi, Star s,
-                                                          double* __restrict__ res) {
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < G.nlocal;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int i, j, k;
-    mg_ijk(G, idx, i, j, k);
-    const int64_t row = idx - i;
-    const double zm = k > 0 ? x[idx - G.plane] : lo[idx];
-    const double zp = k < G.nzl - 1 ? x[idx + G.plane] : hi[idx - (int64_t)k * G.plane];
-    const double ym = x[idx + (int64_t)(wrapm(j - 1, G.ny) - j) * G.nx];
-    const double yp = x[idx + (int64_t)(wrapm(j + 1, G.ny) - j) * G.nx];
-    const double xm = x[row + wrapm(i - 1, G.nx)];
-    const double xp = x[row + wrapm(i + 1, G.nx)];
-    double ax = s.cz * zm;
-    ax = ax + s.cy * ym;
-    ax = ax + s.cx * xm;
-    ax = ax + s.cc * x[idx];
-    ax = ax + s.cx * xp;
-    ax = ax + s.cy * yp;
-    ax = ax + s.cz * zp;
-    res[idx] = b[idx] - ax;
+                                                          double* __restrict__ res, const int* skip) {
+  if (skip && *skip) return;
+  const int64_t npairs = G.nlocal >> 1;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npairs;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const PairPos P = pair_pos(G, q);
+    const int64_t row = P.idx - P.i0;
+    const dv2 xc = *(const dv2*)(x + P.idx);
+    const dv2 bc = *(const dv2*)(b + P.idx);
+    const int64_t pid = P.idx - (int64_t)P.k * G.plane;
+    const dv2 zm = P.k > 0 ? *(const dv2*)(x + P.idx - G.plane) : *(const dv2*)(lo + pid);
+    const dv2 zp = P.k < G.nzl - 1 ? *(const dv2*)(x + P.idx + G.plane) : *(const dv2*)(hi + pid);
+    const dv2 ym = *(const dv2*)(x + P.idx + (int64_t)(wrapm(P.j - 1, G.ny) - P.j) * G.nx);
+    const dv2 yp = *(const dv2*)(x + P.idx + (int64_t)(wrapm(P.j + 1, G.ny) - P.j) * G.nx);
+    const double xl = x[row + wrapm(P.i0 - 1, G.nx)];
+    const double xr = x[row + wrapm(P.i0 + 2, G.nx)];
+    double a0 = s.cz * zm.x;
+    a0 = a0 + s.cy * ym.x;
+    a0 = a0 + s.cx * xl;
+    a0 = a0 + s.cc * xc.x;
+    a0 = a0 + s.cx * xc.y;
+    a0 = a0 + s.cy * yp.x;
+    a0 = a0 + s.cz * zp.x;
+    double a1 = s.cz * zm.y;
+    a1 = a1 + s.cy * ym.y;
+    a1 = a1 + s.cx * xc.x;
+    a1 = a1 + s.cc * xc.y;
+    a1 = a1 + s.cx * xr;
+    a1 = a1 + s.cy * yp.y;
+    a1 = a1 + s.cz * zp.y;
+    dv2 o;
+    o.x = bc.x - a0;
+    o.y = bc.y - a1;
+    *(dv2*)(res + P.idx) = o;
   }
+}
+
+__device__ __forceinline__ void mg_ijk(const MgGeo& G, int64_t idx, int& i, int& j, int& k) {
+  const uint32_t u = (uint32_t)idx, nx = (uint32_t)G.nx;
+  const uint32_t row = u / nx;
+  i = (int)(u - row * nx);
+  k = (int)(row / (uint32_t)G.ny);
+  j = (int)(row - (uint32_t)k * (uint32_t)G.ny);
 }
 
 // b_c = R res_f, R = P^T / 8: 4 x 4 x 4 fine cells (2I-1 .. 2I+2 per direction)
 __global__ __launch_bounds__(256) void mg_restrict_kernel(MgGeo F, const double* __restrict__ rf,
                                                           const double* __restrict__ lo,
                                                           const double* __restrict__ hi, MgGeo Cg,
-                                                          double* __restrict__ bc) {
+                                                          double* __restrict__ bc, const int* skip) {
+  if (skip && *skip) return;
   const double w[4] = {0.125, 0.375, 0.375, 0.125};
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < Cg.nlocal;
        idx += (int64_t)gridDim.x * blockDim.x) {
     int I, J, K;
     mg_ijk(Cg, idx, I, J, K);
+    const int xl = wrapm(2 * I - 1, F.nx), xr = wrapm(2 * I + 2, F.nx);
     double sz = 0.0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -151,9 +237,11 @@ __global__ __launch_bounds__(256) void mg_restrict_kernel(MgGeo F, const double*
 #pragma unroll
       for (int bb = 0; bb < 4; ++bb) {
         const double* row = pl + (int64_t)wrapm(2 * J - 1 + bb, F.ny) * F.nx;
-        double sx = 0.0;
-#pragma unroll
-        for (int a = 0; a < 4; ++a) sx = sx + w[a] * row[wrapm(2 * I - 1 + a, F.nx)];
+        const dv2 mid = *(const dv2*)(row + 2 * I);
+        double sx = w[0] * row[xl];
+        sx = sx + w[1] * mid.x;
+        sx = sx + w[2] * mid.y;
+        sx = sx + w[3] * row[xr];
         sy = sy + w[bb] * sx;
       }
       sz = sz + w[c] * sy;
@@ -162,37 +250,48 @@ __global__ __launch_bounds__(256) void mg_restrict_kernel(MgGeo F, const double*
   }
 }
 
-// x_f += P x_c (trilinear, cell-centred: near parent 3/4, far parent 1/4 per direction)
+// x_f += P x_c for both points of the pair (trilinear, cell-centred: near parent 3/4, far 1/4)
 __global__ __launch_bounds__(256) void mg_prolong_kernel(MgGeo F, double* __restrict__ xf, MgGeo Cg,
                                                          const double* __restrict__ xc,
                                                          const double* __restrict__ lo,
-                                                         const double* __restrict__ hi) {
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < F.nlocal;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int i, j, k;
-    mg_ijk(F, idx, i, j, k);
-    const int I = i >> 1, J = j >> 1, K = k >> 1;
-    const int fI = wrapm((i & 1) ? I + 1 : I - 1, Cg.nx);
-    const int fJ = wrapm((j & 1) ? J + 1 : J - 1, Cg.ny);
-    const int fK = (k & 1) ? K + 1 : K - 1;
+                                                         const double* __restrict__ hi,
+                                                         const int* skip) {
+  if (skip && *skip) return;
+  const int64_t npairs = F.nlocal >> 1;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npairs;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const PairPos P = pair_pos(F, q);
+    const int I = P.i0 >> 1, J = P.j >> 1, K = P.k >> 1;
+    const int fI0 = wrapm(I - 1, Cg.nx), fI1 = wrapm(I + 1, Cg.nx);
+    const int fJ = wrapm((P.j & 1) ? J + 1 : J - 1, Cg.ny);
+    const int fK = (P.k & 1) ? K + 1 : K - 1;
     const double* pn = xc + (int64_t)K * Cg.plane;
     const double* pf = fK < 0 ? lo : (fK >= Cg.nzl ? hi : xc + (int64_t)fK * Cg.plane);
     const int64_t rn = (int64_t)J * Cg.nx, rf = (int64_t)fJ * Cg.nx;
-    const double vn = 0.75 * (0.75 * pn[rn + I] + 0.25 * pn[rn + fI]) +
-                      0.25 * (0.75 * pn[rf + I] + 0.25 * pn[rf + fI]);
-    const double vf = 0.75 * (0.75 * pf[rn + I] + 0.25 * pf[rn + fI]) +
-                      0.25 * (0.75 * pf[rf + I] + 0.25 * pf[rf + fI]);
-    xf[idx] = xf[idx] + (0.75 * vn + 0.25 * vf);
+    // point i0 (even): far parent I-1; point i0+1 (odd): far parent I+1
+    const double vn0 = 0.75 * (0.75 * pn[rn + I] + 0.25 * pn[rn + fI0]) +
+                       0.25 * (0.75 * pn[rf + I] + 0.25 * pn[rf + fI0]);
+    const double vf0 = 0.75 * (0.75 * pf[rn + I] + 0.25 * pf[rn + fI0]) +
+                       0.25 * (0.75 * pf[rf + I] + 0.25 * pf[rf + fI0]);
+    const double vn1 = 0.75 * (0.75 * pn[rn + I] + 0.25 * pn[rn + fI1]) +
+                       0.25 * (0.75 * pn[rf + I] + 0.25 * pn[rf + fI1]);
+    const double vf1 = 0.75 * (0.75 * pf[rn + I] + 0.25 * pf[rn + fI1]) +
+                       0.25 * (0.75 * pf[rf + I] + 0.25 * pf[rf + fI1]);
+    dv2 o = *(const dv2*)(xf + P.idx);
+    o.x = o.x + (0.75 * vn0 + 0.25 * vf0);
+    o.y = o.y + (0.75 * vn1 + 0.25 * vf1);
+    *(dv2*)(xf + P.idx) = o;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
+// one thread per item (no grid-stride loop unless the grid would exceed 2^30 blocks)
 static int mg_blocks(pb_ctx* ctx, int64_t n) {
+  (void)ctx;
   int64_t b = (n + 255) / 256;
-  const int64_t cap = (int64_t)ctx->num_cus * 16;
-  return (int)std::max<int64_t>(1, std::min(b, cap));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, (int64_t)1 << 30));
 }
 
 // ghost planes of v on level L: in place (1 rank) or exchanged (N ranks)
@@ -209,23 +308,25 @@ static int ghosts(MgLevel& L, const double* v, const double** lo, const double**
   return PB_OK;
 }
 
-static int smooth(Mg* mg, MgLevel& L, int color, bool zero_init) {
+// mode 0: half-sweep of `color`; mode 1: zero-initialised red + black half-sweeps fused
+static int smooth(Mg* mg, MgLevel& L, int color, int mode) {
   const double *lo = nullptr, *hi = nullptr;
-  if (!zero_init) PB_TRY(ghosts(L, L.x, &lo, &hi));
+  PB_TRY(ghosts(L, mode == 1 ? L.b : L.x, &lo, &hi));
   const MgGeo G = L.geo();
-  hipLaunchKernelGGL(mg_smooth_kernel, dim3(mg_blocks(mg->ctx, G.nlocal)), dim3(256), 0,
+  hipLaunchKernelGGL(mg_smooth_kernel, dim3(mg_blocks(mg->ctx, G.nlocal / 2)), dim3(256), 0,
                      mg->ctx->stream, G, L.x, (const double*)L.b, lo, hi, L.s, mg->omega, color,
-                     zero_init ? 1 : 0);
+                     mode, mg->skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
 
 // coarsest level: `coarse_its` symmetric red-black sweeps from zero (red, black, red, black, ...)
 static int coarse_solve(Mg* mg, MgLevel& L) {
-  PB_TRY(smooth(mg, L, 0, true));
-  for (int it = 0; it < mg->coarse_its; ++it) {
-    PB_TRY(smooth(mg, L, 1, false));
-    PB_TRY(smooth(mg, L, 0, false));
+  PB_TRY(smooth(mg, L, 0, 1));  // red from zero + black
+  PB_TRY(smooth(mg, L, 0, 0));
+  for (int it = 1; it < mg->coarse_its; ++it) {
+    PB_TRY(smooth(mg, L, 1, 0));
+    PB_TRY(smooth(mg, L, 0, 0));
   }
   return PB_OK;
 }
@@ -271,6 +372,8 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
       return set_error(PB_ERR_UNSUPPORTED,
                        "red-black SOR / multigrid needs even grid extents (got %lld x %lld x %lld)",
                        (long long)g->n[0], (long long)g->n[1], (long long)g->n[2]);
+  if (g->nlocal >= ((int64_t)1 << 32))
+    return set_error(PB_ERR_UNSUPPORTED, "multigrid: more than 2^32 points on one GPU");
   if (!(omega > 0.0 && omega < 2.0)) return set_error(PB_ERR_ARG, "SOR omega must be in (0, 2)");
   Mg* mg = new Mg();
   mg->ctx = ctx;
@@ -321,8 +424,9 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
   return PB_OK;
 }
 
-int mg_apply(Mg* mg, const double* r, double* z) {
+int mg_apply(Mg* mg, const double* r, double* z, const int* skip) {
   ScopedTimer tm(mg->ctx, "mg_apply");
+  mg->skip = skip;
   const int L = (int)mg->lv.size();
   mg->lv[0].b = const_cast<double*>(r);
   mg->lv[0].x = z;
@@ -330,32 +434,40 @@ int mg_apply(Mg* mg, const double* r, double* z) {
   for (int l = 0; l < L - 1; ++l) {  // down: pre-smooth (red, black), residual, restrict
     MgLevel& F = mg->lv[l];
     MgLevel& Cl = mg->lv[l + 1];
-    PB_TRY(smooth(mg, F, 0, true));
-    PB_TRY(smooth(mg, F, 1, false));
+    {
+      ScopedTimer t1(ctx, l == 0 ? "mg_fine_smooth_first" : "mg_coarse_levels");
+      PB_TRY(smooth(mg, F, 0, 1));  // red from zero + black
+    }
+    ScopedTimer t2(ctx, l == 0 ? "mg_fine_resid_restrict" : "mg_coarse_levels");
     const double *lo, *hi;
     PB_TRY(ghosts(F, F.x, &lo, &hi));
     const MgGeo G = F.geo();
-    hipLaunchKernelGGL(mg_residual_kernel, dim3(mg_blocks(ctx, G.nlocal)), dim3(256), 0,
-                       ctx->stream, G, (const double*)F.x, (const double*)F.b, lo, hi, F.s, F.res);
+    hipLaunchKernelGGL(mg_residual_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0,
+                       ctx->stream, G, (const double*)F.x, (const double*)F.b, lo, hi, F.s, F.res,
+                       mg->skip);
     PB_HIP(hipGetLastError());
     PB_TRY(ghosts(F, F.res, &lo, &hi));
     const MgGeo CG = Cl.geo();
     hipLaunchKernelGGL(mg_restrict_kernel, dim3(mg_blocks(ctx, CG.nlocal)), dim3(256), 0,
-                       ctx->stream, G, (const double*)F.res, lo, hi, CG, Cl.b);
+                       ctx->stream, G, (const double*)F.res, lo, hi, CG, Cl.b, mg->skip);
     PB_HIP(hipGetLastError());
   }
-  PB_TRY(coarse_solve(mg, mg->lv[L - 1]));
+  {
+    ScopedTimer t3(ctx, L > 1 ? "mg_coarse_levels" : "mg_fine_smooth_first");
+    PB_TRY(coarse_solve(mg, mg->lv[L - 1]));
+  }
   for (int l = L - 2; l >= 0; --l) {  // up: prolongate + correct, post-smooth (black, red)
     MgLevel& F = mg->lv[l];
     MgLevel& Cl = mg->lv[l + 1];
+    ScopedTimer t4(ctx, l == 0 ? "mg_fine_prolong_post" : "mg_coarse_levels");
     const double *lo, *hi;
     PB_TRY(ghosts(Cl, Cl.x, &lo, &hi));
     const MgGeo G = F.geo(), CG = Cl.geo();
-    hipLaunchKernelGGL(mg_prolong_kernel, dim3(mg_blocks(ctx, G.nlocal)), dim3(256), 0, ctx->stream,
-                       G, F.x, CG, (const double*)Cl.x, lo, hi);
+    hipLaunchKernelGGL(mg_prolong_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0, ctx->stream,
+                       G, F.x, CG, (const double*)Cl.x, lo, hi, mg->skip);
     PB_HIP(hipGetLastError());
-    PB_TRY(smooth(mg, F, 1, false));
-    PB_TRY(smooth(mg, F, 0, false));
+    PB_TRY(smooth(mg, F, 1, 0));
+    PB_TRY(smooth(mg, F, 0, 0));
   }
   return PB_OK;
 }

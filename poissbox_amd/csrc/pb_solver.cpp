@@ -206,6 +206,9 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   if (opts) k->opts = *opts;
   else pb_ksp_opts_default(&k->opts);
   if (k->opts.check_every < 1) k->opts.check_every = 8;
+  // SOR / MG iterations are expensive and few: poll the device flag more often
+  if ((k->opts.pc_type == PB_PC_SOR || k->opts.pc_type == PB_PC_MG) && k->opts.check_every > 2)
+    k->opts.check_every = 2;
   const int pc = k->opts.pc_type;
   if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG) {
     delete k;
@@ -289,7 +292,7 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   st.ntot = (double)(g->n[0] * g->n[1] * g->n[2]);
   const char* dx = getenv("PB_CG_DEFER_X");
   k->defer_x = !(dx && atoi(dx) == 0);
-  if (!fused_kind(k->A->kind) || k->mg) k->defer_x = false;  // generic path: x every iteration
+  if (!fused_kind(k->A->kind)) k->defer_x = false;  // generic path: x every iteration
   st.defer_x = k->defer_x ? 1 : 0;
   PB_HIP(hipMemcpyAsync(k->d_st, &st, sizeof(st), hipMemcpyHostToDevice, ctx->stream));
   if (k->mg) {
@@ -342,46 +345,53 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
   PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
   PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, k->r, k->d_st));
-  PB_TRY(mg_apply(k->mg, k->r, k->z));
+  PB_TRY(mg_apply(k->mg, k->r, k->z, &k->d_st->done));
   PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
 }
 
 static int enqueue_iteration(pb_ksp* k) {
-  if (k->mg) return enqueue_pc_iteration(k);
-  if (!fused_kind(k->A->kind)) return enqueue_generic_iteration(k);
+  if (!fused_kind(k->A->kind)) return k->mg ? enqueue_pc_iteration(k) : enqueue_generic_iteration(k);
   pb_grid* g = k->A->grid;
   pb_ctx* ctx = g->ctx;
   Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};
   const int64_t i = k->host_iter;  // == device iteration index until convergence
   double* p_old = k->pb[i % 2];
   double* p_new = k->pb[(i + 1) % 2];
-  PB_TRY(launch_cg_boundary(g, k->r, p_old, k->d_st));
+  // Jacobi: pass A builds z = dinv*r - mu on the fly; SOR / MG: z is stored (dinv = 1)
+  const double* zsrc = k->mg ? k->z : k->r;
+  PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st));
   StencilPlanes gp;
   int nparts = 0;
   if (ctx->nranks == 1) {
     gp.ghost_lo = g->bnd_hi;  // p_new of plane nzl-1 wraps below plane 0
     gp.ghost_hi = g->bnd_lo;
-    PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
+    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
   } else if (g->nzl < 3) {
     PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
-    PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
+    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
   } else {
     // the p-plane halo exchange (RCCL, comm stream) overlaps pass A's interior planes
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
     int nb1 = 0, nb2 = 0;
     PB_TRY(halo_begin(g, g->bnd_lo, g->bnd_hi));
-    PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1));
+    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1));
     PB_TRY(halo_end(g));
-    PB_TRY(launch_cg_pass_a(g, s, k->r, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1, &nb2));
+    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1, &nb2));
     nparts = nb1 + nb2;
   }
   PB_TRY(cg_finalize_pass_a(ctx, nparts, k->d_st));
   PB_TRY(launch_cg_pass_b(g, s, p_new, p_old, k->x->d, k->r, gp, k->d_st, k->d_hist,
-                          k->h_done_dev, i, k->defer_x));
+                          k->h_done_dev, i, k->defer_x, !k->mg));
+  if (k->mg) {  // z = M^-1 r, then the residual sums over z
+    PB_TRY(mg_apply(k->mg, k->r, k->z, &k->d_st->done));
+    int np = 0;
+    PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
+    PB_TRY(cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, i));
+  }
   return PB_OK;
 }
 

@@ -801,7 +801,7 @@ int cg_finalize_stage2(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* 
 
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
                      double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
-                     int64_t host_iter, bool defer_x) {
+                     int64_t host_iter, bool defer_x, bool finalize) {
   {
     if (!defer_x) {
       ScopedTimer tm(g->ctx, "cg_pass_b");
@@ -817,6 +817,7 @@ int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p
                         PassB<1>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done));
     }
   }
+  if (!finalize) return PB_OK;  // preconditioned path: the sums come from z = M^-1 r later
   return cg_reduce_update(g->ctx, 2, stencil_blocks(g, PLANES_ALL), 4, st, hist, h_done, host_iter);
 }
 

@@ -1,0 +1,83 @@
+"""Full KSPSolve to rtol 1e-10 (SURVEY.md §8d timing (iii)) with -pc_type jacobi | sor | mg on one
+GPU: iterations, wall time of the solve (inputs resident, HIP-synchronised), per-iteration time,
+and the multigrid V-cycle time. One JSON line per (n, pc). The oracle's CPU solve is timed at 64^3
+beside it (1 core).
+
+usage: python scripts/bench_solve.py [n ...]   (default 256 512)
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import poissbox_amd as pb  # noqa: E402
+
+SEED = 20231015
+
+
+def main():
+    sizes = [int(a) for a in sys.argv[1:]] or [256, 512]
+    ctx = pb.Context(0)
+    for n in sizes:
+        n3 = (n, n, n)
+        h = (1.0 / n,) * 3
+        da = pb.DA(ctx, n3)
+        P, A, x, b = pb.initialise_linear_system(da, h)
+        xt = pb.Vec(da)
+        xt.set_random(SEED)
+        A.mult(xt, b)
+        for pc in os.environ.get("PCS", "mg,sor,jacobi").split(","):
+            if pc == "sor" and n > 256:
+                continue
+            opts = pb.ksp_options(["-pc_type", pc, "-ksp_rtol", "1e-10"])
+            k = pb.KSP(A, P, opts)
+            k.solve(b, x)  # warm-up (allocations, first-touch)
+            ctx.sync()
+            ctx.set_timing(True)
+            ctx.reset_timing()
+            t0 = time.perf_counter()
+            reason, its, hist = k.solve(b, x)
+            ctx.sync()
+            dt = time.perf_counter() - t0
+            mg_ms, mg_cnt = ctx.timing("mg_apply")
+            parts = {}
+            for nm in ("mg_fine_smooth_first", "mg_fine_resid_restrict", "mg_fine_prolong_post",
+                       "mg_coarse_levels", "cg_pass_a", "cg_pass_b", "cg_pass_b_even",
+                       "cg_pass_b_odd"):
+                ms_, c_ = ctx.timing(nm)
+                if c_ and mg_cnt:
+                    parts[nm] = ms_ / mg_cnt
+            ctx.set_timing(False)
+            r = pb.Vec(da)
+            A.mult(x, r)
+            r.axpy(-1.0, b)
+            out = {"n": n, "pc": pc, "reason": int(reason), "its": int(its), "solve_ms": dt * 1e3,
+                   "ms_per_it": dt * 1e3 / max(its, 1), "levels": k.pc_levels,
+                   "rel_residual": r.norm() / b.norm(),
+                   "mg_apply_ms": (mg_ms / mg_cnt) if mg_cnt else None,
+                   "per_apply_ms": parts}
+            print(json.dumps(out), flush=True)
+            r.destroy()
+            k.destroy()
+        for o in (P, A, x, b, xt):
+            o.destroy()
+        da.destroy()
+    if os.environ.get("NO_CPU"):
+        return
+    # CPU restatement at 64^3 (1 core)
+    from oracle import oracle as O
+    n3 = (64, 64, 64)
+    h = (1 / 64,) * 3
+    bb = O.stencil(O.fill_random(64 ** 3, SEED), n3, h)
+    for pc in ("mg", "jacobi"):
+        t0 = time.perf_counter()
+        _, reason, its, _ = O.cg_solve(bb, n3, h, rtol=1e-10, pc=pc)
+        print(json.dumps({"n": 64, "pc": pc, "cpu_oracle_1core": True, "its": its,
+                          "solve_ms": (time.perf_counter() - t0) * 1e3}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
