@@ -63,6 +63,13 @@ typedef int (*pb_sendrecv_fn)(void* user, const double* send_lo, const double* s
 typedef int (*pb_allreduce_fn)(void* user, double* vals, int count);
 int pb_ctx_set_host_transport(pb_ctx* ctx, pb_sendrecv_fn sendrecv, pb_allreduce_fn allreduce,
                               void* user);
+/* Host all-to-all for the compact operators' z-slab <-> y-slab transposes: send_counts[p]
+ * doubles go to rank p (blocks contiguous in rank order in `send`), recv_counts[p] arrive from
+ * rank p (contiguous in rank order in `recv`). Needed only for the compact operator on a split
+ * grid with the host transport; RCCL contexts use grouped ncclSend/ncclRecv. */
+typedef int (*pb_alltoallv_fn)(void* user, const double* send, const int64_t* send_counts,
+                               double* recv, const int64_t* recv_counts);
+int pb_ctx_set_host_alltoallv(pb_ctx* ctx, pb_alltoallv_fn alltoallv, void* user);
 int pb_ctx_get_rank(const pb_ctx* ctx, int* rank, int* nranks);
 int pb_ctx_sync(pb_ctx* ctx);  /* stream synchronize (≙ MPI_Barrier for device work) */
 int pb_ctx_barrier(pb_ctx* ctx); /* synchronize + all ranks rendezvous */

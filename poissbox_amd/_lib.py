@@ -36,6 +36,7 @@ class KspResult(C.Structure):
 
 SENDRECV_FN = C.CFUNCTYPE(C.c_int, c_p, P_d, P_d, P_d, P_d, c_i64)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, c_p, P_d, C.c_int)
+ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, c_p, P_d, P_i64, P_d, P_i64)
 
 # name -> argtypes (all functions return int error codes unless listed in _RESTYPES)
 _SIGS = {
@@ -44,6 +45,7 @@ _SIGS = {
     "pb_comm_unique_id": [C.c_char_p],
     "pb_ctx_create": [C.c_int, C.c_int, C.c_int, C.c_char_p, C.POINTER(c_p)],
     "pb_ctx_set_host_transport": [c_p, SENDRECV_FN, ALLREDUCE_FN, c_p],
+    "pb_ctx_set_host_alltoallv": [c_p, ALLTOALLV_FN, c_p],
     "pb_ctx_get_rank": [c_p, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pb_ctx_sync": [c_p],
     "pb_ctx_barrier": [c_p],

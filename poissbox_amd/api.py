@@ -64,8 +64,10 @@ class Context:
         self.rank, self.nranks = rank, nranks
         self._keep = []
 
-    def set_host_transport(self, sendrecv, allreduce):
-        """sendrecv(send_lo, send_hi) -> (recv_lo, recv_hi) numpy arrays; allreduce(vals) -> vals."""
+    def set_host_transport(self, sendrecv, allreduce, alltoallv=None):
+        """sendrecv(send_lo, send_hi) -> (recv_lo, recv_hi) numpy arrays; allreduce(vals) -> vals;
+        alltoallv(list of per-rank send blocks, list of per-rank receive sizes) -> list of
+        per-rank received blocks (optional; the compact operator on a split grid needs it)."""
 
         def _sr(user, s_lo, s_hi, r_lo, r_hi, count):
             try:
@@ -91,6 +93,31 @@ class Context:
         f1, f2 = L.SENDRECV_FN(_sr), L.ALLREDUCE_FN(_ar)
         self._keep += [f1, f2]
         L.call("pb_ctx_set_host_transport", self.h, f1, f2, None)
+        if alltoallv is None:
+            return
+
+        def _a2a(user, send, scount, recv, rcount):
+            try:
+                P = self.nranks
+                sc = [int(scount[p]) for p in range(P)]
+                rc = [int(rcount[p]) for p in range(P)]
+                sa = np.ctypeslib.as_array(send, shape=(max(sum(sc), 1),))
+                so = np.concatenate([[0], np.cumsum(sc)])
+                blocks = [sa[so[p]:so[p + 1]].copy() for p in range(P)]
+                got = alltoallv(blocks, rc)
+                ra = np.ctypeslib.as_array(recv, shape=(max(sum(rc), 1),))
+                ro = np.concatenate([[0], np.cumsum(rc)])
+                for p in range(P):
+                    assert got[p].size == rc[p], (p, got[p].size, rc[p])
+                    ra[ro[p]:ro[p + 1]] = got[p]
+                return 0
+            except Exception as e:  # pragma: no cover
+                print("host alltoallv failed:", e)
+                return 1
+
+        f3 = L.ALLTOALLV_FN(_a2a)
+        self._keep.append(f3)
+        L.call("pb_ctx_set_host_alltoallv", self.h, f3, None)
 
     def sync(self):
         L.call("pb_ctx_sync", self.h)

@@ -224,86 +224,113 @@ static int launch_pass(pb_ctx* ctx, FastPass& p) {
   return PB_OK;
 }
 
-int64_t compact_fast_work_len(const pb_grid* g) { return 4 * g->nlocal; }
+// ---- the three passes on an explicit box (nx, ny, nz) whose lines along the pass axis are
+// complete: the caller's grid on one rank, the y-slab of the transposed data for the Z pass on N
+// ranks. Register line solves where n = 64*C supports them, the LDS-PCR kernel otherwise. ----
+static bool reg_lines(int64_t n) {
+  static const bool lines_ok = env_int("PB_COMPACT_LINES", 1) != 0;
+  return lines_ok && compact_lines_supported(n);
+}
 
-// lapl(f) into out; work: 4N doubles (u, v, s, t)
+// Z: u = Jz f, v = Lz f
+int compact_pass_z(pb_ctx* ctx, const int64_t d[3], double h, const double* f, double* u, double* v) {
+  const int64_t nx = d[0], ny = d[1], nz = d[2];
+  if (nz > kTile) return set_error(PB_ERR_UNSUPPORTED, "compact fast path: n > %d", kTile);
+  if (reg_lines(nz)) return compact_lines_pass(ctx, d, 2, h, f, nullptr, u, v);
+  FastPass p{};  // lines along k; tile = consecutive i for fixed j
+  p.n = (int)nz;
+  p.layout = 0;
+  p.ninner = (int)nx;
+  p.nouter = (int)ny;
+  p.li = 1;
+  p.lo = nx;
+  p.es = nx * ny;
+  p.nterms = 2;
+  p.term[0] = Term{0, 0, 0};
+  p.term[1] = Term{1, 0, 1};
+  p.ops[0] = make_op(0, nz, h);
+  p.ops[1] = make_op(1, nz, h);
+  p.in[0] = f;
+  p.out[0] = u;
+  p.out[1] = v;
+  p.nout = 2;
+  return launch_pass(ctx, p);
+}
+
+// Y: s = Jy u, t = Ly u + Jy v
+int compact_pass_y(pb_ctx* ctx, const int64_t d[3], double h, const double* u, const double* v,
+                   double* s_, double* t) {
+  const int64_t nx = d[0], ny = d[1], nz = d[2];
+  if (ny > kTile) return set_error(PB_ERR_UNSUPPORTED, "compact fast path: n > %d", kTile);
+  if (reg_lines(ny)) return compact_lines_pass(ctx, d, 1, h, u, v, s_, t);
+  FastPass p{};  // lines along j; tile = consecutive i for fixed k
+  p.n = (int)ny;
+  p.layout = 0;
+  p.ninner = (int)nx;
+  p.nouter = (int)nz;
+  p.li = 1;
+  p.lo = nx * ny;
+  p.es = nx;
+  p.nterms = 3;
+  p.term[0] = Term{0, 0, 0};  // s = Jy u
+  p.term[1] = Term{1, 0, 1};  // t = Ly u
+  p.term[2] = Term{0, 1, 1};  //   + Jy v
+  p.ops[0] = make_op(0, ny, h);
+  p.ops[1] = make_op(1, ny, h);
+  p.in[0] = u;
+  p.in[1] = v;
+  p.out[0] = s_;
+  p.out[1] = t;
+  p.nout = 2;
+  return launch_pass(ctx, p);
+}
+
+// X: out = Lx s + Jx t
+int compact_pass_x(pb_ctx* ctx, const int64_t d[3], double h, const double* s_, const double* t,
+                   double* out) {
+  const int64_t nx = d[0], ny = d[1], nz = d[2];
+  if (nx > kTile) return set_error(PB_ERR_UNSUPPORTED, "compact fast path: n > %d", kTile);
+  if (reg_lines(nx)) return compact_lines_pass(ctx, d, 0, h, s_, t, out, nullptr);
+  FastPass p{};  // lines along i (contiguous); tile = consecutive j for fixed k
+  p.n = (int)nx;
+  p.layout = 1;
+  p.ninner = (int)ny;
+  p.nouter = (int)nz;
+  p.li = nx;
+  p.lo = nx * ny;
+  p.es = 1;
+  p.nterms = 2;
+  p.term[0] = Term{1, 0, 0};  // out = Lx s
+  p.term[1] = Term{0, 1, 0};  //     + Jx t
+  p.ops[0] = make_op(0, nx, h);
+  p.ops[1] = make_op(1, nx, h);
+  p.in[0] = s_;
+  p.in[1] = t;
+  p.out[0] = out;
+  p.nout = 1;
+  return launch_pass(ctx, p);
+}
+
+// work doubles: 4 N (u, v, s, t) on one rank; on N ranks also the y-slab fields and the
+// transpose staging (compact_dist.cpp)
+int64_t compact_fast_work_len(const pb_grid* g) {
+  if (g->ctx->nranks == 1) return 4 * g->nlocal;
+  return 4 * g->nlocal + compact_dist_work_len(g);
+}
+
+// lapl(f) into out
 int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* out, double* work) {
   ScopedTimer tm(g->ctx, "compact_lapl_fast");
-  const int64_t nx = g->n[0], ny = g->n[1], nz = g->nzl, N = g->nlocal;
-  double *u = work, *v = work + N, *s = work + 2 * N, *t = work + 3 * N;
-  for (int d = 0; d < 3; ++d)
-    if (g->n[d] > kTile) return set_error(PB_ERR_UNSUPPORTED, "compact fast path: n > %d", kTile);
-  static const bool lines_ok = env_int("PB_COMPACT_LINES", 1) != 0;
-  auto reg = [&](int64_t n) { return lines_ok && compact_lines_supported(n); };
-  if (reg(nz)) {
-    PB_TRY(compact_lines_pass(g, 2, dx[2], f, nullptr, u, v));
-  } else {  // Z: lines along k; tile = consecutive i for fixed j
-    FastPass p{};
-    p.n = (int)nz;
-    p.layout = 0;
-    p.ninner = (int)nx;
-    p.nouter = (int)ny;
-    p.li = 1;
-    p.lo = nx;
-    p.es = nx * ny;
-    p.nterms = 2;
-    p.term[0] = Term{0, 0, 0};
-    p.term[1] = Term{1, 0, 1};
-    p.ops[0] = make_op(0, nz, dx[2]);
-    p.ops[1] = make_op(1, nz, dx[2]);
-    p.in[0] = f;
-    p.out[0] = u;
-    p.out[1] = v;
-    p.nout = 2;
-    PB_TRY(launch_pass(g->ctx, p));
+  const int64_t N = g->nlocal;
+  double *u = work, *v = work + N, *s_ = work + 2 * N, *t = work + 3 * N;
+  const int64_t d[3] = {g->n[0], g->n[1], g->nzl};
+  if (g->ctx->nranks == 1) {
+    PB_TRY(compact_pass_z(g->ctx, d, dx[2], f, u, v));
+  } else {  // z-lines span the slabs: transpose to y-slabs, Z pass, transpose u, v back
+    PB_TRY(compact_dist_pass_z(g, dx[2], f, u, v, work + 4 * N));
   }
-  if (reg(ny)) {
-    PB_TRY(compact_lines_pass(g, 1, dx[1], u, v, s, t));
-  } else {  // Y: lines along j; tile = consecutive i for fixed k
-    FastPass p{};
-    p.n = (int)ny;
-    p.layout = 0;
-    p.ninner = (int)nx;
-    p.nouter = (int)nz;
-    p.li = 1;
-    p.lo = nx * ny;
-    p.es = nx;
-    p.nterms = 3;
-    p.term[0] = Term{0, 0, 0};  // s = Jy u
-    p.term[1] = Term{1, 0, 1};  // t = Ly u
-    p.term[2] = Term{0, 1, 1};  //   + Jy v
-    p.ops[0] = make_op(0, ny, dx[1]);
-    p.ops[1] = make_op(1, ny, dx[1]);
-    p.in[0] = u;
-    p.in[1] = v;
-    p.out[0] = s;
-    p.out[1] = t;
-    p.nout = 2;
-    PB_TRY(launch_pass(g->ctx, p));
-  }
-  if (reg(nx)) {
-    PB_TRY(compact_lines_pass(g, 0, dx[0], s, t, out, nullptr));
-  } else {  // X: lines along i (contiguous); tile = consecutive j for fixed k
-    FastPass p{};
-    p.n = (int)nx;
-    p.layout = 1;
-    p.ninner = (int)ny;
-    p.nouter = (int)nz;
-    p.li = nx;
-    p.lo = nx * ny;
-    p.es = 1;
-    p.nterms = 2;
-    p.term[0] = Term{1, 0, 0};  // out = Lx s
-    p.term[1] = Term{0, 1, 0};  //     + Jx t
-    p.ops[0] = make_op(0, nx, dx[0]);
-    p.ops[1] = make_op(1, nx, dx[0]);
-    p.in[0] = s;
-    p.in[1] = t;
-    p.out[0] = out;
-    p.nout = 1;
-    PB_TRY(launch_pass(g->ctx, p));
-  }
-  return PB_OK;
+  PB_TRY(compact_pass_y(g->ctx, d, dx[1], u, v, s_, t));
+  return compact_pass_x(g->ctx, d, dx[0], s_, t, out);
 }
 
 }  // namespace pb
@@ -311,8 +338,6 @@ int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* o
 extern "C" int pb_compact_lapl_fast(pb_grid* g, const double dx[3], const pb_vec* f, pb_vec* out) {
   using namespace pb;
   PB_CHECK_ARG(g && dx && f && out && f != out, "bad lapl args");
-  if (g->ctx->nranks != 1)
-    return set_error(PB_ERR_UNSUPPORTED, "compact operators on a split grid: not yet");
   double* ws = nullptr;
   PB_TRY(ctx_scratch(g->ctx, (size_t)compact_fast_work_len(g), &ws));
   int rc = compact_lapl_fast(g, dx, f->d, out->d, ws);

@@ -522,13 +522,13 @@ static int launch_lines(pb_ctx* ctx, LinePass& p, int64_t n, int64_t nouter) {
 }
 
 // One pass of the factorised Laplacian with register line solves. axis: 2 = Z, 1 = Y, 0 = X.
-int compact_lines_pass(pb_grid* g, int axis, double h, const double* in0, const double* in1,
-                       double* out0, double* out1) {
-  const int64_t nx = g->n[0], ny = g->n[1], nz = g->nzl;
+int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, const double* in0,
+                       const double* in1, double* out0, double* out1) {
+  const int64_t nx = dims[0], ny = dims[1], nz = dims[2];
   const int64_t n = axis == 2 ? nz : (axis == 1 ? ny : nx);
   const int C = (int)(n / 64);
   static const char* names[3] = {"compact_lines_x", "compact_lines_y", "compact_lines_z"};
-  ScopedTimer tm(g->ctx, names[axis]);
+  ScopedTimer tm(ctx, names[axis]);
   LinePass p{};
   static const int ablate = env_int("PB_LINES_ABLATE", 0);
   p.ablate = ablate;
@@ -543,14 +543,14 @@ int compact_lines_pass(pb_grid* g, int axis, double h, const double* in0, const 
     p.lo = nx;
     p.es = nx * ny;
     p.ninner = (int)nx;
-    return launch_lines<0, 0>(g->ctx, p, n, ny);
+    return launch_lines<0, 0>(ctx, p, n, ny);
   }
   if (axis == 1) {
     p.li = 1;
     p.lo = nx * ny;
     p.es = nx;
     p.ninner = (int)nx;
-    return launch_lines<0, 1>(g->ctx, p, n, nz);
+    return launch_lines<0, 1>(ctx, p, n, nz);
   }
   p.li = nx;
   p.lo = nx * ny;
@@ -559,17 +559,17 @@ int compact_lines_pass(pb_grid* g, int axis, double h, const double* in0, const 
   static const int xdirect = env_int("PB_LINES_XDIRECT", 1);
   if (xdirect) {
     switch (C) {
-      case 1: return launch_x_direct<1>(g->ctx, p, ny * nz);
-      case 2: return launch_x_direct<2>(g->ctx, p, ny * nz);
-      case 3: return launch_x_direct<3>(g->ctx, p, ny * nz);
-      case 4: return launch_x_direct<4>(g->ctx, p, ny * nz);
-      case 6: return launch_x_direct<6>(g->ctx, p, ny * nz);
-      case 8: return launch_x_direct<8>(g->ctx, p, ny * nz);
-      case 12: return launch_x_direct<12>(g->ctx, p, ny * nz);
-      case 16: return launch_x_direct<16>(g->ctx, p, ny * nz);
+      case 1: return launch_x_direct<1>(ctx, p, ny * nz);
+      case 2: return launch_x_direct<2>(ctx, p, ny * nz);
+      case 3: return launch_x_direct<3>(ctx, p, ny * nz);
+      case 4: return launch_x_direct<4>(ctx, p, ny * nz);
+      case 6: return launch_x_direct<6>(ctx, p, ny * nz);
+      case 8: return launch_x_direct<8>(ctx, p, ny * nz);
+      case 12: return launch_x_direct<12>(ctx, p, ny * nz);
+      case 16: return launch_x_direct<16>(ctx, p, ny * nz);
     }
   }
-  return launch_lines<1, 2>(g->ctx, p, n, nz);
+  return launch_lines<1, 2>(ctx, p, n, nz);
 }
 
 }  // namespace pb

@@ -68,6 +68,10 @@ struct pb_ctx {
   pb_sendrecv_fn h_sendrecv = nullptr;
   pb_allreduce_fn h_allreduce = nullptr;
   void* h_user = nullptr;
+  pb_alltoallv_fn h_alltoallv = nullptr;
+  void* h_a2a_user = nullptr;
+  double* h_a2a = nullptr;  // pinned staging for the host all-to-all (send | recv)
+  size_t h_a2a_len = 0;
   // reduction scratch
   double* d_partials = nullptr;   // [max_blocks * 8]
   int64_t partials_cap = 0;
@@ -193,8 +197,20 @@ inline int env_int(const char* name, int dflt) {
 
 // ---- register-resident line solves (pb_compact_lines.hip) ----
 bool compact_lines_supported(int64_t n);
-int compact_lines_pass(pb_grid* g, int axis, double h, const double* in0, const double* in1,
-                       double* out0, double* out1);
+int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, const double* in0,
+                       const double* in1, double* out0, double* out1);
+// the three passes of the factorised compact Laplacian on a box with complete lines
+int compact_pass_z(pb_ctx* ctx, const int64_t d[3], double h, const double* f, double* u, double* v);
+int compact_pass_y(pb_ctx* ctx, const int64_t d[3], double h, const double* u, const double* v,
+                   double* s, double* t);
+int compact_pass_x(pb_ctx* ctx, const int64_t d[3], double h, const double* s, const double* t,
+                   double* out);
+// ---- multi-rank Z pass: z-slab <-> y-slab all-to-all transposes (compact_dist.cpp) ----
+int64_t compact_dist_work_len(const pb_grid* g);
+int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double* v, double* work);
+// all-to-all with per-peer counts; blocks are contiguous in rank order on both sides
+int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,
+                     const int64_t* rcount);
 int launch_cg_generic_p(pb_grid* g, const double* r, double* p, CgState* st);
 int launch_cg_generic_dot(pb_grid* g, const double* p, const double* w, CgState* st, int* nparts);
 int launch_cg_generic_xr(pb_grid* g, const double* p, const double* w, double* x, double* r,

@@ -135,6 +135,57 @@ int halo_end(pb_grid* g) {
   return PB_OK;
 }
 
+int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,
+                     const int64_t* rcount) {
+  ScopedTimer tm(ctx, "alltoallv");
+  const int P = ctx->nranks;
+  std::vector<int64_t> so(P + 1, 0), ro(P + 1, 0);
+  for (int p = 0; p < P; ++p) {
+    so[p + 1] = so[p] + scount[p];
+    ro[p + 1] = ro[p] + rcount[p];
+  }
+  if (P == 1) {
+    if (scount[0])
+      PB_HIP(hipMemcpyAsync(recv, send, scount[0] * sizeof(double), hipMemcpyDeviceToDevice,
+                            ctx->stream));
+    return PB_OK;
+  }
+  if (ctx->comm) {
+    PB_NCCL(ncclGroupStart());
+    for (int p = 0; p < P; ++p) {
+      if (p == ctx->rank) continue;
+      if (scount[p])
+        PB_NCCL(ncclSend(send + so[p], (size_t)scount[p], ncclDouble, p, ctx->comm, ctx->stream));
+      if (rcount[p])
+        PB_NCCL(ncclRecv(recv + ro[p], (size_t)rcount[p], ncclDouble, p, ctx->comm, ctx->stream));
+    }
+    PB_NCCL(ncclGroupEnd());
+    const int me = ctx->rank;
+    if (scount[me])
+      PB_HIP(hipMemcpyAsync(recv + ro[me], send + so[me], scount[me] * sizeof(double),
+                            hipMemcpyDeviceToDevice, ctx->stream));
+    return PB_OK;
+  }
+  if (!ctx->h_alltoallv)
+    return set_error(PB_ERR_COMM, "host transport without an alltoallv callback");
+  const size_t need = (size_t)(so[P] + ro[P]);
+  if (need > ctx->h_a2a_len) {
+    if (ctx->h_a2a) PB_HIP(hipHostFree(ctx->h_a2a));
+    ctx->h_a2a = nullptr;
+    PB_HIP(hipHostMalloc(&ctx->h_a2a, need * sizeof(double), hipHostMallocDefault));
+    ctx->h_a2a_len = need;
+  }
+  double* hs = ctx->h_a2a;
+  double* hr = ctx->h_a2a + so[P];
+  PB_HIP(hipMemcpyAsync(hs, send, so[P] * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  PB_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->h_alltoallv(ctx->h_a2a_user, hs, scount, hr, rcount) != 0)
+    return set_error(PB_ERR_COMM, "host alltoallv callback failed");
+  PB_HIP(hipMemcpyAsync(recv, hr, ro[P] * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  PB_HIP(hipStreamSynchronize(ctx->stream));
+  return PB_OK;
+}
+
 int ctx_scratch(pb_ctx* ctx, size_t n, double** out) {
   if (n > ctx->scratch_len) {
     PB_HIP(hipStreamSynchronize(ctx->stream));  // previous users of the old buffer are done
@@ -266,6 +317,13 @@ int pb_ctx_set_host_transport(pb_ctx* ctx, pb_sendrecv_fn sr, pb_allreduce_fn ar
   return PB_OK;
 }
 
+int pb_ctx_set_host_alltoallv(pb_ctx* ctx, pb_alltoallv_fn fn, void* user) {
+  PB_CHECK_ARG(ctx && fn, "bad host alltoallv");
+  ctx->h_alltoallv = fn;
+  ctx->h_a2a_user = user;
+  return PB_OK;
+}
+
 int pb_ctx_get_rank(const pb_ctx* ctx, int* rank, int* nranks) {
   PB_CHECK_ARG(ctx, "ctx is NULL");
   if (rank) *rank = ctx->rank;
@@ -297,6 +355,7 @@ int pb_ctx_destroy(pb_ctx* ctx) {
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->h_a2a) (void)hipHostFree(ctx->h_a2a);
   (void)hipFree(ctx->d_partials);
   (void)hipFree(ctx->d_scalars);
   (void)hipHostFree(ctx->h_scalars);

@@ -65,10 +65,6 @@ int pb_op_create(pb_grid* g, int kind, const double deltas[3], pb_op** out) {
   op->cz = s.cz;
   op->cc = s.cc;
   if (kind == PB_OP_COMPACT) {
-    if (g->ctx->nranks != 1) {
-      delete op;
-      return set_error(PB_ERR_UNSUPPORTED, "compact operator on a split grid is not supported yet");
-    }
     op->work_len = compact_fast_work_len(g);
     if (hipMalloc(&op->work, (size_t)op->work_len * sizeof(double)) != hipSuccess) {
       delete op;

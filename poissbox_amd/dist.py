@@ -65,3 +65,25 @@ class GlooTransport:
         v = self.torch.from_numpy(np.ascontiguousarray(vals, dtype=np.float64).copy())
         self.dist.all_reduce(v, group=self.group)
         return v.numpy()
+
+    def alltoallv(self, blocks, recv_sizes):
+        """blocks[p] goes to rank p; returns the blocks received from every rank
+        (recv_sizes[p] doubles from rank p)."""
+        t = self.torch
+        out = [None] * self.world
+        out[self.rank] = np.array(blocks[self.rank], copy=True)
+        reqs, bufs = [], {}
+        for p in range(self.world):
+            if p == self.rank:
+                continue
+            bufs[p] = t.empty(int(recv_sizes[p]), dtype=t.float64)
+            if recv_sizes[p]:
+                reqs.append(self.dist.irecv(bufs[p], p, self.group, tag=3))
+            if len(blocks[p]):
+                reqs.append(self.dist.isend(t.from_numpy(np.ascontiguousarray(blocks[p])), p,
+                                            self.group, tag=3))
+        for q in reqs:
+            q.wait()
+        for p, b in bufs.items():
+            out[p] = b.numpy()
+        return out

@@ -163,3 +163,17 @@ def test_distributed_cg_matches_single_rank(world):
     for reason, its, hist in _run(world, _slab_cg):
         assert (reason, its) == (ro, itso)
         assert np.max(np.abs(np.array(hist) - ho) / ho) < 1e-9
+
+
+def _a2a_protocol(rank, world, tr):
+    blocks = [np.full(p + 1 + rank, 10.0 * rank + p) for p in range(world)]
+    sizes = [rank + 1 + p for p in range(world)]   # rank p sends me rank + 1 + p doubles
+    return [b.tolist() for b in tr.alltoallv(blocks, sizes)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_alltoallv_protocol(world):
+    res = _run(world, _a2a_protocol)
+    for rank, got in enumerate(res):
+        for p in range(world):
+            assert got[p] == [10.0 * p + rank] * (rank + 1 + p)

@@ -19,7 +19,7 @@ N3 = (24, 20, 13)
 def _gpu_rank(rank, world, tr):
     import poissbox_amd as pb
     ctx = pb.Context(0, rank, world)
-    ctx.set_host_transport(tr.sendrecv, tr.allreduce)
+    ctx.set_host_transport(tr.sendrecv, tr.allreduce, tr.alltoallv)
     da = pb.DA(ctx, N3)
     (_, _, k0), (_, _, nk) = da.get_corners()
     h = da.spacing
@@ -46,6 +46,34 @@ def test_multiprocess_cg_on_one_gpu(world):
         assert (reason, its) == (ro, itso)
         assert np.max(np.abs(hist - ho) / ho) < 1e-7
         assert np.max(np.abs(xs - xz[k0:k0 + nk].reshape(-1))) <= 1e-6 * np.max(np.abs(xo))
+
+
+def _gpu_rank_compact(rank, world, tr):
+    import poissbox_amd as pb
+    n = (64, 32, 64)
+    ctx = pb.Context(0, rank, world)
+    ctx.set_host_transport(tr.sendrecv, tr.allreduce, tr.alltoallv)
+    da = pb.DA(ctx, n, (2 * np.pi,) * 3)
+    (_, _, k0), (_, _, nk) = da.get_corners()
+    from oracle import oracle as O
+    f = O.fill_random(int(np.prod(n)), 5).reshape(n[2], -1)
+    fv, out = pb.Vec(da), pb.Vec(da)
+    fv.set_values(f[k0:k0 + nk])
+    pb.compact_lapl_fast(da, da.spacing, fv, out)
+    res = (k0, nk, out.get_values())
+    ctx.destroy()
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multiprocess_compact_lapl(world):
+    """z-slab <-> y-slab transposes through the gloo alltoallv between processes."""
+    from oracle import oracle as O
+    n = (64, 32, 64)
+    h = tuple(2 * np.pi / m for m in n)
+    ref = O.lapl(O.fill_random(int(np.prod(n)), 5), n, h).reshape(n[2], -1)
+    for k0, nk, y in _run(world, _gpu_rank_compact):
+        assert np.max(np.abs(y - ref[k0:k0 + nk].reshape(-1))) <= 1e-12 * np.max(np.abs(ref))
 
 
 def test_bench_two_ranks_host_transport():
