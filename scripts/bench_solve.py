@@ -24,8 +24,16 @@ def main():
     for n in sizes:
         n3 = (n, n, n)
         h = (1.0 / n,) * 3
-        da = pb.DA(ctx, n3)
-        P, A, x, b = pb.initialise_linear_system(da, h)
+        op = os.environ.get("OP", "star7")
+        if op == "compact":  # config 5 shape: compact A, 7-point P, periodic 2*pi box
+            h = (2 * np.pi / n,) * 3
+            da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+            P = pb.Mat(da, pb.ASSEMBLED27, h)
+            A = pb.Mat(da, pb.COMPACT, h)
+            x, b = pb.Vec(da), pb.Vec(da)
+        else:
+            da = pb.DA(ctx, n3)
+            P, A, x, b = pb.initialise_linear_system(da, h)
         xt = pb.Vec(da)
         xt.set_random(SEED)
         A.mult(xt, b)
@@ -46,7 +54,7 @@ def main():
             parts = {}
             for nm in ("mg_fine_smooth_first", "mg_fine_resid_restrict", "mg_fine_prolong_post",
                        "mg_coarse_levels", "cg_pass_a", "cg_pass_b", "cg_pass_b_even",
-                       "cg_pass_b_odd"):
+                       "cg_pass_b_odd", "compact_lapl_fast"):
                 ms_, c_ = ctx.timing(nm)
                 if c_ and mg_cnt:
                     parts[nm] = ms_ / mg_cnt
@@ -54,7 +62,7 @@ def main():
             r = pb.Vec(da)
             A.mult(x, r)
             r.axpy(-1.0, b)
-            out = {"n": n, "pc": pc, "reason": int(reason), "its": int(its), "solve_ms": dt * 1e3,
+            out = {"n": n, "op": op, "pc": pc, "reason": int(reason), "its": int(its), "solve_ms": dt * 1e3,
                    "ms_per_it": dt * 1e3 / max(its, 1), "levels": k.pc_levels,
                    "rel_residual": r.norm() / b.norm(),
                    "mg_apply_ms": (mg_ms / mg_cnt) if mg_cnt else None,
