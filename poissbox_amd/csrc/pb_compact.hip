@@ -354,9 +354,14 @@ int pb_pcr_alpha_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_st
                          int64_t elem_stride, double alpha, double* d) {
   PB_CHECK_ARG(ctx && d, "bad pcr args");
   PB_CHECK_ARG(n >= 3 && n <= 4096 && nbatch >= 1, "pcr: 3 <= n <= 4096");
-  PB_CHECK_ARG((n & (n - 1)) == 0, "pcr: n must be a power of two");
-  LineMap lm{nbatch, line_stride, 0, elem_stride};
   ScopedTimer tm(ctx, "pcr");
+  static const int lines_ok = env_int("PB_PCR_LINES", 1);
+  if (lines_ok) {  // register-resident factorised solve with cross-lane scans (n = 64*C)
+    const int rc = lines_solve_batched(ctx, n, nbatch, line_stride, elem_stride, alpha, d);
+    if (rc != PB_ERR_UNSUPPORTED) return rc;
+  }
+  PB_CHECK_ARG((n & (n - 1)) == 0, "pcr: n must be a power of two (or 64*{1,2,3,4,6,8,12,16})");
+  LineMap lm{nbatch, line_stride, 0, elem_stride};
   hipLaunchKernelGGL(pcr_alpha_kernel, dim3((unsigned)nbatch), dim3(256), 4 * n * sizeof(double),
                      ctx->stream, n, lm, alpha, d);
   PB_HIP(hipGetLastError());

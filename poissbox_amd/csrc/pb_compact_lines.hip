@@ -318,7 +318,7 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
     tile_put(lds, nl, pre);
     __syncthreads();
     if (K::PF) {
-      if (PASS == 0) {
+      if (PASS == 0 || PASS == 3) {
         if (tn < ntiles) tile_fetch(p, p.in0, base_n, nl_n, pre);
       } else {
         tile_fetch(p, p.in1, base, nl, pre);
@@ -330,6 +330,13 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
       if (l >= nl) continue;
       double x[C], r[C];
       chunk_read<C>(lds, l, lane, x);
+      if (PASS == 3) {  // batched (alpha, 1, alpha) periodic solve
+#pragma unroll
+        for (int m = 0; m < C; ++m) r[m] = x[m];
+        line_solve<C>(r, p.J, lane);
+        chunk_write<C>(lds, l, lane, r);
+        continue;
+      }
       if (PASS != 2) {
         line_op<C>(x, r, p.J, lane, p.ablate);
         chunk_write<C>(lds, l, lane, r);
@@ -337,6 +344,10 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
       line_op<C>(x, keep[j], p.L, lane, p.ablate);
     }
     __syncthreads();
+    if (PASS == 3) {
+      tile_store<C, LAYOUT, TL, V, NT>(p, p.out0, lds, base, nl);
+      continue;
+    }
     if (PASS == 0) {
       tile_store<C, LAYOUT, TL, V, NT>(p, p.out0, lds, base, nl);
       __syncthreads();
@@ -446,6 +457,85 @@ static int launch_x_direct(pb_ctx* ctx, LinePass& p, int64_t nlines) {
   return PB_OK;
 }
 
+// batched solve on contiguous lines (element stride 1, line stride li): one wave per line,
+// redistributed through a wave-private LDS strip like the X pass
+template <int C>
+__global__ __launch_bounds__(256) void lines_solve_direct(LinePass p, int64_t nlines) {
+  constexpr int LP = Lds<C>::LP, CP = Lds<C>::CP;
+  __shared__ double strip[4][LP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t line = (int64_t)blockIdx.x * 4 + wave;
+  if (line >= nlines) return;
+  double* sl = strip[wave];
+  const int64_t off = line * p.li;
+  constexpr int NP = 32 * C;
+  constexpr int R = (NP + 63) / 64;
+  dv2 a[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = lane + 64 * r;
+    if (NP % 64 == 0 || q < NP) a[r] = __builtin_nontemporal_load((const dv2*)(p.in0 + off) + q);
+  }
+  auto w = [&](int e) { return (e / C) * CP + (e % C); };
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = lane + 64 * r;
+    if (NP % 64 == 0 || q < NP) {
+      sl[w(2 * q)] = a[r].x;
+      sl[w(2 * q + 1)] = a[r].y;
+    }
+  }
+  wave_sync();
+  double x[C];
+#pragma unroll
+  for (int m = 0; m < C; ++m) x[m] = sl[lane * CP + m];
+  line_solve<C>(x, p.J, lane);
+  wave_sync();
+#pragma unroll
+  for (int m = 0; m < C; ++m) sl[lane * CP + m] = x[m];
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int q = lane + 64 * r;
+    if (NP % 64 == 0 || q < NP) {
+      dv2 o;
+      o.x = sl[w(2 * q)];
+      o.y = sl[w(2 * q + 1)];
+      __builtin_nontemporal_store(o, (dv2*)(p.out0 + off) + q);
+    }
+  }
+}
+
+template <int C>
+static int launch_solve_direct(pb_ctx* ctx, LinePass& p, int64_t nlines) {
+  hipLaunchKernelGGL(lines_solve_direct<C>, dim3((unsigned)((nlines + 3) / 4)), dim3(256), 0,
+                     ctx->stream, p, nlines);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+static LineOp make_solve_op(double alpha, int C) {
+  LineOp o{};
+  const double q = 2.0 * alpha / (1.0 + std::sqrt(1.0 - 4.0 * alpha * alpha));
+  o.mq = -q;
+  o.inv_kappa = q / alpha;
+  double pw = 1.0;
+  for (int m = 0; m < C; ++m) {
+    pw *= -q;
+    o.pw[m] = pw;
+  }
+  double g = pw;
+  int s = 0;
+  for (; s < 6; ++s) {
+    if (std::fabs(g) < 1e-24) break;
+    o.gs[s] = g;
+    g = g * g;
+  }
+  o.nsteps = s;
+  o.corr = s == 6 ? 1.0 / (1.0 - g) : 1.0;
+  return o;
+}
+
 bool compact_lines_supported(int64_t n) {
   if (n % 64) return false;
   const int64_t C = n / 64;
@@ -478,7 +568,8 @@ static int launch_lines_v(pb_ctx* ctx, LinePass& p, int64_t nouter) {
 // 16-byte pairs when the contiguous direction has even length (always for LAYOUT 1, n = 64*C)
 template <int C, int LAYOUT, int PASS, class K>
 static int launch_lines_k(pb_ctx* ctx, LinePass& p, int64_t nouter) {
-  if (LAYOUT == 1 || (p.ninner % 2 == 0 && p.li == 1 && p.lo % 2 == 0 && p.es % 2 == 0))
+  if (LAYOUT == 1 || (p.ninner % 2 == 0 && p.li == 1 && p.lo % 2 == 0 && p.es % 2 == 0 &&
+                      ((uintptr_t)p.in0 & 15) == 0 && ((uintptr_t)p.out0 & 15) == 0))
     return launch_lines_v<C, LAYOUT, PASS, K, 2>(ctx, p, nouter);
   return launch_lines_v<C, LAYOUT, PASS, K, 1>(ctx, p, nouter);
 }
@@ -570,6 +661,42 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
     }
   }
   return launch_lines<1, 2>(ctx, p, n, nz);
+}
+
+// Batched periodic (alpha, 1, alpha) solve, in place, n = 64*C points per line: contiguous
+// lines (elem_stride 1) one wave each; interleaved lines (line_stride 1) through the LDS tile
+// transpose. Returns PB_ERR_UNSUPPORTED for other layouts (the caller falls back to LDS PCR).
+int lines_solve_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                        int64_t elem_stride, double alpha, double* d) {
+  if (!compact_lines_supported(n) || !(alpha > 0.0 && alpha < 0.5))
+    return PB_ERR_UNSUPPORTED;
+  const int C = (int)(n / 64);
+  LinePass p{};
+  p.in0 = d;
+  p.out0 = d;
+  p.J = make_solve_op(alpha, C);
+  const bool al16 = ((uintptr_t)d & 15) == 0;
+  if (elem_stride == 1 && line_stride % 2 == 0 && al16 && line_stride >= n) {
+    p.li = line_stride;
+    switch (C) {
+      case 1: return launch_solve_direct<1>(ctx, p, nbatch);
+      case 2: return launch_solve_direct<2>(ctx, p, nbatch);
+      case 3: return launch_solve_direct<3>(ctx, p, nbatch);
+      case 4: return launch_solve_direct<4>(ctx, p, nbatch);
+      case 6: return launch_solve_direct<6>(ctx, p, nbatch);
+      case 8: return launch_solve_direct<8>(ctx, p, nbatch);
+      case 12: return launch_solve_direct<12>(ctx, p, nbatch);
+      case 16: return launch_solve_direct<16>(ctx, p, nbatch);
+    }
+  }
+  if (line_stride == 1 && elem_stride >= nbatch) {
+    p.li = 1;
+    p.lo = 0;
+    p.es = elem_stride;
+    p.ninner = (int)nbatch;
+    return launch_lines<0, 3>(ctx, p, n, 1);
+  }
+  return PB_ERR_UNSUPPORTED;
 }
 
 }  // namespace pb

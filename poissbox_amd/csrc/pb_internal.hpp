@@ -199,6 +199,9 @@ inline int env_int(const char* name, int dflt) {
 bool compact_lines_supported(int64_t n);
 int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, const double* in0,
                        const double* in1, double* out0, double* out1);
+// batched periodic (alpha,1,alpha) solve in registers (n = 64*C); PB_ERR_UNSUPPORTED otherwise
+int lines_solve_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                        int64_t elem_stride, double alpha, double* d);
 // the three passes of the factorised compact Laplacian on a box with complete lines
 int compact_pass_z(pb_ctx* ctx, const int64_t d[3], double h, const double* f, double* u, double* v);
 int compact_pass_y(pb_ctx* ctx, const int64_t d[3], double h, const double* u, const double* v,

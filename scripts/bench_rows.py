@@ -7,7 +7,7 @@ Prints one JSON line per row: {"row", "kernel", "size", "avg_ms", "bytes_per_dof
   a2 CG iteration (fused, deferred) 60 B/DoF    512^3 (passes reported by bench.py)
   a12 tdma (general, batched)       48 B/DoF    512 x 512^2 lines (read a,b,c,d; write b,d)
   a13 tdma_periodic (batched)       40 B/DoF    512 x 512^2 lines (read a,b,c,d; write d)
-  PCR (alpha,1,alpha) batched       16 B/DoF    512 x 512^2 lines
+  PCR (alpha,1,alpha) batched       16 B/DoF    512 x 512^2 lines, interleaved and contiguous
   a15 compact 1-D (grad_1d)         16 B/DoF    512 x 512^2 lines (reference order, bit-exact)
   a16 compact lapl, reference order 80 B/DoF*   256^3   (*the 3-pass algorithmic minimum)
   a16 compact lapl, 3-pass + PCR    80 B/DoF    512^3 and 256^3
@@ -108,7 +108,9 @@ def main():
     row("a13", "tdma_periodic (Sherman-Morrison, one lane per line)", "512 x 512^2", n * nb, 40, ms,
         {"dofs_per_s_1core": n / tc, "sample": "oracle pbo_tdma_periodic, one 512 line"})
     ms = timed(ctx, lambda: pb.pcr_alpha_batched(ctx, n, nb, 1, nb, 0.3, bufs["d"]), 5, "pcr")
-    row("PCR", "pcr_alpha (one workgroup per line, LDS)", "512 x 512^2", n * nb, 16, ms)
+    row("PCR", "batched (a,1,a) solve, interleaved lines", "512 x 512^2", n * nb, 16, ms)
+    ms = timed(ctx, lambda: pb.pcr_alpha_batched(ctx, n, nb, n, 1, 0.3, bufs["d"]), 5, "pcr")
+    row("PCR", "batched (a,1,a) solve, contiguous lines", "512 x 512^2", n * nb, 16, ms)
     ms = timed(ctx, lambda: pb.compact_1d_batched(ctx, 0, -1, 0.01, n, nb, 1, nb, bufs["a"],
                                                   bufs["d"]), 5, "compact_1d")
     f1 = host["a"][:n].copy()

@@ -405,6 +405,33 @@ def test_pcr_alpha_matches_thomas(ctx):
         buf.free()
 
 
+@pytest.mark.parametrize("n,nb,layout,alpha", [(512, 37, "contig", 3 / 10), (512, 64, "inter", 9 / 62),
+                                               (192, 20, "contig", 3 / 10), (128, 33, "inter", 3 / 10),
+                                               (64, 6, "contig", 9 / 62), (1024, 8, "inter", 3 / 10),
+                                               (96, 4, "contig", 3 / 10)])
+def test_pcr_batched_layouts(ctx, n, nb, layout, alpha):
+    """Batched periodic (alpha,1,alpha) solve in both layouts of the batched API: contiguous lines
+    (register path, one wave per line), interleaved lines (LDS tile transpose), and an n the
+    register path does not take (96: LDS PCR fallback is power-of-two only -> error)."""
+    rng = np.random.default_rng(n + nb)
+    d = rng.random((nb, n)) * 2 - 1
+    ref = np.stack([O.tdma(np.full(n, alpha), np.ones(n), np.full(n, alpha), row,
+                           periodic=True)[1] for row in d])
+    host = d if layout == "contig" else np.ascontiguousarray(d.T)
+    buf = Dev(host.reshape(-1))
+    ls, es = (n, 1) if layout == "contig" else (1, nb)
+    if n == 96:
+        with pytest.raises(pb.PbError):
+            pb.pcr_alpha_batched(ctx, n, nb, ls, es, alpha, buf.p)
+        buf.free()
+        return
+    pb.pcr_alpha_batched(ctx, n, nb, ls, es, alpha, buf.p)
+    got = buf.get().reshape(host.shape)
+    got = got if layout == "contig" else got.T
+    assert np.max(np.abs(got - ref)) <= 1e-13 * np.max(np.abs(ref))
+    buf.free()
+
+
 # ---------------------------------------------------------------------------------------------
 # compact Laplacian fast path (3-pass factorisation + PCR) and CG with the compact operator
 # ---------------------------------------------------------------------------------------------
