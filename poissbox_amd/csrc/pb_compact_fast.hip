@@ -314,7 +314,7 @@ int compact_pass_x(pb_ctx* ctx, const int64_t d[3], double h, const double* s_, 
 // work doubles: 4 N (u, v, s, t) on one rank; on N ranks also the y-slab fields and the
 // transpose staging (compact_dist.cpp)
 int64_t compact_fast_work_len(const pb_grid* g) {
-  if (g->ctx->nranks == 1) return 4 * g->nlocal;
+  if (!g->ctx->split) return 4 * g->nlocal;
   return 4 * g->nlocal + compact_dist_work_len(g);
 }
 
@@ -324,7 +324,7 @@ int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* o
   const int64_t N = g->nlocal;
   double *u = work, *v = work + N, *s_ = work + 2 * N, *t = work + 3 * N;
   const int64_t d[3] = {g->n[0], g->n[1], g->nzl};
-  if (g->ctx->nranks == 1) {
+  if (!g->ctx->split) {
     PB_TRY(compact_pass_z(g->ctx, d, dx[2], f, u, v));
   } else {  // z-lines span the slabs: transpose to y-slabs, Z pass, transpose u, v back
     PB_TRY(compact_dist_pass_z(g, dx[2], f, u, v, work + 4 * N));

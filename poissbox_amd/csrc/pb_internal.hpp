@@ -60,6 +60,9 @@ struct pb_ctx {
   int device = 0;
   int rank = 0;
   int nranks = 1;
+  // decomposed code paths (halo exchange, allreduce, transposes): nranks > 1, or one rank with
+  // PB_FORCE_COMM=1 (a 1-rank RCCL communicator: exercises the RCCL paths on a single GPU)
+  bool split = false;
   hipStream_t stream = nullptr;
   hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with interior planes
   hipEvent_t ev_ready = nullptr, ev_done = nullptr;

@@ -297,7 +297,7 @@ static int mg_blocks(pb_ctx* ctx, int64_t n) {
 // ghost planes of v on level L: in place (1 rank) or exchanged (N ranks)
 static int ghosts(MgLevel& L, const double* v, const double** lo, const double** hi) {
   pb_grid* g = L.g;
-  if (g->ctx->nranks == 1) {
+  if (!g->ctx->split) {
     *lo = v + (g->nzl - 1) * g->plane;
     *hi = v;
     return PB_OK;

@@ -77,7 +77,7 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
   pb_ctx* ctx = g->ctx;
   ScopedTimer tm(ctx, "halo");
   const int64_t cnt = g->plane;
-  if (ctx->nranks == 1) {
+  if (!ctx->split) {
     PB_HIP(hipMemcpyAsync(g->ghost_lo, hi, cnt * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
     PB_HIP(hipMemcpyAsync(g->ghost_hi, lo, cnt * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
     return PB_OK;
@@ -112,7 +112,7 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
 
 int halo_begin(pb_grid* g, const double* lo, const double* hi) {
   pb_ctx* ctx = g->ctx;
-  if (ctx->nranks == 1 || !ctx->comm) return halo_exchange(g, lo, hi);
+  if (!ctx->split || !ctx->comm) return halo_exchange(g, lo, hi);
   const int64_t cnt = g->plane;
   const int down = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
   const int up = (ctx->rank + 1) % ctx->nranks;
@@ -130,7 +130,7 @@ int halo_begin(pb_grid* g, const double* lo, const double* hi) {
 
 int halo_end(pb_grid* g) {
   pb_ctx* ctx = g->ctx;
-  if (ctx->nranks == 1 || !ctx->comm) return PB_OK;
+  if (!ctx->split || !ctx->comm) return PB_OK;
   PB_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_done, 0));
   return PB_OK;
 }
@@ -144,7 +144,7 @@ int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, dou
     so[p + 1] = so[p] + scount[p];
     ro[p + 1] = ro[p] + rcount[p];
   }
-  if (P == 1) {
+  if (P == 1 && !ctx->comm) {
     if (scount[0])
       PB_HIP(hipMemcpyAsync(recv, send, scount[0] * sizeof(double), hipMemcpyDeviceToDevice,
                             ctx->stream));
@@ -201,7 +201,7 @@ int ctx_scratch(pb_ctx* ctx, size_t n, double** out) {
 }
 
 int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
-  if (ctx->nranks == 1) return PB_OK;
+  if (!ctx->split) return PB_OK;
   ScopedTimer tm(ctx, "allreduce");
   if (ctx->h_allreduce) {
     PB_HIP(hipMemcpyAsync(ctx->h_scalars + 16, d_vals, count * sizeof(double), hipMemcpyDeviceToHost,
@@ -305,6 +305,13 @@ int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb
     memcpy(&id, uid, 128);
     PB_NCCL(ncclCommInitRank(&ctx->comm, nranks, id, rank));
   }
+  ctx->split = nranks > 1;
+  if (nranks == 1 && env_int("PB_FORCE_COMM", 0)) {
+    ncclUniqueId id;
+    PB_NCCL(ncclGetUniqueId(&id));
+    PB_NCCL(ncclCommInitRank(&ctx->comm, 1, id, 0));
+    ctx->split = true;
+  }
   *out = ctx;
   return PB_OK;
 }
@@ -340,7 +347,7 @@ int pb_ctx_sync(pb_ctx* ctx) {
 int pb_ctx_barrier(pb_ctx* ctx) {
   PB_CHECK_ARG(ctx, "ctx is NULL");
   PB_HIP(hipStreamSynchronize(ctx->stream));
-  if (ctx->nranks > 1) {
+  if (ctx->split) {
     PB_TRY(allreduce_device(ctx, ctx->d_scalars + 32, 1));
     PB_HIP(hipStreamSynchronize(ctx->stream));
   }

@@ -81,7 +81,7 @@ static int op_apply_raw(pb_op* op, const double* x, double* y) {
   if (op->kind == PB_OP_COMPACT) return compact_lapl_fast(g, op->deltas, x, y, op->work);
   // STAR7 and ASSEMBLED27 (the assembled BOX matrix has the same 7 non-zeros per row)
   StencilPlanes gp;
-  if (g->ctx->nranks == 1) {
+  if (!g->ctx->split) {
     gp.ghost_lo = x + (g->nzl - 1) * g->plane;  // periodic wrap: no copy
     gp.ghost_hi = x;
     return launch_star7_apply(g, s, x, y, gp, PLANES_ALL);
@@ -359,7 +359,7 @@ static int enqueue_iteration(pb_ksp* k) {
   PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st));
   StencilPlanes gp;
   int nparts = 0;
-  if (ctx->nranks == 1) {
+  if (!ctx->split) {
     gp.ghost_lo = g->bnd_hi;  // p_new of plane nzl-1 wraps below plane 0
     gp.ghost_hi = g->bnd_lo;
     PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));

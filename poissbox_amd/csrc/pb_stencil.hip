@@ -733,7 +733,7 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
 static int cg_reduce_update(pb_ctx* ctx, int stage, int nparts, int width, CgState* st,
                             double* hist, int* h_done, int64_t host_iter) {
   double* sums = ctx->d_scalars;
-  if (ctx->nranks == 1) {
+  if (!ctx->split) {
     hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
                        nparts, width, sums, 3, stage, st, hist, h_done, host_iter);
     PB_HIP(hipGetLastError());

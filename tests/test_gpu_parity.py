@@ -7,6 +7,7 @@ restatement (reduction order differs), same iteration count and stopping reason.
 """
 import ctypes as C
 import queue
+import os
 import threading
 
 import numpy as np
@@ -664,3 +665,38 @@ def test_multirank_cg_compact_operator_mg():
         k = min(len(hist), len(ho))
         assert np.max(np.abs(hist[:k - 1] - ho[:k - 1]) / ho[:k - 1]) < 1e-6
         assert np.max(np.abs(xs - xo.reshape(32, -1)[k0:k0 + nk].reshape(-1))) <= 1e-6 * np.max(np.abs(xo))
+
+
+def test_rccl_code_paths_one_rank_communicator():
+    """PB_FORCE_COMM=1 gives a 1-rank context an RCCL communicator and the decomposed code paths:
+    the halo exchange (ncclSend/ncclRecv to self, interior/boundary overlap split), the RCCL
+    allreduce of the CG sums, the compact transposes and the MG level halos -- the paths the
+    multi-GPU driver runs, exercised on one GPU (two ranks cannot share a device under RCCL)."""
+    os.environ["PB_FORCE_COMM"] = "1"
+    try:
+        ctx = pb.Context(0)
+    finally:
+        del os.environ["PB_FORCE_COMM"]
+    n3 = (32, 24, 16)
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    xt = O.fill_random(N, SEED)
+    b = O.stencil(xt, n3, h)
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    y = pb.Vec(da)
+    xv = pb.Vec(da)
+    xv.set_values(xt)
+    A.mult(xv, y)
+    assert np.array_equal(y.get_values(), b)
+    bv.set_values(b)
+    for pc in ("jacobi", "mg"):
+        xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-9, pc=pc)
+        reason, its, hist = pb.solve(P, A, x, bv, ["-pc_type", pc, "-ksp_rtol", "1e-9"])
+        assert (reason, its) == (ro, itso)
+        assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
+    hc = tuple(2 * np.pi / m for m in n3)
+    ref = O.lapl(xt, n3, hc)
+    pb.compact_lapl_fast(da, hc, xv, y)
+    assert np.max(np.abs(y.get_values() - ref)) <= FAST_RTOL * np.max(np.abs(ref))
+    ctx.destroy()
