@@ -125,6 +125,10 @@ int pb_op_create(pb_grid* grid, int kind, const double deltas[3], pb_op** op);
 int pb_op_apply(pb_op* op, const pb_vec* x, pb_vec* y); /* ≙ MatMult(A, x, y) */
 int pb_op_get_diagonal(const pb_op* op, double* diag);  /* constant diagonal of the 7-pt P */
 int pb_op_destroy(pb_op* op);
+/* ≙ MatGetOwnershipRange / VecGetOwnershipRange (src/example.f90:137-147): global row range
+ * [first, next) owned by this rank (rank-contiguous natural order of the z-slab split). */
+int pb_op_get_ownership_range(const pb_op* op, int64_t* first, int64_t* next);
+int pb_vec_get_ownership_range(const pb_vec* v, int64_t* first, int64_t* next);
 
 /* ---- KSP (replaces solve(P, A, x, b), src/poissbox.f90:269-298 -> KSPSolve) ---- */
 enum pb_ksp_type { PB_KSP_CG = 0 };

@@ -77,6 +77,8 @@ _SIGS = {
     "pb_op_apply": [c_p, c_p, c_p],
     "pb_op_get_diagonal": [c_p, P_d],
     "pb_op_destroy": [c_p],
+    "pb_op_get_ownership_range": [c_p, P_i64, P_i64],
+    "pb_vec_get_ownership_range": [c_p, P_i64, P_i64],
     "pb_ksp_opts_default": [C.POINTER(KspOpts)],
     "pb_ksp_opts_parse": [C.POINTER(KspOpts), C.c_int, C.POINTER(C.c_char_p)],
     "pb_ksp_create": [c_p, c_p, C.POINTER(KspOpts), C.POINTER(c_p)],

@@ -106,6 +106,22 @@ int pb_op_apply(pb_op* op, const pb_vec* x, pb_vec* y) {
   return op_apply_raw(op, x->d, y->d);
 }
 
+int pb_op_get_ownership_range(const pb_op* op, int64_t* first, int64_t* next) {
+  PB_CHECK_ARG(op && first && next, "bad args");
+  const pb_grid* g = op->grid;
+  *first = g->k0 * g->plane;
+  *next = (g->k0 + g->nzl) * g->plane;
+  return PB_OK;
+}
+
+int pb_vec_get_ownership_range(const pb_vec* v, int64_t* first, int64_t* next) {
+  PB_CHECK_ARG(v && first && next, "bad args");
+  const pb_grid* g = v->grid;
+  *first = g->k0 * g->plane;
+  *next = (g->k0 + g->nzl) * g->plane;
+  return PB_OK;
+}
+
 int pb_op_get_diagonal(const pb_op* op, double* diag) {
   PB_CHECK_ARG(op && diag, "bad args");
   *diag = op->cc;

@@ -14,7 +14,7 @@ program poissbox_demo
   integer :: ierr, n1, its, reason
   integer, dimension(3) :: n
   real(pb_dp), dimension(3) :: h
-  real(pb_dp) :: error, xsum, rnorm
+  real(pb_dp) :: error, rnorm
   type(tDM) :: da
   type(tMat) :: P, A
   type(tVec) :: x, b, x2
@@ -26,7 +26,8 @@ program poissbox_demo
 
   call PoissboxInitialize(0, ierr)
   if (ierr /= 0) stop 1
-  print *, "Running poissbox on ", 1, " GPU"
+  print *, "Running poissbox on ", 1, " ranks"
+  print *, "Hello from ", 0
 
   call initialise_grid(n, da, ierr)
   call check_grid(n, da)
@@ -35,11 +36,9 @@ program poissbox_demo
   ctx%grid_deltas = h
   call initialise_linear_system(da, ctx, P, A, x, b, ierr)
   if (ierr /= 0) stop 1
+  call check_linear_system(n, P, x, b)
 
-  ! set_solution (src/example.f90:154-199): x = 2(0.5 - U)
-  call VecSetRandom(x, 20231015_c_int64_t, ierr)
-  call VecSum(x, xsum, ierr)
-  print *, "Rank ", 0, "XSUM of the specified solution: ", xsum
+  call set_solution(da, x)
   print *, "Calling MatMult"
   call MatMult(A, x, b, ierr)
   call check_lapl(da, x, b)
@@ -86,6 +85,49 @@ contains
     print *, "(DMDA): Rank ", 0, " has ", ni * nj * nk, " of ", ni * nj * nk, &
          " expected: ", product(nglobal)
   end subroutine check_grid
+
+  !! src/example.f90:118-152: row ownership of P, x and b against the global DoF count
+  subroutine check_linear_system(nglobal, M, x, b)
+    integer, dimension(3), intent(in) :: nglobal
+    type(tMat), intent(in) :: M
+    type(tVec), intent(in) :: x, b
+    integer :: myrow, nextrow, ierr
+    call MatGetOwnershipRange(M, myrow, nextrow, ierr)
+    print *, "(M): Rank ", 0, " has ", nextrow - myrow, " rows of ", nextrow - myrow, &
+         " expected: ", product(nglobal)
+    call VecGetOwnershipRange(x, myrow, nextrow, ierr)
+    print *, "(x): Rank ", 0, " has ", nextrow - myrow, " rows of ", nextrow - myrow, &
+         " expected: ", product(nglobal)
+    call VecGetOwnershipRange(b, myrow, nextrow, ierr)
+    print *, "(b): Rank ", 0, " has ", nextrow - myrow, " rows of ", nextrow - myrow, &
+         " expected: ", product(nglobal)
+  end subroutine check_linear_system
+
+  !! src/example.f90:154-199: x = 2(0.5 - U) on the owned block; the sum computed directly over
+  !! the owned values (host loop, as the reference's xsum) against VecSum (device reduction)
+  subroutine set_solution(da, x)
+    type(tDM), intent(in) :: da
+    type(tVec), intent(inout) :: x
+    integer :: istart, jstart, kstart, ni, nj, nk, ierr, i, j, k
+    real(pb_dp), allocatable :: xdof(:, :, :)
+    real(pb_dp) :: xs, xsum_v
+    call DMDAGetCorners(da, istart, jstart, kstart, ni, nj, nk, ierr)
+    call VecSetRandom(x, 20231015_c_int64_t, ierr)
+    allocate(xdof(ni, nj, nk))
+    call VecGetValues(x, xdof, ierr)
+    xs = 0.0_pb_dp
+    do k = 1, nk
+       do j = 1, nj
+          do i = 1, ni
+             xs = xs + xdof(i, j, k)
+          end do
+       end do
+    end do
+    deallocate(xdof)
+    call VecSum(x, xsum_v, ierr)
+    print *, "Rank ", 0, "Delta of XSUM norms computed directly and from X: ", xsum_v - xs, &
+         xsum_v, xs
+  end subroutine set_solution
 
   !! src/example.f90:201-233: ||A x - pointwise(x)||_2 (identical kernels -> 0)
   subroutine check_lapl(da, x, b)

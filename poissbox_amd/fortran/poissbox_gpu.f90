@@ -61,7 +61,7 @@ module poissbox_gpu
 
   public :: PoissboxInitialize, PoissboxFinalize
   public :: initialise_grid, initialise_linear_system, solve, compute_lapl_pointwise
-  public :: DMDAGetCorners, MatMult, MatDestroy
+  public :: DMDAGetCorners, MatMult, MatDestroy, MatGetOwnershipRange, VecGetOwnershipRange
   public :: VecDuplicate, VecCopy, VecAXPY, VecNorm, VecSum, VecSet, VecDestroy
   public :: VecSetRandom, VecGetValues, VecSetValues, pb_error_string
 
@@ -158,6 +158,18 @@ module poissbox_gpu
      integer(c_int) function c_pb_op_destroy(op) bind(C, name="pb_op_destroy")
        import :: c_int, c_ptr
        type(c_ptr), value :: op
+     end function
+     integer(c_int) function c_pb_op_get_ownership_range(op, first, next) &
+          bind(C, name="pb_op_get_ownership_range")
+       import :: c_int, c_ptr, c_int64_t
+       type(c_ptr), value :: op
+       integer(c_int64_t) :: first, next
+     end function
+     integer(c_int) function c_pb_vec_get_ownership_range(v, first, next) &
+          bind(C, name="pb_vec_get_ownership_range")
+       import :: c_int, c_ptr, c_int64_t
+       type(c_ptr), value :: v
+       integer(c_int64_t) :: first, next
      end function
      integer(c_int) function c_pb_ksp_opts_default(o) bind(C, name="pb_ksp_opts_default")
        import :: c_int, pb_ksp_opts
@@ -330,6 +342,26 @@ contains
     ierr = c_pb_op_apply(op%h, x%h, b%h)
     ierr = c_pb_op_destroy(op%h)
   end subroutine compute_lapl_pointwise
+
+  !! ≙ MatGetOwnershipRange (src/example.f90:137): rows [myrow, nextrow) on this rank
+  subroutine MatGetOwnershipRange(A, myrow, nextrow, ierr)
+    type(tMat), intent(in) :: A
+    integer, intent(out) :: myrow, nextrow, ierr
+    integer(c_int64_t) :: f, n
+    ierr = c_pb_op_get_ownership_range(A%h, f, n)
+    myrow = int(f)
+    nextrow = int(n)
+  end subroutine MatGetOwnershipRange
+
+  !! ≙ VecGetOwnershipRange (src/example.f90:142,147)
+  subroutine VecGetOwnershipRange(x, myrow, nextrow, ierr)
+    type(tVec), intent(in) :: x
+    integer, intent(out) :: myrow, nextrow, ierr
+    integer(c_int64_t) :: f, n
+    ierr = c_pb_vec_get_ownership_range(x%h, f, n)
+    myrow = int(f)
+    nextrow = int(n)
+  end subroutine VecGetOwnershipRange
 
   subroutine MatDestroy(A, ierr)
     type(tMat), intent(inout) :: A

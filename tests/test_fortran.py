@@ -32,6 +32,14 @@ def test_fortran_demo_matches_oracle():
     assert out.returncode == 0, out.stdout + out.stderr
     txt = out.stdout
     assert re.search(r"has\s+32768\s+of\s+32768\s+expected:\s+32768", txt)
+    # check_linear_system (src/example.f90:118-152): P, x, b rows = global DoF
+    for tag in ("M", "x", "b"):
+        assert re.search(r"\(%s\): Rank\s+0\s+has\s+32768\s+rows of\s+32768\s+expected:\s+32768" % tag, txt)
+    # set_solution's XSUM check (:194-197): host sum vs VecSum, equal up to summation order
+    xs = re.search(r"Delta of XSUM norms computed directly and from X:\s+(\S+)\s+(\S+)\s+(\S+)", txt)
+    assert xs and abs(float(xs.group(1))) <= 1e-9 * 32768
+    from oracle import oracle as O2
+    assert abs(float(xs.group(3)) - O2.fill_random(32 ** 3, 20231015).sum()) <= 1e-9 * 32768
     num = lambda pat: float(re.search(pat + r"\s+(\S+)", txt).group(1))
     assert num(r"pointwise calculation:") == 0.0   # same kernel: exact
     assert num(r"Ax - Px =") == 0.0                # same 7 non-zeros
