@@ -81,6 +81,9 @@ struct pb_ctx {
   double* d_scalars = nullptr;    // small device scalars for vector reductions
   double* h_scalars = nullptr;    // pinned mirror
   int num_cus = 256;
+  // z-march direction of the next standalone stencil apply (alternates: each apply starts on
+  // the planes the previous one touched last, which are still in the Infinity Cache)
+  int zflip = 0;
   // context-owned scratch for the one-shot compact / tridiagonal entry points (grown on demand;
   // every use is ordered on `stream`, so one buffer serves all of them)
   double* scratch = nullptr;
@@ -187,7 +190,6 @@ int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p
                      double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
                      int64_t host_iter, bool defer_x, bool finalize = true);
 int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
-int stencil_blocks(pb_grid* g, int mode);  // partial-sum slots a stencil pass writes
 
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----
 int64_t compact_fast_work_len(const pb_grid* g);

@@ -35,6 +35,7 @@ struct Geo {
   int k_lo, k_hi, kstride;  // chunk c covers planes [k_lo + c*kstride, min(+kc, k_hi))
   int remap;  // XCD-aware block remap on/off (PB_XCD_REMAP, default on)
   int nt;     // non-temporal output stores (PB_STENCIL_NT, default on)
+  int rev;    // march each chunk downwards (k from the top plane to the bottom one)
 };
 
 template <int V>
@@ -375,19 +376,25 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
       }
     };
 
-    // prologue: planes kb-1, kb combined; raw plane kb+1 and plane kb's operands in flight
-    issue_zrow(kb - 1);
+    // prologue: planes kf-dir, kf combined; raw plane kf+dir and plane kf's operands in flight.
+    // Marching downwards (g.rev) lets a kernel start on the planes its predecessor touched last
+    // (still in the 256 MiB Infinity Cache); per-point arithmetic is unchanged (zm/zp swap).
+    const int dir = g.rev ? -1 : 1;
+    const int kf = g.rev ? ke - 1 : kb;
+    const int nk = ke - kb;
+    issue_zrow(kf - dir);
     take_zrow(q0);
-    issue_zrow(kb);
+    issue_zrow(kf);
     take_zrow(q1);
-    issue_plane_ops(kb);
-    issue_zrow(kb + 1);
-    for (int k = kb; k < ke; ++k) {
-      take_zrow(q2);                    // plane k+1 (in flight since the previous step)
+    issue_plane_ops(kf);
+    issue_zrow(kf + dir);
+    for (int m = 0; m < nk; ++m) {
+      const int k = kf + m * dir;
+      take_zrow(q2);                    // plane k+dir (in flight since the previous step)
       take_plane_ops();                 // halo/edges/operands of plane k
       issue_ops_now(k);
-      if (k + 2 <= ke) issue_zrow(k + 2);
-      if (k + 1 < ke) issue_plane_ops(k + 1);
+      if (m + 2 <= nk) issue_zrow(k + 2 * dir);
+      if (m + 1 < nk) issue_plane_ops(k + dir);
       const int64_t base = (int64_t)k * g.plane;
 #pragma unroll
       for (int t = 0; t < TY; ++t) {
@@ -404,13 +411,15 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
           const double xp = e == V - 1 ? xrl : q1[t][e + 1];
           const double ym = t == 0 ? hdn[e] : q1[t - 1][e];
           const double yp = t == TY - 1 ? hup[e] : q1[t + 1][e];
-          double s = cz * q0[t][e];
+          const double zm = g.rev ? q2[t][e] : q0[t][e];
+          const double zp = g.rev ? q0[t][e] : q2[t][e];
+          double s = cz * zm;
           s = s + cy * ym;
           s = s + cx * xm;
           s = s + cc * q1[t][e];
           s = s + cx * xp;
           s = s + cy * yp;
-          s = s + cz * q2[t][e];
+          s = s + cz * zp;
           w[e] = s;
         }
         if (active) ep.template put<V>(base + (int64_t)(j0 + t) * nx + i0, q1[t], w, opc[t], acc, g.nt);
@@ -433,8 +442,9 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 // Plane sets: PLANES_ALL = [0, nzl); PLANES_INTERIOR = [1, nzl-1) (no ghost plane is read);
 // PLANES_BOUNDARY = {0, nzl-1} (the two planes that read ghosts) -- the split lets the halo
 // exchange of a multi-rank step overlap the interior.
-static Geo make_geo(pb_grid* g, int V, int TY, int mode) {
+static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev) {
   Geo geo;
+  geo.rev = env_int("PB_ZALT", 1) ? rev : 0;
   geo.nx = (int)g->n[0];
   geo.ny = (int)g->n[1];
   geo.nzl = (int)g->nzl;
@@ -456,7 +466,8 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode) {
   geo.k_hi = mode == PLANES_INTERIOR ? geo.nzl - 1 : geo.nzl;
   const int nk = geo.k_hi - geo.k_lo;
   const int columns = geo.nsegx * geo.ntile;
-  // 3 workgroups per CU: long z-chunks (few chunk-boundary re-reads)
+  // 3 workgroups per CU: long z-chunks (few chunk-boundary re-reads). Measured at 512^3: also
+  // best for the CG passes whose registers allow only 2 resident per CU (768 blocks beat 512)
   int target = env_int("PB_STENCIL_BLOCKS", 3 * g->ctx->num_cus);
   int nchunk = (target + columns - 1) / columns;
   if (nchunk > nk) nchunk = nk;
@@ -477,8 +488,8 @@ static int pick_ty(int ny) {
 
 template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
-                    const Epi& ep, const int* skip, int mode, int part_off, int* nb_out) {
-  Geo geo = make_geo(g, V, TY, mode);
+                    const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev) {
+  Geo geo = make_geo(g, V, TY, mode, rev);
   const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
   constexpr int NS = Epi::NS > 0 ? Epi::NS : 1;
   if ((part_off + nblocks) * NS > g->ctx->partials_cap)
@@ -495,33 +506,31 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
 template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                       const Epi& ep, const int* skip, int mode = PLANES_ALL, int part_off = 0,
-                      int* nb_out = nullptr) {
+                      int* nb_out = nullptr, int rev = 0) {
   const bool vec2 = (g->n[0] % 2) == 0;
   const int ty = pick_ty((int)g->n[1]);
   if (vec2) {
     switch (ty) {
-      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
-      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
-      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
+      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
+      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
+      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
     }
   }
   switch (ty) {
-    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
-    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
-    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out);
+    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
+    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
+    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
   }
-}
-
-int stencil_blocks(pb_grid* g, int mode) {
-  const bool vec2 = (g->n[0] % 2) == 0;
-  Geo geo = make_geo(g, vec2 ? 2 : 1, pick_ty((int)g->n[1]), mode);
-  return geo.nsegx * geo.ntile * geo.nchunk;
 }
 
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
                        const StencilPlanes& gp, int mode) {
   ScopedTimer tm(g->ctx, "stencil");
-  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, nullptr, mode);
+  // alternate the march direction between applies (the boundary launch of a split apply is one
+  // plane per chunk, direction-free, and does not flip it)
+  const int rev = g->ctx->zflip;
+  if (mode != PLANES_BOUNDARY) g->ctx->zflip ^= 1;
+  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, nullptr, mode, 0, nullptr, rev);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -802,23 +811,27 @@ int cg_finalize_stage2(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* 
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
                      double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
                      int64_t host_iter, bool defer_x, bool finalize) {
+  int nparts = 0;
   {
     if (!defer_x) {
       ScopedTimer tm(g->ctx, "cg_pass_b");
       PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<2>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done));
+                        PassB<2>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done,
+                        PLANES_ALL, 0, &nparts, 1));
     } else if (host_iter % 2 == 0) {
       ScopedTimer tm(g->ctx, "cg_pass_b_even");
       PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<0>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done));
+                        PassB<0>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done,
+                        PLANES_ALL, 0, &nparts, 1));
     } else {
       ScopedTimer tm(g->ctx, "cg_pass_b_odd");
       PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<1>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done));
+                        PassB<1>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done,
+                        PLANES_ALL, 0, &nparts, 1));
     }
   }
   if (!finalize) return PB_OK;  // preconditioned path: the sums come from z = M^-1 r later
-  return cg_reduce_update(g->ctx, 2, stencil_blocks(g, PLANES_ALL), 4, st, hist, h_done, host_iter);
+  return cg_reduce_update(g->ctx, 2, nparts, 4, st, hist, h_done, host_iter);
 }
 
 // x += alpha * p (the pending half of the deferred solution update)

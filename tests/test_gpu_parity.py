@@ -73,7 +73,8 @@ def test_stencil_bit_exact(ctx, n):
     y = yv.get_values()
     ref = O.stencil(x, n, h, faithful=N <= 40000)
     assert np.array_equal(y, ref), np.max(np.abs(y - ref))
-    # assembled-P kind applies the same 7 non-zeros
+    # assembled-P kind applies the same 7 non-zeros (this second apply marches the other z
+    # direction: consecutive applies alternate, so both directions are checked)
     P = pb.Mat(da, pb.ASSEMBLED27)
     P.mult(xv, yv)
     assert np.array_equal(yv.get_values(), ref)
