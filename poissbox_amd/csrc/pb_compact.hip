@@ -29,61 +29,94 @@ struct LineMap {
   __device__ __forceinline__ int64_t base(int64_t l) const { return (l % m1) * s1 + (l / m1) * s2; }
 };
 
+// The recurrences carry b'[i-1], c[i-1], d'[i-1] (and u'[i-1]) in registers, so each sweep
+// touches every array once: tdma 4R+2W forward, 3R+1W backward (80 B/DoF of traffic for 48
+// algorithmic); tdma_periodic 4R+3W forward, 4R+2W backward, 2R+1W correction (128 B/DoF for
+// 40). The operations and their order are the reference's, element by element.
 __global__ __launch_bounds__(64) void tdma_kernel(int64_t n, int64_t nb, LineMap lm,
-                                                  const double* __restrict__ a, double* b,
-                                                  const double* __restrict__ c, double* d) {
+                                                  const double* __restrict__ a,
+                                                  double* __restrict__ b,
+                                                  const double* __restrict__ c,
+                                                  double* __restrict__ d) {
   const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= nb) return;
   const int64_t o = lm.base(l), es = lm.es;
   // fwd_sweep :90-94
+  double bp = b[o], cp = c[o], dp = d[o];
   for (int64_t i = 1; i < n; ++i) {
-    const double w = a[o + i * es] / b[o + (i - 1) * es];
-    b[o + i * es] = b[o + i * es] - w * c[o + (i - 1) * es];
-    d[o + i * es] = d[o + i * es] - w * d[o + (i - 1) * es];
+    const int64_t e = o + i * es;
+    const double w = a[e] / bp;
+    bp = b[e] - w * cp;
+    dp = d[e] - w * dp;
+    cp = c[e];
+    b[e] = bp;
+    d[e] = dp;
   }
   // bwd_sweep :110-113
-  d[o + (n - 1) * es] = d[o + (n - 1) * es] / b[o + (n - 1) * es];
-  for (int64_t i = n - 2; i >= 0; --i)
-    d[o + i * es] = (d[o + i * es] - c[o + i * es] * d[o + (i + 1) * es]) / b[o + i * es];
+  double xn = dp / bp;
+  d[o + (n - 1) * es] = xn;
+  for (int64_t i = n - 2; i >= 0; --i) {
+    const int64_t e = o + i * es;
+    xn = (d[e] - c[e] * xn) / b[e];
+    d[e] = xn;
+  }
 }
 
 // tdma_periodic :34-74; the two auxiliary Thomas solves share one forward elimination of bmod
-// (the reference recomputes bmod identically for the second solve). scratch: 2*n per line.
+// (the reference recomputes bmod identically for the second solve). scratch: 2*n per line,
+// element i of line l at [i*nb + l] (coalesced across lines).
 __global__ __launch_bounds__(64) void tdma_periodic_kernel(int64_t n, int64_t nb, LineMap lm,
                                                            const double* __restrict__ a,
                                                            const double* __restrict__ b,
                                                            const double* __restrict__ c,
-                                                           double* d, double* scratch) {
+                                                           double* __restrict__ d,
+                                                           double* __restrict__ scratch) {
   const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= nb) return;
   const int64_t o = lm.base(l), es = lm.es;
-  double* bm = scratch + l;               // bm[i] at bm[i*nb]  (coalesced across lines)
+  double* bm = scratch + l;  // modified diagonal
   double* u = scratch + n * nb + l;
   const double a0 = a[o], cn = c[o + (n - 1) * es];
   const double gamma = -b[o];
-  for (int64_t i = 0; i < n; ++i) {
-    bm[i * nb] = b[o + i * es];
-    u[i * nb] = 0.0;
-  }
-  bm[0] = bm[0] - gamma;
-  bm[(n - 1) * nb] = bm[(n - 1) * nb] - cn * a0 / gamma;
-  u[0] = gamma;
-  u[(n - 1) * nb] = cn;
+  // bb(1) = b(1) - gamma, bb(n) = b(n) - c(n) a(1) / gamma; u = [gamma, 0, ..., 0, c(n)]
+  double bp = b[o] - gamma;
+  if (n == 1) bp = bp - cn * a0 / gamma;
+  double up = n == 1 ? cn : gamma;
+  double dp = d[o], cp = c[o];
+  bm[0] = bp;
+  u[0] = up;
   for (int64_t i = 1; i < n; ++i) {
-    const double w = a[o + i * es] / bm[(i - 1) * nb];
-    bm[i * nb] = bm[i * nb] - w * c[o + (i - 1) * es];
-    d[o + i * es] = d[o + i * es] - w * d[o + (i - 1) * es];
-    u[i * nb] = u[i * nb] - w * u[(i - 1) * nb];
+    const int64_t e = o + i * es;
+    double bi = b[e];
+    if (i == n - 1) bi = bi - cn * a0 / gamma;
+    const double ui = i == n - 1 ? cn : 0.0;
+    const double w = a[e] / bp;
+    bp = bi - w * cp;
+    dp = d[e] - w * dp;
+    up = ui - w * up;
+    cp = c[e];
+    bm[i * nb] = bp;
+    d[e] = dp;
+    u[i * nb] = up;
   }
-  d[o + (n - 1) * es] = d[o + (n - 1) * es] / bm[(n - 1) * nb];
-  u[(n - 1) * nb] = u[(n - 1) * nb] / bm[(n - 1) * nb];
+  double yn = dp / bp, zn = up / bp;
+  const double ylast = yn, zlast = zn;
+  d[o + (n - 1) * es] = yn;
+  u[(n - 1) * nb] = zn;
   for (int64_t i = n - 2; i >= 0; --i) {
-    d[o + i * es] = (d[o + i * es] - c[o + i * es] * d[o + (i + 1) * es]) / bm[i * nb];
-    u[i * nb] = (u[i * nb] - c[o + i * es] * u[(i + 1) * nb]) / bm[i * nb];
+    const int64_t e = o + i * es;
+    const double ci = c[e], bi = bm[i * nb];
+    yn = (d[e] - ci * yn) / bi;
+    zn = (u[i * nb] - ci * zn) / bi;
+    d[e] = yn;
+    u[i * nb] = zn;
   }
-  const double num = d[o] + (a0 / gamma) * d[o + (n - 1) * es];
-  const double den = 1.0 + (u[0] + (a0 / gamma) * u[(n - 1) * nb]);
-  for (int64_t i = 0; i < n; ++i) d[o + i * es] = d[o + i * es] - (u[i * nb] * num) / den;
+  const double num = yn + (a0 / gamma) * ylast;
+  const double den = 1.0 + (zn + (a0 / gamma) * zlast);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t e = o + i * es;
+    d[e] = d[e] - (u[i * nb] * num) / den;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -163,27 +196,38 @@ __global__ __launch_bounds__(64) void compact_line_kernel(
   const double* W = fac;
   const double* BM = fac + n;
   const double* U = fac + 2 * n;
-  auto F = [&](int64_t i) -> double {
-    i = i < 0 ? i + n : (i >= n ? i - n : i);
+  auto F = [&](int64_t i) -> double {  // periodic input
+    i %= n;
+    if (i < 0) i += n;
     double v = in[o + i * es];
     if (in2) v = v + in2[o + i * es];
     return v;
   };
-  auto rhs = [&](int64_t i) -> double {
-    const double f0 = F(i + shift), fm1 = F(i - 1 + shift);
-    const double f1 = F(i + 1 + shift), fm2 = F(i - 2 + shift);
+  // sliding window f(i+shift-2 .. i+shift+1): one input load per point
+  double fm2 = F(shift - 2), fm1 = F(shift - 1), f0 = F(shift), f1 = F(shift + 1);
+  auto rhs = [&]() -> double {
     return sc.a * (f0 + sc.sign * fm1) + sc.b * (f1 + sc.sign * fm2);
   };
+  auto advance = [&](int64_t i) {  // window of point i -> window of point i+1
+    fm2 = fm1;
+    fm1 = f0;
+    f0 = f1;
+    int64_t k = i + shift + 2;  // <= n + 1 (i <= n - 2)
+    if (k >= n) k -= n;
+    f1 = in[o + k * es];
+    if (in2) f1 = f1 + in2[o + k * es];
+  };
   // forward sweep: d[i] = rhs[i] - W[i] * d[i-1]
-  double prev = rhs(0);
+  double prev = rhs();
   out[o] = prev;
   for (int64_t i = 1; i < n; ++i) {
-    const double di = rhs(i) - W[i] * prev;
+    advance(i - 1);
+    const double di = rhs() - W[i] * prev;
     out[o + i * es] = di;
     prev = di;
   }
-  // backward sweep
-  double next = out[o + (n - 1) * es] / BM[n - 1];
+  // backward sweep (d[n-1] is still in a register)
+  double next = prev / BM[n - 1];
   out[o + (n - 1) * es] = next;
   const double dlast = next;
   for (int64_t i = n - 2; i >= 0; --i) {

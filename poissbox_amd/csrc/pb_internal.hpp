@@ -171,6 +171,14 @@ struct StencilPlanes {
 enum { PLANES_ALL = 0, PLANES_INTERIOR = 1, PLANES_BOUNDARY = 2 };
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
                        const StencilPlanes& gp, int mode);
+// red-black SOR half-sweep in place (first = 1: zero-start red + black fused, x written from b)
+// and the multigrid residual, on the stencil engine (pb_mg.hip)
+struct CgState;
+int launch_mg_sor(pb_grid* g, const Star& s, double* x, const double* b, const StencilPlanes& gp,
+                  double omega, int color, int first, const int* skip,
+                  const CgState* sums_st = nullptr, int* nparts = nullptr);
+int launch_mg_residual(pb_grid* g, const Star& s, const double* x, const double* b,
+                       const StencilPlanes& gp, double* res, const int* skip);
 
 // CG state (device resident; all scalars computed on device, host only polls `done`)
 struct CgState {
@@ -251,7 +259,10 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
               double omega, Mg** out);
 // z = M^-1 r (zero initial guess); skip: optional device flag (CG's `done`) -- when set, the
 // kernels exit at entry (halo exchanges still run, so ranks stay matched)
-int mg_apply(Mg* mg, const double* r, double* z, const int* skip = nullptr);
+// sums_st: also take CG's residual sums of z (t = z - mu_old: t, t^2, t.r, r) in the last
+// half-sweep when it runs on the stencil engine; *nparts = partial-sum blocks written, 0 if not
+int mg_apply(Mg* mg, const double* r, double* z, const int* skip = nullptr,
+             const CgState* sums_st = nullptr, int* nparts = nullptr);
 int mg_levels(const Mg* mg);
 void mg_destroy(Mg* mg);
 // deterministic level count for a global grid split over nranks z-slabs (every rank agrees)

@@ -54,6 +54,15 @@ struct Mg {
   int coarse_its = 1;
   double* mem = nullptr;
   const int* skip = nullptr;  // device flag: when set, the kernels of this apply exit at entry
+  // SOR half-sweeps and residuals of levels whose planes hold >= engine_min_plane points run on
+  // the z-marching stencil engine (PB_MG_ENGINE_MIN_PLANE; smaller levels: per-pair kernels,
+  // whose short z-chunks would not amortise the engine's prologue)
+  int64_t engine_min_plane = 256 * 256;
+  // prolongation (PB_MG_PROLONG_CELL): 0 one thread per fine pair, 1 one thread per coarse cell,
+  // 2 one thread per coarse column marching in z (levels of >= restrict_z_min_cols columns)
+  int prolong_cell = 2;
+  int restrict_z = 1;    // restriction marching in z per coarse column (PB_MG_RESTRICT_Z) on
+  int64_t restrict_z_min_cols = 4096;  // coarse levels of >= this many columns
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -250,6 +259,60 @@ __global__ __launch_bounds__(256) void mg_restrict_kernel(MgGeo F, const double*
   }
 }
 
+// The same restriction, one thread per coarse (I, J) column marching over a chunk of coarse
+// planes: the x-y weighted sum sy of each fine plane is formed once and kept in a 4-plane
+// window (the per-cell kernel forms it twice); the z sum is the per-cell kernel's, same order.
+__device__ __forceinline__ double restrict_xy(const MgGeo& F, const double* pl, int I, int J,
+                                              int xl, int xr) {
+  const double w[4] = {0.125, 0.375, 0.375, 0.125};
+  double sy = 0.0;
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb) {
+    const double* row = pl + (int64_t)wrapm(2 * J - 1 + bb, F.ny) * F.nx;
+    const dv2 mid = *(const dv2*)(row + 2 * I);
+    double sx = w[0] * row[xl];
+    sx = sx + w[1] * mid.x;
+    sx = sx + w[2] * mid.y;
+    sx = sx + w[3] * row[xr];
+    sy = sy + w[bb] * sx;
+  }
+  return sy;
+}
+
+__global__ __launch_bounds__(256) void mg_restrict_z_kernel(MgGeo F, const double* __restrict__ rf,
+                                                            const double* __restrict__ lo,
+                                                            const double* __restrict__ hi,
+                                                            MgGeo Cg, int kc,
+                                                            double* __restrict__ bc,
+                                                            const int* skip) {
+  if (skip && *skip) return;
+  const int64_t cols = (int64_t)Cg.nx * Cg.ny;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t col = t % cols;
+  const int K0 = (int)(t / cols) * kc;
+  if (K0 >= Cg.nzl) return;
+  const int K1 = min(K0 + kc, Cg.nzl);
+  const int I = (int)(col % Cg.nx), J = (int)(col / Cg.nx);
+  const int xl = wrapm(2 * I - 1, F.nx), xr = wrapm(2 * I + 2, F.nx);
+  auto plane = [&](int kf) {
+    return kf < 0 ? lo : (kf >= F.nzl ? hi : rf + (int64_t)kf * F.plane);
+  };
+  double s0 = restrict_xy(F, plane(2 * K0 - 1), I, J, xl, xr);
+  double s1 = restrict_xy(F, plane(2 * K0), I, J, xl, xr);
+  for (int K = K0; K < K1; ++K) {
+    const double s2 = restrict_xy(F, plane(2 * K + 1), I, J, xl, xr);
+    const double s3 = restrict_xy(F, plane(2 * K + 2), I, J, xl, xr);
+    double sz = 0.0;
+    sz = sz + 0.125 * s0;
+    sz = sz + 0.375 * s1;
+    sz = sz + 0.375 * s2;
+    sz = sz + 0.125 * s3;
+    bc[(int64_t)K * Cg.plane + col] = sz;
+    s0 = s2;
+    s1 = s3;
+  }
+}
+
 // x_f += P x_c for both points of the pair (trilinear, cell-centred: near parent 3/4, far 1/4)
 __global__ __launch_bounds__(256) void mg_prolong_kernel(MgGeo F, double* __restrict__ xf, MgGeo Cg,
                                                          const double* __restrict__ xc,
@@ -284,6 +347,140 @@ __global__ __launch_bounds__(256) void mg_prolong_kernel(MgGeo F, double* __rest
   }
 }
 
+// The same prolongation, one thread per coarse cell: its 2 x 2 x 2 fine children from the
+// 3 x 3 x 3 coarse neighbourhood (each child by the formula above, same operation order), so a
+// fine row pair is read and written with 16-byte accesses and each coarse value is fetched
+// ~27/8 times per fine point instead of 6.
+__global__ __launch_bounds__(256) void mg_prolong_cell_kernel(MgGeo F, double* __restrict__ xf,
+                                                              MgGeo Cg,
+                                                              const double* __restrict__ xc,
+                                                              const double* __restrict__ lo,
+                                                              const double* __restrict__ hi,
+                                                              const int* skip) {
+  if (skip && *skip) return;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < Cg.nlocal;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int I, J, K;
+    mg_ijk(Cg, idx, I, J, K);
+    const int Im = wrapm(I - 1, Cg.nx), Ip = wrapm(I + 1, Cg.nx);
+    const int Jm = wrapm(J - 1, Cg.ny), Jp = wrapm(J + 1, Cg.ny);
+    const double* pn = xc + (int64_t)K * Cg.plane;
+    const int64_t rn = (int64_t)J * Cg.nx;
+#pragma unroll
+    for (int dk = 0; dk < 2; ++dk) {
+      const int fK = dk ? K + 1 : K - 1;
+      const double* pf = fK < 0 ? lo : (fK >= Cg.nzl ? hi : xc + (int64_t)fK * Cg.plane);
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        const int64_t rf = (int64_t)(dj ? Jp : Jm) * Cg.nx;
+        const double vn0 = 0.75 * (0.75 * pn[rn + I] + 0.25 * pn[rn + Im]) +
+                           0.25 * (0.75 * pn[rf + I] + 0.25 * pn[rf + Im]);
+        const double vf0 = 0.75 * (0.75 * pf[rn + I] + 0.25 * pf[rn + Im]) +
+                           0.25 * (0.75 * pf[rf + I] + 0.25 * pf[rf + Im]);
+        const double vn1 = 0.75 * (0.75 * pn[rn + I] + 0.25 * pn[rn + Ip]) +
+                           0.25 * (0.75 * pn[rf + I] + 0.25 * pn[rf + Ip]);
+        const double vf1 = 0.75 * (0.75 * pf[rn + I] + 0.25 * pf[rn + Ip]) +
+                           0.25 * (0.75 * pf[rf + I] + 0.25 * pf[rf + Ip]);
+        dv2* q = (dv2*)(xf + (int64_t)(2 * K + dk) * F.plane + (int64_t)(2 * J + dj) * F.nx + 2 * I);
+        dv2 o = *q;
+        o.x = o.x + (0.75 * vn0 + 0.25 * vf0);
+        o.y = o.y + (0.75 * vn1 + 0.25 * vf1);
+        *q = o;
+      }
+    }
+  }
+}
+
+// The same prolongation, one thread per coarse (I, J) column marching over a chunk of coarse
+// planes: the 3 x 3 coarse values of planes K-1, K, K+1 stay in registers (each coarse value is
+// loaded ~3 times per coarse cell instead of 27), children by the formula above.
+struct Coarse9 {
+  double v[3][3];  // [row Jm, J, Jp][col Im, I, Ip]
+};
+__device__ __forceinline__ void load9(const double* pl, int64_t rm, int64_t r0, int64_t rp, int Im,
+                                      int I, int Ip, Coarse9& c) {
+  const int64_t rows[3] = {rm, r0, rp};
+  const int cols[3] = {Im, I, Ip};
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) c.v[a][b] = pl[rows[a] + cols[b]];
+}
+
+__global__ __launch_bounds__(256) void mg_prolong_z_kernel(MgGeo F, double* __restrict__ xf, MgGeo Cg,
+                                                           int kc, const double* __restrict__ xc,
+                                                           const double* __restrict__ lo,
+                                                           const double* __restrict__ hi,
+                                                           const int* skip) {
+  if (skip && *skip) return;
+  const int64_t cols = (int64_t)Cg.nx * Cg.ny;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t col = t % cols;
+  const int K0 = (int)(t / cols) * kc;
+  if (K0 >= Cg.nzl) return;
+  const int K1 = min(K0 + kc, Cg.nzl);
+  const int I = (int)(col % Cg.nx), J = (int)(col / Cg.nx);
+  const int Im = wrapm(I - 1, Cg.nx), Ip = wrapm(I + 1, Cg.nx);
+  const int64_t rm = (int64_t)wrapm(J - 1, Cg.ny) * Cg.nx, r0 = (int64_t)J * Cg.nx,
+                rp = (int64_t)wrapm(J + 1, Cg.ny) * Cg.nx;
+  auto plane = [&](int K) {
+    return K < 0 ? lo : (K >= Cg.nzl ? hi : xc + (int64_t)K * Cg.plane);
+  };
+  Coarse9 cm, c0, cp;
+  load9(plane(K0 - 1), rm, r0, rp, Im, I, Ip, cm);
+  load9(plane(K0), rm, r0, rp, Im, I, Ip, c0);
+  for (int K = K0; K < K1; ++K) {
+    load9(plane(K + 1), rm, r0, rp, Im, I, Ip, cp);
+    // all four fine pairs are loaded before any is stored (the stores would otherwise order
+    // each later load behind them)
+    dv2* q[2][2];
+    dv2 ov[2][2];
+#pragma unroll
+    for (int dk = 0; dk < 2; ++dk)
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        q[dk][dj] = (dv2*)(xf + (int64_t)(2 * K + dk) * F.plane + (int64_t)(2 * J + dj) * F.nx + 2 * I);
+        ov[dk][dj] = *q[dk][dj];
+      }
+#pragma unroll
+    for (int dk = 0; dk < 2; ++dk) {
+      const Coarse9& pf = dk ? cp : cm;  // far plane: K+1 for odd fine k, K-1 for even
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        const int f = dj ? 2 : 0;  // far row: J+1 for odd fine j, J-1 for even
+        const double vn0 = 0.75 * (0.75 * c0.v[1][1] + 0.25 * c0.v[1][0]) +
+                           0.25 * (0.75 * c0.v[f][1] + 0.25 * c0.v[f][0]);
+        const double vf0 = 0.75 * (0.75 * pf.v[1][1] + 0.25 * pf.v[1][0]) +
+                           0.25 * (0.75 * pf.v[f][1] + 0.25 * pf.v[f][0]);
+        const double vn1 = 0.75 * (0.75 * c0.v[1][1] + 0.25 * c0.v[1][2]) +
+                           0.25 * (0.75 * c0.v[f][1] + 0.25 * c0.v[f][2]);
+        const double vf1 = 0.75 * (0.75 * pf.v[1][1] + 0.25 * pf.v[1][2]) +
+                           0.25 * (0.75 * pf.v[f][1] + 0.25 * pf.v[f][2]);
+        dv2 o = ov[dk][dj];
+        o.x = o.x + (0.75 * vn0 + 0.25 * vf0);
+        o.y = o.y + (0.75 * vn1 + 0.25 * vf1);
+        ov[dk][dj] = o;
+      }
+    }
+#pragma unroll
+    for (int dk = 0; dk < 2; ++dk)
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) *q[dk][dj] = ov[dk][dj];
+    cm = c0;
+    c0 = cp;
+  }
+}
+
+// chunks of coarse planes for the z-marching transfer kernels: ~16 resident waves per CU, at
+// least 4 coarse planes per chunk
+static int transfer_chunk(pb_ctx* ctx, int64_t cols, int64_t nzl, int64_t* nchunk_out) {
+  int64_t nchunk = ((int64_t)ctx->num_cus * 1024 + cols - 1) / cols;
+  nchunk = std::max<int64_t>(1, std::min<int64_t>(nchunk, nzl / 4));
+  const int kc = (int)((nzl + nchunk - 1) / nchunk);
+  *nchunk_out = (nzl + kc - 1) / kc;
+  return kc;
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -308,10 +505,17 @@ static int ghosts(MgLevel& L, const double* v, const double** lo, const double**
   return PB_OK;
 }
 
-// mode 0: half-sweep of `color`; mode 1: zero-initialised red + black half-sweeps fused
-static int smooth(Mg* mg, MgLevel& L, int color, int mode) {
+// mode 0: half-sweep of `color`; mode 1: zero-initialised red + black half-sweeps fused.
+// sums_st (mode 0, engine path only): also take CG's residual sums of the output (*nparts set)
+static int smooth(Mg* mg, MgLevel& L, int color, int mode, const CgState* sums_st = nullptr,
+                  int* nparts = nullptr) {
   const double *lo = nullptr, *hi = nullptr;
   PB_TRY(ghosts(L, mode == 1 ? L.b : L.x, &lo, &hi));
+  if (L.g->plane >= mg->engine_min_plane) {
+    const StencilPlanes gp{lo, hi};
+    return launch_mg_sor(L.g, L.s, L.x, L.b, gp, mg->omega, color, mode == 1, mg->skip,
+                         mode == 0 ? sums_st : nullptr, mode == 0 ? nparts : nullptr);
+  }
   const MgGeo G = L.geo();
   hipLaunchKernelGGL(mg_smooth_kernel, dim3(mg_blocks(mg->ctx, G.nlocal / 2)), dim3(256), 0,
                      mg->ctx->stream, G, L.x, (const double*)L.b, lo, hi, L.s, mg->omega, color,
@@ -321,12 +525,13 @@ static int smooth(Mg* mg, MgLevel& L, int color, int mode) {
 }
 
 // coarsest level: `coarse_its` symmetric red-black sweeps from zero (red, black, red, black, ...)
-static int coarse_solve(Mg* mg, MgLevel& L) {
+static int coarse_solve(Mg* mg, MgLevel& L, const CgState* sums_st, int* nparts) {
   PB_TRY(smooth(mg, L, 0, 1));  // red from zero + black
-  PB_TRY(smooth(mg, L, 0, 0));
-  for (int it = 1; it < mg->coarse_its; ++it) {
+  const int its = mg->coarse_its;
+  PB_TRY(smooth(mg, L, 0, 0, its == 1 ? sums_st : nullptr, nparts));
+  for (int it = 1; it < its; ++it) {
     PB_TRY(smooth(mg, L, 1, 0));
-    PB_TRY(smooth(mg, L, 0, 0));
+    PB_TRY(smooth(mg, L, 0, 0, it == its - 1 ? sums_st : nullptr, nparts));
   }
   return PB_OK;
 }
@@ -424,9 +629,15 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
   return PB_OK;
 }
 
-int mg_apply(Mg* mg, const double* r, double* z, const int* skip) {
+int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState* sums_st,
+             int* nparts) {
+  if (nparts) *nparts = 0;
   ScopedTimer tm(mg->ctx, "mg_apply");
   mg->skip = skip;
+  mg->engine_min_plane = env_int("PB_MG_ENGINE_MIN_PLANE", 256 * 256);
+  mg->prolong_cell = env_int("PB_MG_PROLONG_CELL", 2);
+  mg->restrict_z = env_int("PB_MG_RESTRICT_Z", 1);
+  mg->restrict_z_min_cols = env_int("PB_MG_RESTRICT_Z_MIN_COLS", 4096);
   const int L = (int)mg->lv.size();
   mg->lv[0].b = const_cast<double*>(r);
   mg->lv[0].x = z;
@@ -442,19 +653,31 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip) {
     const double *lo, *hi;
     PB_TRY(ghosts(F, F.x, &lo, &hi));
     const MgGeo G = F.geo();
-    hipLaunchKernelGGL(mg_residual_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0,
-                       ctx->stream, G, (const double*)F.x, (const double*)F.b, lo, hi, F.s, F.res,
-                       mg->skip);
-    PB_HIP(hipGetLastError());
+    if (F.g->plane >= mg->engine_min_plane) {
+      PB_TRY(launch_mg_residual(F.g, F.s, F.x, F.b, StencilPlanes{lo, hi}, F.res, mg->skip));
+    } else {
+      hipLaunchKernelGGL(mg_residual_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0,
+                         ctx->stream, G, (const double*)F.x, (const double*)F.b, lo, hi, F.s,
+                         F.res, mg->skip);
+      PB_HIP(hipGetLastError());
+    }
     PB_TRY(ghosts(F, F.res, &lo, &hi));
     const MgGeo CG = Cl.geo();
-    hipLaunchKernelGGL(mg_restrict_kernel, dim3(mg_blocks(ctx, CG.nlocal)), dim3(256), 0,
-                       ctx->stream, G, (const double*)F.res, lo, hi, CG, Cl.b, mg->skip);
+    const int64_t cols = (int64_t)CG.nx * CG.ny;
+    if (mg->restrict_z && cols >= mg->restrict_z_min_cols) {
+      int64_t nchunk = 1;
+      const int kc = transfer_chunk(ctx, cols, CG.nzl, &nchunk);
+      hipLaunchKernelGGL(mg_restrict_z_kernel, dim3(mg_blocks(ctx, cols * nchunk)), dim3(256), 0,
+                         ctx->stream, G, (const double*)F.res, lo, hi, CG, kc, Cl.b, mg->skip);
+    } else {
+      hipLaunchKernelGGL(mg_restrict_kernel, dim3(mg_blocks(ctx, CG.nlocal)), dim3(256), 0,
+                         ctx->stream, G, (const double*)F.res, lo, hi, CG, Cl.b, mg->skip);
+    }
     PB_HIP(hipGetLastError());
   }
   {
     ScopedTimer t3(ctx, L > 1 ? "mg_coarse_levels" : "mg_fine_smooth_first");
-    PB_TRY(coarse_solve(mg, mg->lv[L - 1]));
+    PB_TRY(coarse_solve(mg, mg->lv[L - 1], L == 1 ? sums_st : nullptr, nparts));
   }
   for (int l = L - 2; l >= 0; --l) {  // up: prolongate + correct, post-smooth (black, red)
     MgLevel& F = mg->lv[l];
@@ -463,11 +686,21 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip) {
     const double *lo, *hi;
     PB_TRY(ghosts(Cl, Cl.x, &lo, &hi));
     const MgGeo G = F.geo(), CG = Cl.geo();
-    hipLaunchKernelGGL(mg_prolong_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0, ctx->stream,
-                       G, F.x, CG, (const double*)Cl.x, lo, hi, mg->skip);
+    const int64_t cols = (int64_t)CG.nx * CG.ny;
+    if (mg->prolong_cell == 2 && cols >= mg->restrict_z_min_cols) {
+      int64_t nchunk = 1;
+      const int kc = transfer_chunk(ctx, cols, CG.nzl, &nchunk);
+      hipLaunchKernelGGL(mg_prolong_z_kernel, dim3(mg_blocks(ctx, cols * nchunk)), dim3(256), 0,
+                         ctx->stream, G, F.x, CG, kc, (const double*)Cl.x, lo, hi, mg->skip);
+    } else if (mg->prolong_cell)
+      hipLaunchKernelGGL(mg_prolong_cell_kernel, dim3(mg_blocks(ctx, CG.nlocal)), dim3(256), 0,
+                         ctx->stream, G, F.x, CG, (const double*)Cl.x, lo, hi, mg->skip);
+    else
+      hipLaunchKernelGGL(mg_prolong_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0,
+                         ctx->stream, G, F.x, CG, (const double*)Cl.x, lo, hi, mg->skip);
     PB_HIP(hipGetLastError());
     PB_TRY(smooth(mg, F, 1, 0));
-    PB_TRY(smooth(mg, F, 0, 0));
+    PB_TRY(smooth(mg, F, 0, 0, l == 0 ? sums_st : nullptr, nparts));
   }
   return PB_OK;
 }

@@ -313,9 +313,9 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
     PB_HIP(hipMemcpyAsync(k->r, b->d, vb, hipMemcpyDeviceToDevice, ctx->stream));
     PB_HIP(hipMemsetAsync(x->d, 0, vb, ctx->stream));
     PB_HIP(hipMemsetAsync(k->pb[0], 0, vb, ctx->stream));
-    PB_TRY(mg_apply(k->mg, k->r, k->z));
     int np = 0;
-    PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
+    PB_TRY(mg_apply(k->mg, k->r, k->z, nullptr, k->d_st, &np));
+    if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
     PB_TRY(cg_finalize_init(ctx, np, k->d_st, k->d_hist, k->h_done_dev));
   } else {
     PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->pb[0], k->d_st, st.dinv, k->d_hist,
@@ -357,8 +357,8 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
   PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
   PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, k->r, k->d_st));
-  PB_TRY(mg_apply(k->mg, k->r, k->z, &k->d_st->done));
-  PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
+  PB_TRY(mg_apply(k->mg, k->r, k->z, &k->d_st->done, k->d_st, &np));
+  if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
 }
 
@@ -399,9 +399,9 @@ static int enqueue_iteration(pb_ksp* k) {
   PB_TRY(launch_cg_pass_b(g, s, p_new, p_old, k->x->d, k->r, gp, k->d_st, k->d_hist,
                           k->h_done_dev, i, k->defer_x, !k->mg));
   if (k->mg) {  // z = M^-1 r, then the residual sums over z
-    PB_TRY(mg_apply(k->mg, k->r, k->z, &k->d_st->done));
     int np = 0;
-    PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
+    PB_TRY(mg_apply(k->mg, k->r, k->z, &k->d_st->done, k->d_st, &np));
+    if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
     PB_TRY(cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, i));
   }
   return PB_OK;

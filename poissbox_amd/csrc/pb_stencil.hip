@@ -36,6 +36,7 @@ struct Geo {
   int remap;  // XCD-aware block remap on/off (PB_XCD_REMAP, default on)
   int nt;     // non-temporal output stores (PB_STENCIL_NT, default on)
   int rev;    // march each chunk downwards (k from the top plane to the bottom one)
+  int k0;     // global index of local plane 0 (red-black colouring)
 };
 
 template <int V>
@@ -67,6 +68,7 @@ __device__ __forceinline__ void store_row(double* p, int64_t idx, const double (
 // ---------------------------------------------------------------------------------------------
 struct PlainLoad {
   static constexpr int NR = 1;
+  static constexpr bool GHOST_RAW = false;  // ghost planes hold raw values to transform
   const double* __restrict__ x;
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ const double* src(int) const { return x; }
@@ -78,6 +80,7 @@ struct CgState;
 __device__ __forceinline__ double cg_bb(const CgState* st);
 struct CombineLoad {
   static constexpr int NR = 2;
+  static constexpr bool GHOST_RAW = false;
   const double* __restrict__ r;
   const double* __restrict__ p;
   const CgState* st;
@@ -103,6 +106,7 @@ struct CombineLoad {
 // ---------------------------------------------------------------------------------------------
 struct StoreY {
   static constexpr int NS = 0, NE = 0;
+  static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = true;
   double* __restrict__ y;
   __device__ __forceinline__ void prepare() {}
@@ -118,6 +122,7 @@ struct StoreY {
 // CG pass A: store p_new, accumulate p.w (VecXDot(P, W))
 struct PassA {
   static constexpr int NS = 1, NE = 0;
+  static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = true;
   double* __restrict__ p_new;
   __device__ __forceinline__ void prepare() {}
@@ -143,6 +148,7 @@ struct PassA {
 template <int XU>
 struct PassB {
   static constexpr int NS = 4, NE = XU == 1 ? 3 : (XU == 2 ? 2 : 1);
+  static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = XU != 1;
   double* __restrict__ x;
   double* __restrict__ r;
@@ -323,7 +329,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
           double raw[NR];
 #pragma unroll
           for (int a = 0; a < NR; ++a) raw[a] = zr[a][t][e];
-          q[t][e] = zr_ghost ? zr[0][t][e] : ld.value(raw);
+          q[t][e] = (zr_ghost && !Load::GHOST_RAW) ? zr[0][t][e] : ld.value(raw);
         }
     };
     auto issue_plane_ops = [&](int kk) {  // halo rows, edges, epilogue operands of own plane kk
@@ -404,25 +410,42 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         const double fromR = dpp_from_upper(q1[t][0]);
         const double xl0 = needL ? eL : fromL;
         const double xrl = needR ? eR : fromR;
-        double w[V];
+        if constexpr (Epi::RAW) {  // the epilogue combines the 7 values itself
+          double nzm[V], nym[V], nxm[V], nxp[V], nyp[V], nzp[V];
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-          const double xm = e == 0 ? xl0 : q1[t][e - 1];
-          const double xp = e == V - 1 ? xrl : q1[t][e + 1];
-          const double ym = t == 0 ? hdn[e] : q1[t - 1][e];
-          const double yp = t == TY - 1 ? hup[e] : q1[t + 1][e];
-          const double zm = g.rev ? q2[t][e] : q0[t][e];
-          const double zp = g.rev ? q0[t][e] : q2[t][e];
-          double s = cz * zm;
-          s = s + cy * ym;
-          s = s + cx * xm;
-          s = s + cc * q1[t][e];
-          s = s + cx * xp;
-          s = s + cy * yp;
-          s = s + cz * zp;
-          w[e] = s;
+          for (int e = 0; e < V; ++e) {
+            nxm[e] = e == 0 ? xl0 : q1[t][e - 1];
+            nxp[e] = e == V - 1 ? xrl : q1[t][e + 1];
+            nym[e] = t == 0 ? hdn[e] : q1[t - 1][e];
+            nyp[e] = t == TY - 1 ? hup[e] : q1[t + 1][e];
+            nzm[e] = g.rev ? q2[t][e] : q0[t][e];
+            nzp[e] = g.rev ? q0[t][e] : q2[t][e];
+          }
+          if (active)
+            ep.template put_raw<V>(base + (int64_t)(j0 + t) * nx + i0, i0 + j0 + t + g.k0 + k,
+                                   nzm, nym, nxm, q1[t], nxp, nyp, nzp, opc[t], acc, g.nt);
+        } else {
+          double w[V];
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            const double xm = e == 0 ? xl0 : q1[t][e - 1];
+            const double xp = e == V - 1 ? xrl : q1[t][e + 1];
+            const double ym = t == 0 ? hdn[e] : q1[t - 1][e];
+            const double yp = t == TY - 1 ? hup[e] : q1[t + 1][e];
+            const double zm = g.rev ? q2[t][e] : q0[t][e];
+            const double zp = g.rev ? q0[t][e] : q2[t][e];
+            double s = cz * zm;
+            s = s + cy * ym;
+            s = s + cx * xm;
+            s = s + cc * q1[t][e];
+            s = s + cx * xp;
+            s = s + cy * yp;
+            s = s + cz * zp;
+            w[e] = s;
+          }
+          if (active)
+            ep.template put<V>(base + (int64_t)(j0 + t) * nx + i0, q1[t], w, opc[t], acc, g.nt);
         }
-        if (active) ep.template put<V>(base + (int64_t)(j0 + t) * nx + i0, q1[t], w, opc[t], acc, g.nt);
       }
 #pragma unroll
       for (int t = 0; t < TY; ++t)
@@ -445,6 +468,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev) {
   Geo geo;
   geo.rev = env_int("PB_ZALT", 1) ? rev : 0;
+  geo.k0 = (int)g->k0;
   geo.nx = (int)g->n[0];
   geo.ny = (int)g->n[1];
   geo.nzl = (int)g->nzl;
@@ -534,10 +558,124 @@ int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
 }
 
 // ---------------------------------------------------------------------------------------------
+// Red-black SOR smoothing and the multigrid residual on the engine (pb_mg.hip; oracle
+// pbo_mg_apply). PETSc PCSOR update form x = (1 - w) x + w (b - sum_nb c x_nb) / c_centre,
+// neighbour sum in the order z-, y-, x-, x+, y+, z+. A half-sweep updates the points with
+// (i + j + k_global) % 2 == color in place: their neighbours all carry the other colour, which
+// the half-sweep does not modify, so halo rows read from other waves are the same whether or not
+// those waves have stored their plane yet (the stored other-colour values are bit-identical).
+// ---------------------------------------------------------------------------------------------
+// the red values of the first half-sweep from x = 0: (1 - w) * 0 + w * ((b - 0) / c)
+struct Red0Load {
+  static constexpr int NR = 1;
+  static constexpr bool GHOST_RAW = true;  // ghost planes are b's: transform them too
+  const double* __restrict__ b;
+  double cc, omega;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ const double* src(int) const { return b; }
+  __device__ __forceinline__ double value(const double* raw) const {
+    const double t = (raw[0] - 0.0) / cc;
+    return (1.0 - omega) * 0.0 + omega * t;
+  }
+};
+
+// SUMS: the last half-sweep of a preconditioner apply inside CG also takes the residual sums of
+// its output z against r = b (t = z - mu_old: sum t, t^2, t.r, r -- cg_pc_sums_kernel's)
+template <bool SUMS>
+struct SorHalfT {
+  static constexpr int NS = SUMS ? 4 : 0, NE = 1;
+  static constexpr bool PREFETCH = true, RAW = true;
+  double* x;
+  const double* __restrict__ b;
+  double cx, cy, cz, cc, omega;
+  int color;  // points with (i + j + k_global) % 2 == color are updated
+  int first;  // 1: black half-sweep after the zero-start red one (x_old = 0, field = Red0Load)
+  const CgState* st;
+  double mu;
+  __device__ __forceinline__ void prepare();
+  __device__ __forceinline__ const double* src(int) const { return b; }
+  template <int V>
+  __device__ __forceinline__ void put_raw(int64_t idx, int par, const double (&zm)[V],
+                                          const double (&ym)[V], const double (&xm)[V],
+                                          const double (&c)[V], const double (&xp)[V],
+                                          const double (&yp)[V], const double (&zp)[V],
+                                          const double (&op)[1][V], double* acc, int nt) const {
+    double o[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      double nb = cz * zm[e];
+      nb = nb + cy * ym[e];
+      nb = nb + cx * xm[e];
+      nb = nb + cx * xp[e];
+      nb = nb + cy * yp[e];
+      nb = nb + cz * zp[e];
+      const double t = (op[0][e] - nb) / cc;
+      const double xo = first ? 0.0 : c[e];
+      const double xn = (1.0 - omega) * xo + omega * t;
+      o[e] = ((par + e) & 1) == color ? xn : c[e];
+      if constexpr (SUMS) {
+        const double rv = op[0][e];
+        const double t2 = o[e] - mu;
+        acc[0] += t2;
+        acc[1] += t2 * t2;
+        acc[2] += t2 * rv;
+        acc[3] += rv;
+      }
+    }
+    store_row<V>(x, idx, o, nt);
+    (void)acc;
+  }
+};
+typedef SorHalfT<false> SorHalf;
+
+// res = b - A x (the reference operator's summation order)
+struct ResidEpi {
+  static constexpr int NS = 0, NE = 1;
+  static constexpr bool PREFETCH = true, RAW = false;
+  double* __restrict__ res;
+  const double* __restrict__ b;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ const double* src(int) const { return b; }
+  template <int V>
+  __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
+                                      double (&op)[1][V], double*, int nt) const {
+    double o[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = op[0][e] - w[e];
+    store_row<V>(res, idx, o, nt);
+    (void)c;
+  }
+};
+
+int launch_mg_sor(pb_grid* g, const Star& s, double* x, const double* b, const StencilPlanes& gp,
+                  double omega, int color, int first, const int* skip, const CgState* sums_st,
+                  int* nparts) {
+  ScopedTimer tm(g->ctx, "mg_sor");
+  if (sums_st) {  // partial sums -> ctx->d_partials[0 .. nparts*4)
+    SorHalfT<true> ep{x, b, s.cx, s.cy, s.cz, s.cc, omega, color, 0, sums_st, 0.0};
+    return launch_any(g, s, PlainLoad{x}, gp, ep, skip, PLANES_ALL, 0, nparts);
+  }
+  SorHalf ep{x, b, s.cx, s.cy, s.cz, s.cc, omega, first ? 1 : color, first, nullptr, 0.0};
+  if (first) return launch_any(g, s, Red0Load{b, s.cc, omega}, gp, ep, skip);
+  return launch_any(g, s, PlainLoad{x}, gp, ep, skip);
+}
+
+int launch_mg_residual(pb_grid* g, const Star& s, const double* x, const double* b,
+                       const StencilPlanes& gp, double* res, const int* skip) {
+  ScopedTimer tm(g->ctx, "mg_residual");
+  return launch_any(g, s, PlainLoad{x}, gp, ResidEpi{res, b}, skip);
+}
+
+// ---------------------------------------------------------------------------------------------
 // CG (PETSc KSPSolve_CG + PCJacobi + MatNullSpace), device-resident state
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ double cg_bb(const CgState* st) {
   return st->it == 0 ? 0.0 : st->beta / st->betaold;
+}
+
+template <bool SUMS>
+__device__ __forceinline__ void SorHalfT<SUMS>::prepare() {
+  if constexpr (SUMS) mu = st->mu;
 }
 
 template <int XU>

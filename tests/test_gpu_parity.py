@@ -515,10 +515,23 @@ def test_cg_with_compact_operator(ctx):
 # SOR / geometric multigrid preconditioners -- parity against the oracle's
 # restatement of the same V-cycle (bit-exact PC apply), CG histories within HIST_RTOL
 # ---------------------------------------------------------------------------------------------
+# kernel selections of the V-cycle (all bit-identical): default thresholds (small test grids run
+# the per-pair kernels), and every level forced onto the stencil-engine SOR/residual kernels and
+# the z-marching restriction / prolongation; the per-coarse-cell and per-fine-pair prolongations
+MG_KERNELS = {"default": {},
+              "engine": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
+              "cell": {"PB_MG_PROLONG_CELL": "1", "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
+              "legacy": {"PB_MG_ENGINE_MIN_PLANE": "1000000000", "PB_MG_RESTRICT_Z": "0",
+                         "PB_MG_PROLONG_CELL": "0"}}
+
+
+@pytest.mark.parametrize("kern", sorted(MG_KERNELS))
 @pytest.mark.parametrize("pc,n3,levels", [("sor", (16, 12, 8), 0), ("mg", (32, 32, 32), 0),
                                           ("mg", (64, 48, 32), 0), ("mg", (32, 16, 24), 2),
-                                          ("mg", (8, 8, 8), 0)])
-def test_pc_apply_bit_exact(ctx, pc, n3, levels):
+                                          ("mg", (8, 8, 8), 0), ("mg", (256, 256, 32), 0)])
+def test_pc_apply_bit_exact(ctx, monkeypatch, kern, pc, n3, levels):
+    for k_, v_ in MG_KERNELS[kern].items():
+        monkeypatch.setenv(k_, v_)
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
     r = O.fill_random(N, 11)
@@ -534,8 +547,13 @@ def test_pc_apply_bit_exact(ctx, pc, n3, levels):
     k.destroy()
 
 
+@pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("pc,n", [("sor", 32), ("mg", 32), ("mg", 64)])
-def test_cg_sor_mg_matches_oracle(ctx, pc, n):
+def test_cg_sor_mg_matches_oracle(ctx, monkeypatch, kern, pc, n):
+    """CG + SOR / MG. 'engine': every level on the stencil-engine kernels, so the last half-sweep
+    of each PC apply also takes the CG residual sums (no separate pass)."""
+    for k_, v_ in MG_KERNELS[kern].items():
+        monkeypatch.setenv(k_, v_)
     n3 = (n, n, n)
     N = n ** 3
     h = (1.0 / n,) * 3
@@ -578,9 +596,12 @@ def test_mg_rejects_odd_extents(ctx):
         pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
 
 
+@pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("nranks,n", [(2, (16, 16, 32)), (4, (16, 16, 32)), (3, (16, 16, 12))])
-def test_multirank_mg_bit_exact_and_cg(nranks, n):
+def test_multirank_mg_bit_exact_and_cg(monkeypatch, kern, nranks, n):
     """Slab-decomposed V-cycle (halo exchanges per level) equals the single-grid restatement."""
+    for k_, v_ in MG_KERNELS[kern].items():
+        monkeypatch.setenv(k_, v_)
     N = int(np.prod(n))
     h = tuple(1.0 / m for m in n)
     r = O.fill_random(N, 3)
