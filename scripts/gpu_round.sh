@@ -1,6 +1,6 @@
 #!/bin/bash
 # Full GPU-box pass: parity tests + smoke + bench (gpu_check.sh), then a rocprofv3 kernel-trace
-# stats run of the same bench, the PMC passes and the per-row measurements. Stops at the first
+# stats run of the same bench, the PMC passes, the per-row measurements and full solves. Stops at the first
 # failing step (exit status of that step).
 set -u
 R=$GRAFT_REPO_ROOT
@@ -10,4 +10,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o benc
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R && bash scripts/gpu_pmc.sh || exit $?
 cd $R && timeout -k 10 900 python scripts/bench_rows.py > gpurun_out/rows.jsonl 2> gpurun_out/rows.err
-rc=$?; echo "rows rc=$rc"; exit $rc
+rc=$?; echo "rows rc=$rc"; [ $rc -eq 0 ] || exit $rc
+PCS=mg,jacobi timeout -k 10 600 python scripts/bench_solve.py 256 512 > gpurun_out/solve.jsonl 2> gpurun_out/solve.err
+rc=$?; echo "solve rc=$rc"; exit $rc
