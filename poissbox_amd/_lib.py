@@ -8,7 +8,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpoissbox_gpu.so")
+# PB_LIB: load an alternative build of the same ABI (kernel-variant experiments, scripts/)
+LIB_PATH = os.environ.get("PB_LIB") or os.path.join(_HERE, "libpoissbox_gpu.so")
 
 c_i64 = C.c_int64
 c_d = C.c_double

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -90,6 +91,7 @@ struct pb_ctx {
   size_t scratch_len = 0;
   // timing
   bool timing = false;
+  bool roctx = false;  // PB_ROCTX=1: roctx ranges around every timed phase (rocprofv3 --marker-trace)
   std::map<std::string, pb::TimerSlot> timers;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
@@ -145,10 +147,12 @@ struct ScopedTimer {
   const char* name;
   hipEvent_t ev0 = nullptr;
   ScopedTimer(pb_ctx* c, const char* n) : ctx(c), name(n) {
+    if (ctx->roctx) roctxRangePushA(name);
     if (ctx->timing) timer_begin(ctx, name, &ev0);
   }
   ~ScopedTimer() {
     if (ctx->timing) timer_end(ctx, name, ev0);
+    if (ctx->roctx) roctxRangePop();
   }
 };
 

@@ -291,6 +291,7 @@ int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
       cus > 0)
     ctx->num_cus = cus;
+  ctx->roctx = env_int("PB_ROCTX", 0) != 0;
   PB_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
   PB_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
   PB_HIP(hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming));

@@ -494,6 +494,7 @@ int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
 
 int pb_ksp_solve(pb_ksp* k, const pb_vec* b, pb_vec* x, pb_ksp_result* res, double* history,
                  int64_t cap) {
+  ScopedTimer tm(k->A->grid->ctx, "KSPSolve");
   PB_TRY(pb_ksp_begin(k, b, x));
   PB_TRY(pb_ksp_iterate(k, k->opts.max_it + 2 * (int64_t)k->opts.check_every));
   return pb_ksp_end(k, res, history, cap);

@@ -25,7 +25,10 @@ namespace pb {
 
 typedef double dv2 __attribute__((ext_vector_type(2)));
 
-static constexpr int kWaves = 4;
+#ifndef PB_KWAVES
+#define PB_KWAVES 4  // waves per workgroup (stacked in y)
+#endif
+static constexpr int kWaves = PB_KWAVES;
 static constexpr int kThreads = 64 * kWaves;
 
 struct Geo {
@@ -106,7 +109,8 @@ struct CombineLoad {
 // ---------------------------------------------------------------------------------------------
 struct StoreY {
   static constexpr int NS = 0, NE = 0;
-  static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
+  static constexpr bool RAW = false;
+  static constexpr int WGCU = 3;  // workgroups per CU the grid is sized for  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = true;
   double* __restrict__ y;
   __device__ __forceinline__ void prepare() {}
@@ -122,7 +126,8 @@ struct StoreY {
 // CG pass A: store p_new, accumulate p.w (VecXDot(P, W))
 struct PassA {
   static constexpr int NS = 1, NE = 0;
-  static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
+  static constexpr bool RAW = false;
+  static constexpr int WGCU = 3;  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = true;
   double* __restrict__ p_new;
   __device__ __forceinline__ void prepare() {}
@@ -148,7 +153,9 @@ struct PassA {
 template <int XU>
 struct PassB {
   static constexpr int NS = 4, NE = XU == 1 ? 3 : (XU == 2 ? 2 : 1);
-  static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
+  static constexpr bool RAW = false;
+  // one workgroup per CU (z-chunks of half the slab at 512^3): 8-10 % faster than 3 per CU
+  static constexpr int WGCU = 1;  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = XU != 1;
   double* __restrict__ x;
   double* __restrict__ r;
@@ -216,8 +223,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 template <int NS>
 __device__ __forceinline__ void block_partials(double* acc, double* parts) {
   if constexpr (NS > 0) {
-    __shared__ double red[kWaves][NS];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // any block size up to 16 waves (the engine's kWaves, 256-thread elementwise kernels)
+    __shared__ double red[16][NS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       double v = acc[s];
@@ -233,7 +241,7 @@ __device__ __forceinline__ void block_partials(double* acc, double* parts) {
     if (threadIdx.x < NS) {
       double v = 0.0;
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) v += red[w][threadIdx.x];
+      for (int w = 0; w < nw; ++w) v += red[w][threadIdx.x];
       parts[(int64_t)blockIdx.x * NS + threadIdx.x] = v;
     }
   }
@@ -465,7 +473,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 // Plane sets: PLANES_ALL = [0, nzl); PLANES_INTERIOR = [1, nzl-1) (no ghost plane is read);
 // PLANES_BOUNDARY = {0, nzl-1} (the two planes that read ghosts) -- the split lets the halo
 // exchange of a multi-rank step overlap the interior.
-static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev) {
+static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   Geo geo;
   geo.rev = env_int("PB_ZALT", 1) ? rev : 0;
   geo.k0 = (int)g->k0;
@@ -490,9 +498,10 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev) {
   geo.k_hi = mode == PLANES_INTERIOR ? geo.nzl - 1 : geo.nzl;
   const int nk = geo.k_hi - geo.k_lo;
   const int columns = geo.nsegx * geo.ntile;
-  // 3 workgroups per CU: long z-chunks (few chunk-boundary re-reads). Measured at 512^3: also
-  // best for the CG passes whose registers allow only 2 resident per CU (768 blocks beat 512)
-  int target = env_int("PB_STENCIL_BLOCKS", 3 * g->ctx->num_cus);
+  // wgcu (the epilogue's WGCU) workgroups per CU: long z-chunks, few chunk-boundary re-reads.
+  // Measured at 512^3: 3 per CU for the matvec and pass A (768 blocks beat 512 even where the
+  // registers allow only 2 resident), 1 per CU for pass B
+  int target = env_int("PB_STENCIL_BLOCKS", wgcu * g->ctx->num_cus);
   int nchunk = (target + columns - 1) / columns;
   if (nchunk > nk) nchunk = nk;
   if (nchunk < 1) nchunk = 1;
@@ -512,8 +521,9 @@ static int pick_ty(int ny) {
 
 template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
-                    const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev) {
-  Geo geo = make_geo(g, V, TY, mode, rev);
+                    const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev,
+                    int wgcu) {
+  Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU);
   const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
   constexpr int NS = Epi::NS > 0 ? Epi::NS : 1;
   if ((part_off + nblocks) * NS > g->ctx->partials_cap)
@@ -530,20 +540,20 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
 template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                       const Epi& ep, const int* skip, int mode = PLANES_ALL, int part_off = 0,
-                      int* nb_out = nullptr, int rev = 0) {
+                      int* nb_out = nullptr, int rev = 0, int wgcu = 0) {
   const bool vec2 = (g->n[0] % 2) == 0;
   const int ty = pick_ty((int)g->n[1]);
   if (vec2) {
     switch (ty) {
-      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
-      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
-      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
+      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
+      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
+      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
     }
   }
   switch (ty) {
-    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
-    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
-    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev);
+    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
+    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
+    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
   }
 }
 
@@ -585,6 +595,7 @@ template <bool SUMS>
 struct SorHalfT {
   static constexpr int NS = SUMS ? 4 : 0, NE = 1;
   static constexpr bool PREFETCH = true, RAW = true;
+  static constexpr int WGCU = 1;  // (the zero-start sweep overrides: 3)
   double* x;
   const double* __restrict__ b;
   double cx, cy, cz, cc, omega;
@@ -632,6 +643,7 @@ typedef SorHalfT<false> SorHalf;
 struct ResidEpi {
   static constexpr int NS = 0, NE = 1;
   static constexpr bool PREFETCH = true, RAW = false;
+  static constexpr int WGCU = 1;
   double* __restrict__ res;
   const double* __restrict__ b;
   __device__ __forceinline__ void prepare() {}
@@ -656,7 +668,8 @@ int launch_mg_sor(pb_grid* g, const Star& s, double* x, const double* b, const S
     return launch_any(g, s, PlainLoad{x}, gp, ep, skip, PLANES_ALL, 0, nparts);
   }
   SorHalf ep{x, b, s.cx, s.cy, s.cz, s.cc, omega, first ? 1 : color, first, nullptr, 0.0};
-  if (first) return launch_any(g, s, Red0Load{b, s.cc, omega}, gp, ep, skip);
+  if (first)  // measured: the zero-start sweep prefers 3 workgroups per CU, the others 1
+    return launch_any(g, s, Red0Load{b, s.cc, omega}, gp, ep, skip, PLANES_ALL, 0, nullptr, 0, 3);
   return launch_any(g, s, PlainLoad{x}, gp, ep, skip);
 }
 

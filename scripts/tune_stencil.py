@@ -29,7 +29,7 @@ base_env = dict(os.environ)
 for rnd in range(rounds):
     for i, cfg in enumerate(configs):
         for k in ("PB_STENCIL_TY", "PB_STENCIL_BLOCKS", "PB_XCD_REMAP", "PB_CG_DEFER_X",
-                  "PB_ZALT", "PB_STENCIL_NT"):
+                  "PB_ZALT", "PB_STENCIL_NT", "PB_CG_DEFER_X"):
             if k in base_env:
                 os.environ[k] = base_env[k]
             else:
