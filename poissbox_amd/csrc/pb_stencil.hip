@@ -503,6 +503,14 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   // registers allow only 2 resident), 1 per CU for pass B
   int target = env_int("PB_STENCIL_BLOCKS", wgcu * g->ctx->num_cus);
   int nchunk = (target + columns - 1) / columns;
+  // z-chunks shorter than PB_STENCIL_KCMIN (64) planes re-read too many boundary planes (2 per
+  // chunk): use fewer, longer chunks, but keep at least one workgroup per CU (256^3: 8 chunks of
+  // 32 planes instead of 24 of 11, measured 8-15 % faster)
+  const int kcmin = env_int("PB_STENCIL_KCMIN", 64);
+  if (!getenv("PB_STENCIL_BLOCKS") && kcmin > 0 && nk / nchunk < kcmin) {
+    const int floor_cu = (g->ctx->num_cus + columns - 1) / columns;
+    nchunk = std::max(nk / kcmin, floor_cu);
+  }
   if (nchunk > nk) nchunk = nk;
   if (nchunk < 1) nchunk = 1;
   geo.kc = (nk + nchunk - 1) / nchunk;

@@ -28,8 +28,7 @@ acc = {i: {"mv": [], "a": [], "b": [], "be": [], "it": []} for i in range(len(co
 base_env = dict(os.environ)
 for rnd in range(rounds):
     for i, cfg in enumerate(configs):
-        for k in ("PB_STENCIL_TY", "PB_STENCIL_BLOCKS", "PB_XCD_REMAP", "PB_CG_DEFER_X",
-                  "PB_ZALT", "PB_STENCIL_NT", "PB_CG_DEFER_X"):
+        for k in set().union(*configs):  # every key any config sets: back to the base env
             if k in base_env:
                 os.environ[k] = base_env[k]
             else:
