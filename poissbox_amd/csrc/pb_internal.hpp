@@ -181,6 +181,11 @@ struct CgState;
 int launch_mg_sor(pb_grid* g, const Star& s, double* x, const double* b, const StencilPlanes& gp,
                   double omega, int color, int first, const int* skip,
                   const CgState* sums_st = nullptr, int* nparts = nullptr);
+// both red-black half-sweeps (c1 first) in one pass, out of place, one rank (pb_stencil.hip)
+bool sor_sweep2_supported(const pb_grid* g);
+int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double* b, double* xout,
+                      double omega, int c1, const int* skip, const CgState* sums_st = nullptr,
+                      int* nparts = nullptr);
 int launch_mg_residual(pb_grid* g, const Star& s, const double* x, const double* b,
                        const StencilPlanes& gp, double* res, const int* skip);
 

@@ -394,6 +394,7 @@ __global__ __launch_bounds__(256) void mg_prolong_cell_kernel(MgGeo F, double* _
 // The same prolongation, one thread per coarse (I, J) column marching over a chunk of coarse
 // planes: the 3 x 3 coarse values of planes K-1, K, K+1 stay in registers (each coarse value is
 // loaded ~3 times per coarse cell instead of 27), children by the formula above.
+// xout = xf + P xc (xout may be xf: in place).
 struct Coarse9 {
   double v[3][3];  // [row Jm, J, Jp][col Im, I, Ip]
 };
@@ -407,7 +408,8 @@ __device__ __forceinline__ void load9(const double* pl, int64_t rm, int64_t r0, 
     for (int b = 0; b < 3; ++b) c.v[a][b] = pl[rows[a] + cols[b]];
 }
 
-__global__ __launch_bounds__(256) void mg_prolong_z_kernel(MgGeo F, double* __restrict__ xf, MgGeo Cg,
+__global__ __launch_bounds__(256) void mg_prolong_z_kernel(MgGeo F, const double* xf,
+                                                           double* xout, MgGeo Cg,
                                                            int kc, const double* __restrict__ xc,
                                                            const double* __restrict__ lo,
                                                            const double* __restrict__ hi,
@@ -433,14 +435,14 @@ __global__ __launch_bounds__(256) void mg_prolong_z_kernel(MgGeo F, double* __re
     load9(plane(K + 1), rm, r0, rp, Im, I, Ip, cp);
     // all four fine pairs are loaded before any is stored (the stores would otherwise order
     // each later load behind them)
-    dv2* q[2][2];
+    int64_t q[2][2];
     dv2 ov[2][2];
 #pragma unroll
     for (int dk = 0; dk < 2; ++dk)
 #pragma unroll
       for (int dj = 0; dj < 2; ++dj) {
-        q[dk][dj] = (dv2*)(xf + (int64_t)(2 * K + dk) * F.plane + (int64_t)(2 * J + dj) * F.nx + 2 * I);
-        ov[dk][dj] = *q[dk][dj];
+        q[dk][dj] = (int64_t)(2 * K + dk) * F.plane + (int64_t)(2 * J + dj) * F.nx + 2 * I;
+        ov[dk][dj] = *(const dv2*)(xf + q[dk][dj]);
       }
 #pragma unroll
     for (int dk = 0; dk < 2; ++dk) {
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(256) void mg_prolong_z_kernel(MgGeo F, double* __re
 #pragma unroll
     for (int dk = 0; dk < 2; ++dk)
 #pragma unroll
-      for (int dj = 0; dj < 2; ++dj) *q[dk][dj] = ov[dk][dj];
+      for (int dj = 0; dj < 2; ++dj) *(dv2*)(xout + q[dk][dj]) = ov[dk][dj];
     cm = c0;
     c0 = cp;
   }
@@ -687,11 +689,16 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     PB_TRY(ghosts(Cl, Cl.x, &lo, &hi));
     const MgGeo G = F.geo(), CG = Cl.geo();
     const int64_t cols = (int64_t)CG.nx * CG.ny;
+    bool fused = false;
     if (mg->prolong_cell == 2 && cols >= mg->restrict_z_min_cols) {
       int64_t nchunk = 1;
       const int kc = transfer_chunk(ctx, cols, CG.nzl, &nchunk);
+      // fused post-smoothing: prolongate into the residual scratch, then both half-sweeps in one
+      // pass back into F.x (which also takes CG's residual sums on level 0)
+      fused = F.res && F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g);
       hipLaunchKernelGGL(mg_prolong_z_kernel, dim3(mg_blocks(ctx, cols * nchunk)), dim3(256), 0,
-                         ctx->stream, G, F.x, CG, kc, (const double*)Cl.x, lo, hi, mg->skip);
+                         ctx->stream, G, (const double*)F.x, fused ? F.res : F.x, CG, kc,
+                         (const double*)Cl.x, lo, hi, mg->skip);
     } else if (mg->prolong_cell)
       hipLaunchKernelGGL(mg_prolong_cell_kernel, dim3(mg_blocks(ctx, CG.nlocal)), dim3(256), 0,
                          ctx->stream, G, F.x, CG, (const double*)Cl.x, lo, hi, mg->skip);
@@ -699,8 +706,13 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
       hipLaunchKernelGGL(mg_prolong_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0,
                          ctx->stream, G, F.x, CG, (const double*)Cl.x, lo, hi, mg->skip);
     PB_HIP(hipGetLastError());
-    PB_TRY(smooth(mg, F, 1, 0));
-    PB_TRY(smooth(mg, F, 0, 0, l == 0 ? sums_st : nullptr, nparts));
+    if (fused) {
+      PB_TRY(launch_sor_sweep2(F.g, F.s, F.res, F.b, F.x, mg->omega, 1, mg->skip,
+                               l == 0 ? sums_st : nullptr, l == 0 ? nparts : nullptr));
+    } else {
+      PB_TRY(smooth(mg, F, 1, 0));
+      PB_TRY(smooth(mg, F, 0, 0, l == 0 ? sums_st : nullptr, nparts));
+    }
   }
   return PB_OK;
 }

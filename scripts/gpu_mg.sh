@@ -3,7 +3,7 @@
 # several kernel configurations (MG_CONFIGS: ';'-separated env assignments, '-' = defaults).
 set -u
 mkdir -p gpurun_out
-timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -x --timeout 120 --timeout-method thread -k "mg or sor or pc_apply or multirank" > gpurun_out/pt_mg.log 2>&1
+timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -x --timeout 120 --timeout-method thread -k "mg or sor or pc_apply or multirank or fused" > gpurun_out/pt_mg.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pt_mg.log; [ $rc -eq 0 ] || exit $rc
 IFS=';' read -ra CFGS <<< "${MG_CONFIGS:--}"
 i=0

@@ -570,6 +570,35 @@ def test_cg_sor_mg_matches_oracle(ctx, monkeypatch, kern, pc, n):
         assert its <= 16  # h-independent V-cycle preconditioning
 
 
+@pytest.mark.parametrize("kern", ["default", "engine", "legacy"])
+def test_cg_mg_fused_post_smoothing(ctx, monkeypatch, kern):
+    """x extent >= 128: the V-cycle's post-smoothing runs as ONE fused two-colour pass (out of
+    place, with CG's residual sums on level 0); history / solution within the CG bar, PC apply
+    bit-identical to the oracle."""
+    for k_, v_ in MG_KERNELS[kern].items():
+        monkeypatch.setenv(k_, v_)
+    n3 = (128, 128, 32)
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-10, pc="mg")
+    r = O.fill_random(N, 7)
+    zref = O.mg_apply(r, n3, h, pc="mg")
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg", "-ksp_rtol", "1e-10"]))
+    rv, zv = pb.Vec(da), pb.Vec(da)
+    rv.set_values(r)
+    k.pc_apply(rv, zv)
+    assert np.array_equal(zv.get_values(), zref)
+    bv.set_values(b)
+    reason, its, hist = k.solve(bv, x)
+    assert reason == ro == 2 and its == itso
+    assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
+    assert np.max(np.abs(x.get_values() - xo)) <= 1e-6 * np.max(np.abs(xo))
+    k.destroy()
+
+
 def test_cg_compact_operator_mg_pc(ctx):
     """Config 5 shape: compact A inside CG, MG-SOR preconditioner on the 7-point P."""
     n3 = (32, 32, 32)
