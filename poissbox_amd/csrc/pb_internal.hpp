@@ -91,6 +91,7 @@ struct pb_ctx {
   size_t scratch_len = 0;
   // timing
   bool timing = false;
+  std::vector<std::string> timing_only;  // PB_TIMING_ONLY="a,b": time only these phases
   bool roctx = false;  // PB_ROCTX=1: roctx ranges around every timed phase (rocprofv3 --marker-trace)
   std::map<std::string, pb::TimerSlot> timers;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -142,16 +143,20 @@ void timer_begin(pb_ctx* ctx, const char* name, hipEvent_t* ev);
 void timer_end(pb_ctx* ctx, const char* name, hipEvent_t ev0);
 void timers_collect(pb_ctx* ctx);
 
+bool timer_wanted(const pb_ctx* ctx, const char* name);
+
 struct ScopedTimer {
   pb_ctx* ctx;
   const char* name;
   hipEvent_t ev0 = nullptr;
+  bool on = false;
   ScopedTimer(pb_ctx* c, const char* n) : ctx(c), name(n) {
     if (ctx->roctx) roctxRangePushA(name);
-    if (ctx->timing) timer_begin(ctx, name, &ev0);
+    on = ctx->timing && timer_wanted(ctx, name);
+    if (on) timer_begin(ctx, name, &ev0);
   }
   ~ScopedTimer() {
-    if (ctx->timing) timer_end(ctx, name, ev0);
+    if (on) timer_end(ctx, name, ev0);
     if (ctx->roctx) roctxRangePop();
   }
 };
@@ -171,6 +176,9 @@ int allreduce_device(pb_ctx* ctx, double* d_vals, int count);
 struct StencilPlanes {
   const double* ghost_lo;  // plane at k = -1
   const double* ghost_hi;  // plane at k = nzl
+  // one rank: read the periodic wrap planes of the loader's raw arrays in place (k mod nzl)
+  // instead of ghost planes (which then need not exist)
+  bool wrap = false;
 };
 enum { PLANES_ALL = 0, PLANES_INTERIOR = 1, PLANES_BOUNDARY = 2 };
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,

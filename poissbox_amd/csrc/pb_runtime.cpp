@@ -46,6 +46,13 @@ static hipEvent_t take_event(pb_ctx* ctx) {
   return e;
 }
 
+bool timer_wanted(const pb_ctx* ctx, const char* name) {
+  if (ctx->timing_only.empty()) return true;
+  for (const auto& n : ctx->timing_only)
+    if (n == name) return true;
+  return false;
+}
+
 void timer_begin(pb_ctx* ctx, const char*, hipEvent_t* ev) {
   *ev = take_event(ctx);
   (void)hipEventRecord(*ev, ctx->stream);
@@ -379,6 +386,22 @@ int pb_ctx_destroy(pb_ctx* ctx) {
 int pb_ctx_set_timing(pb_ctx* ctx, int enable) {
   PB_CHECK_ARG(ctx, "ctx is NULL");
   ctx->timing = enable != 0;
+  // PB_TIMING_ONLY (comma-separated phase names): record events around those phases only, so a
+  // timed region is not perturbed by event records around every kernel
+  ctx->timing_only.clear();
+  const char* only = getenv("PB_TIMING_ONLY");
+  if (enable && only && *only) {
+    std::string cur;
+    for (const char* c = only;; ++c) {
+      if (*c == ',' || *c == '\0') {
+        if (!cur.empty()) ctx->timing_only.push_back(cur);
+        cur.clear();
+        if (!*c) break;
+      } else {
+        cur += *c;
+      }
+    }
+  }
   return PB_OK;
 }
 

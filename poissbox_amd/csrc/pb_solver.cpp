@@ -372,20 +372,23 @@ static int enqueue_iteration(pb_ksp* k) {
   double* p_new = k->pb[(i + 1) % 2];
   // Jacobi: pass A builds z = dinv*r - mu on the fly; SOR / MG: z is stored (dinv = 1)
   const double* zsrc = k->mg ? k->z : k->r;
-  PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st));
   StencilPlanes gp;
   int nparts = 0;
   if (!ctx->split) {
-    gp.ghost_lo = g->bnd_hi;  // p_new of plane nzl-1 wraps below plane 0
-    gp.ghost_hi = g->bnd_lo;
+    // periodic wrap read in place: pass A combines r, p_old of the wrap planes itself and pass B
+    // reads p_new's wrap planes (no boundary-plane kernel on one rank)
+    gp.ghost_lo = gp.ghost_hi = nullptr;
+    gp.wrap = true;
     PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
   } else if (g->nzl < 3) {
+    PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st));
     PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
     PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
   } else {
     // the p-plane halo exchange (RCCL, comm stream) overlaps pass A's interior planes
+    PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st));
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
     int nb1 = 0, nb2 = 0;

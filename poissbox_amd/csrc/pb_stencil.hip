@@ -40,6 +40,7 @@ struct Geo {
   int nt;     // non-temporal output stores (PB_STENCIL_NT, default on)
   int rev;    // march each chunk downwards (k from the top plane to the bottom one)
   int k0;     // global index of local plane 0 (red-black colouring)
+  int wrap;   // planes -1 / nzl are the periodic wrap of the raw arrays (StencilPlanes::wrap)
 };
 
 template <int V>
@@ -315,6 +316,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
     double opc[TY][NE][V], opn[Epi::PREFETCH ? TY : 1][NE][V];
 
     auto issue_zrow = [&](int kk) {  // raw rows of plane kk in [-1, nzl] -> zr
+      if (g.wrap) kk = kk < 0 ? kk + g.nzl : (kk >= g.nzl ? kk - g.nzl : kk);
       zr_ghost = kk < 0 || kk >= g.nzl;
       if (zr_ghost) {
         const double* gp = kk < 0 ? ghost_lo : ghost_hi;
@@ -484,6 +486,7 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   Geo geo;
   geo.rev = env_int("PB_ZALT", 1) ? rev : 0;
   geo.k0 = (int)g->k0;
+  geo.wrap = 0;
   geo.nx = (int)g->n[0];
   geo.ny = (int)g->n[1];
   geo.nzl = (int)g->nzl;
@@ -539,6 +542,7 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
                     const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev,
                     int wgcu) {
   Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU);
+  geo.wrap = gp.wrap && !g->ctx->split ? 1 : 0;
   const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
   constexpr int NS = Epi::NS > 0 ? Epi::NS : 1;
   if ((part_off + nblocks) * NS > g->ctx->partials_cap)
