@@ -702,7 +702,10 @@ int launch_mg_sor(pb_grid* g, const Star& s, double* x, const double* b, const S
 // Per point: read xin and b once, write xout once (24 B/DoF instead of 2 x 24). Arithmetic per
 // point is the two half-sweeps' (SorHalf / mg_smooth_kernel), so results are bit-identical.
 // ---------------------------------------------------------------------------------------------
-static constexpr int kTY2 = 2;          // own rows per wave
+#ifndef PB_SWEEP2_TY
+#define PB_SWEEP2_TY 3  // measured: 3 beats 2 (0.97 vs 1.09 ms at 512^3) and 1 (1.24)
+#endif
+static constexpr int kTY2 = PB_SWEEP2_TY;  // own rows per wave
 static constexpr int kRW = kTY2 + 4;    // xin rows held: j0-2 .. j0+TY2+1
 static constexpr int kSegOut = 112;     // outputs per wave segment (lanes 4..59): 896 B, whole
                                         // 128-B lines, so no line is written by two waves
@@ -868,7 +871,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
         double ov[2];
         ov[0] = a1 ? s1[1][r][0] : v;
         ov[1] = a1 ? v : s1[1][r][1];
-        if (out_ok) {
+        if (out_ok && j0 + r - 2 < ny) {  // rows past ny (last tile) would wrap: not ours
           store_row<2>(xout, base + ro[r], ov, g.nt);
           if constexpr (SUMS) {
 #pragma unroll
