@@ -194,6 +194,9 @@ bool sor_sweep2_supported(const pb_grid* g);
 int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double* b, double* xout,
                       double omega, int c1, const int* skip, const CgState* sums_st = nullptr,
                       int* nparts = nullptr);
+// pre-smoothing from zero (red + black half-sweeps) fused with the residual: x, res from b
+int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double* x, double* res,
+                              double omega, const int* skip);
 int launch_mg_residual(pb_grid* g, const Star& s, const double* x, const double* b,
                        const StencilPlanes& gp, double* res, const int* skip);
 

@@ -647,17 +647,26 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
   for (int l = 0; l < L - 1; ++l) {  // down: pre-smooth (red, black), residual, restrict
     MgLevel& F = mg->lv[l];
     MgLevel& Cl = mg->lv[l + 1];
+    // one rank, large level: zero-start red + black half-sweeps and the residual in one pass
+    const bool fused = F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g) &&
+                       env_int("PB_MG_PRESMOOTH_FUSED", 1);
     {
       ScopedTimer t1(ctx, l == 0 ? "mg_fine_smooth_first" : "mg_coarse_levels");
-      PB_TRY(smooth(mg, F, 0, 1));  // red from zero + black
+      if (fused)
+        PB_TRY(launch_presmooth_residual(F.g, F.s, F.b, F.x, F.res, mg->omega, mg->skip));
+      else
+        PB_TRY(smooth(mg, F, 0, 1));  // red from zero + black
     }
     ScopedTimer t2(ctx, l == 0 ? "mg_fine_resid_restrict" : "mg_coarse_levels");
     const double *lo, *hi;
-    PB_TRY(ghosts(F, F.x, &lo, &hi));
     const MgGeo G = F.geo();
-    if (F.g->plane >= mg->engine_min_plane) {
+    if (fused) {
+      // residual already in F.res
+    } else if (F.g->plane >= mg->engine_min_plane) {
+      PB_TRY(ghosts(F, F.x, &lo, &hi));
       PB_TRY(launch_mg_residual(F.g, F.s, F.x, F.b, StencilPlanes{lo, hi}, F.res, mg->skip));
     } else {
+      PB_TRY(ghosts(F, F.x, &lo, &hi));
       hipLaunchKernelGGL(mg_residual_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0,
                          ctx->stream, G, (const double*)F.x, (const double*)F.b, lo, hi, F.s,
                          F.res, mg->skip);

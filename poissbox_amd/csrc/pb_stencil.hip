@@ -718,12 +718,17 @@ struct Sweep2Geo {
   int k0, remap, nt;
 };
 
-template <bool SUMS>
+// M = 0: SOR sweep (first colour c1, then the other) of xin -> xout.
+// M = 1: pre-smoothing from x = 0 plus residual: S1 = the zero-start red + black half-sweeps
+//        (red = w D^-1 b, black from those -- Red0Load + SorHalf's arithmetic; xin = b, c1 = 1),
+//        xout = S1 and res = b - A S1 (the residual kernel's summation order).
+template <bool SUMS, int M>
 __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, double cx, double cy,
                                                                double cz, double cc, double omega,
                                                                int c1, const double* __restrict__ xin,
                                                                const double* __restrict__ b,
                                                                double* __restrict__ xout,
+                                                               double* __restrict__ res,
                                                                const CgState* st, double* parts,
                                                                const int* skip) {
   if (skip && *skip) return;
@@ -783,6 +788,23 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
 #pragma unroll
       for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, base + ro[r], dst[r]);
     };
+    // M = 1: b values of plane kk -> the x of the zero-start red half-sweep (red: w D^-1 b,
+    // black: still 0)
+    auto xform = [&](double (&v)[kRW][2], int kk) {
+      if constexpr (M == 1) {
+        const int kp = kpar(kk);
+#pragma unroll
+        for (int r = 0; r < kRW; ++r)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const double t = (v[r][e] - 0.0) / cc;
+            const double red = (1.0 - omega) * 0.0 + omega * t;
+            v[r][e] = ((par_row[r] + e + kp) & 1) == 0 ? red : 0.0;
+          }
+      }
+      (void)v;
+      (void)kk;
+    };
     // first half-sweep at plane kk (rows 1 .. kRW-2): x planes xm (kk-1), xc (kk), xp (kk+1)
     auto half1 = [&](const double (&xm)[kRW][2], const double (&xc)[kRW][2],
                      const double (&xp)[kRW][2], const double (&bb)[kRW][2], int kk,
@@ -822,9 +844,13 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
       ldx(xq[0], kb - 1);
       ldx(xq[1], kb);
       ldb(bb, kb - 1);
+      xform(xa, kb - 2);
+      xform(xq[0], kb - 1);
+      xform(xq[1], kb);
       half1(xa, xq[0], xq[1], bb, kb - 1, s1[0]);
       ldx(xq[2], kb + 1);
       ldb(bq[0], kb);
+      xform(xq[2], kb + 1);
       half1(xq[0], xq[1], xq[2], bq[0], kb, s1[1]);
       // shift x queue to (kb, kb+1, kb+2)
 #pragma unroll
@@ -836,6 +862,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
         }
       ldx(xq[2], kb + 2);
       ldb(bq[1], kb + 1);
+      xform(xq[2], kb + 2);
     }
     for (int k = kb; k < ke; ++k) {
       const bool more = k + 1 < ke;
@@ -849,6 +876,29 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
       const int64_t base = pl(k);
 #pragma unroll
       for (int r = 2; r < 2 + kTY2; ++r) {
+        if constexpr (M == 1) {  // x = S1; res = b - A S1 (z-, y-, x-, c, x+, y+, z+)
+          const double lo = dpp_from_lower(s1[1][r][1]);
+          const double hi = dpp_from_upper(s1[1][r][0]);
+          double rv[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const double xl = e == 0 ? lo : s1[1][r][0];
+            const double xr = e == 1 ? hi : s1[1][r][1];
+            double a = cz * s1[0][r][e];
+            a = a + cy * s1[1][r - 1][e];
+            a = a + cx * xl;
+            a = a + cc * s1[1][r][e];
+            a = a + cx * xr;
+            a = a + cy * s1[1][r + 1][e];
+            a = a + cz * s1[2][r][e];
+            rv[e] = bq[0][r][e] - a;
+          }
+          if (out_ok && j0 + r - 2 < ny) {
+            store_row<2>(xout, base + ro[r], s1[1][r], g.nt);
+            store_row<2>(res, base + ro[r], rv, g.nt);
+          }
+          continue;
+        }
         const bool a1 = ((par_row[r] + kp) & 1) == c1;  // second-colour point is element 1
         const double lo = dpp_from_lower(s1[1][r][1]);
         const double hi = dpp_from_upper(s1[1][r][0]);
@@ -899,6 +949,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
           bq[0][r][e] = bq[1][r][e];
           bq[1][r][e] = bn[r][e];
         }
+      xform(xq[2], k + 3);
     }
   }
   if constexpr (SUMS) block_partials<4>(acc, parts);
@@ -910,11 +961,7 @@ bool sor_sweep2_supported(const pb_grid* g) {
          g->n[1] >= 8 && g->nzl >= 4 && env_int("PB_MG_SWEEP2", 1) != 0;
 }
 
-int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double* b, double* xout,
-                      double omega, int c1, const int* skip, const CgState* sums_st, int* nparts) {
-  ScopedTimer tm(g->ctx, "mg_sor_sweep2");
-  if (xin == xout) return set_error(PB_ERR_ARG, "fused SOR sweep must run out of place");
-  Sweep2Geo geo;
+static int64_t sweep2_geo(pb_grid* g, Sweep2Geo& geo) {
   geo.nx = (int)g->n[0];
   geo.ny = (int)g->n[1];
   geo.nzl = (int)g->nzl;
@@ -932,20 +979,42 @@ int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double
   nchunk = std::min(nchunk, std::max(1, geo.nzl / 16));
   geo.kc = (geo.nzl + nchunk - 1) / nchunk;
   geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
-  const int64_t nblocks = (int64_t)columns * geo.nchunk;
+  return (int64_t)columns * geo.nchunk;
+}
+
+int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double* b, double* xout,
+                      double omega, int c1, const int* skip, const CgState* sums_st, int* nparts) {
+  ScopedTimer tm(g->ctx, "mg_sor_sweep2");
+  if (xin == xout) return set_error(PB_ERR_ARG, "fused SOR sweep must run out of place");
+  Sweep2Geo geo;
+  const int64_t nblocks = sweep2_geo(g, geo);
   if (sums_st) {
     if (nblocks * 4 > g->ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
                        (long long)nblocks);
-    hipLaunchKernelGGL(sor_sweep2_kernel<true>, dim3((unsigned)nblocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((sor_sweep2_kernel<true, 0>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
-                       sums_st, g->ctx->d_partials, skip);
+                       (double*)nullptr, sums_st, g->ctx->d_partials, skip);
     if (nparts) *nparts = (int)nblocks;
   } else {
-    hipLaunchKernelGGL(sor_sweep2_kernel<false>, dim3((unsigned)nblocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((sor_sweep2_kernel<false, 0>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
-                       (const CgState*)nullptr, (double*)nullptr, skip);
+                       (double*)nullptr, (const CgState*)nullptr, (double*)nullptr, skip);
   }
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double* x, double* res,
+                              double omega, const int* skip) {
+  ScopedTimer tm(g->ctx, "mg_presmooth_residual");
+  if (b == x || b == res || x == res)
+    return set_error(PB_ERR_ARG, "fused pre-smoothing + residual must run out of place");
+  Sweep2Geo geo;
+  const int64_t nblocks = sweep2_geo(g, geo);
+  hipLaunchKernelGGL((sor_sweep2_kernel<false, 1>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+                     g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, 1, b, b, x, res,
+                     (const CgState*)nullptr, (double*)nullptr, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }

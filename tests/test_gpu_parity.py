@@ -522,7 +522,9 @@ MG_KERNELS = {"default": {},
               "engine": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
               "cell": {"PB_MG_PROLONG_CELL": "1", "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
               "legacy": {"PB_MG_ENGINE_MIN_PLANE": "1000000000", "PB_MG_RESTRICT_Z": "0",
-                         "PB_MG_PROLONG_CELL": "0"}}
+                         "PB_MG_PROLONG_CELL": "0"},
+              "unfused": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_SWEEP2": "0",
+                          "PB_MG_PRESMOOTH_FUSED": "0"}}
 
 
 @pytest.mark.parametrize("kern", sorted(MG_KERNELS))
@@ -570,7 +572,7 @@ def test_cg_sor_mg_matches_oracle(ctx, monkeypatch, kern, pc, n):
         assert its <= 16  # h-independent V-cycle preconditioning
 
 
-@pytest.mark.parametrize("kern", ["default", "engine", "legacy"])
+@pytest.mark.parametrize("kern", ["default", "engine", "legacy", "unfused"])
 def test_cg_mg_fused_post_smoothing(ctx, monkeypatch, kern):
     """x extent >= 128: the V-cycle's post-smoothing runs as ONE fused two-colour pass (out of
     place, with CG's residual sums on level 0); history / solution within the CG bar, PC apply
