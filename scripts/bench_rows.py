@@ -50,6 +50,27 @@ def wall(fn, reps):
     return (time.perf_counter() - t) / reps
 
 
+TIME_REF = os.path.join(REPO, "oracle", "_ref", "time_ref")
+
+
+def ref_cpu(op, n, seconds, port_fn, port_sample):
+    """CPU rate of the REAL reference routine (flang-built from /root/reference sources by
+    `make -C oracle ref`, oracle/time_ref.f90), one core; the oracle's restatement when that
+    binary is absent."""
+    import subprocess
+    if os.path.exists(TIME_REF):
+        try:
+            out = subprocess.run([TIME_REF, op, str(n), str(seconds)], capture_output=True, text=True,
+                                 timeout=60 + 4 * seconds, check=True).stdout
+            d = json.loads(out.strip().splitlines()[-1])
+            return {"dofs_per_s_1core": d["dofs_per_s"], "kind": "reference",
+                    "sample": f"reference {op} (src/tridsol.f90 / src/compact_schemes.f90 via "
+                              f"oracle/time_ref.f90), n={n}, {d['reps']} reps in {d['seconds']:.2f} s"}
+        except Exception as e:  # fall back to the restatement
+            print(f"time_ref {op}: {e}", file=sys.stderr)
+    return {"dofs_per_s_1core": port_fn(), "kind": "port", "sample": port_sample}
+
+
 def row(name, kernel, size, dofs, bytes_per_dof, ms, cpu=None):
     gbps = bytes_per_dof * dofs / (ms / 1e3) / 1e9
     out = {"row": name, "kernel": kernel, "size": size, "avg_ms": ms, "bytes_per_dof": bytes_per_dof,
@@ -99,14 +120,15 @@ def main():
     ms = timed(ctx, lambda: pb.tdma_batched(ctx, n, nb, 1, nb, bufs["a"], bufs["b"], bufs["c"],
                                             bufs["d"], periodic=False), 5, "tdma")
     a1, b1, c1, d1 = (host[k][:n * 64].reshape(n, 64)[:, 0].copy() for k in "abcd")
-    tc = wall(lambda: O.tdma(a1, b1, c1, d1), 200)
     row("a12", "tdma (Thomas, one lane per line)", "512 x 512^2", n * nb, 48, ms,
-        {"dofs_per_s_1core": n / tc, "sample": "oracle pbo_tdma, one 512 line"})
+        ref_cpu("tdma", n, 2, lambda: n / wall(lambda: O.tdma(a1, b1, c1, d1), 200),
+                "oracle pbo_tdma, one 512 line"))
     ms = timed(ctx, lambda: pb.tdma_batched(ctx, n, nb, 1, nb, bufs["a"], bufs["b"], bufs["c"],
                                             bufs["d"], periodic=True), 5, "tdma")
-    tc = wall(lambda: O.tdma(a1, b1, c1, d1, periodic=True), 200)
     row("a13", "tdma_periodic (Sherman-Morrison, one lane per line)", "512 x 512^2", n * nb, 40, ms,
-        {"dofs_per_s_1core": n / tc, "sample": "oracle pbo_tdma_periodic, one 512 line"})
+        ref_cpu("tdma_periodic", n, 2,
+                lambda: n / wall(lambda: O.tdma(a1, b1, c1, d1, periodic=True), 200),
+                "oracle pbo_tdma_periodic, one 512 line"))
     ms = timed(ctx, lambda: pb.pcr_alpha_batched(ctx, n, nb, 1, nb, 0.3, bufs["d"]), 5, "pcr")
     row("PCR", "batched (a,1,a) solve, interleaved lines", "512 x 512^2", n * nb, 16, ms)
     ms = timed(ctx, lambda: pb.pcr_alpha_batched(ctx, n, nb, n, 1, 0.3, bufs["d"]), 5, "pcr")
@@ -114,9 +136,9 @@ def main():
     ms = timed(ctx, lambda: pb.compact_1d_batched(ctx, 0, -1, 0.01, n, nb, 1, nb, bufs["a"],
                                                   bufs["d"]), 5, "compact_1d")
     f1 = host["a"][:n].copy()
-    tc = wall(lambda: O.grad_1d(f1, 0.01), 200)
     row("a15", "grad_1d (reference order, one lane per line)", "512 x 512^2", n * nb, 16, ms,
-        {"dofs_per_s_1core": n / tc, "sample": "oracle pbo_grad_1d, one 512 line"})
+        ref_cpu("grad_1d", n, 2, lambda: n / wall(lambda: O.grad_1d(f1, 0.01), 200),
+                "oracle pbo_grad_1d, one 512 line"))
     for v in bufs.values():
         hip.hipFree(v)
 
@@ -131,8 +153,10 @@ def main():
         cpu = None
         if m == 256:
             fc = O.fill_random(64 ** 3, 5)
-            tc = wall(lambda: O.lapl(fc, (64, 64, 64), (2 * np.pi / 64,) * 3), 1)
-            cpu = {"dofs_per_s_1core": 64 ** 3 / tc, "sample": "oracle pbo_lapl (reference order), 64^3"}
+            cpu = ref_cpu("lapl", 64, 3,
+                          lambda: 64 ** 3 / wall(lambda: O.lapl(fc, (64, 64, 64),
+                                                                (2 * np.pi / 64,) * 3), 1),
+                          "oracle pbo_lapl (reference order), 64^3")
         row("a16", "compact lapl 3-pass + PCR", f"{m}^3", m ** 3, 80, ms, cpu)
         if m == 256:
             ms = timed(ctx, lambda: pb.compact_lapl(da, h, f, out), 2, "compact_lapl")
