@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--base", type=int, default=512, help="per-GPU cube edge (default 512)")
     ap.add_argument("--matvecs", type=int, default=20)
+    ap.add_argument("--grid", default=None,
+                    help="nx,ny,nz global grid override (diagnostics; default: weak scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                     help="multi-rank transport: RCCL (default) or the gloo host transport "
@@ -96,8 +98,20 @@ def main():
         import torch
         device = local_rank % max(1, torch.cuda.device_count())
 
-    n = global_grid(world, args.base)
-    ctx = pb.Context(device, rank, world, uid)
+    n = tuple(int(v) for v in args.grid.split(",")) if args.grid else global_grid(world, args.base)
+    # RCCL prints a version banner on stdout when a communicator is created; keep stdout for the
+    # one JSON line (the banner goes to stderr)
+    import ctypes
+    libc = ctypes.CDLL(None)
+    sys.stdout.flush()
+    saved_fd = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        ctx = pb.Context(device, rank, world, uid)
+    finally:
+        libc.fflush(None)
+        os.dup2(saved_fd, 1)
+        os.close(saved_fd)
     if dist and args.transport == "host":
         tr = GlooTransport(dist)
         ctx.set_host_transport(tr.sendrecv, tr.allreduce)
