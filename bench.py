@@ -79,6 +79,12 @@ def main():
                          "(lets several ranks share one GPU for testing)")
     args = ap.parse_args()
 
+    # stdout carries exactly one JSON line (rank 0): everything else any library prints on fd 1 --
+    # gloo's connection messages, RCCL's version banner -- is sent to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -99,19 +105,7 @@ def main():
         device = local_rank % max(1, torch.cuda.device_count())
 
     n = tuple(int(v) for v in args.grid.split(",")) if args.grid else global_grid(world, args.base)
-    # RCCL prints a version banner on stdout when a communicator is created; keep stdout for the
-    # one JSON line (the banner goes to stderr)
-    import ctypes
-    libc = ctypes.CDLL(None)
-    sys.stdout.flush()
-    saved_fd = os.dup(1)
-    os.dup2(2, 1)
-    try:
-        ctx = pb.Context(device, rank, world, uid)
-    finally:
-        libc.fflush(None)
-        os.dup2(saved_fd, 1)
-        os.close(saved_fd)
+    ctx = pb.Context(device, rank, world, uid)
     if dist and args.transport == "host":
         tr = GlooTransport(dist)
         ctx.set_host_transport(tr.sendrecv, tr.allreduce)
@@ -244,7 +238,7 @@ def main():
                 pass
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     for o in (ksp, y, xt, x, b, A, P):
         o.destroy()
     da.destroy()
