@@ -1,0 +1,106 @@
+// pb_device.hpp -- device-side helpers shared by the stencil engine (pb_stencil.hip) and the
+// fused multigrid sweeps (pb_mg_sweep.hip): 16-byte row loads/stores, DPP wave shifts, the
+// deterministic block reduction of partial sums, the XCD-aware block order.
+#pragma once
+#include "pb_internal.hpp"
+
+namespace pb {
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
+#ifndef PB_KWAVES
+#define PB_KWAVES 4  // waves per workgroup (stacked in y)
+#endif
+static constexpr int kWaves = PB_KWAVES;
+static constexpr int kThreads = 64 * kWaves;
+
+template <int V>
+__device__ __forceinline__ void load_row(const double* __restrict__ p, int64_t idx, double (&v)[V]) {
+  if constexpr (V == 2) {
+    const dv2 t = *reinterpret_cast<const dv2*>(p + idx);
+    v[0] = t.x;
+    v[1] = t.y;
+  } else {
+    v[0] = p[idx];
+  }
+}
+template <int V>
+__device__ __forceinline__ void store_row(double* p, int64_t idx, const double (&v)[V], int nt) {
+  if constexpr (V == 2) {
+    dv2 t;
+    t.x = v[0];
+    t.y = v[1];
+    if (nt) __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p + idx));
+    else *reinterpret_cast<dv2*>(p + idx) = t;
+  } else {
+    if (nt) __builtin_nontemporal_store(v[0], p + idx);
+    else p[idx] = v[0];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cross-lane helpers (DPP wave shifts: VALU only, no LDS traffic)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double dpp_from_lower(double v) {  // lane l <- lane l-1 (wave_shr:1)
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_from_upper(double v) {  // lane l <- lane l+1 (wave_shl:1)
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Block-level deterministic reduction of NS partial sums -> parts[block*NS + s]
+// ---------------------------------------------------------------------------------------------
+template <int NS>
+__device__ __forceinline__ void block_partials(double* acc, double* parts) {
+  if constexpr (NS > 0) {
+    // any block size up to 16 waves (the engine's kWaves, 256-thread elementwise kernels)
+    __shared__ double red[16][NS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      double v = acc[s];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+      acc[s] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) red[wid][s] = acc[s];
+    }
+    __syncthreads();
+    if (threadIdx.x < NS) {
+      double v = 0.0;
+#pragma unroll
+      for (int w = 0; w < nw; ++w) v += red[w][threadIdx.x];
+      parts[(int64_t)blockIdx.x * NS + threadIdx.x] = v;
+    }
+  }
+}
+
+// XCD-aware block order (speed only, bijective): the dispatcher deals blocks round-robin over the
+// 8 XCDs, so each XCD gets a contiguous range of logical blocks -- neighbouring tiles then share
+// the XCD's L2 and their halo rows hit there.
+__device__ __forceinline__ int xcd_block(int remap) {
+  int b = blockIdx.x;
+  if (remap) {
+    const int nb = gridDim.x, q = nb / 8, r = nb % 8;
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  return b;
+}
+
+}  // namespace pb

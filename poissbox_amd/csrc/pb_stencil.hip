@@ -19,17 +19,9 @@
 //     chosen per plane, so no ghost copy is made on one rank.
 // Summation order per point matches the reference dot product with its zero terms dropped:
 // z-, y-, x-, centre, x+, y+, z+ (built with -ffp-contract=off => bit-identical to the oracle).
-#include "pb_internal.hpp"
+#include "pb_device.hpp"
 
 namespace pb {
-
-typedef double dv2 __attribute__((ext_vector_type(2)));
-
-#ifndef PB_KWAVES
-#define PB_KWAVES 4  // waves per workgroup (stacked in y)
-#endif
-static constexpr int kWaves = PB_KWAVES;
-static constexpr int kThreads = 64 * kWaves;
 
 struct Geo {
   int nx, ny, nzl;
@@ -42,30 +34,6 @@ struct Geo {
   int k0;     // global index of local plane 0 (red-black colouring)
   int wrap;   // planes -1 / nzl are the periodic wrap of the raw arrays (StencilPlanes::wrap)
 };
-
-template <int V>
-__device__ __forceinline__ void load_row(const double* __restrict__ p, int64_t idx, double (&v)[V]) {
-  if constexpr (V == 2) {
-    const dv2 t = *reinterpret_cast<const dv2*>(p + idx);
-    v[0] = t.x;
-    v[1] = t.y;
-  } else {
-    v[0] = p[idx];
-  }
-}
-template <int V>
-__device__ __forceinline__ void store_row(double* p, int64_t idx, const double (&v)[V], int nt) {
-  if constexpr (V == 2) {
-    dv2 t;
-    t.x = v[0];
-    t.y = v[1];
-    if (nt) __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p + idx));
-    else *reinterpret_cast<dv2*>(p + idx) = t;
-  } else {
-    if (nt) __builtin_nontemporal_store(v[0], p + idx);
-    else p[idx] = v[0];
-  }
-}
 
 // ---------------------------------------------------------------------------------------------
 // Loaders: NR raw arrays per point, combined into the field value by value().
@@ -197,58 +165,6 @@ struct PassB {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Cross-lane helpers (DPP wave shifts: VALU only, no LDS traffic)
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ double dpp_from_lower(double v) {  // lane l <- lane l-1 (wave_shr:1)
-  const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double dpp_from_upper(double v) {  // lane l <- lane l+1 (wave_shl:1)
-  const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double readlane_d(double v, int l) {
-  const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_readlane((int)b, l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Block-level deterministic reduction of NS partial sums -> parts[block*NS + s]
-// ---------------------------------------------------------------------------------------------
-template <int NS>
-__device__ __forceinline__ void block_partials(double* acc, double* parts) {
-  if constexpr (NS > 0) {
-    // any block size up to 16 waves (the engine's kWaves, 256-thread elementwise kernels)
-    __shared__ double red[16][NS];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      double v = acc[s];
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-      acc[s] = v;
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) red[wid][s] = acc[s];
-    }
-    __syncthreads();
-    if (threadIdx.x < NS) {
-      double v = 0.0;
-#pragma unroll
-      for (int w = 0; w < nw; ++w) v += red[w][threadIdx.x];
-      parts[(int64_t)blockIdx.x * NS + threadIdx.x] = v;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // The stencil engine
 // ---------------------------------------------------------------------------------------------
 template <int V, int TY, class Load, class Epi>
@@ -273,12 +189,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   // XCD-aware remap (speed only): the dispatcher deals blocks round-robin over the 8 XCDs, so
   // give each XCD a contiguous range of logical tiles -- y/x-neighbouring tiles then share the
   // XCD's L2 and their halo rows hit there. Bijective for any grid size.
-  int b = blockIdx.x;
-  if (g.remap) {
-    const int nb = gridDim.x, q = nb / 8, r = nb % 8;
-    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
-    b = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-  }
+  int b = xcd_block(g.remap);
   const int seg = b % g.nsegx;
   b /= g.nsegx;
   const int tile = b % g.ntile;
@@ -690,333 +601,6 @@ int launch_mg_sor(pb_grid* g, const Star& s, double* x, const double* b, const S
   if (first)  // measured: the zero-start sweep prefers 3 workgroups per CU, the others 1
     return launch_any(g, s, Red0Load{b, s.cc, omega}, gp, ep, skip, PLANES_ALL, 0, nullptr, 0, 3);
   return launch_any(g, s, PlainLoad{x}, gp, ep, skip);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Fused red-black SOR sweep: both half-sweeps (colour c1, then 1 - c1) in ONE pass, out of place
-// (xout != xin), one rank. The second half-sweep at point p needs first-half values S1 at p's
-// neighbours, and S1 needs xin at distance 1 from those: a wave holds xin for TY2 + 4 rows and
-// three planes, computes S1 for the TY2 + 2 middle rows one plane ahead, and the second half for
-// its TY2 own rows. x-halo by overlap: a wave spans 64 pairs but stores only lanes 4..59 (112
-// points, whole 128-B lines; neighbouring segments overlap), so every x-neighbour is a DPP shift.
-// Per point: read xin and b once, write xout once (24 B/DoF instead of 2 x 24). Arithmetic per
-// point is the two half-sweeps' (SorHalf / mg_smooth_kernel), so results are bit-identical.
-// ---------------------------------------------------------------------------------------------
-#ifndef PB_SWEEP2_TY
-#define PB_SWEEP2_TY 3  // measured: 3 beats 2 (0.97 vs 1.09 ms at 512^3) and 1 (1.24)
-#endif
-static constexpr int kTY2 = PB_SWEEP2_TY;  // own rows per wave
-static constexpr int kRW = kTY2 + 4;    // xin rows held: j0-2 .. j0+TY2+1
-static constexpr int kSegOut = 112;     // outputs per wave segment (lanes 4..59): 896 B, whole
-                                        // 128-B lines, so no line is written by two waves
-static constexpr int kSegLead = 4;      // halo pairs left of the outputs (>= 1 needed)
-
-struct Sweep2Geo {
-  int nx, ny, nzl;
-  int64_t plane;
-  int nseg, ntile, kc, nchunk;
-  int k0, remap, nt;
-};
-
-// M = 0: SOR sweep (first colour c1, then the other) of xin -> xout.
-// M = 1: pre-smoothing from x = 0 plus residual: S1 = the zero-start red + black half-sweeps
-//        (red = w D^-1 b, black from those -- Red0Load + SorHalf's arithmetic; xin = b, c1 = 1),
-//        xout = S1 and res = b - A S1 (the residual kernel's summation order).
-template <bool SUMS, int M>
-__global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, double cx, double cy,
-                                                               double cz, double cc, double omega,
-                                                               int c1, const double* __restrict__ xin,
-                                                               const double* __restrict__ b,
-                                                               double* __restrict__ xout,
-                                                               double* __restrict__ res,
-                                                               const CgState* st, double* parts,
-                                                               const int* skip) {
-  if (skip && *skip) return;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  const double mu = SUMS ? st->mu : 0.0;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int bid = blockIdx.x;
-  if (g.remap) {
-    const int nb = gridDim.x, q = nb / 8, r = nb % 8;
-    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-  }
-  const int seg = bid % g.nseg;
-  bid /= g.nseg;
-  const int tile = bid % g.ntile;
-  const int chunk = bid / g.ntile;
-  const int j0 = (tile * kWaves + wid) * kTY2;
-  const int kb = chunk * g.kc;
-  const int ke = min(kb + g.kc, g.nzl);
-  const int nx = g.nx, ny = g.ny, nz = g.nzl;
-  int ip = seg * kSegOut + 2 * (lane - kSegLead);  // this lane's pair (x wraps periodically)
-  if (ip < 0) ip += nx;
-  if (ip >= nx) ip -= nx;
-  const int o = seg * kSegOut + 2 * (lane - kSegLead);  // output pair
-  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
-  if (j0 < ny && kb < nz) {
-    int64_t ro[kRW];
-    int par_row[kRW];  // (i + j) parity base of each row for element 0
-#pragma unroll
-    for (int r = 0; r < kRW; ++r) {
-      int j = j0 - 2 + r;
-      if (j < 0) j += ny;
-      if (j >= ny) j -= ny;
-      ro[r] = (int64_t)j * nx + ip;
-      par_row[r] = (ip + j) & 1;
-    }
-    auto pl = [&](int kk) -> int64_t {  // periodic plane (one rank)
-      kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
-      return (int64_t)kk * g.plane;
-    };
-    auto kpar = [&](int kk) -> int {
-      kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
-      return (g.k0 + kk) & 1;
-    };
-    double xq[3][kRW][2];  // xin planes k, k+1, k+2
-    double xn[kRW][2];     // prefetch: plane k+3
-    double s1[3][kRW][2];  // S1 planes k-1, k, k+1 (rows 1 .. kRW-2)
-    double bq[2][kRW][2];  // b planes k, k+1 (rows 1 .. kRW-2)
-    double bn[kRW][2];     // prefetch: b plane k+2
-    auto ldx = [&](double (&dst)[kRW][2], int kk) {
-      const int64_t base = pl(kk);
-#pragma unroll
-      for (int r = 0; r < kRW; ++r) load_row<2>(xin, base + ro[r], dst[r]);
-    };
-    auto ldb = [&](double (&dst)[kRW][2], int kk) {
-      const int64_t base = pl(kk);
-#pragma unroll
-      for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, base + ro[r], dst[r]);
-    };
-    // M = 1: b values of plane kk -> the x of the zero-start red half-sweep (red: w D^-1 b,
-    // black: still 0)
-    auto xform = [&](double (&v)[kRW][2], int kk) {
-      if constexpr (M == 1) {
-        const int kp = kpar(kk);
-#pragma unroll
-        for (int r = 0; r < kRW; ++r)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double t = (v[r][e] - 0.0) / cc;
-            const double red = (1.0 - omega) * 0.0 + omega * t;
-            v[r][e] = ((par_row[r] + e + kp) & 1) == 0 ? red : 0.0;
-          }
-      }
-      (void)v;
-      (void)kk;
-    };
-    // first half-sweep at plane kk (rows 1 .. kRW-2): x planes xm (kk-1), xc (kk), xp (kk+1)
-    auto half1 = [&](const double (&xm)[kRW][2], const double (&xc)[kRW][2],
-                     const double (&xp)[kRW][2], const double (&bb)[kRW][2], int kk,
-                     double (&out)[kRW][2]) {
-      const int kp = kpar(kk);
-#pragma unroll
-      for (int r = 1; r < kRW - 1; ++r) {
-        // the pair holds one point of each colour; which element is c1 is wave-uniform (pairs
-        // start at even i), so only that element is updated -- one division per pair
-        const bool a1 = ((par_row[r] + kp) & 1) != c1;  // c1 point is element 1
-        const double lo = dpp_from_lower(xc[r][1]);
-        const double hi = dpp_from_upper(xc[r][0]);
-        const double xl = a1 ? xc[r][0] : lo;
-        const double xr = a1 ? hi : xc[r][1];
-        const double zm = a1 ? xm[r][1] : xm[r][0];
-        const double ym = a1 ? xc[r - 1][1] : xc[r - 1][0];
-        const double yp = a1 ? xc[r + 1][1] : xc[r + 1][0];
-        const double zp = a1 ? xp[r][1] : xp[r][0];
-        const double bv = a1 ? bb[r][1] : bb[r][0];
-        const double xo = a1 ? xc[r][1] : xc[r][0];
-        double nb = cz * zm;
-        nb = nb + cy * ym;
-        nb = nb + cx * xl;
-        nb = nb + cx * xr;
-        nb = nb + cy * yp;
-        nb = nb + cz * zp;
-        const double t = (bv - nb) / cc;
-        const double v = (1.0 - omega) * xo + omega * t;
-        out[r][0] = a1 ? xc[r][0] : v;
-        out[r][1] = a1 ? v : xc[r][1];
-      }
-    };
-    // prologue: S1 at planes kb-1 and kb
-    {
-      double xa[kRW][2], bb[kRW][2];
-      ldx(xa, kb - 2);
-      ldx(xq[0], kb - 1);
-      ldx(xq[1], kb);
-      ldb(bb, kb - 1);
-      xform(xa, kb - 2);
-      xform(xq[0], kb - 1);
-      xform(xq[1], kb);
-      half1(xa, xq[0], xq[1], bb, kb - 1, s1[0]);
-      ldx(xq[2], kb + 1);
-      ldb(bq[0], kb);
-      xform(xq[2], kb + 1);
-      half1(xq[0], xq[1], xq[2], bq[0], kb, s1[1]);
-      // shift x queue to (kb, kb+1, kb+2)
-#pragma unroll
-      for (int r = 0; r < kRW; ++r)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          xq[0][r][e] = xq[1][r][e];
-          xq[1][r][e] = xq[2][r][e];
-        }
-      ldx(xq[2], kb + 2);
-      ldb(bq[1], kb + 1);
-      xform(xq[2], kb + 2);
-    }
-    for (int k = kb; k < ke; ++k) {
-      const bool more = k + 1 < ke;
-      if (more) {
-        ldx(xn, k + 3);
-        ldb(bn, k + 2);
-      }
-      half1(xq[0], xq[1], xq[2], bq[1], k + 1, s1[2]);  // S1 at plane k+1
-      // second half-sweep at plane k, own rows 2 .. 2+TY2-1
-      const int kp = kpar(k);
-      const int64_t base = pl(k);
-#pragma unroll
-      for (int r = 2; r < 2 + kTY2; ++r) {
-        if constexpr (M == 1) {  // x = S1; res = b - A S1 (z-, y-, x-, c, x+, y+, z+)
-          const double lo = dpp_from_lower(s1[1][r][1]);
-          const double hi = dpp_from_upper(s1[1][r][0]);
-          double rv[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double xl = e == 0 ? lo : s1[1][r][0];
-            const double xr = e == 1 ? hi : s1[1][r][1];
-            double a = cz * s1[0][r][e];
-            a = a + cy * s1[1][r - 1][e];
-            a = a + cx * xl;
-            a = a + cc * s1[1][r][e];
-            a = a + cx * xr;
-            a = a + cy * s1[1][r + 1][e];
-            a = a + cz * s1[2][r][e];
-            rv[e] = bq[0][r][e] - a;
-          }
-          if (out_ok && j0 + r - 2 < ny) {
-            store_row<2>(xout, base + ro[r], s1[1][r], g.nt);
-            store_row<2>(res, base + ro[r], rv, g.nt);
-          }
-          continue;
-        }
-        const bool a1 = ((par_row[r] + kp) & 1) == c1;  // second-colour point is element 1
-        const double lo = dpp_from_lower(s1[1][r][1]);
-        const double hi = dpp_from_upper(s1[1][r][0]);
-        const double xl = a1 ? s1[1][r][0] : lo;
-        const double xr = a1 ? hi : s1[1][r][1];
-        const double zm = a1 ? s1[0][r][1] : s1[0][r][0];
-        const double ym = a1 ? s1[1][r - 1][1] : s1[1][r - 1][0];
-        const double yp = a1 ? s1[1][r + 1][1] : s1[1][r + 1][0];
-        const double zp = a1 ? s1[2][r][1] : s1[2][r][0];
-        const double bv = a1 ? bq[0][r][1] : bq[0][r][0];
-        const double xo = a1 ? xq[0][r][1] : xq[0][r][0];
-        double nb = cz * zm;
-        nb = nb + cy * ym;
-        nb = nb + cx * xl;
-        nb = nb + cx * xr;
-        nb = nb + cy * yp;
-        nb = nb + cz * zp;
-        const double t = (bv - nb) / cc;
-        const double v = (1.0 - omega) * xo + omega * t;
-        double ov[2];
-        ov[0] = a1 ? s1[1][r][0] : v;
-        ov[1] = a1 ? v : s1[1][r][1];
-        if (out_ok && j0 + r - 2 < ny) {  // rows past ny (last tile) would wrap: not ours
-          store_row<2>(xout, base + ro[r], ov, g.nt);
-          if constexpr (SUMS) {
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const double rv = bq[0][r][e];
-              const double t2 = ov[e] - mu;
-              acc[0] += t2;
-              acc[1] += t2 * t2;
-              acc[2] += t2 * rv;
-              acc[3] += rv;
-            }
-          }
-        }
-      }
-      // rotate queues
-#pragma unroll
-      for (int r = 0; r < kRW; ++r)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          s1[0][r][e] = s1[1][r][e];
-          s1[1][r][e] = s1[2][r][e];
-          xq[0][r][e] = xq[1][r][e];
-          xq[1][r][e] = xq[2][r][e];
-          xq[2][r][e] = xn[r][e];
-          bq[0][r][e] = bq[1][r][e];
-          bq[1][r][e] = bn[r][e];
-        }
-      xform(xq[2], k + 3);
-    }
-  }
-  if constexpr (SUMS) block_partials<4>(acc, parts);
-}
-
-// 1 rank, even extents, nx >= 128: the fused sweep applies (else two half-sweeps)
-bool sor_sweep2_supported(const pb_grid* g) {
-  return !g->ctx->split && g->n[0] >= 128 && g->n[0] % 2 == 0 && g->n[1] % 2 == 0 &&
-         g->n[1] >= 8 && g->nzl >= 4 && env_int("PB_MG_SWEEP2", 1) != 0;
-}
-
-static int64_t sweep2_geo(pb_grid* g, Sweep2Geo& geo) {
-  geo.nx = (int)g->n[0];
-  geo.ny = (int)g->n[1];
-  geo.nzl = (int)g->nzl;
-  geo.plane = g->plane;
-  geo.nseg = (geo.nx + kSegOut - 1) / kSegOut;
-  geo.ntile = (geo.ny + kWaves * kTY2 - 1) / (kWaves * kTY2);
-  geo.k0 = (int)g->k0;
-  geo.remap = env_int("PB_XCD_REMAP", 1);
-  geo.nt = env_int("PB_STENCIL_NT", 1);
-  const int columns = geo.nseg * geo.ntile;
-  // chunks: ~PB_SWEEP2_WGCU (16) workgroups per CU (many rounds: the loop is latency-bound),
-  // at least 16 planes per chunk
-  const int target = env_int("PB_SWEEP2_WGCU", 16) * g->ctx->num_cus;
-  int nchunk = std::max(1, (target + columns - 1) / columns);
-  nchunk = std::min(nchunk, std::max(1, geo.nzl / 16));
-  geo.kc = (geo.nzl + nchunk - 1) / nchunk;
-  geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
-  return (int64_t)columns * geo.nchunk;
-}
-
-int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double* b, double* xout,
-                      double omega, int c1, const int* skip, const CgState* sums_st, int* nparts) {
-  ScopedTimer tm(g->ctx, "mg_sor_sweep2");
-  if (xin == xout) return set_error(PB_ERR_ARG, "fused SOR sweep must run out of place");
-  Sweep2Geo geo;
-  const int64_t nblocks = sweep2_geo(g, geo);
-  if (sums_st) {
-    if (nblocks * 4 > g->ctx->partials_cap)
-      return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
-                       (long long)nblocks);
-    hipLaunchKernelGGL((sor_sweep2_kernel<true, 0>), dim3((unsigned)nblocks), dim3(kThreads), 0,
-                       g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
-                       (double*)nullptr, sums_st, g->ctx->d_partials, skip);
-    if (nparts) *nparts = (int)nblocks;
-  } else {
-    hipLaunchKernelGGL((sor_sweep2_kernel<false, 0>), dim3((unsigned)nblocks), dim3(kThreads), 0,
-                       g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
-                       (double*)nullptr, (const CgState*)nullptr, (double*)nullptr, skip);
-  }
-  PB_HIP(hipGetLastError());
-  return PB_OK;
-}
-
-int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double* x, double* res,
-                              double omega, const int* skip) {
-  ScopedTimer tm(g->ctx, "mg_presmooth_residual");
-  if (b == x || b == res || x == res)
-    return set_error(PB_ERR_ARG, "fused pre-smoothing + residual must run out of place");
-  Sweep2Geo geo;
-  const int64_t nblocks = sweep2_geo(g, geo);
-  hipLaunchKernelGGL((sor_sweep2_kernel<false, 1>), dim3((unsigned)nblocks), dim3(kThreads), 0,
-                     g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, 1, b, b, x, res,
-                     (const CgState*)nullptr, (double*)nullptr, skip);
-  PB_HIP(hipGetLastError());
-  return PB_OK;
 }
 
 int launch_mg_residual(pb_grid* g, const Star& s, const double* x, const double* b,

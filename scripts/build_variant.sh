@@ -8,7 +8,7 @@ C=$R/poissbox_amd/csrc
 B=/tmp/pb_variant_$name
 mkdir -p $B $R/variants
 objs=""
-for f in pb_runtime.cpp pb_solver.cpp pb_stencil.hip pb_vecops.hip pb_compact.hip pb_compact_fast.hip pb_compact_lines.hip pb_cg_generic.hip pb_mg.hip pb_compact_dist.hip; do
+for f in pb_runtime.cpp pb_solver.cpp pb_stencil.hip pb_vecops.hip pb_compact.hip pb_compact_fast.hip pb_compact_lines.hip pb_cg_generic.hip pb_mg.hip pb_mg_sweep.hip pb_compact_dist.hip; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off "$@" -I$R/include -I/opt/rocm/include -x hip -c $C/$f -o $B/$f.o &
   objs="$objs $B/$f.o"
 done
