@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         for (int t = 0; t < TY; ++t)
 #pragma unroll
           for (int a = 0; a < Epi::NE; ++a)
-            load_row<V>(ep.src(a), base + (int64_t)(j0 + t) * nx + ic, opn[t][a]);
+            load_row_nt<V>(ep.src(a), base + (int64_t)(j0 + t) * nx + ic, opn[t][a]);
       }
     };
     auto issue_ops_now = [&](int kk) {  // operands without prefetch: plane kk straight to opc
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         for (int t = 0; t < TY; ++t)
 #pragma unroll
           for (int a = 0; a < Epi::NE; ++a)
-            load_row<V>(ep.src(a), base + (int64_t)(j0 + t) * nx + ic, opc[t][a]);
+            load_row_nt<V>(ep.src(a), base + (int64_t)(j0 + t) * nx + ic, opc[t][a]);
       }
     };
     auto take_plane_ops = [&]() {
