@@ -9,14 +9,18 @@
 //     wave-instruction) of TY consecutive y-rows and marches in z over a chunk of planes, keeping
 //     planes k-1, k, k+1 of its rows in registers (each plane is read from HBM once per chunk);
 //   * software pipeline: while plane k is computed, plane k+2 of the z-queue and the halo rows,
-//     segment edges and epilogue operands (x, r in CG pass B) of plane k+1 are in flight -- the
-//     grid is sized to 2 workgroups per CU, so registers, not occupancy, buy the latency hiding;
+//     segment edges and epilogue operands (r, x, p_prev in CG pass B; non-temporal loads, they
+//     are read once) of plane k+1 are in flight -- the grid is one resident round of 1-3
+//     workgroups per CU (Epi::WGCU), so registers, not occupancy, buy the latency hiding;
+//   * each chunk is marched upwards or downwards (Geo::rev): consecutive kernels start on the
+//     planes their predecessor touched last, still in the Infinity Cache;
 //   * x-neighbours come from the neighbouring lane (DPP wave shift); the two segment-end values
 //     of all TY rows come from ONE masked load, broadcast with readlane; y-neighbours come from
 //     the wave's own rows, the tile's top/bottom rows from the neighbouring tile (L2 hit: tiles
 //     are remapped so neighbours share an XCD);
 //   * z ghosts (periodic wrap or the neighbouring rank's plane) are read through plane pointers
-//     chosen per plane, so no ghost copy is made on one rank.
+//     chosen per plane, or (Geo::wrap, one rank) as the wrap planes of the raw input arrays, so no
+//     ghost copy is made on one rank.
 // Summation order per point matches the reference dot product with its zero terms dropped:
 // z-, y-, x-, centre, x+, y+, z+ (built with -ffp-contract=off => bit-identical to the oracle).
 #include "pb_device.hpp"
