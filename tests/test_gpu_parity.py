@@ -152,7 +152,11 @@ HIST_RTOL = 1e-7  # relative tolerance on every ||z_k|| of the history (reductio
 
 
 @pytest.mark.parametrize("n,rtol", [(16, 1e-5), (32, 1e-5), (32, 1e-10), (64, 1e-10),
-                                    ((24, 20, 12), 1e-8)])
+                                    ((24, 20, 12), 1e-8),
+                                    # odd x (one point per lane), rows per wave 2 / 1, odd z,
+                                    # several x-segments, partial segment, long z-chunks
+                                    ((17, 18, 9), 1e-8), ((130, 6, 33), 1e-8),
+                                    ((256, 64, 96), 1e-6)])
 def test_cg_matches_petsc_semantics(ctx, n, rtol):
     n3 = (n, n, n) if isinstance(n, int) else n
     N = int(np.prod(n3))
