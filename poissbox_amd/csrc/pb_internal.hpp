@@ -112,6 +112,10 @@ struct pb_grid {
   double* bnd_lo = nullptr;
   double* bnd_hi = nullptr;
   double* h_stage = nullptr;  // pinned host staging for the host transport (4 planes)
+  // two-deep ghosts for the fused multigrid sweeps on N ranks (allocated on first use):
+  // ghost2 = [planes -2, -1 | nzl, nzl+1], h_stage2 = host staging (8 planes)
+  double* ghost2 = nullptr;
+  double* h_stage2 = nullptr;
 };
 
 struct pb_vec {
@@ -168,6 +172,11 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi);
 // Split form: begin (RCCL on the context's comm stream after an event on the compute stream;
 // host transport: synchronous), end (compute stream waits for the exchange).
 int halo_begin(pb_grid* g, const double* lo, const double* hi);
+// np-plane exchange into explicit buffers: send the np planes at `lo` (first owned) to rank-1
+// and at `hi` (last owned) to rank+1; rlo receives the np planes below the slab (from rank-1),
+// rhi the np planes above it (from rank+1). Stream ordered; one rank: periodic copies.
+int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, double* rlo,
+                    double* rhi);
 int halo_end(pb_grid* g);
 // In-place SUM allreduce of `count` device doubles (stream ordered).
 int allreduce_device(pb_ctx* ctx, double* d_vals, int count);

@@ -647,7 +647,7 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
   for (int l = 0; l < L - 1; ++l) {  // down: pre-smooth (red, black), residual, restrict
     MgLevel& F = mg->lv[l];
     MgLevel& Cl = mg->lv[l + 1];
-    // one rank, large level: zero-start red + black half-sweeps and the residual in one pass
+    // large level: zero-start red + black half-sweeps and the residual in one pass
     const bool fused = F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g) &&
                        env_int("PB_MG_PRESMOOTH_FUSED", 1);
     {

@@ -1,4 +1,5 @@
-// pb_mg_sweep.hip -- fused red-black SOR passes for the multigrid preconditioner (pb_mg.hip):
+// pb_mg_sweep.hip -- fused red-black SOR passes for the multigrid preconditioner (pb_mg.hip), on
+// one rank or N (two-deep z ghosts exchanged per pass):
 // both half-sweeps of a post-smoothing in one pass, and the zero-start pre-smoothing fused with
 // the residual. Same per-point arithmetic as the half-sweep / residual kernels (SorHalf, ResidEpi
 // in pb_stencil.hip, restated in oracle/pb_oracle.c pbo_mg_apply), hence bit-identical results.
@@ -32,13 +33,19 @@ struct Sweep2Geo {
   int64_t plane;
   int nseg, ntile, kc, nchunk;
   int k0, remap, nt;
+  // N ranks (split): xin's planes -2, -1, nzl, nzl+1 at xg[0..3], b's planes -1 / nzl at
+  // bg_lo / bg_hi; one rank reads the periodic wrap in place
+  int split;
+  const double* xg;
+  const double* bg_lo;
+  const double* bg_hi;
 };
 
 // M = 0: SOR sweep (first colour c1, then the other) of xin -> xout.
 // M = 1: pre-smoothing from x = 0 plus residual: S1 = the zero-start red + black half-sweeps
 //        (red = w D^-1 b, black from those -- Red0Load + SorHalf's arithmetic; xin = b, c1 = 1),
 //        xout = S1 and res = b - A S1 (the residual kernel's summation order).
-template <bool SUMS, int M>
+template <bool SUMS, int M, bool SPLIT>
 __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, double cx, double cy,
                                                                double cz, double cc, double omega,
                                                                int c1, const double* __restrict__ xin,
@@ -76,13 +83,22 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
       ro[r] = (int64_t)j * nx + ip;
       par_row[r] = (ip + j) & 1;
     }
-    auto pl = [&](int kk) -> int64_t {  // periodic plane (one rank)
-      kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
+    // one rank: periodic plane offsets into xin / b; N ranks: own planes or the ghost planes
+    auto pl = [&](int kk) -> int64_t {
+      if constexpr (!SPLIT) kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
       return (int64_t)kk * g.plane;
     };
-    auto kpar = [&](int kk) -> int {
-      kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
+    auto kpar = [&](int kk) -> int {  // colour parity of plane kk (global index)
+      if constexpr (!SPLIT) kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
       return (g.k0 + kk) & 1;
+    };
+    auto xplane = [&](int kk) -> const double* {  // N ranks: xin plane kk in [-2, nzl+1]
+      if (kk >= 0 && kk < nz) return xin + (int64_t)kk * g.plane;
+      return g.xg + (int64_t)(kk < 0 ? kk + 2 : kk - nz + 2) * g.plane;
+    };
+    auto bplane = [&](int kk) -> const double* {  // N ranks: b plane kk in [-1, nzl]
+      if (kk >= 0 && kk < nz) return b + (int64_t)kk * g.plane;
+      return kk < 0 ? g.bg_lo : g.bg_hi;
     };
     double xq[3][kRW][2];  // xin planes k, k+1, k+2
     double xn[kRW][2];     // prefetch: plane k+3
@@ -90,14 +106,26 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
     double bq[2][kRW][2];  // b planes k, k+1 (rows 1 .. kRW-2)
     double bn[kRW][2];     // prefetch: b plane k+2
     auto ldx = [&](double (&dst)[kRW][2], int kk) {
-      const int64_t base = pl(kk);
+      if constexpr (SPLIT) {
+        const double* P = xplane(kk);
 #pragma unroll
-      for (int r = 0; r < kRW; ++r) load_row<2>(xin, base + ro[r], dst[r]);
+        for (int r = 0; r < kRW; ++r) load_row<2>(P, ro[r], dst[r]);
+      } else {
+        const int64_t base = pl(kk);
+#pragma unroll
+        for (int r = 0; r < kRW; ++r) load_row<2>(xin, base + ro[r], dst[r]);
+      }
     };
     auto ldb = [&](double (&dst)[kRW][2], int kk) {
-      const int64_t base = pl(kk);
+      if constexpr (SPLIT) {
+        const double* P = bplane(kk);
 #pragma unroll
-      for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, base + ro[r], dst[r]);
+        for (int r = 1; r < kRW - 1; ++r) load_row<2>(P, ro[r], dst[r]);
+      } else {
+        const int64_t base = pl(kk);
+#pragma unroll
+        for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, base + ro[r], dst[r]);
+      }
     };
     // M = 1: b values of plane kk -> the x of the zero-start red half-sweep (red: w D^-1 b,
     // black: still 0)
@@ -266,10 +294,31 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
   if constexpr (SUMS) block_partials<4>(acc, parts);
 }
 
-// 1 rank, even extents, nx >= 128: the fused sweep applies (else two half-sweeps)
+// even extents, nx >= 128, >= 4 planes per rank: the fused sweep applies (else two half-sweeps)
 bool sor_sweep2_supported(const pb_grid* g) {
-  return !g->ctx->split && g->n[0] >= 128 && g->n[0] % 2 == 0 && g->n[1] % 2 == 0 &&
-         g->n[1] >= 8 && g->nzl >= 4 && env_int("PB_MG_SWEEP2", 1) != 0;
+  return g->n[0] >= 128 && g->n[0] % 2 == 0 && g->n[1] % 2 == 0 && g->n[1] >= 8 &&
+         g->nzl >= 4 && env_int("PB_MG_SWEEP2", 1) != 0;
+}
+
+// N ranks: two-deep ghosts of xin (and, when b is another array, one-deep ghosts of b)
+static int sweep2_ghosts(pb_grid* g, const double* xin, const double* b, Sweep2Geo& geo) {
+  geo.split = g->ctx->split ? 1 : 0;
+  geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
+  if (!geo.split) return PB_OK;
+  if (!g->ghost2 && hipMalloc(&g->ghost2, 4 * (size_t)g->plane * sizeof(double)) != hipSuccess)
+    return set_error(PB_ERR_ALLOC, "two-deep ghost planes: out of device memory");
+  PB_TRY(halo_exchange_n(g, xin, xin + (g->nzl - 2) * g->plane, 2, g->ghost2,
+                         g->ghost2 + 2 * g->plane));
+  geo.xg = g->ghost2;
+  if (b == xin) {
+    geo.bg_lo = g->ghost2 + g->plane;      // plane -1
+    geo.bg_hi = g->ghost2 + 2 * g->plane;  // plane nzl
+  } else {
+    PB_TRY(halo_exchange(g, b, b + (g->nzl - 1) * g->plane));
+    geo.bg_lo = g->ghost_lo;
+    geo.bg_hi = g->ghost_hi;
+  }
+  return PB_OK;
 }
 
 static int64_t sweep2_geo(pb_grid* g, Sweep2Geo& geo) {
@@ -299,16 +348,17 @@ int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double
   if (xin == xout) return set_error(PB_ERR_ARG, "fused SOR sweep must run out of place");
   Sweep2Geo geo;
   const int64_t nblocks = sweep2_geo(g, geo);
+  PB_TRY(sweep2_ghosts(g, xin, b, geo));
   if (sums_st) {
     if (nblocks * 4 > g->ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
                        (long long)nblocks);
-    hipLaunchKernelGGL((sor_sweep2_kernel<true, 0>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((geo.split ? sor_sweep2_kernel<true, 0, true> : sor_sweep2_kernel<true, 0, false>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
                        (double*)nullptr, sums_st, g->ctx->d_partials, skip);
     if (nparts) *nparts = (int)nblocks;
   } else {
-    hipLaunchKernelGGL((sor_sweep2_kernel<false, 0>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((geo.split ? sor_sweep2_kernel<false, 0, true> : sor_sweep2_kernel<false, 0, false>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
                        (double*)nullptr, (const CgState*)nullptr, (double*)nullptr, skip);
   }
@@ -323,7 +373,8 @@ int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double
     return set_error(PB_ERR_ARG, "fused pre-smoothing + residual must run out of place");
   Sweep2Geo geo;
   const int64_t nblocks = sweep2_geo(g, geo);
-  hipLaunchKernelGGL((sor_sweep2_kernel<false, 1>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+  PB_TRY(sweep2_ghosts(g, b, b, geo));
+  hipLaunchKernelGGL((geo.split ? sor_sweep2_kernel<false, 1, true> : sor_sweep2_kernel<false, 1, false>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                      g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, 1, b, b, x, res,
                      (const CgState*)nullptr, (double*)nullptr, skip);
   PB_HIP(hipGetLastError());

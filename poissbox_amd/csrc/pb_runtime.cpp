@@ -117,6 +117,47 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
   return PB_OK;
 }
 
+int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, double* rlo,
+                    double* rhi) {
+  pb_ctx* ctx = g->ctx;
+  ScopedTimer tm(ctx, "halo");
+  const int64_t cnt = (int64_t)np * g->plane;
+  const size_t bytes = (size_t)cnt * sizeof(double);
+  if (!ctx->split) {
+    PB_HIP(hipMemcpyAsync(rlo, hi, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    PB_HIP(hipMemcpyAsync(rhi, lo, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    return PB_OK;
+  }
+  const int down = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
+  const int up = (ctx->rank + 1) % ctx->nranks;
+  if (ctx->h_sendrecv) {
+    if (np > 2) return set_error(PB_ERR_UNSUPPORTED, "host halo of %d planes", np);
+    if (!g->h_stage2)
+      PB_HIP(hipHostMalloc(&g->h_stage2, 8 * (size_t)g->plane * sizeof(double),
+                           hipHostMallocDefault));
+    double* s_lo = g->h_stage2;
+    double* s_hi = s_lo + cnt;
+    double* r_lo = s_hi + cnt;
+    double* r_hi = r_lo + cnt;
+    PB_HIP(hipMemcpyAsync(s_lo, lo, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    PB_HIP(hipMemcpyAsync(s_hi, hi, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    PB_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->h_sendrecv(ctx->h_user, s_lo, s_hi, r_lo, r_hi, cnt) != 0)
+      return set_error(PB_ERR_COMM, "host sendrecv callback failed");
+    PB_HIP(hipMemcpyAsync(rlo, r_lo, bytes, hipMemcpyHostToDevice, ctx->stream));
+    PB_HIP(hipMemcpyAsync(rhi, r_hi, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return PB_OK;
+  }
+  // the two-phase order of halo_exchange (pairs correctly when down == up)
+  PB_NCCL(ncclGroupStart());
+  PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->stream));
+  PB_NCCL(ncclRecv(rhi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->stream));
+  PB_NCCL(ncclSend(hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->stream));
+  PB_NCCL(ncclRecv(rlo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->stream));
+  PB_NCCL(ncclGroupEnd());
+  return PB_OK;
+}
+
 int halo_begin(pb_grid* g, const double* lo, const double* hi) {
   pb_ctx* ctx = g->ctx;
   if (!ctx->split || !ctx->comm) return halo_exchange(g, lo, hi);
@@ -475,7 +516,9 @@ int pb_grid_destroy(pb_grid* g) {
   if (!g) return PB_OK;
   (void)hipStreamSynchronize(g->ctx->stream);
   (void)hipFree(g->ghost_lo);
+  if (g->ghost2) (void)hipFree(g->ghost2);
   if (g->h_stage) (void)hipHostFree(g->h_stage);
+  if (g->h_stage2) (void)hipHostFree(g->h_stage2);
   delete g;
   return PB_OK;
 }

@@ -632,9 +632,13 @@ def test_mg_rejects_odd_extents(ctx):
 
 
 @pytest.mark.parametrize("kern", ["default", "engine"])
-@pytest.mark.parametrize("nranks,n", [(2, (16, 16, 32)), (4, (16, 16, 32)), (3, (16, 16, 12))])
+@pytest.mark.parametrize("nranks,n", [(2, (16, 16, 32)), (4, (16, 16, 32)), (3, (16, 16, 12)),
+                                        (2, (128, 16, 32)), (3, (128, 8, 12))])
 def test_multirank_mg_bit_exact_and_cg(monkeypatch, kern, nranks, n):
-    """Slab-decomposed V-cycle (halo exchanges per level) equals the single-grid restatement."""
+    """Slab-decomposed V-cycle (halo exchanges per level) equals the single-grid restatement.
+
+    nx = 128 cases take the fused two-colour sweeps on the fine level (two-deep z ghosts,
+    nzl = 16 and 4 planes per rank)."""
     for k_, v_ in MG_KERNELS[kern].items():
         monkeypatch.setenv(k_, v_)
     N = int(np.prod(n))
