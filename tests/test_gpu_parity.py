@@ -728,7 +728,7 @@ def test_multirank_cg_compact_operator_mg():
         assert np.max(np.abs(xs - xo.reshape(32, -1)[k0:k0 + nk].reshape(-1))) <= 1e-6 * np.max(np.abs(xo))
 
 
-def test_rccl_code_paths_one_rank_communicator():
+def test_rccl_code_paths_one_rank_communicator(monkeypatch):
     """PB_FORCE_COMM=1 gives a 1-rank context an RCCL communicator and the decomposed code paths:
     the halo exchange (ncclSend/ncclRecv to self, interior/boundary overlap split), the RCCL
     allreduce of the CG sums, the compact transposes and the MG level halos -- the paths the
@@ -760,4 +760,19 @@ def test_rccl_code_paths_one_rank_communicator():
     ref = O.lapl(xt, n3, hc)
     pb.compact_lapl_fast(da, hc, xv, y)
     assert np.max(np.abs(y.get_values() - ref)) <= FAST_RTOL * np.max(np.abs(ref))
+    # fused MG sweeps on a decomposed grid: two-deep z ghosts through ncclSend/ncclRecv
+    n3 = (128, 16, 16)
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    r = O.fill_random(N, 3)
+    ref = O.mg_apply(r, n3, h, pc="mg")
+    for k_, v_ in MG_KERNELS["engine"].items():
+        monkeypatch.setenv(k_, v_)
+    da = pb.DA(ctx, n3)
+    P, A, _, _ = pb.initialise_linear_system(da, h)
+    k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
+    rv, zv = pb.Vec(da), pb.Vec(da)
+    rv.set_values(r)
+    k.pc_apply(rv, zv)
+    assert np.array_equal(zv.get_values(), ref)
     ctx.destroy()
