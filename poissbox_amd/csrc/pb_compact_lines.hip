@@ -299,19 +299,15 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
     nl = min(TL, p.ninner - inner0);
     base = (int64_t)outer * p.lo + (int64_t)inner0 * p.li;
   };
-  TileRegs<C, LAYOUT, TL, V, NT> pre;
   int t = blockIdx.x;
   if (t >= ntiles) return;
-  int64_t base;
-  int nl;
-  tile_of(t, base, nl);
-  if (K::PF) tile_fetch(p, p.in0, base, nl, pre);
   double keep[LPW][C];
-  for (; t < ntiles; t += gridDim.x) {
+  // one tile: its input registers `pre` go to LDS, then (PF) tile tn's input is fetched into them
+  // while this tile is solved and stored
+  auto step = [&](int t, TileRegs<C, LAYOUT, TL, V, NT>& pre, int tn) {
+    int64_t base, base_n = 0;
+    int nl, nl_n = 0;
     tile_of(t, base, nl);
-    const int tn = t + gridDim.x;
-    int64_t base_n = 0;
-    int nl_n = 0;
     if (K::PF && tn < ntiles) tile_of(tn, base_n, nl_n);
     __syncthreads();  // previous tile's LDS reads are done
     if (!K::PF) tile_fetch(p, p.in0, base, nl, pre);
@@ -335,7 +331,7 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
         for (int m = 0; m < C; ++m) r[m] = x[m];
         line_solve<C>(r, p.J, lane);
         chunk_write<C>(lds, l, lane, r);
-        continue;
+        continue;  // (per line)
       }
       if (PASS != 2) {
         line_op<C>(x, r, p.J, lane, p.ablate);
@@ -346,7 +342,7 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
     __syncthreads();
     if (PASS == 3) {
       tile_store<C, LAYOUT, TL, V, NT>(p, p.out0, lds, base, nl);
-      continue;
+      return;
     }
     if (PASS == 0) {
       tile_store<C, LAYOUT, TL, V, NT>(p, p.out0, lds, base, nl);
@@ -358,7 +354,7 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
       }
       __syncthreads();
       tile_store<C, LAYOUT, TL, V, NT>(p, p.out1, lds, base, nl);
-      continue;
+      return;
     }
     if (PASS == 1) {
       tile_store<C, LAYOUT, TL, V, NT>(p, p.out0, lds, base, nl);
@@ -381,6 +377,33 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
     }
     __syncthreads();
     tile_store<C, LAYOUT, TL, V, NT>(p, PASS == 1 ? p.out1 : p.out0, lds, base, nl);
+  };
+  if constexpr (K::PF == 2) {  // two tiles' inputs in flight (single-input passes)
+    static_assert(PASS == 0 || PASS == 3, "PF = 2: single-input passes only");
+    const int G = gridDim.x;
+    TileRegs<C, LAYOUT, TL, V, NT> ra, rb;
+    int64_t b0;
+    int n0;
+    tile_of(t, b0, n0);
+    tile_fetch(p, p.in0, b0, n0, ra);
+    if (t + G < ntiles) {
+      tile_of(t + G, b0, n0);
+      tile_fetch(p, p.in0, b0, n0, rb);
+    }
+    for (; t < ntiles; t += 2 * G) {
+      step(t, ra, t + 2 * G);
+      if (t + G >= ntiles) break;
+      step(t + G, rb, t + 3 * G);
+    }
+  } else {
+    TileRegs<C, LAYOUT, TL, V, NT> pre;
+    if (K::PF) {
+      int64_t b0;
+      int n0;
+      tile_of(t, b0, n0);
+      tile_fetch(p, p.in0, b0, n0, pre);
+    }
+    for (; t < ntiles; t += gridDim.x) step(t, pre, t + gridDim.x);
   }
 }
 
@@ -574,9 +597,11 @@ static int launch_lines_k(pb_ctx* ctx, LinePass& p, int64_t nouter) {
   return launch_lines_v<C, LAYOUT, PASS, K, 1>(ctx, p, nouter);
 }
 
-// Launch shapes (measured at 512^3, profiles/r01/tune_compact.jsonl): strided passes use 16-line
-// tiles (128-B row segments, two blocks per CU), the contiguous X pass 8-line tiles. C > 8 keeps
-// 8-line tiles for LDS. PB_LINES_CFG = 1..6 selects an alternative shape (tuning, C = 4 and 8).
+// Launch shapes (measured at 512^3, profiles/r01/tune_compact*.jsonl): strided passes use 16-line
+// tiles (128-B row segments, two blocks per CU), the contiguous X pass 8-line tiles; the batched
+// interleaved solve (PASS 3: little compute per tile to hide the next tile's loads under) 32-line
+// tiles with two tiles' inputs in flight. C > 8 keeps 8-line tiles for LDS. PB_LINES_CFG = 1..10
+// selects an alternative shape (tuning, C = 4 and 8).
 template <int C, int LAYOUT, int PASS>
 static int launch_lines_c(pb_ctx* ctx, LinePass& p, int64_t nouter) {
   static const int cfg = env_int("PB_LINES_CFG", 0);
@@ -588,10 +613,28 @@ static int launch_lines_c(pb_ctx* ctx, LinePass& p, int64_t nouter) {
       case 4: return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 0>>(ctx, p, nouter);
       case 5: return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 1>>(ctx, p, nouter);
       case 6: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 0>>(ctx, p, nouter);
+      case 7:
+        if constexpr (PASS == 0 || PASS == 3)
+          return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 2>>(ctx, p, nouter);
+        break;
+      case 8:
+        if constexpr (PASS == 0 || PASS == 3)
+          return launch_lines_k<C, LAYOUT, PASS, LineCfg<8, 8, 2>>(ctx, p, nouter);
+        break;
+      case 9:
+        if constexpr (PASS == 0 || PASS == 3)
+          return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 2>>(ctx, p, nouter);
+        break;
+      case 10:
+        if constexpr (PASS == 0 || PASS == 3)
+          return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 8, 2>>(ctx, p, nouter);
+        break;
       default: break;
     }
   }
-  if constexpr (LAYOUT == 0 && C <= 8)
+  if constexpr (LAYOUT == 0 && C <= 8 && PASS == 3)  // batched solve: 0.62 -> 0.48 ms at 512
+    return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 2>>(ctx, p, nouter);
+  else if constexpr (LAYOUT == 0 && C <= 8)
     return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 1>>(ctx, p, nouter);
   else
     return launch_lines_k<C, LAYOUT, PASS, LineCfg<8, 8, 0>>(ctx, p, nouter);

@@ -33,6 +33,18 @@ def main():
         if cnt:
             avg = ms / cnt
             res[name] = {"ms": round(avg, 4), "GBps": round(b * m ** 3 / avg / 1e6, 1)}
+    # batched (alpha, 1, alpha) solve over m^2 interleaved lines of m points (the PCR row)
+    dp, _ = out.device_ptr()
+    for _ in range(5):
+        pb.pcr_alpha_batched(ctx, m, m * m, 1, m * m, 0.3, dp)
+    ctx.sync()
+    ctx.reset_timing()
+    for _ in range(20):
+        pb.pcr_alpha_batched(ctx, m, m * m, 1, m * m, 0.3, dp)
+    ctx.sync()
+    ms, cnt = ctx.timing("pcr")
+    if cnt:
+        res["pcr_interleaved"] = {"ms": round(ms / cnt, 4), "GBps": round(16 * m ** 3 / (ms / cnt) / 1e6, 1)}
     print(json.dumps(res), flush=True)
 
 

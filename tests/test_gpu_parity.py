@@ -414,11 +414,14 @@ def test_pcr_alpha_matches_thomas(ctx):
 @pytest.mark.parametrize("n,nb,layout,alpha", [(512, 37, "contig", 3 / 10), (512, 64, "inter", 9 / 62),
                                                (192, 20, "contig", 3 / 10), (128, 33, "inter", 3 / 10),
                                                (64, 6, "contig", 9 / 62), (1024, 8, "inter", 3 / 10),
-                                               (96, 4, "contig", 3 / 10)])
+                                               (96, 4, "contig", 3 / 10), (64, 20005, "inter", 9 / 62),
+                                               (128, 9001, "inter", 3 / 10)])
 def test_pcr_batched_layouts(ctx, n, nb, layout, alpha):
     """Batched periodic (alpha,1,alpha) solve in both layouts of the batched API: contiguous lines
     (register path, one wave per line), interleaved lines (LDS tile transpose), and an n the
-    register path does not take (96: LDS PCR fallback is power-of-two only -> error)."""
+    register path does not take (96: LDS PCR fallback is power-of-two only -> error). The large
+    interleaved batches give every persistent block several tiles (two-deep input prefetch) and a
+    ragged last tile."""
     rng = np.random.default_rng(n + nb)
     d = rng.random((nb, n)) * 2 - 1
     ref = np.stack([O.tdma(np.full(n, alpha), np.ones(n), np.full(n, alpha), row,
