@@ -133,13 +133,14 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
       if constexpr (M == 1) {
         const int kp = kpar(kk);
 #pragma unroll
-        for (int r = 0; r < kRW; ++r)
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double t = (v[r][e] - 0.0) / cc;
-            const double red = (1.0 - omega) * 0.0 + omega * t;
-            v[r][e] = ((par_row[r] + e + kp) & 1) == 0 ? red : 0.0;
-          }
+        for (int r = 0; r < kRW; ++r) {
+          // one red point per pair, at a wave-uniform element: one division per pair
+          const bool red1 = ((par_row[r] + kp) & 1) != 0;  // the red point is element 1
+          const double t = ((red1 ? v[r][1] : v[r][0]) - 0.0) / cc;
+          const double red = (1.0 - omega) * 0.0 + omega * t;
+          v[r][0] = red1 ? 0.0 : red;
+          v[r][1] = red1 ? red : 0.0;
+        }
       }
       (void)v;
       (void)kk;
