@@ -21,9 +21,19 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X spec (MI355X_MICROARCH.md "Chip-level parameters")
 PASS_A_BYTES = 24            # pass A: read r, p_old; write p_new
-PASS_B_EVEN_BYTES = 24       # pass B, even iteration: read p (stencil), r; write r (x deferred)
-PASS_B_ODD_BYTES = 48        # pass B, odd iteration: read p, p_prev, x, r; write x, r
-CG_ITER_BYTES = 60           # per CG iteration on average (SURVEY §8d's fused lower bound is 80)
+PASS_B_EVEN_BYTES = 24       # pass B without x update: read p (stencil), r; write r (x deferred)
+# the x update every D-th iteration (PB_CG_DEFER_X = D, default 4): pass B reads p_i (stencil),
+# r, x and p_{i-1} .. p_{i-D+1}, writes r and x
+PASS_B_X_BYTES = {0: 40, 2: 48, 4: 64}
+PASS_B_X_NAME = {0: "cg_pass_b", 2: "cg_pass_b_odd", 4: "cg_pass_b_x4"}
+
+
+def cg_iter_bytes(defer):
+    """Algorithmic bytes per DoF of one CG iteration, averaged over a deferral cycle
+    (58 at D = 4; SURVEY §8d's fused 2-pass lower bound without deferral is 80)."""
+    if defer == 0:
+        return PASS_A_BYTES + PASS_B_X_BYTES[0]
+    return PASS_A_BYTES + ((defer - 1) * PASS_B_EVEN_BYTES + PASS_B_X_BYTES[defer]) / defer
 MATVEC_BYTES = 16            # y = A x: read x, write y
 SEED = 20231015
 
@@ -95,6 +105,8 @@ def main():
     import poissbox_amd as pb
     from poissbox_amd.dist import GlooTransport, broadcast_uid, init_from_env
 
+    dx = int(os.environ.get("PB_CG_DEFER_X", "4"))  # the solver's deferral depth (pb_solver.cpp)
+    defer = 0 if dx == 0 else (2 if dx == 2 else 4)
     rank, world, local_rank, dist = init_from_env("gloo")   # control plane only
     uid = None
     device = local_rank
@@ -127,7 +139,7 @@ def main():
         dist.barrier()
     # timed region: HIP events around the roofline kernel only (events around every launch would
     # add ~2 % of gaps to the measured step)
-    os.environ["PB_TIMING_ONLY"] = "cg_pass_b_odd"
+    os.environ["PB_TIMING_ONLY"] = "cg_pass_a"
     ctx.set_timing(True)
     ctx.reset_timing()
     t0 = time.perf_counter()
@@ -138,7 +150,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = t1 - t0
-    ms_b, cnt_b = ctx.timing("cg_pass_b_odd")
+    ms_a, cnt_a = ctx.timing("cg_pass_a")
     ctx.set_timing(False)
     os.environ.pop("PB_TIMING_ONLY", None)
     # per-kernel diagnostics of the other passes: a few more iterations, every launch timed
@@ -146,7 +158,11 @@ def main():
     ctx.reset_timing()
     ksp.iterate(diag_steps)
     ctx.sync()
-    ms_a, cnt_a = ctx.timing("cg_pass_a")
+    ms_b, cnt_b = ctx.timing(PASS_B_X_NAME[defer])
+    for d_, nm in PASS_B_X_NAME.items():  # the library's deferral depth, from the pass it ran
+        if cnt_b == 0 and ctx.timing(nm)[1] > 0:
+            defer = d_
+            ms_b, cnt_b = ctx.timing(nm)
     ms_be, cnt_be = ctx.timing("cg_pass_b_even")
     ctx.set_timing(False)
     reason, its, hist = ksp.end()
@@ -199,27 +215,31 @@ def main():
                            if world > 1 else ""),
                        "ksp": "-ksp_type cg -pc_type jacobi, constant null space, rtol=0 (fixed iterations)"},
             "iter_per_s": args.steps / elapsed,
-            "achieved_GBps_cg": CG_ITER_BYTES * N / (elapsed / args.steps) / 1e9,
+            "achieved_GBps_cg": cg_iter_bytes(defer) * N / (elapsed / args.steps) / 1e9,
+            # the dominant kernel: pass A runs every iteration and takes the largest share of
+            # the step (44 % at D = 4); it is timed with HIP events inside the timed region
             "roofline": {"bound": "hbm",
-                         "kernel": "cg_pass_b_odd (stencil of p + r update + deferred x update + 4 sums)",
-                         "achieved": gbs(PASS_B_ODD_BYTES, t_b), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs(PASS_B_ODD_BYTES, t_b) / HBM_PEAK_GBS,
-                         "traffic": None, "bytes_per_dof": PASS_B_ODD_BYTES,
-                         "avg_launch_ms": t_b * 1e3},
+                         "kernel": "cg_pass_a (p = z + beta p fused into the 7-point stencil of p, "
+                                   "store p, p.Ap sums)",
+                         "achieved": gbs(PASS_A_BYTES, t_a), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs(PASS_A_BYTES, t_a) / HBM_PEAK_GBS,
+                         "traffic": None, "bytes_per_dof": PASS_A_BYTES,
+                         "avg_launch_ms": t_a * 1e3},
             "kernels": {
                 "cg_pass_a": {"avg_ms": t_a * 1e3, "GBps": gbs(PASS_A_BYTES, t_a),
                               "frac": gbs(PASS_A_BYTES, t_a) / HBM_PEAK_GBS, "bytes_per_dof": PASS_A_BYTES},
                 "cg_pass_b_even": {"avg_ms": t_be * 1e3, "GBps": gbs(PASS_B_EVEN_BYTES, t_be),
                                    "frac": gbs(PASS_B_EVEN_BYTES, t_be) / HBM_PEAK_GBS,
                                    "bytes_per_dof": PASS_B_EVEN_BYTES},
-                "cg_pass_b_odd": {"avg_ms": t_b * 1e3, "GBps": gbs(PASS_B_ODD_BYTES, t_b),
-                                  "frac": gbs(PASS_B_ODD_BYTES, t_b) / HBM_PEAK_GBS,
-                                  "bytes_per_dof": PASS_B_ODD_BYTES},
+                PASS_B_X_NAME[defer]: {"avg_ms": t_b * 1e3, "GBps": gbs(PASS_B_X_BYTES[defer], t_b),
+                                       "frac": gbs(PASS_B_X_BYTES[defer], t_b) / HBM_PEAK_GBS,
+                                       "bytes_per_dof": PASS_B_X_BYTES[defer]},
                 "matvec_star7": {"avg_ms": t_mv * 1e3, "GBps": gbs(MATVEC_BYTES, t_mv),
                                  "frac": gbs(MATVEC_BYTES, t_mv) / HBM_PEAK_GBS,
                                  "dofs_per_s": nloc / t_mv if t_mv > 0 else 0.0,
                                  "bytes_per_dof": MATVEC_BYTES},
             },
+            "cg_x_update_every": defer,
             "ksp_state": {"reason": pb.REASONS.get(reason, reason), "its": its,
                           "rnorm0": float(hist[0]), "rnorm_last": float(hist[-1])},
         }
@@ -228,9 +248,9 @@ def main():
             try:
                 tr = json.load(open(traffic_file))
                 key = f"{n[0]}x{n[1]}x{n[2]}"
-                if key in tr and "cg_pass_b_odd" in tr[key]:
-                    out["roofline"]["traffic"] = tr[key]["cg_pass_b_odd"]["bytes_per_launch"]
-                    out["roofline"]["traffic_source"] = tr[key]["cg_pass_b_odd"].get("source")
+                if key in tr and "cg_pass_a" in tr[key]:
+                    out["roofline"]["traffic"] = tr[key]["cg_pass_a"]["bytes_per_launch"]
+                    out["roofline"]["traffic_source"] = tr[key]["cg_pass_a"].get("source")
                 for role, kv in out["kernels"].items():
                     if role in tr.get(key, {}):
                         kv["traffic"] = tr[key][role]["bytes_per_launch"]

@@ -210,10 +210,14 @@ int launch_mg_residual(pb_grid* g, const Star& s, const double* x, const double*
                        const StencilPlanes& gp, double* res, const int* skip);
 
 // CG state (device resident; all scalars computed on device, host only polls `done`)
+// Deferred solution update (defer_x = D in {0, 2, 4}): x += sum of alpha_m p_m over D
+// iterations in the pass B of every D-th iteration; pend_* describe what is still pending
+// (alphas pa[0 .. pend_count-1] of iterations pend_iter, pend_iter + 1, ...).
 struct CgState {
-  double beta, betaold, dpi, dpiold, alpha, alpha_prev, pend_alpha, mu, dp, ttol, rnorm0;
+  double beta, betaold, dpi, dpiold, alpha, alpha_prev, mu, dp, ttol, rnorm0;
+  double pa[3];
   double rtol, atol, dtol, dinv, ntot;
-  int64_t it, its, max_it, nhist, pend_iter;
+  int64_t it, its, max_it, nhist, pend_iter, pend_count;
   int reason, done, pc, nullspace, defer_x;
 };
 int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p, CgState* st,
@@ -223,9 +227,10 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
                      double* p_new, const StencilPlanes& gp, CgState* st, int mode, int part_off,
                      int* nblocks);
 int cg_finalize_pass_a(pb_ctx* ctx, int nparts, CgState* st);
-int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
-                     double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
-                     int64_t host_iter, bool defer_x, bool finalize = true);
+// p_prev[m] = p of iteration host_iter - 1 - m (m < 3; only the first defer-1 are read)
+int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
+                     double* x, double* r, const StencilPlanes& gp, CgState* st, double* hist,
+                     int* h_done, int64_t host_iter, int defer, bool finalize = true);
 int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
 
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----

@@ -116,28 +116,31 @@ struct PassA {
 
 // CG pass B: r += (-a) w with w = A p recomputed; then the PC/null-space sums of the new
 // residual: s = dinv*r, t = s - mu_old:  sum t, sum t^2, sum t*r, sum r.
-// The solution update is deferred to every second iteration (x is not part of the recurrence):
-//   XU = 0 (even iteration i): no x traffic, alpha_i p_i stays pending;
-//   XU = 1 (odd iteration i):  x += (alpha_{i-1} p_{i-1} + alpha_i p_i), p_{i-1} is still
-//                              resident in the other p buffer;
+// The solution update is deferred over D iterations (x is not part of the recurrence; D = 4 by
+// default, 2 or 0 by PB_CG_DEFER_X), the directions kept in a ring of D p buffers:
+//   XU = 0 (i % D < D-1):      no x traffic, alpha_i p_i stays pending;
+//   XU = 3 (D = 4, i % 4 = 3): x += a_{i-3} p_{i-3} + a_{i-2} p_{i-2} + a_{i-1} p_{i-1} + a_i p_i
+//   XU = 1 (D = 2, odd i):     x += (alpha_{i-1} p_{i-1} + alpha_i p_i);
 //   XU = 2 (no deferral):      x += alpha_i p_i every iteration.
 // Operands are prefetched one plane ahead (XU = 1: 3 operand rows, 238 VGPRs -- one workgroup
 // per CU is all the grid uses; measured 2 % faster than loading them in the plane's own step).
 template <int XU>
 struct PassB {
-  static constexpr int NS = 4, NE = XU == 1 ? 3 : (XU == 2 ? 2 : 1);
+  static constexpr int NS = 4, NE = XU == 1 ? 3 : (XU == 2 ? 2 : (XU == 3 ? 5 : 1));
   static constexpr bool RAW = false;
   // one workgroup per CU (z-chunks of half the slab at 512^3): 8-10 % faster than 3 per CU
   static constexpr int WGCU = 1;  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = true;
   double* __restrict__ x;
   double* __restrict__ r;
-  const double* __restrict__ p_prev;
+  const double* __restrict__ p_prev;  // p of iteration i-1
+  const double* __restrict__ p_m2;    // XU = 3: p of iterations i-2, i-3
+  const double* __restrict__ p_m3;
   const CgState* st;
-  double alpha, alpha_prev, dinv, mu;
+  double alpha, alpha_prev, dinv, mu, a2, a3;
   __device__ __forceinline__ void prepare();
   __device__ __forceinline__ const double* src(int a) const {
-    return a == 0 ? r : (a == 1 ? x : p_prev);
+    return a == 0 ? r : (a == 1 ? x : (a == 2 ? p_prev : (a == 3 ? p_m2 : p_m3)));
   }
   template <int V>
   __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
@@ -163,6 +166,17 @@ struct PassB {
       double xv[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) xv[e] = op[1][e] + alpha * c[e];
+      store_row<V>(x, idx, xv, nt);
+    } else if constexpr (XU == 3) {  // x += a_{i-3} p_{i-3} + a_{i-2} p_{i-2} + a_{i-1} p_{i-1} + a_i p_i
+      double xv[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        double u = a3 * op[4][e];
+        u = u + a2 * op[3][e];
+        u = u + alpha_prev * op[2][e];
+        u = u + alpha * c[e];
+        xv[e] = op[1][e] + u;
+      }
       store_row<V>(x, idx, xv, nt);
     }
   }
@@ -631,6 +645,11 @@ __device__ __forceinline__ void PassB<XU>::prepare() {
   alpha_prev = st->alpha_prev;
   dinv = st->dinv;
   mu = st->mu;
+  if constexpr (XU == 3) {  // pending alphas of iterations i-3, i-2, i-1
+    a3 = st->pa[0];
+    a2 = st->pa[1];
+    alpha_prev = st->pa[2];
+  }
 }
 
 // r = b, x = 0, p = 0 and the sums of s = dinv*r (t = s - 0)
@@ -723,6 +742,7 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
     st->alpha = 0.0;
     st->alpha_prev = 0.0;
     st->pend_iter = -1;
+    st->pend_count = 0;
     st->reason = 0;
     st->done = 0;
     if (st->nhist > 0) hist[0] = dp;
@@ -785,12 +805,17 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
       zr = S[2] - delta * S[3];
     }
     const double dp = sqrt(zz > 0.0 ? zz : 0.0);
-    // even iterations leave alpha_i p_i pending in x; odd ones applied both (PassB<XU>)
-    if (st->defer_x && i % 2 == 0) {
-      st->pend_iter = i;
-      st->pend_alpha = st->alpha;
+    // iterations i % D < D-1 leave alpha_i p_i pending in x; the last of each D applied them all
+    // (PassB<XU>)
+    const int D = st->defer_x;
+    const int m = D > 0 ? (int)(i % D) : 0;
+    if (D > 0 && m < D - 1) {
+      st->pa[m] = st->alpha;
+      st->pend_iter = i - m;
+      st->pend_count = m + 1;
     } else {
       st->pend_iter = -1;
+      st->pend_count = 0;
     }
     st->dp = dp;
     st->its = i + 1;
@@ -893,26 +918,32 @@ int cg_finalize_stage2(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* 
   return cg_reduce_update(ctx, 2, nparts, 4, st, hist, h_done, host_iter);
 }
 
-int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* p_prev, double* x,
-                     double* r, const StencilPlanes& gp, CgState* st, double* hist, int* h_done,
-                     int64_t host_iter, bool defer_x, bool finalize) {
+int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
+                     double* x, double* r, const StencilPlanes& gp, CgState* st, double* hist,
+                     int* h_done, int64_t host_iter, int defer, bool finalize) {
   int nparts = 0;
   {
-    if (!defer_x) {
+    const double* pp = p_prev[0];
+    if (defer == 0) {
       ScopedTimer tm(g->ctx, "cg_pass_b");
       PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<2>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done,
-                        PLANES_ALL, 0, &nparts, 1));
-    } else if (host_iter % 2 == 0) {
+                        PassB<2>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                        &st->done, PLANES_ALL, 0, &nparts, 1));
+    } else if (host_iter % defer != defer - 1) {
       ScopedTimer tm(g->ctx, "cg_pass_b_even");
       PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<0>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done,
-                        PLANES_ALL, 0, &nparts, 1));
-    } else {
+                        PassB<0>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                        &st->done, PLANES_ALL, 0, &nparts, 1));
+    } else if (defer == 2) {
       ScopedTimer tm(g->ctx, "cg_pass_b_odd");
       PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<1>{x, r, p_prev, st, 0.0, 0.0, 0.0, 0.0}, &st->done,
-                        PLANES_ALL, 0, &nparts, 1));
+                        PassB<1>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                        &st->done, PLANES_ALL, 0, &nparts, 1));
+    } else {
+      ScopedTimer tm(g->ctx, "cg_pass_b_x4");
+      PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
+                        PassB<3>{x, r, pp, p_prev[1], p_prev[2], st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                        &st->done, PLANES_ALL, 0, &nparts, 1));
     }
   }
   if (!finalize) return PB_OK;  // preconditioned path: the sums come from z = M^-1 r later

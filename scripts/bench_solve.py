@@ -54,7 +54,7 @@ def main():
             parts = {}
             for nm in ("mg_fine_smooth_first", "mg_fine_resid_restrict", "mg_fine_prolong_post",
                        "mg_coarse_levels", "cg_pass_a", "cg_pass_b", "cg_pass_b_even",
-                       "cg_pass_b_odd", "compact_lapl_fast"):
+                       "cg_pass_b_odd", "cg_pass_b_x4", "compact_lapl_fast"):
                 ms_, c_ = ctx.timing(nm)
                 if c_ and mg_cnt:
                     parts[nm] = ms_ / mg_cnt

@@ -21,6 +21,7 @@ ROLES = {
     "cg_pass_a": r"star7_kernel<.*CombineLoad, pb::PassA",
     "cg_pass_b_even": r"star7_kernel<.*PassB<0>",
     "cg_pass_b_odd": r"star7_kernel<.*PassB<1>",
+    "cg_pass_b_x4": r"star7_kernel<.*PassB<3>",
 }
 
 

@@ -50,7 +50,10 @@ for rnd in range(rounds):
         ctx.sync()
         it_ms = (time.perf_counter() - t0) / 32 * 1e3
         mv, pa = ctx.timing("stencil"), ctx.timing("cg_pass_a")
-        pbb = ctx.timing("cg_pass_b_odd")
+        # the pass B that applies the deferred x update (PB_CG_DEFER_X = 4 / 2 / 0)
+        pbb = ctx.timing("cg_pass_b_x4")
+        if pbb[1] == 0:
+            pbb = ctx.timing("cg_pass_b_odd")
         if pbb[1] == 0:
             pbb = ctx.timing("cg_pass_b")
         pbe = ctx.timing("cg_pass_b_even")
@@ -64,7 +67,9 @@ for rnd in range(rounds):
         acc[i]["it"].append(it_ms)
 for i, cfg in enumerate(configs):
     out = {"cfg": cfg}
-    for key, nbytes in (("mv", 16), ("a", 24), ("b", 48), ("be", 24), ("it", 60)):
+    dfx = int(os.environ.get("PB_CG_DEFER_X", "4"))
+    bx, it_b = {0: (40, 64), 2: (48, 60)}.get(dfx, (64, 58))
+    for key, nbytes in (("mv", 16), ("a", 24), ("b", bx), ("be", 24), ("it", it_b)):
         v = acc[i][key]
         out[key + "_min_ms"] = min(v)
         out[key + "_med_ms"] = statistics.median(v)

@@ -201,6 +201,29 @@ def test_cg_pc_none_and_max_it(ctx):
     assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
 
 
+@pytest.mark.parametrize("defer", ["0", "2", "4"])
+@pytest.mark.parametrize("max_it", [8, 9, 10, 11])
+def test_cg_deferred_x_update(ctx, monkeypatch, defer, max_it):
+    """The solution update deferred over D iterations (PB_CG_DEFER_X = D; 4 is the default):
+    stopping at every position of the cycle (0-3 updates still pending, flushed at the end)
+    gives the oracle's x (summation order differs: rounding level) and the same history."""
+    monkeypatch.setenv("PB_CG_DEFER_X", defer)
+    n3 = (32, 24, 16)
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=max_it)
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(P, A, x, bv, ["-ksp_rtol", "0", "-ksp_atol", "0",
+                                               "-ksp_divtol", "1e300",
+                                               "-ksp_max_it", str(max_it)])
+    assert (reason, its) == (ro, itso) == (-3, max_it)
+    assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
+    assert np.max(np.abs(x.get_values() - xo)) <= 1e-12 * np.max(np.abs(xo))
+
+
 def test_cg_zero_rhs_converges_immediately(ctx):
     n3 = (8, 8, 8)
     da = pb.DA(ctx, n3)
