@@ -82,7 +82,7 @@ struct CombineLoad {
 // ---------------------------------------------------------------------------------------------
 struct StoreY {
   static constexpr int NS = 0, NE = 0;
-  static constexpr bool RAW = false;
+  static constexpr bool RAW = false, TALL = true;
   static constexpr int WGCU = 3;  // workgroups per CU the grid is sized for  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = true;
   double* __restrict__ y;
@@ -485,12 +485,31 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
   return PB_OK;
 }
 
+// Epi::TALL (optional trait): on planes of >= 512^2 points the epilogue runs 8 rows per wave
+// with one workgroup per CU (the matvec: 0.404 -> 0.377-0.388 ms at 512^3; the CG passes measured
+// no better or slower that way, profiles/r01/tune_ty8.txt)
+template <class E, class = void>
+struct TallOf {
+  static constexpr bool v = false;
+};
+template <class E>
+struct TallOf<E, std::void_t<decltype(E::TALL)>> {
+  static constexpr bool v = E::TALL;
+};
+
 template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                       const Epi& ep, const int* skip, int mode = PLANES_ALL, int part_off = 0,
                       int* nb_out = nullptr, int rev = 0, int wgcu = 0) {
   const bool vec2 = (g->n[0] % 2) == 0;
   const int ty = pick_ty((int)g->n[1]);
+  if constexpr (TallOf<Epi>::v) {
+    const int tall = env_int("PB_STENCIL_TALL", 1);  // read per launch (A/B tuning)
+    if (vec2 && ty == 4 && tall && !getenv("PB_STENCIL_TY") && g->n[1] % 8 == 0 &&
+        g->plane >= (int64_t)512 * 512)
+      return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev,
+                            wgcu > 0 ? wgcu : 1);
+  }
   if (vec2) {
     switch (ty) {
       case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);

@@ -61,7 +61,9 @@ def grid_vec(ctx, n, values=None, L=(1.0, 1.0, 1.0)):
 # 7-point operator (mfmult / compute_lapl_pointwise)
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("n", [(3, 3, 3), (16, 16, 16), (17, 12, 9), (130, 18, 7), (64, 64, 64),
-                               (256, 8, 5), (20, 36, 11), (128, 128, 4), (512, 64, 128)])
+                               (256, 8, 5), (20, 36, 11), (128, 128, 4), (512, 64, 128),
+                               # planes of >= 512^2 points: 8 rows per wave (StoreY::TALL)
+                               (512, 512, 6), (1024, 256, 5), (512, 520, 3)])
 def test_stencil_bit_exact(ctx, n):
     N = int(np.prod(n))
     x = O.fill_random(N, SEED + N)
