@@ -99,7 +99,7 @@ struct StoreY {
 // CG pass A: store p_new, accumulate p.w (VecXDot(P, W))
 struct PassA {
   static constexpr int NS = 1, NE = 0;
-  static constexpr bool RAW = false;
+  static constexpr bool RAW = false, TALL = true;
   static constexpr int WGCU = 3;  // put() takes the Laplacian, not the 7 values
   static constexpr bool PREFETCH = true;
   double* __restrict__ p_new;
@@ -486,8 +486,8 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
 }
 
 // Epi::TALL (optional trait): on planes of >= 512^2 points the epilogue runs 8 rows per wave
-// with one workgroup per CU (the matvec: 0.404 -> 0.377-0.388 ms at 512^3; the CG passes measured
-// no better or slower that way, profiles/r01/tune_ty8.txt)
+// with one workgroup per CU (at 512^3: matvec 0.402 -> 0.386 ms, pass A 0.616 -> 0.586 ms; the
+// pass B variants are slower that way and keep 4 rows, profiles/r01/tune_ty8.txt)
 template <class E, class = void>
 struct TallOf {
   static constexpr bool v = false;
