@@ -505,8 +505,9 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
   const int ty = pick_ty((int)g->n[1]);
   if constexpr (TallOf<Epi>::v) {
     const int tall = env_int("PB_STENCIL_TALL", 1);  // read per launch (A/B tuning)
+    const int64_t tall_min = env_int("PB_STENCIL_TALL_MIN_PLANE", 512 * 512);
     if (vec2 && ty == 4 && tall && !getenv("PB_STENCIL_TY") && g->n[1] % 8 == 0 &&
-        g->plane >= (int64_t)512 * 512)
+        g->plane >= tall_min)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev,
                             wgcu > 0 ? wgcu : 1);
   }
