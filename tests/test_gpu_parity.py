@@ -329,9 +329,11 @@ def test_multirank_stencil_bit_exact(nranks, n):
         assert np.array_equal(y, ref[k0:k0 + nk].reshape(-1))
 
 
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_multirank_cg(nranks):
-    n = (16, 16, 12)
+@pytest.mark.parametrize("nranks,n", [(2, (16, 16, 12)), (3, (16, 16, 12)),
+                                       # 512^2 planes: tall pass A / matvec on the interior and
+                                       # boundary launches of a decomposed step (nzl = 6, 4)
+                                       (2, (512, 512, 12)), (3, (512, 512, 12))])
+def test_multirank_cg(nranks, n):
     N = int(np.prod(n))
     h = tuple(1.0 / m for m in n)
     b = O.stencil(O.fill_random(N, SEED), n, h)
@@ -790,6 +792,18 @@ def test_rccl_code_paths_one_rank_communicator(monkeypatch):
     ref = O.lapl(xt, n3, hc)
     pb.compact_lapl_fast(da, hc, xv, y)
     assert np.max(np.abs(y.get_values() - ref)) <= FAST_RTOL * np.max(np.abs(ref))
+    # 512^2 planes (tall pass A / matvec) on the interior + boundary launches with RCCL halos
+    n3 = (512, 512, 6)
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-6)
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(P, A, x, bv, ["-ksp_rtol", "1e-6"])
+    assert (reason, its) == (ro, itso)
+    assert np.max(np.abs(hist - ho) / ho) < HIST_RTOL
     # fused MG sweeps on a decomposed grid: two-deep z ghosts through ncclSend/ncclRecv
     n3 = (128, 16, 16)
     N = int(np.prod(n3))
