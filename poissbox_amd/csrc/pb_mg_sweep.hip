@@ -354,12 +354,14 @@ int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double
     if (nblocks * 4 > g->ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
                        (long long)nblocks);
-    hipLaunchKernelGGL((geo.split ? sor_sweep2_kernel<true, 0, true> : sor_sweep2_kernel<true, 0, false>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+    auto kern = geo.split ? sor_sweep2_kernel<true, 0, true> : sor_sweep2_kernel<true, 0, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
                        (double*)nullptr, sums_st, g->ctx->d_partials, skip);
     if (nparts) *nparts = (int)nblocks;
   } else {
-    hipLaunchKernelGGL((geo.split ? sor_sweep2_kernel<false, 0, true> : sor_sweep2_kernel<false, 0, false>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+    auto kern = geo.split ? sor_sweep2_kernel<false, 0, true> : sor_sweep2_kernel<false, 0, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
                        (double*)nullptr, (const CgState*)nullptr, (double*)nullptr, skip);
   }
@@ -375,7 +377,8 @@ int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double
   Sweep2Geo geo;
   const int64_t nblocks = sweep2_geo(g, geo);
   PB_TRY(sweep2_ghosts(g, b, b, geo));
-  hipLaunchKernelGGL((geo.split ? sor_sweep2_kernel<false, 1, true> : sor_sweep2_kernel<false, 1, false>), dim3((unsigned)nblocks), dim3(kThreads), 0,
+  auto kern = geo.split ? sor_sweep2_kernel<false, 1, true> : sor_sweep2_kernel<false, 1, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
                      g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, 1, b, b, x, res,
                      (const CgState*)nullptr, (double*)nullptr, skip);
   PB_HIP(hipGetLastError());

@@ -83,7 +83,7 @@ struct CombineLoad {
 struct StoreY {
   static constexpr int NS = 0, NE = 0;
   static constexpr bool RAW = false, TALL = true;
-  static constexpr int WGCU = 3;  // workgroups per CU the grid is sized for  // put() takes the Laplacian, not the 7 values
+  static constexpr int WGCU = 3;  // workgroups per CU the grid is sized for
   static constexpr bool PREFETCH = true;
   double* __restrict__ y;
   __device__ __forceinline__ void prepare() {}
@@ -99,8 +99,8 @@ struct StoreY {
 // CG pass A: store p_new, accumulate p.w (VecXDot(P, W))
 struct PassA {
   static constexpr int NS = 1, NE = 0;
-  static constexpr bool RAW = false, TALL = true;
-  static constexpr int WGCU = 3;  // put() takes the Laplacian, not the 7 values
+  static constexpr bool RAW = false, TALL = true;  // put() takes the Laplacian; 8-row tiles
+  static constexpr int WGCU = 3;                   // (4-row tiles; 1 with 8 rows)
   static constexpr bool PREFETCH = true;
   double* __restrict__ p_new;
   __device__ __forceinline__ void prepare() {}
@@ -127,9 +127,9 @@ struct PassA {
 template <int XU>
 struct PassB {
   static constexpr int NS = 4, NE = XU == 1 ? 3 : (XU == 2 ? 2 : (XU == 3 ? 5 : 1));
-  static constexpr bool RAW = false;
+  static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
   // one workgroup per CU (z-chunks of half the slab at 512^3): 8-10 % faster than 3 per CU
-  static constexpr int WGCU = 1;  // put() takes the Laplacian, not the 7 values
+  static constexpr int WGCU = 1;
   static constexpr bool PREFETCH = true;
   double* __restrict__ x;
   double* __restrict__ r;
@@ -167,7 +167,7 @@ struct PassB {
 #pragma unroll
       for (int e = 0; e < V; ++e) xv[e] = op[1][e] + alpha * c[e];
       store_row<V>(x, idx, xv, nt);
-    } else if constexpr (XU == 3) {  // x += a_{i-3} p_{i-3} + a_{i-2} p_{i-2} + a_{i-1} p_{i-1} + a_i p_i
+    } else if constexpr (XU == 3) {  // x += a3 p_{i-3} + a2 p_{i-2} + alpha_prev p_{i-1} + alpha p_i
       double xv[V];
 #pragma unroll
       for (int e = 0; e < V; ++e) {
