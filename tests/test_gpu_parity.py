@@ -206,7 +206,7 @@ def test_cg_pc_none_and_max_it(ctx):
 
 
 @pytest.mark.parametrize("defer", ["0", "2", "4"])
-@pytest.mark.parametrize("max_it", [8, 9, 10, 11])
+@pytest.mark.parametrize("max_it", [1, 2, 3, 8, 9, 10, 11])
 def test_cg_deferred_x_update(ctx, monkeypatch, defer, max_it):
     """The solution update deferred over D iterations (PB_CG_DEFER_X = D; 4 is the default):
     stopping at every position of the cycle (0-3 updates still pending, flushed at the end)
