@@ -92,6 +92,8 @@ struct pb_ctx {
   // timing
   bool timing = false;
   std::vector<std::string> timing_only;  // PB_TIMING_ONLY="a,b": time only these phases
+  int timing_every = 1;  // PB_TIMING_EVERY=n: events around every n-th call of a phase only
+  std::map<std::string, int64_t> timer_calls;
   bool roctx = false;  // PB_ROCTX=1: roctx ranges around every timed phase (rocprofv3 --marker-trace)
   std::map<std::string, pb::TimerSlot> timers;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -147,7 +149,7 @@ void timer_begin(pb_ctx* ctx, const char* name, hipEvent_t* ev);
 void timer_end(pb_ctx* ctx, const char* name, hipEvent_t ev0);
 void timers_collect(pb_ctx* ctx);
 
-bool timer_wanted(const pb_ctx* ctx, const char* name);
+bool timer_wanted(pb_ctx* ctx, const char* name);
 
 struct ScopedTimer {
   pb_ctx* ctx;

@@ -1,5 +1,6 @@
 // pb_runtime.cpp -- host runtime of libpoissbox_gpu: errors, context (device, stream, RCCL),
 // slab grid, vectors, halo exchange and allreduce, the operator entry point and kernel timing.
+#include <algorithm>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -46,11 +47,12 @@ static hipEvent_t take_event(pb_ctx* ctx) {
   return e;
 }
 
-bool timer_wanted(const pb_ctx* ctx, const char* name) {
-  if (ctx->timing_only.empty()) return true;
+bool timer_wanted(pb_ctx* ctx, const char* name) {
+  bool want = ctx->timing_only.empty();
   for (const auto& n : ctx->timing_only)
-    if (n == name) return true;
-  return false;
+    if (n == name) want = true;
+  if (!want || ctx->timing_every <= 1) return want;
+  return ctx->timer_calls[name]++ % ctx->timing_every == 0;  // sampled phase
 }
 
 void timer_begin(pb_ctx* ctx, const char*, hipEvent_t* ev) {
@@ -430,6 +432,8 @@ int pb_ctx_set_timing(pb_ctx* ctx, int enable) {
   // PB_TIMING_ONLY (comma-separated phase names): record events around those phases only, so a
   // timed region is not perturbed by event records around every kernel
   ctx->timing_only.clear();
+  ctx->timer_calls.clear();
+  ctx->timing_every = std::max(1, env_int("PB_TIMING_EVERY", 1));
   const char* only = getenv("PB_TIMING_ONLY");
   if (enable && only && *only) {
     std::string cur;
