@@ -71,7 +71,31 @@ def cpu_baseline(seconds=12.0):
             "iter_per_s": its / el,
             "sample": f"256^3 grid, {its} CG iterations (+setup) of oracle/pb_oracle.c "
                       f"(PETSc KSPCG+PCJacobi+MatNullSpace sequence, 7-point, OpenMP {threads} "
-                      f"threads) in {el:.1f} s on the GPU box host"}
+                      f"threads) in {el:.1f} s on the GPU box host",
+            "variants": cpu_variants(threads)}
+
+
+def cpu_variants(threads, iters=40):
+    """SURVEY §8(d)'s other CPU rows, a few seconds each on 128^3: the optimised 7-point CG on
+    one core, and the reference-faithful operator (27-term pointwise dot product per point, as
+    src/poissbox.f90:128-148 evaluates it) on one core and on all of them. Fixed iteration
+    count (rtol = atol = 0), the same PETSc scalar sequence."""
+    from oracle import oracle as O
+    n = (128, 128, 128)
+    N = 128 ** 3
+    h = (1 / 128,) * 3
+    b = O.stencil(O.fill_random(N, SEED), n, h, nthreads=threads)
+    out = []
+    for faithful, nt in ((False, 1), (True, 1), (True, threads)):
+        k = iters if not faithful or nt > 1 else iters // 4
+        t0 = time.perf_counter()
+        _, _, its, _ = O.cg_solve(b, n, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=k,
+                                  faithful=faithful, nthreads=nt)
+        el = time.perf_counter() - t0
+        out.append({"op": "faithful 27-term" if faithful else "7-point", "cores": nt,
+                    "value": N * its / el, "unit": "DoF-updates/s",
+                    "sample": f"128^3 grid, {its} CG + Jacobi iterations (+setup) in {el:.2f} s"})
+    return out
 
 
 def main():

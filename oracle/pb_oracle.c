@@ -63,8 +63,11 @@ double pbo_diag(const double h[3]) {
  * for every owned point, dot_product(reshape(xdof(i-1:i+1, j-1:j+1, k-1:k+1)), reshape(coeffs))
  * with the coefficients rebuilt per point (:143) and periodic ghosts (DM_BOUNDARY_PERIODIC,
  * :192). Summation runs over all 27 entries in column-major order, starting from 0. */
-void pbo_stencil_apply27(const int64_t n[3], const double h[3], const double* x, double* y) {
+static void stencil27_mt(const int64_t n[3], const double h[3], const double* x, double* y,
+                         int nt) {
   const int64_t nx = n[0], ny = n[1], nz = n[2];
+  (void)nt; /* points are independent: any thread count gives the same bits */
+#pragma omp parallel for num_threads(nt) schedule(static) collapse(2) if (nt > 1)
   for (int64_t k = 0; k < nz; ++k)
     for (int64_t j = 0; j < ny; ++j)
       for (int64_t i = 0; i < nx; ++i) {
@@ -79,6 +82,9 @@ void pbo_stencil_apply27(const int64_t n[3], const double h[3], const double* x,
             }
         y[IDX(i, j, k, nx, ny)] = s;
       }
+}
+void pbo_stencil_apply27(const int64_t n[3], const double h[3], const double* x, double* y) {
+  stencil27_mt(n, h, x, y, 1);
 }
 
 /* Same operator with the 20 zero terms dropped. For finite x, 0*f adds +-0 to a running sum that
@@ -414,7 +420,7 @@ static void pc_apply(int64_t N, const double* r, double* z, double dinv, int pc,
 static void op_apply(const int64_t n[3], const double h[3], const double* x, double* y, int kind,
                      int nt) {
   if (kind == 1)
-    pbo_stencil_apply27(n, h, x, y);
+    stencil27_mt(n, h, x, y, nt); /* faithful operator; one core = one reference MPI rank */
   else if (kind == 2)
     pbo_lapl(n, x, h, y); /* compact A; P (Jacobi diag) stays the 7-point */
   else

@@ -125,6 +125,21 @@ def test_stencil_fast_equals_faithful():
         assert np.array_equal(O.stencil(x, n, h), O.stencil(x, n, h, faithful=True))
 
 
+def test_faithful_cg_thread_invariant():
+    """CG on the faithful 27-term operator (the bench's CPU variant) has the same iterates on
+    1 and 4 threads, and the same history as the 7-term operator (bit-identical stencils)."""
+    n = (16, 12, 10)
+    h = tuple(1.0 / m for m in n)
+    b = O.stencil(O.fill_random(int(np.prod(n)), 5), n, h)
+    x1, r1, k1, h1 = O.cg_solve(b, n, h, rtol=1e-8, faithful=True, nthreads=1)
+    x4, r4, k4, h4 = O.cg_solve(b, n, h, rtol=1e-8, faithful=True, nthreads=4)
+    x7, r7, k7, h7 = O.cg_solve(b, n, h, rtol=1e-8, faithful=False, nthreads=1)
+    assert (r1, k1) == (r4, k4) == (r7, k7)
+    assert np.array_equal(x1, x7) and np.array_equal(h1, h7)
+    # thread count changes only the order of the OpenMP reductions (dots, sums)
+    assert np.allclose(h1, h4, rtol=1e-12, atol=0) and np.allclose(x1, x4, rtol=1e-10, atol=1e-14)
+
+
 def test_assembled_equals_stencil_interior():
     """P.x (sorted-column AIJ sums) equals A.x up to summation order (src/example.f90:235-261
     prints ||Ax - Px||, ~0)."""
