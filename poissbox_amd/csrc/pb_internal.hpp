@@ -243,6 +243,18 @@ inline int env_int(const char* name, int dflt) {
   const char* s = getenv(name);
   return s ? atoi(s) : dflt;
 }
+// Field-sized device allocations (vectors, KSP work vectors). PB_ALLOC_CONTIGUOUS=1 asks for
+// physically contiguous memory (hipDeviceMallocContiguous): fewer translation misses when a
+// kernel streams many 1 GiB arrays at once (A/B knob for the x-update pass).
+inline hipError_t field_alloc(void** p, size_t bytes) {
+  static const int contiguous = env_int("PB_ALLOC_CONTIGUOUS", 0);
+  if (contiguous) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+  return hipMalloc(p, bytes);
+}
+template <class T>
+inline hipError_t field_alloc(T** p, size_t bytes) {
+  return field_alloc(reinterpret_cast<void**>(p), bytes);
+}
 
 // ---- register-resident line solves (pb_compact_lines.hip) ----
 bool compact_lines_supported(int64_t n);

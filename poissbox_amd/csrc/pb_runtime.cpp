@@ -535,7 +535,7 @@ int pb_vec_create(pb_grid* g, pb_vec** out) {
   pb_vec* v = new pb_vec();
   v->grid = g;
   v->nlocal = g->nlocal;
-  if (hipMalloc(&v->d, (size_t)v->nlocal * sizeof(double)) != hipSuccess) {
+  if (field_alloc(&v->d, (size_t)v->nlocal * sizeof(double)) != hipSuccess) {
     delete v;
     return set_error(PB_ERR_ALLOC, "vector of %lld doubles: out of device memory",
                      (long long)g->nlocal);

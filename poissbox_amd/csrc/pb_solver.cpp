@@ -244,13 +244,13 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
       return rc;
     }
   }
-  if (hipMalloc(&k->r, vb) != hipSuccess || hipMalloc(&k->pb[0], vb) != hipSuccess ||
-      hipMalloc(&k->pb[1], vb) != hipSuccess) {
+  if (field_alloc(&k->r, vb) != hipSuccess || field_alloc(&k->pb[0], vb) != hipSuccess ||
+      field_alloc(&k->pb[1], vb) != hipSuccess) {
     delete k;
     return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
   }
   if (!fused_kind(A->kind) || k->mg) {
-    if (hipMalloc(&k->w, vb) != hipSuccess || hipMalloc(&k->z, vb) != hipSuccess) {
+    if (field_alloc(&k->w, vb) != hipSuccess || field_alloc(&k->z, vb) != hipSuccess) {
       if (k->mg) mg_destroy(k->mg);
       delete k;
       return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
@@ -314,7 +314,7 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   st.defer_x = k->defer_x;
   if (k->defer_x == 4 && !k->pb[2]) {
     const size_t vb = (size_t)g->nlocal * sizeof(double);
-    if (hipMalloc(&k->pb[2], vb) != hipSuccess || hipMalloc(&k->pb[3], vb) != hipSuccess)
+    if (field_alloc(&k->pb[2], vb) != hipSuccess || field_alloc(&k->pb[3], vb) != hipSuccess)
       return set_error(PB_ERR_ALLOC, "CG direction buffers: out of device memory");
   }
   PB_HIP(hipMemcpyAsync(k->d_st, &st, sizeof(st), hipMemcpyHostToDevice, ctx->stream));
