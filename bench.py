@@ -75,7 +75,7 @@ def cpu_baseline(seconds=12.0):
             "variants": cpu_variants(threads)}
 
 
-def cpu_variants(threads, iters=40):
+def cpu_variants(threads, iters=100):
     """SURVEY §8(d)'s other CPU rows, a few seconds each on 128^3: the optimised 7-point CG on
     one core, and the reference-faithful operator (27-term pointwise dot product per point, as
     src/poissbox.f90:128-148 evaluates it) on one core and on all of them. Fixed iteration

@@ -159,8 +159,9 @@ HIST_RTOL = 1e-7  # relative tolerance on every ||z_k|| of the history (reductio
                                     # several x-segments, partial segment, long z-chunks
                                     ((17, 18, 9), 1e-8), ((130, 6, 33), 1e-8),
                                     ((256, 64, 96), 1e-6),
-                                    # planes of 512^2: pass A with 8 rows per wave (TALL)
-                                    ((512, 512, 4), 1e-6)])
+                                    # planes of 512^2: pass A with 8 rows per wave (TALL);
+                                    # 256^2: 4 rows, short z
+                                    ((512, 512, 4), 1e-6), ((256, 256, 6), 1e-6)])
 def test_cg_matches_petsc_semantics(ctx, n, rtol):
     n3 = (n, n, n) if isinstance(n, int) else n
     N = int(np.prod(n3))
