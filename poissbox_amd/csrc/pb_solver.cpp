@@ -95,7 +95,9 @@ static int op_apply_raw(pb_op* op, const double* x, double* y) {
     PB_TRY(halo_exchange(g, x, x + (g->nzl - 1) * g->plane));
     return launch_star7_apply(g, s, x, y, gp, PLANES_ALL);
   }
-  // interior planes overlap the halo exchange; the two boundary planes follow it
+  // interior planes overlap the halo exchange; the two boundary planes follow it (timed as one
+  // apply: interior launch, wait for the exchange, boundary launch)
+  ScopedTimer tm(g->ctx, "stencil");
   PB_TRY(halo_begin(g, x, x + (g->nzl - 1) * g->plane));
   PB_TRY(launch_star7_apply(g, s, x, y, gp, PLANES_INTERIOR));
   PB_TRY(halo_end(g));
@@ -406,6 +408,7 @@ static int enqueue_iteration(pb_ksp* k) {
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
     int nb1 = 0, nb2 = 0;
+    ScopedTimer tm(ctx, "cg_pass_a");  // the whole pass A (both launches and the wait)
     PB_TRY(halo_begin(g, g->bnd_lo, g->bnd_hi));
     PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1));
     PB_TRY(halo_end(g));

@@ -525,9 +525,18 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
   }
 }
 
+// Timer names: a whole-grid launch is "<name>"; the two launches of a split apply (interior
+// planes, then the boundary planes after the halo exchange) are "<name>_interior" and
+// "<name>_boundary", and the caller times the apply as a whole under "<name>" (pb_solver.cpp),
+// so "<name>" always averages complete applies over all owned planes.
+static const char* timer_name(int mode, const char* all, const char* interior,
+                              const char* boundary) {
+  return mode == PLANES_ALL ? all : (mode == PLANES_INTERIOR ? interior : boundary);
+}
+
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
                        const StencilPlanes& gp, int mode) {
-  ScopedTimer tm(g->ctx, "stencil");
+  ScopedTimer tm(g->ctx, timer_name(mode, "stencil", "stencil_interior", "stencil_boundary"));
   // alternate the march direction between applies (the boundary launch of a split apply is one
   // plane per chunk, direction-free, and does not flip it)
   const int rev = g->ctx->zflip;
@@ -920,7 +929,8 @@ int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState
 int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
                      double* p_new, const StencilPlanes& gp, CgState* st, int mode, int part_off,
                      int* nblocks) {
-  ScopedTimer tm(g->ctx, "cg_pass_a");
+  ScopedTimer tm(g->ctx,
+                 timer_name(mode, "cg_pass_a", "cg_pass_a_interior", "cg_pass_a_boundary"));
   return launch_any(g, s, CombineLoad{r, p_old, st, 0.0, 0.0, 0.0}, gp, PassA{p_new}, &st->done,
                     mode, part_off, nblocks);
 }

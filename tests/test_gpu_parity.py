@@ -821,3 +821,38 @@ def test_rccl_code_paths_one_rank_communicator(monkeypatch):
     k.pc_apply(rv, zv)
     assert np.array_equal(zv.get_values(), ref)
     ctx.destroy()
+
+
+def test_split_apply_timers_cover_whole_applies():
+    """On a decomposed grid a matvec / CG pass A is two launches (interior planes, then the
+    boundary planes after the halo exchange). The "stencil" and "cg_pass_a" timers that bench.py
+    prices against all owned DoF count one entry per complete apply; the launches keep their own
+    "_interior" / "_boundary" names."""
+    os.environ["PB_FORCE_COMM"] = "1"
+    try:
+        ctx = pb.Context(0)
+    finally:
+        del os.environ["PB_FORCE_COMM"]
+    n3 = (64, 64, 16)
+    h = tuple(1.0 / m for m in n3)
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    xv, y = pb.Vec(da), pb.Vec(da)
+    xv.set_values(O.fill_random(int(np.prod(n3)), SEED))
+    A.mult(xv, bv)
+    ctx.sync()
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    for _ in range(5):
+        A.mult(xv, y)
+    pb.solve(P, A, x, bv, ["-ksp_rtol", "0", "-ksp_atol", "0", "-ksp_max_it", "6"])
+    ctx.sync()
+    ms, cnt = ctx.timing("stencil")
+    assert cnt == 5 and ms > 0
+    for part in ("stencil_interior", "stencil_boundary"):
+        assert ctx.timing(part)[1] == 5
+    a_ms, a_cnt = ctx.timing("cg_pass_a")
+    ai, bi = ctx.timing("cg_pass_a_interior"), ctx.timing("cg_pass_a_boundary")
+    assert a_cnt == ai[1] == bi[1] >= 6
+    assert a_ms >= ai[0] + bi[0] - 1e-6  # the apply spans both launches
+    ctx.set_timing(False)
