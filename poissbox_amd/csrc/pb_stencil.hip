@@ -103,12 +103,14 @@ struct PassA {
   static constexpr int WGCU = 3;                   // (4-row tiles; 1 with 8 rows)
   static constexpr bool PREFETCH = true;
   double* __restrict__ p_new;
+  int nt_p;  // non-temporal p stores (PB_PASSA_NT, default on; cached stores, which pass B could
+             // re-read from the Infinity Cache, measured within noise: profiles/r01/ab_passa_nt.txt)
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ const double* src(int) const { return nullptr; }
   template <int V>
   __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
                                       double (&)[1][V], double* acc, int nt) const {
-    store_row<V>(p_new, idx, c, nt);
+    store_row<V>(p_new, idx, c, nt && nt_p);
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[0] += w[e] * c[e];
   }
@@ -931,8 +933,9 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
                      int* nblocks) {
   ScopedTimer tm(g->ctx,
                  timer_name(mode, "cg_pass_a", "cg_pass_a_interior", "cg_pass_a_boundary"));
-  return launch_any(g, s, CombineLoad{r, p_old, st, 0.0, 0.0, 0.0}, gp, PassA{p_new}, &st->done,
-                    mode, part_off, nblocks);
+  const int nt_p = env_int("PB_PASSA_NT", 1);  // read per launch (A/B tuning)
+  return launch_any(g, s, CombineLoad{r, p_old, st, 0.0, 0.0, 0.0}, gp, PassA{p_new, nt_p},
+                    &st->done, mode, part_off, nblocks);
 }
 
 int cg_finalize_init(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done) {
