@@ -50,52 +50,116 @@ def global_grid(ngpus, base=512):
     return tuple(n)
 
 
-def cpu_baseline(seconds=12.0):
-    """The oracle (C restatement of PETSc KSPCG + PCJacobi + null space, 7-point, OpenMP) timed
-    on this host on a bounded 256^3 sample."""
-    from oracle import oracle as O
-    threads = int(os.environ.get("PB_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    n = (256, 256, 256)
-    N = 256 ** 3
-    h = (1 / 256,) * 3
-    b = O.stencil(O.fill_random(N, SEED), n, h, nthreads=threads)
-    O.cg_fixed(b, n, h, 1, nthreads=threads)  # warm
-    its, t0 = 0, time.perf_counter()
-    while True:
-        O.cg_fixed(b, n, h, 2, nthreads=threads)
-        its += 2
-        el = time.perf_counter() - t0
-        if el >= seconds or its >= 200:
-            break
-    return {"value": N * its / el, "unit": "DoF-updates/s", "cores": threads, "kind": "port",
-            "iter_per_s": its / el,
-            "sample": f"256^3 grid, {its} CG iterations (+setup) of oracle/pb_oracle.c "
-                      f"(PETSc KSPCG+PCJacobi+MatNullSpace sequence, 7-point, OpenMP {threads} "
-                      f"threads) in {el:.1f} s on the GPU box host",
-            "variants": cpu_variants(threads)}
+def host_info():
+    """nproc / lscpu of the host the CPU baseline runs on (record both), and the
+    cores this process may use: its CPU affinity, the cgroup quota and OMP_NUM_THREADS (the GPU
+    box exports its per-GPU CPU share there) -- the machine's total is usually larger."""
+    import subprocess
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except Exception:
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = -(-int(q) // int(per))
+    except Exception:
+        pass
+    info["cgroup_cpus"] = quota
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    for cmd, key in ((["nproc"], "nproc"), (["lscpu"], "lscpu")):
+        try:
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=10).stdout
+        except Exception:
+            out = ""
+        if key == "nproc":
+            info["nproc"] = int(out.strip()) if out.strip().isdigit() else None
+        else:
+            keep = ("Model name", "CPU(s)", "Thread(s) per core", "Core(s) per socket",
+                    "Socket(s)", "NUMA node(s)", "L3 cache", "CPU max MHz")
+            info["lscpu"] = {k.strip(): v.strip() for k, v in
+                             (l.split(":", 1) for l in out.splitlines() if ":" in l)
+                             if k.strip() in keep}
+    usable = [info["affinity"] or 1]
+    if quota:
+        usable.append(quota)
+    if (info["omp_num_threads"] or "").isdigit():
+        usable.append(int(info["omp_num_threads"]))
+    info["usable_cores"] = max(1, min(usable))
+    try:
+        pv = subprocess.run(["pkg-config", "--modversion", "petsc"], capture_output=True,
+                            text=True, timeout=10)
+        info["petsc"] = pv.stdout.strip() if pv.returncode == 0 else "absent (pkg-config petsc fails)"
+    except Exception:
+        info["petsc"] = "absent (no pkg-config)"
+    return info
 
 
-def cpu_variants(threads, iters=100):
-    """SURVEY §8(d)'s other CPU rows, a few seconds each on 128^3: the optimised 7-point CG on
-    one core, and the reference-faithful operator (27-term pointwise dot product per point, as
-    src/poissbox.f90:128-148 evaluates it) on one core and on all of them. Fixed iteration
-    count (rtol = atol = 0), the same PETSc scalar sequence."""
+def _cpu_row(O, n, rtol, max_it, threads):
+    """One CPU-baseline row: the oracle's PETSc-sequence CG + Jacobi (constant null space) on the
+    §8(d) synthetic system, to convergence (rtol > 0) or for a fixed max_it iterations."""
+    N = n ** 3
+    h = (1.0 / n,) * 3
+    b = O.stencil(O.fill_random(N, SEED), (n, n, n), h, nthreads=threads)
+    t0 = time.perf_counter()
+    x, reason, its, hist = O.cg_solve(b, (n, n, n), h, rtol=rtol, atol=0.0 if rtol == 0 else 1e-50,
+                                      dtol=1e300 if rtol == 0 else 1e5, max_it=max_it,
+                                      nthreads=threads)
+    el = time.perf_counter() - t0
+    r = O.stencil(x, (n, n, n), h, nthreads=threads) - b
+    row = {"grid": f"{n}^3", "cores": threads, "rtol": rtol, "its": its,
+           "reason": reason, "seconds": el, "iter_per_s": its / el,
+           "dofs_updates_per_s": N * its / el,
+           "GBps_at_80B": 80 * N * its / el / 1e9, "GBps_at_176B": 176 * N * its / el / 1e9,
+           "true_residual": float(np.linalg.norm(r)),
+           "true_residual_rel": float(np.linalg.norm(r) / np.linalg.norm(b)),
+           "rnorm_last": float(hist[-1])}
+    del b, x, r
+    return row
+
+
+def cpu_baseline(mode="full"):
+    """SURVEY.md §8(d) / BASELINE.md §4 CPU baseline, timed on this host: the oracle's C
+    restatement of PETSc KSPCG + PCJacobi + MatNullSpace (7-point, OpenMP) -- PETSc itself is
+    absent from the image -- on all usable cores and on 1 core: 64^3 to rtol 1e-5 and 1e-10,
+    256^3 to rtol 1e-10, 512^3 for a fixed 50 iterations (the headline `value`, the same
+    workload as the GPU line). mode "quick" keeps only the 512^3 rows (10 iterations on 1 core)."""
     from oracle import oracle as O
-    n = (128, 128, 128)
-    N = 128 ** 3
-    h = (1 / 128,) * 3
-    b = O.stencil(O.fill_random(N, SEED), n, h, nthreads=threads)
-    out = []
-    for faithful, nt in ((False, 1), (True, 1), (True, threads)):
-        k = iters if not faithful or nt > 1 else iters // 4
-        t0 = time.perf_counter()
-        _, _, its, _ = O.cg_solve(b, n, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=k,
-                                  faithful=faithful, nthreads=nt)
-        el = time.perf_counter() - t0
-        out.append({"op": "faithful 27-term" if faithful else "7-point", "cores": nt,
-                    "value": N * its / el, "unit": "DoF-updates/s",
-                    "sample": f"128^3 grid, {its} CG + Jacobi iterations (+setup) in {el:.2f} s"})
-    return out
+    info = host_info()
+    T = int(os.environ.get("PB_CPU_THREADS", info["usable_cores"]))
+    budget = float(os.environ.get("PB_CPU_BUDGET_S", "300"))
+    rows, skipped = [], []
+    # headline row first; then the rest, each skipped if its predicted time (from the measured
+    # rate of the same core count) would overrun the budget
+    plan = [(512, 0.0, 50, T)]
+    if mode == "full":
+        plan += [(64, 1e-5, 10000, T), (64, 1e-10, 10000, T), (64, 1e-5, 10000, 1),
+                 (64, 1e-10, 10000, 1), (256, 1e-10, 10000, T), (512, 0.0, 50, 1),
+                 (256, 1e-10, 10000, 1)]
+    else:
+        plan += [(512, 0.0, 10, 1)]
+    t_start = time.perf_counter()
+    for n, rtol, max_it, t in plan:
+        rate = [r["dofs_updates_per_s"] for r in rows if r["cores"] == t]
+        est_its = max_it if rtol == 0 else 2.8 * n  # ~2.8 n its to rtol 1e-10 (BASELINE.md §2)
+        est = n ** 3 * est_its / min(rate) if rate else 0.0
+        if time.perf_counter() - t_start + est > budget:
+            skipped.append(f"{n}^3 rtol={rtol} cores={t} (predicted {est:.0f} s over the "
+                           f"{budget:.0f} s budget)")
+            continue
+        rows.append(_cpu_row(O, n, rtol, max_it, t))
+        print(f"cpu baseline row: {json.dumps(rows[-1])}", file=sys.stderr, flush=True)
+    head = [r for r in rows if r["grid"] == "512^3" and r["cores"] == T][0]
+    return {"value": head["dofs_updates_per_s"], "unit": "DoF-updates/s", "cores": T,
+            "kind": "port", "iter_per_s": head["iter_per_s"],
+            "sample": f"512^3 grid, {head['its']} CG + Jacobi iterations (fixed count) of "
+                      f"oracle/pb_oracle.c (PETSc KSPCG+PCJacobi+MatNullSpace sequence, 7-point, "
+                      f"OpenMP {T} threads) in {head['seconds']:.1f} s on the GPU box host; "
+                      f"rows: 64^3 and 256^3 to convergence and 512^3 x 50 its, on {T} cores "
+                      f"and on 1",
+            "host": info, "rows": rows, "skipped_rows": skipped, "variants": cpu_variants(T)}
 
 
 def main():
@@ -108,6 +172,8 @@ def main():
     ap.add_argument("--grid", default=None,
                     help="nx,ny,nz global grid override (diagnostics; default: weak scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline", choices=("full", "quick", "none"), default="full",
+                    help="SURVEY §8(d) CPU rows: full (default), quick (512^3 only) or none")
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                     help="multi-rank transport: RCCL (default) or the gloo host transport "
                          "(lets several ranks share one GPU for testing)")
@@ -282,8 +348,8 @@ def main():
                         kv["traffic"] = tr[key][role]["bytes_per_launch"]
             except Exception:
                 pass
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline()
+        if world == 1 and not args.no_cpu_baseline and args.cpu_baseline != "none":
+            out["cpu_baseline"] = cpu_baseline(args.cpu_baseline)
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     for o in (ksp, y, xt, x, b, A, P):
         o.destroy()

@@ -137,7 +137,8 @@ enum pb_pc_type { PB_PC_NONE = 0, PB_PC_JACOBI = 1, PB_PC_SOR = 2, PB_PC_MG = 3 
 enum pb_ksp_reason {
   PB_KSP_ITERATING = 0, PB_KSP_CONVERGED_RTOL = 2, PB_KSP_CONVERGED_ATOL = 3,
   PB_KSP_CONVERGED_ITS = 4, PB_KSP_DIVERGED_ITS = -3, PB_KSP_DIVERGED_DTOL = -4,
-  PB_KSP_DIVERGED_NANORINF = -9, PB_KSP_DIVERGED_INDEFINITE_MAT = -10
+  PB_KSP_DIVERGED_INDEFINITE_PC = -8, PB_KSP_DIVERGED_NANORINF = -9,
+  PB_KSP_DIVERGED_INDEFINITE_MAT = -10
 };
 typedef struct {
   double rtol;       /* -ksp_rtol   (PETSc default 1e-5)  */
@@ -159,6 +160,8 @@ typedef struct {
   int64_t its;
   double rnorm;      /* last ||z||_2 (KSP_NORM_PRECONDITIONED) */
   double rnorm0;
+  int64_t nhist;     /* residual norms logged (≙ KSPGetResidualHistory's count): its + 1, or its
+                        after a breakdown exit (beta = 0, indefinite PC / matrix) */
 } pb_ksp_result;
 int pb_ksp_opts_default(pb_ksp_opts* opts);
 /* Parses PETSc-style options (-ksp_type, -pc_type, -ksp_rtol, -ksp_atol, -ksp_divtol,
@@ -171,8 +174,8 @@ int pb_ksp_opts_parse(pb_ksp_opts* opts, int argc, const char* const* argv);
 
 /* KSPCreate + KSPSetOperators(ksp, A, P) + options. P supplies the Jacobi diagonal. */
 int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** ksp);
-/* KSPSolve(ksp, b, x): x0 = 0 (guess_zero). history (optional, may be NULL): ||z_k||, k=0..its,
- * capacity history_cap entries. */
+/* KSPSolve(ksp, b, x): x0 = 0 (guess_zero). history (optional, may be NULL): the res->nhist
+ * logged norms ||z_k|| (k = 0 .. nhist-1), at most history_cap entries written. */
 int pb_ksp_solve(pb_ksp* ksp, const pb_vec* b, pb_vec* x, pb_ksp_result* res, double* history,
                  int64_t history_cap);
 /* Split form used by benchmarks: setup (r = b, z, ||z0||), then exactly `iters` iterations

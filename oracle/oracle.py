@@ -104,17 +104,18 @@ def cg_solve(b, n, h, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi"
              nullspace=True, faithful=False, nthreads=1, op="star7", mg_levels=0,
              mg_coarse_its=8, omega=1.0, nranks=1):
     """KSPSolve(-ksp_type cg -pc_type jacobi|none|sor|mg) with the constant null space.
-    Returns (x, reason, its, history[:its+1])."""
+    Returns (x, reason, its, history): the norms KSPLogResidualHistory logged (its + 1 of them,
+    its after a breakdown exit)."""
     b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1)
     x = np.empty_like(b)
     hist = np.zeros(int(max_it) + 2)
-    its = C.c_int64(0)
+    its, nlog = C.c_int64(0), C.c_int64(0)
     kind = 2 if op == "compact" else (1 if faithful else 0)
     o = KspOpts(rtol, atol, dtol, max_it, PC_CODES[pc], int(nullspace), kind, nthreads,
                 mg_levels, mg_coarse_its, omega, nranks)
-    reason = lib().pbo_cg_solve(_n3(n), _h3(h), C.byref(o), _p(b), _p(x), _p(hist), C.byref(its))
-    k = its.value
-    return x, reason, k, hist[:k + 1].copy()
+    reason = lib().pbo_cg_solve(_n3(n), _h3(h), C.byref(o), _p(b), _p(x), _p(hist), C.byref(its),
+                                C.byref(nlog))
+    return x, reason, its.value, hist[:nlog.value].copy()
 
 
 def mg_plan_levels(n, nranks=1, levels=0):

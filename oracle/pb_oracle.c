@@ -203,7 +203,7 @@ void pbo_fill_random(int64_t count, uint64_t seed, int64_t g0, double* x) {
 enum {
   KSP_CONVERGED_ITERATING = 0, KSP_CONVERGED_RTOL = 2, KSP_CONVERGED_ATOL = 3,
   KSP_DIVERGED_ITS = -3, KSP_DIVERGED_DTOL = -4, KSP_DIVERGED_NANORINF = -9,
-  KSP_DIVERGED_INDEFINITE_MAT = -10
+  KSP_DIVERGED_INDEFINITE_PC = -8, KSP_DIVERGED_INDEFINITE_MAT = -10
 };
 
 static double vdot(int64_t N, const double* a, const double* b, int nt) {
@@ -445,7 +445,7 @@ static void pc_apply_any(const int64_t n[3], const double h[3], const pbo_ksp_op
 }
 
 int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, const double* b,
-                 double* x, double* history, int64_t* its_out) {
+                 double* x, double* history, int64_t* its_out, int64_t* nlog_out) {
   const int64_t N = n[0] * n[1] * n[2];
   const int nt = o->nthreads > 0 ? o->nthreads : 1;
   double* R = (double*)malloc(sizeof(double) * N);
@@ -454,7 +454,7 @@ int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, c
   double* W = (double*)malloc(sizeof(double) * N);
   const double dinv = 1.0 / pbo_diag(h);
   int reason = KSP_CONVERGED_ITERATING;
-  int64_t its = 0;
+  int64_t its = 0, nlog = 0; /* nlog: entries KSPLogResidualHistory wrote */
   double dp, beta, betaold = 0.0, dpi = 0.0, dpiold, ttol, rnorm0;
 
   memset(x, 0, sizeof(double) * N); /* KSPSolve: guess_zero => X = 0 */
@@ -462,17 +462,21 @@ int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, c
   pc_apply_any(n, h, o, R, Z, dinv, nt);
   dp = sqrt(vdot(N, Z, Z, nt)); /* KSP_NORM_PRECONDITIONED */
   history[0] = dp;
+  nlog = 1;
   /* KSPConvergedDefault at n = 0 */
   if (dp != dp || isinf(dp)) { reason = KSP_DIVERGED_NANORINF; goto done; }
   ttol = fmax(o->rtol * dp, o->atol);
   rnorm0 = dp;
   if (dp <= ttol) { reason = dp < o->atol ? KSP_CONVERGED_ATOL : KSP_CONVERGED_RTOL; goto done; }
   beta = vdot(N, Z, R, nt);
+  if (!isfinite(beta)) { reason = KSP_DIVERGED_NANORINF; goto done; } /* KSPCheckDot */
 
   int64_t i = 0;
   do {
     its = i + 1;
     if (beta == 0.0) { reason = KSP_CONVERGED_ATOL; break; }
+    /* PETSc KSPSolve_CG (real scalars): z'r changed sign -> the PC is indefinite */
+    if (i > 0 && beta * betaold < 0.0) { reason = KSP_DIVERGED_INDEFINITE_PC; break; }
     if (i == 0) {
       memcpy(P, Z, sizeof(double) * N);
     } else {
@@ -483,6 +487,7 @@ int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, c
     dpiold = dpi;
     op_apply(n, h, P, W, o->op_kind, nt); /* KSP_MatMult -> mfmult */
     dpi = vdot(N, P, W, nt);
+    if (!isfinite(dpi)) { reason = KSP_DIVERGED_NANORINF; break; } /* KSPCheckDot */
     betaold = beta;
     if (dpi == 0.0 || (i > 0 && ((dpi > 0) - (dpi < 0)) * ((dpiold > 0) - (dpiold < 0)) < 0)) {
       reason = KSP_DIVERGED_INDEFINITE_MAT;
@@ -497,15 +502,18 @@ int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, c
     pc_apply_any(n, h, o, R, Z, dinv, nt);
     dp = sqrt(vdot(N, Z, Z, nt));
     history[i + 1] = dp;
+    nlog = i + 2;
     if (dp != dp || isinf(dp)) { reason = KSP_DIVERGED_NANORINF; break; }
     if (dp <= ttol) { reason = dp < o->atol ? KSP_CONVERGED_ATOL : KSP_CONVERGED_RTOL; break; }
     if (dp >= o->dtol * rnorm0) { reason = KSP_DIVERGED_DTOL; break; }
     beta = vdot(N, Z, R, nt);
+    if (!isfinite(beta)) { reason = KSP_DIVERGED_NANORINF; break; } /* KSPCheckDot */
     i++;
   } while (i < o->max_it);
   if (i >= o->max_it) reason = KSP_DIVERGED_ITS;
 done:
   *its_out = its;
+  if (nlog_out) *nlog_out = nlog;
   free(R); free(Z); free(P); free(W);
   return reason;
 }

@@ -68,9 +68,11 @@ int pbo_mg_plan_levels(const int64_t n[3], int nranks, int levels_req);
 void pbo_mg_apply(const int64_t n[3], const double h[3], int pc_type, int levels, int coarse_its,
                   double omega, int nranks, const double* r, double* z);
 
-/* Returns PETSc KSPConvergedReason; history[0..its] = ||z_k||_2 (len max_it+1). */
+/* Returns PETSc KSPConvergedReason; history[0..nlog) = ||z_k||_2 (capacity max_it+1): the
+ * entries KSPLogResidualHistory wrote -- its+1 normally, its after a breakdown exit (beta = 0,
+ * indefinite PC / matrix, non-finite p.w), which leaves the last iteration without a norm. */
 int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* opts, const double* b,
-                 double* x, double* history, int64_t* its);
+                 double* x, double* history, int64_t* its, int64_t* nlog);
 /* Fixed number of iterations (no stopping test) -- the CPU baseline workload. Returns dp. */
 double pbo_cg_fixed(const int64_t n[3], const double h[3], int64_t iters, int nthreads,
                     const double* b, double* x, double* work /* 4*N */);

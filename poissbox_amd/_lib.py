@@ -32,7 +32,8 @@ class KspOpts(C.Structure):
 
 
 class KspResult(C.Structure):
-    _fields_ = [("reason", C.c_int), ("its", c_i64), ("rnorm", c_d), ("rnorm0", c_d)]
+    _fields_ = [("reason", C.c_int), ("its", c_i64), ("rnorm", c_d), ("rnorm0", c_d),
+                ("nhist", c_i64)]
 
 
 SENDRECV_FN = C.CFUNCTYPE(C.c_int, c_p, P_d, P_d, P_d, P_d, c_i64)

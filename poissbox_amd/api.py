@@ -25,7 +25,8 @@ PC_NONE, PC_JACOBI, PC_SOR, PC_MG = 0, 1, 2, 3
 
 REASONS = {0: "CONVERGED_ITERATING", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",
            4: "CONVERGED_ITS", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",
-           -9: "DIVERGED_NANORINF", -10: "DIVERGED_INDEFINITE_MAT"}
+           -8: "DIVERGED_INDEFINITE_PC", -9: "DIVERGED_NANORINF",
+           -10: "DIVERGED_INDEFINITE_MAT"}
 
 
 def _i64_3(v):
@@ -286,12 +287,13 @@ class KSP:
         self.h = h
 
     def solve(self, b, x):
-        """Returns (reason, its, history[:its+1])."""
+        """Returns (reason, its, history): the res.nhist logged norms (its + 1 of them, its
+        after a breakdown exit)."""
         res = L.KspResult()
         hist = np.zeros(int(self.opts.max_it) + 1)
         L.call("pb_ksp_solve", self.h, b.h, x.h, C.byref(res), _dptr(hist), hist.size)
         self.result = res
-        return res.reason, res.its, hist[: res.its + 1].copy()
+        return res.reason, res.its, hist[: res.nhist].copy()
 
     def begin(self, b, x):
         L.call("pb_ksp_begin", self.h, b.h, x.h)
@@ -304,7 +306,7 @@ class KSP:
         hist = np.zeros(int(self.opts.max_it) + 1)
         L.call("pb_ksp_end", self.h, C.byref(res), _dptr(hist), hist.size)
         self.result = res
-        return res.reason, res.its, hist[: res.its + 1].copy()
+        return res.reason, res.its, hist[: res.nhist].copy()
 
     def pc_apply(self, r, z):
         """PCApply: z = M^-1 r (no null-space removal)."""

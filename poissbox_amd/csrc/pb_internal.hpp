@@ -220,6 +220,8 @@ struct CgState {
   double pa[3];
   double rtol, atol, dtol, dinv, ntot;
   int64_t it, its, max_it, nhist, pend_iter, pend_count;
+  int64_t nlog;  // history entries logged (PETSc KSPLogResidualHistory): its + 1, or its after a
+                 // breakdown exit (beta = 0, indefinite PC / matrix) that skips the last norm
   int reason, done, pc, nullspace, defer_x;
 };
 int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p, CgState* st,

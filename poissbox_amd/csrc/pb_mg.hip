@@ -581,7 +581,10 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
                        (long long)g->n[0], (long long)g->n[1], (long long)g->n[2]);
   if (g->nlocal >= ((int64_t)1 << 32))
     return set_error(PB_ERR_UNSUPPORTED, "multigrid: more than 2^32 points on one GPU");
-  if (!(omega > 0.0 && omega < 2.0)) return set_error(PB_ERR_ARG, "SOR omega must be in (0, 2)");
+  // PETSc PCSORSetOmega rejects omega outside (0, 2); PB_SOR_OMEGA_ANY=1 (diagnostics) accepts
+  // it -- an indefinite SOR preconditioner, e.g. to exercise KSP_DIVERGED_INDEFINITE_PC
+  if (!(omega > 0.0 && omega < 2.0) && !env_int("PB_SOR_OMEGA_ANY", 0))
+    return set_error(PB_ERR_ARG, "SOR omega must be in (0, 2)");
   Mg* mg = new Mg();
   mg->ctx = ctx;
   mg->omega = omega;

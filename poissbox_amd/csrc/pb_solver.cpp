@@ -464,6 +464,7 @@ static const char* reason_name(int r) {
     case PB_KSP_DIVERGED_DTOL: return "DIVERGED_DTOL";
     case PB_KSP_DIVERGED_NANORINF: return "DIVERGED_NANORINF";
     case PB_KSP_DIVERGED_INDEFINITE_MAT: return "DIVERGED_INDEFINITE_MAT";
+    case PB_KSP_DIVERGED_INDEFINITE_PC: return "DIVERGED_INDEFINITE_PC";
     default: return "CONVERGED_ITERATING";
   }
 }
@@ -487,8 +488,10 @@ int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
     res->its = st.its;
     res->rnorm = st.dp;
     res->rnorm0 = st.rnorm0;
+    res->nhist = std::min<int64_t>(st.nlog, k->nhist);
   }
-  const int64_t nh = std::min<int64_t>(st.its + 1, k->nhist);
+  // only the norms the device logged (a breakdown exit leaves the last iteration without one)
+  const int64_t nh = std::min<int64_t>(st.nlog, k->nhist);
   std::vector<double> hist((size_t)std::max<int64_t>(nh, 1));
   if (nh > 0) {
     PB_HIP(hipMemcpyAsync(hist.data(), k->d_hist, (size_t)nh * sizeof(double), hipMemcpyDeviceToHost,

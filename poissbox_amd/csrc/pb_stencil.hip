@@ -777,6 +777,7 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
     st->reason = 0;
     st->done = 0;
     if (st->nhist > 0) hist[0] = dp;
+    st->nlog = st->nhist > 0 ? 1 : 0;
     if (!finite(dp)) {
       st->reason = PB_KSP_DIVERGED_NANORINF;
       st->done = 1;
@@ -850,7 +851,10 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
     }
     st->dp = dp;
     st->its = i + 1;
-    if (i + 1 < st->nhist) hist[i + 1] = dp;
+    if (i + 1 < st->nhist) {
+      hist[i + 1] = dp;
+      st->nlog = i + 2;
+    }
     if (!finite(dp)) {
       st->reason = PB_KSP_DIVERGED_NANORINF;
       st->done = 1;
@@ -873,6 +877,12 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
       } else if (zr == 0.0) {
         st->its = st->it + 1;
         st->reason = PB_KSP_CONVERGED_ATOL;
+        st->done = 1;
+      } else if (zr * st->betaold < 0.0) {
+        // PETSc KSPSolve_CG, top of iteration i+1 (real scalars): beta*betaold < 0 -> the
+        // preconditioner is indefinite (betaold = the beta iteration i used, stage 1)
+        st->its = st->it + 1;
+        st->reason = PB_KSP_DIVERGED_INDEFINITE_PC;
         st->done = 1;
       }
     }

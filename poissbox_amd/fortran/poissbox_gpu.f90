@@ -53,6 +53,7 @@ module poissbox_gpu
      integer(c_int) :: reason
      integer(c_int64_t) :: its
      real(c_double) :: rnorm, rnorm0
+     integer(c_int64_t) :: nhist  ! residual norms logged (its + 1; its after a breakdown exit)
   end type pb_ksp_result
 
   integer(c_int), parameter, public :: PB_OP_STAR7 = 0, PB_OP_COMPACT = 1, PB_OP_ASSEMBLED27 = 2
@@ -292,13 +293,19 @@ contains
     real(pb_dp), intent(out), optional :: rnorm
     type(pb_ksp_opts) :: o
     type(pb_ksp_result) :: res
-    integer :: nargs, i, l
-    character(len=256), allocatable, target :: args(:)
+    integer :: nargs, i, l, lmax
+    character(len=:), allocatable, target :: args(:)
     type(c_ptr), allocatable :: argv(:)
 
     ierr = c_pb_ksp_opts_default(o)
     nargs = command_argument_count()
-    allocate(args(max(nargs, 1)), argv(max(nargs, 1)))
+    lmax = 1  ! buffers sized from the longest argument (+1 for the C terminator)
+    do i = 1, nargs
+       call get_command_argument(i, length=l)
+       lmax = max(lmax, l + 1)
+    end do
+    allocate(character(len=lmax) :: args(max(nargs, 1)))
+    allocate(argv(max(nargs, 1)))
     do i = 1, nargs
        call get_command_argument(i, args(i), l)
        args(i)(l + 1:l + 1) = c_null_char
@@ -336,10 +343,16 @@ contains
     integer, intent(out) :: ierr
     type(tMat) :: op
     real(c_double), dimension(3) :: d
+    integer :: l
     d = grid_deltas
     ierr = c_pb_op_create(da%h, PB_OP_STAR7, d, op%h)
     if (ierr /= 0) return
     ierr = c_pb_op_apply(op%h, x%h, b%h)
+    call check(ierr, "compute_lapl_pointwise")
+    if (ierr /= 0) then  ! keep the apply's error; still release the operator
+       l = c_pb_op_destroy(op%h)
+       return
+    end if
     ierr = c_pb_op_destroy(op%h)
   end subroutine compute_lapl_pointwise
 

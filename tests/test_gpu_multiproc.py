@@ -9,6 +9,7 @@ import sys
 import numpy as np
 import pytest
 
+from parity_bars import check_history, check_x
 from test_dist_cpu import REPO, SEED, _run
 
 pytestmark = pytest.mark.gpu
@@ -44,8 +45,8 @@ def test_multiprocess_cg_on_one_gpu(world):
     for k0, nk, bl, reason, its, hist, xs in _run(world, _gpu_rank):
         assert np.array_equal(bl, bz[k0:k0 + nk].reshape(-1))      # bit-exact distributed A x
         assert (reason, its) == (ro, itso)
-        assert np.max(np.abs(hist - ho) / ho) < 1e-7
-        assert np.max(np.abs(xs - xz[k0:k0 + nk].reshape(-1))) <= 1e-6 * np.max(np.abs(xo))
+        check_history(hist, ho)
+        check_x(xs, xz[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
 
 
 def _gpu_rank_compact(rank, world, tr):

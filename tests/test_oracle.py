@@ -207,3 +207,19 @@ def test_cg_mg_iterations_grid_independent():
         assert np.linalg.norm(r) <= 1e-8 * np.linalg.norm(b)
         its[n] = k
     assert max(its.values()) <= 16 and its[64] <= its[16] + 3, its
+
+
+@pytest.mark.parametrize("pc,omega,n3", [("sor", 2.5, (16, 12, 8)), ("mg", 2.2, (16, 16, 16))])
+def test_cg_indefinite_pc_exit(pc, omega, n3):
+    """PETSc KSPSolve_CG's beta*betaold < 0 test (real scalars): an SOR relaxation factor outside
+    (0, 2) makes the preconditioner indefinite, z.r changes sign and the solve stops with
+    KSP_DIVERGED_INDEFINITE_PC (-8) at the top of that iteration -- its = i + 1 with only the
+    norms 0..i logged (no norm for the iteration that never ran)."""
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(int(np.prod(n3)), 20231015), n3, h)
+    _, reason, its, hist = O.cg_solve(b, n3, h, rtol=1e-10, pc=pc, omega=omega)
+    assert reason == -8
+    assert 1 < its < 10 and len(hist) == its
+    # a definite factor (omega = 1) converges normally and logs its + 1 norms
+    _, reason, its, hist = O.cg_solve(b, n3, h, rtol=1e-10, pc=pc)
+    assert reason == 2 and len(hist) == its + 1
