@@ -120,6 +120,29 @@ def _cpu_row(O, n, rtol, max_it, threads):
     return row
 
 
+def cpu_variants(threads, iters=100):
+    """SURVEY §8(d)'s other CPU rows, a few seconds each on 128^3: the optimised 7-point CG on
+    one core, and the reference-faithful operator (27-term pointwise dot product per point, as
+    src/poissbox.f90:128-148 evaluates it) on one core and on all of them. Fixed iteration
+    count (rtol = atol = 0), the same PETSc scalar sequence."""
+    from oracle import oracle as O
+    n = (128, 128, 128)
+    N = 128 ** 3
+    h = (1 / 128,) * 3
+    b = O.stencil(O.fill_random(N, SEED), n, h, nthreads=threads)
+    out = []
+    for faithful, nt in ((False, 1), (True, 1), (True, threads)):
+        k = iters if not faithful or nt > 1 else iters // 4
+        t0 = time.perf_counter()
+        _, _, its, _ = O.cg_solve(b, n, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=k,
+                                  faithful=faithful, nthreads=nt)
+        el = time.perf_counter() - t0
+        out.append({"op": "faithful 27-term" if faithful else "7-point", "cores": nt,
+                    "value": N * its / el, "unit": "DoF-updates/s",
+                    "sample": f"128^3 grid, {its} CG + Jacobi iterations (+setup) in {el:.2f} s"})
+    return out
+
+
 def cpu_baseline(mode="full"):
     """SURVEY.md §8(d) / BASELINE.md §4 CPU baseline, timed on this host: the oracle's C
     restatement of PETSc KSPCG + PCJacobi + MatNullSpace (7-point, OpenMP) -- PETSc itself is
