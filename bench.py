@@ -4,6 +4,8 @@ fp64 per GPU -- BASELINE.json metric "CG iter/s and DoF-updates/s at 512^3; achi
 A step = one CG iteration over every DoF of the grid (one pass of the KSPSolve hot path).
 Weak scaling: every GPU owns a 512^3 z-slab worth of DoF; the global grid doubles z, y, x in turn
 (N=1: 512^3, N=2: 512x512x1024, N=4: 512x1024x1024, N=8: 1024^3 = SURVEY config 4).
+Strong scaling (--scaling strong [--base 512|1024]): the base^3 grid split over all GPUs.
+N > 1 lines carry per-rank halo / allreduce times (per_rank_comm).
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
 (one rank per GPU; RCCL unique id broadcast over the gloo process group).
 Prints ONE JSON line on rank 0.
@@ -194,6 +196,9 @@ def main():
     ap.add_argument("--matvecs", type=int, default=20)
     ap.add_argument("--grid", default=None,
                     help="nx,ny,nz global grid override (diagnostics; default: weak scaling)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak (default): base^3 DoF per GPU; strong: the base^3 grid split "
+                         "over all GPUs (e.g. --base 512 or 1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline", choices=("full", "quick", "none"), default="full",
                     help="SURVEY §8(d) CPU rows: full (default), quick (512^3 only) or none")
@@ -229,7 +234,12 @@ def main():
         import torch
         device = local_rank % max(1, torch.cuda.device_count())
 
-    n = tuple(int(v) for v in args.grid.split(",")) if args.grid else global_grid(world, args.base)
+    if args.grid:
+        n = tuple(int(v) for v in args.grid.split(","))
+    elif args.scaling == "strong":
+        n = (args.base,) * 3
+    else:
+        n = global_grid(world, args.base)
     ctx = pb.Context(device, rank, world, uid)
     if dist and args.transport == "host":
         tr = GlooTransport(dist)
@@ -279,13 +289,24 @@ def main():
             defer = d_
             ms_b, cnt_b = ctx.timing(nm)
     ms_be, cnt_be = ctx.timing("cg_pass_b_even")
+    # per-rank communication in the diagnostic iterations: the halo exchange on the comm stream
+    # (overlapped with pass A's interior planes), the two scalar allreduces per iteration, and
+    # pass A including its wait for the halo
+    comm = {"rank": rank, "iterations": diag_steps}
+    for nm in ("halo_comm", "allreduce", "cg_pass_a", "halo"):
+        ms_, cnt_ = ctx.timing(nm)
+        comm[f"{nm}_ms_per_iter"] = ms_ / diag_steps
+        comm[f"{nm}_calls"] = cnt_
     ctx.set_timing(False)
     reason, its, hist = ksp.end()
+    per_rank = [comm]
     if dist:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, comm)
 
     # standalone matvec timing (north-star target kernel), outside the timed CG region
     y = pb.Vec(da)
@@ -318,7 +339,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if (args.scaling == "strong" and not args.grid) else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (x_true = SplitMix64 U[-1,1], b = A x_true, x0 = 0)",
@@ -355,6 +376,7 @@ def main():
                                  "bytes_per_dof": MATVEC_BYTES},
             },
             "cg_x_update_every": defer,
+            "per_rank_comm": per_rank if world > 1 else None,
             "ksp_state": {"reason": pb.REASONS.get(reason, reason), "its": its,
                           "rnorm0": float(hist[0]), "rnorm_last": float(hist[-1])},
         }

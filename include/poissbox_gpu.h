@@ -73,6 +73,12 @@ int pb_ctx_set_host_alltoallv(pb_ctx* ctx, pb_alltoallv_fn alltoallv, void* user
 int pb_ctx_get_rank(const pb_ctx* ctx, int* rank, int* nranks);
 int pb_ctx_sync(pb_ctx* ctx);  /* stream synchronize (≙ MPI_Barrier for device work) */
 int pb_ctx_barrier(pb_ctx* ctx); /* synchronize + all ranks rendezvous */
+/* Failure handling on multi-rank contexts (the reference's MPI calls would hang or abort): every
+ * host wait is bounded by PB_COMM_TIMEOUT_MS (default 180000) and checks RCCL's asynchronous
+ * error; a timeout, an RCCL error or a failing host-transport callback aborts the communicator
+ * (ncclCommAbort) and returns PB_ERR_COMM, and every later communicating call on the context
+ * returns PB_ERR_COMM at once. *failed = 1 after such a failure. */
+int pb_ctx_comm_status(const pb_ctx* ctx, int* failed);
 int pb_ctx_destroy(pb_ctx* ctx);
 /* Per-kernel timing with HIP events on the context's stream (off by default). */
 int pb_ctx_set_timing(pb_ctx* ctx, int enable);

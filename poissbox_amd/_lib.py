@@ -51,6 +51,7 @@ _SIGS = {
     "pb_ctx_get_rank": [c_p, C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pb_ctx_sync": [c_p],
     "pb_ctx_barrier": [c_p],
+    "pb_ctx_comm_status": [c_p, C.POINTER(C.c_int)],
     "pb_ctx_destroy": [c_p],
     "pb_ctx_set_timing": [c_p, C.c_int],
     "pb_ctx_get_timing": [c_p, C.c_char_p, P_d, P_i64],

@@ -126,6 +126,13 @@ class Context:
     def barrier(self):
         L.call("pb_ctx_barrier", self.h)
 
+    @property
+    def comm_failed(self):
+        """True after a communication failure (timeout, RCCL error, failing host callback)."""
+        v = C.c_int(0)
+        L.call("pb_ctx_comm_status", self.h, C.byref(v))
+        return bool(v.value)
+
     def set_timing(self, on=True):
         L.call("pb_ctx_set_timing", self.h, int(bool(on)))
 

@@ -168,7 +168,7 @@ static int alpha_factor(pb_ctx* ctx, int64_t n, double alpha, AlphaFactor* out) 
   // hipMemcpy from pageable memory may return before the DMA lands)
   PB_HIP(hipMemcpyAsync(f.dev, all.data(), 3 * n * sizeof(double), hipMemcpyHostToDevice,
                         ctx->stream));
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "compact");
   g_fac[key] = f;
   *out = f;
   return PB_OK;

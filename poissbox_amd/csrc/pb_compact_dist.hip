@@ -98,7 +98,7 @@ int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double
                      const_cast<double*>(f), stage, (int)nx, (int)ny, (int)g->nzl, tab, tab + ny,
                      tab + ny + P, 0);
   PB_HIP(hipGetLastError());
-  PB_HIP(hipStreamSynchronize(ctx->stream));  // htab stays valid until the copy is done
+  PB_SYNC(ctx, "compact transpose");  // htab stays valid until the copy is done
   PB_TRY(alltoallv_device(ctx, stage, zc.data(), fy, yc.data()));
   const int64_t dy[3] = {nx, d.ny_me, nz};
   PB_TRY(compact_pass_z(ctx, dy, h, fy, uy, vy));

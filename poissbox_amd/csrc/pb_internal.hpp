@@ -68,6 +68,11 @@ struct pb_ctx {
   hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with interior planes
   hipEvent_t ev_ready = nullptr, ev_done = nullptr;
   ncclComm_t comm = nullptr;
+  // bounded waits on split contexts (a dead or stalled peer must surface as PB_ERR_COMM, not a
+  // hang): PB_COMM_TIMEOUT_MS per wait; after a failure the communicator is aborted and every
+  // later collective call returns PB_ERR_COMM at once
+  int64_t comm_timeout_ms = 180000;
+  bool comm_failed = false;
   // host transport (tests)
   pb_sendrecv_fn h_sendrecv = nullptr;
   pb_allreduce_fn h_allreduce = nullptr;
@@ -145,8 +150,9 @@ struct Star {
 Star star_coeffs(const double h[3]);
 
 // ---- timing ----
-void timer_begin(pb_ctx* ctx, const char* name, hipEvent_t* ev);
-void timer_end(pb_ctx* ctx, const char* name, hipEvent_t ev0);
+// events on `s` (default: the context stream)
+void timer_begin(pb_ctx* ctx, const char* name, hipEvent_t* ev, hipStream_t s = nullptr);
+void timer_end(pb_ctx* ctx, const char* name, hipEvent_t ev0, hipStream_t s = nullptr);
 void timers_collect(pb_ctx* ctx);
 
 bool timer_wanted(pb_ctx* ctx, const char* name);
@@ -182,6 +188,20 @@ int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, doub
 int halo_end(pb_grid* g);
 // In-place SUM allreduce of `count` device doubles (stream ordered).
 int allreduce_device(pb_ctx* ctx, double* d_vals, int count);
+// Bounded host waits. One rank without a communicator: plain hipStream/EventSynchronize. Split
+// contexts poll (hipStreamQuery / hipEventQuery) and check ncclCommGetAsyncError; a peer error
+// or a wait longer than ctx->comm_timeout_ms aborts the communicator (ncclCommAbort) and returns
+// PB_ERR_COMM. `what` names the wait in the error message.
+int wait_stream(pb_ctx* ctx, hipStream_t s, const char* what);
+int wait_event(pb_ctx* ctx, hipEvent_t ev, const char* what);
+// mark the context's communication as failed (aborting RCCL) and return PB_ERR_COMM
+int comm_fail(pb_ctx* ctx, const char* fmt, ...);
+#define PB_SYNC(ctx, what) PB_TRY(::pb::wait_stream((ctx), (ctx)->stream, (what)))
+#define PB_COMM_OK(ctx)                                                                     \
+  do {                                                                                      \
+    if ((ctx)->comm_failed)                                                                 \
+      return ::pb::set_error(PB_ERR_COMM, "communication failed earlier on this context");  \
+  } while (0)
 
 // ---- kernels (pb_stencil.hip) ----
 struct StencilPlanes {

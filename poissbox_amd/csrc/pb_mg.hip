@@ -564,7 +564,7 @@ int mg_levels(const Mg* mg) { return (int)mg->lv.size(); }
 
 void mg_destroy(Mg* mg) {
   if (!mg) return;
-  (void)hipStreamSynchronize(mg->ctx->stream);
+  (void)wait_stream(mg->ctx, mg->ctx->stream, "mg_destroy");
   for (auto& L : mg->lv)
     if (L.own) pb_grid_destroy(L.g);
   if (mg->mem) (void)hipFree(mg->mem);

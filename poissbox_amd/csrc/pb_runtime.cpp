@@ -1,6 +1,9 @@
 // pb_runtime.cpp -- host runtime of libpoissbox_gpu: errors, context (device, stream, RCCL),
 // slab grid, vectors, halo exchange and allreduce, the operator entry point and kernel timing.
+#include <time.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -55,14 +58,14 @@ bool timer_wanted(pb_ctx* ctx, const char* name) {
   return ctx->timer_calls[name]++ % ctx->timing_every == 0;  // sampled phase
 }
 
-void timer_begin(pb_ctx* ctx, const char*, hipEvent_t* ev) {
+void timer_begin(pb_ctx* ctx, const char*, hipEvent_t* ev, hipStream_t s) {
   *ev = take_event(ctx);
-  (void)hipEventRecord(*ev, ctx->stream);
+  (void)hipEventRecord(*ev, s ? s : ctx->stream);
 }
 
-void timer_end(pb_ctx* ctx, const char* name, hipEvent_t ev0) {
+void timer_end(pb_ctx* ctx, const char* name, hipEvent_t ev0, hipStream_t s) {
   hipEvent_t ev1 = take_event(ctx);
-  (void)hipEventRecord(ev1, ctx->stream);
+  (void)hipEventRecord(ev1, s ? s : ctx->stream);
   ctx->pending.push_back({std::string(name), {ev0, ev1}});
   if (ctx->pending.size() > 4096) timers_collect(ctx);
 }
@@ -81,9 +84,80 @@ void timers_collect(pb_ctx* ctx) {
   ctx->pending.clear();
 }
 
+// ---- bounded waits ----
+int comm_fail(pb_ctx* ctx, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  if (!ctx->comm_failed) {
+    ctx->comm_failed = true;
+    fprintf(stderr, "[poissbox rank %d] communication failure: %s\n", ctx->rank, g_err);
+    if (ctx->comm) {
+      // releases RCCL kernels still waiting for a peer, so the streams can drain
+      (void)ncclCommAbort(ctx->comm);
+      ctx->comm = nullptr;
+    }
+  }
+  return PB_ERR_COMM;
+}
+
+template <class Query>
+static int bounded_wait(pb_ctx* ctx, Query query, const char* what) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  // after a failure, drain for a short while only (never block teardown on a dead peer)
+  const int64_t limit_ms = ctx->comm_failed ? 5000 : ctx->comm_timeout_ms;
+  for (int64_t spin = 0;; ++spin) {
+    const hipError_t e = query();
+    if (e == hipSuccess) return ctx->comm_failed ? set_error(PB_ERR_COMM, "%s after a "
+                                                             "communication failure", what)
+                                                 : PB_OK;
+    if (e != hipErrorNotReady)
+      return set_error(PB_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    if ((spin & 63) == 63) {
+      if (ctx->comm && !ctx->comm_failed) {
+        ncclResult_t ar = ncclSuccess;
+        if (ncclCommGetAsyncError(ctx->comm, &ar) == ncclSuccess && ar != ncclSuccess &&
+            ar != ncclInProgress)
+          return comm_fail(ctx, "%s: RCCL asynchronous error: %s", what, ncclGetErrorString(ar));
+      }
+      const int64_t ms =
+          std::chrono::duration_cast<std::chrono::milliseconds>(clk::now() - t0).count();
+      if (ms > limit_ms) {
+        if (ctx->comm_failed)
+          return set_error(PB_ERR_COMM, "%s: still pending after a communication failure", what);
+        return comm_fail(ctx, "%s: no progress for %lld ms (PB_COMM_TIMEOUT_MS); a peer rank "
+                         "is dead or stalled", what, (long long)ms);
+      }
+    }
+    if (spin > 4096) {  // past the first few hundred microseconds: back off
+      timespec ts{0, 50000};
+      nanosleep(&ts, nullptr);
+    }
+  }
+}
+
+int wait_stream(pb_ctx* ctx, hipStream_t s, const char* what) {
+  if (!ctx->split && !ctx->comm_failed) {
+    PB_HIP(hipStreamSynchronize(s));
+    return PB_OK;
+  }
+  return bounded_wait(ctx, [s] { return hipStreamQuery(s); }, what);
+}
+
+int wait_event(pb_ctx* ctx, hipEvent_t ev, const char* what) {
+  if (!ctx->split && !ctx->comm_failed) {
+    PB_HIP(hipEventSynchronize(ev));
+    return PB_OK;
+  }
+  return bounded_wait(ctx, [ev] { return hipEventQuery(ev); }, what);
+}
+
 // ---- communication ----
 int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
   pb_ctx* ctx = g->ctx;
+  PB_COMM_OK(ctx);
   ScopedTimer tm(ctx, "halo");
   const int64_t cnt = g->plane;
   if (!ctx->split) {
@@ -100,9 +174,9 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
     double* r_hi = g->h_stage + 3 * cnt;
     PB_HIP(hipMemcpyAsync(s_lo, lo, cnt * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     PB_HIP(hipMemcpyAsync(s_hi, hi, cnt * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    PB_HIP(hipStreamSynchronize(ctx->stream));
+    PB_SYNC(ctx, "halo staging");
     if (ctx->h_sendrecv(ctx->h_user, s_lo, s_hi, r_lo, r_hi, cnt) != 0)
-      return set_error(PB_ERR_COMM, "host sendrecv callback failed");
+      return comm_fail(ctx, "host sendrecv callback failed");
     PB_HIP(hipMemcpyAsync(g->ghost_lo, r_lo, cnt * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     PB_HIP(hipMemcpyAsync(g->ghost_hi, r_hi, cnt * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     return PB_OK;
@@ -122,6 +196,7 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
 int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, double* rlo,
                     double* rhi) {
   pb_ctx* ctx = g->ctx;
+  PB_COMM_OK(ctx);
   ScopedTimer tm(ctx, "halo");
   const int64_t cnt = (int64_t)np * g->plane;
   const size_t bytes = (size_t)cnt * sizeof(double);
@@ -143,9 +218,9 @@ int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, doub
     double* r_hi = r_lo + cnt;
     PB_HIP(hipMemcpyAsync(s_lo, lo, bytes, hipMemcpyDeviceToHost, ctx->stream));
     PB_HIP(hipMemcpyAsync(s_hi, hi, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    PB_HIP(hipStreamSynchronize(ctx->stream));
+    PB_SYNC(ctx, "halo staging");
     if (ctx->h_sendrecv(ctx->h_user, s_lo, s_hi, r_lo, r_hi, cnt) != 0)
-      return set_error(PB_ERR_COMM, "host sendrecv callback failed");
+      return comm_fail(ctx, "host sendrecv callback failed");
     PB_HIP(hipMemcpyAsync(rlo, r_lo, bytes, hipMemcpyHostToDevice, ctx->stream));
     PB_HIP(hipMemcpyAsync(rhi, r_hi, bytes, hipMemcpyHostToDevice, ctx->stream));
     return PB_OK;
@@ -162,18 +237,24 @@ int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, doub
 
 int halo_begin(pb_grid* g, const double* lo, const double* hi) {
   pb_ctx* ctx = g->ctx;
+  PB_COMM_OK(ctx);
   if (!ctx->split || !ctx->comm) return halo_exchange(g, lo, hi);
   const int64_t cnt = g->plane;
   const int down = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
   const int up = (ctx->rank + 1) % ctx->nranks;
   PB_HIP(hipEventRecord(ctx->ev_ready, ctx->stream));
   PB_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->ev_ready, 0));
+  // "halo_comm": the exchange itself on the comm stream (overlapped with interior planes)
+  hipEvent_t tev = nullptr;
+  const bool timed = ctx->timing && timer_wanted(ctx, "halo_comm");
+  if (timed) timer_begin(ctx, "halo_comm", &tev, ctx->comm_stream);
   PB_NCCL(ncclGroupStart());
   PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
   PB_NCCL(ncclRecv(g->ghost_hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
   PB_NCCL(ncclSend(hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
   PB_NCCL(ncclRecv(g->ghost_lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
   PB_NCCL(ncclGroupEnd());
+  if (timed) timer_end(ctx, "halo_comm", tev, ctx->comm_stream);
   PB_HIP(hipEventRecord(ctx->ev_done, ctx->comm_stream));
   return PB_OK;
 }
@@ -187,6 +268,7 @@ int halo_end(pb_grid* g) {
 
 int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,
                      const int64_t* rcount) {
+  PB_COMM_OK(ctx);
   ScopedTimer tm(ctx, "alltoallv");
   const int P = ctx->nranks;
   std::vector<int64_t> so(P + 1, 0), ro(P + 1, 0);
@@ -228,17 +310,17 @@ int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, dou
   double* hs = ctx->h_a2a;
   double* hr = ctx->h_a2a + so[P];
   PB_HIP(hipMemcpyAsync(hs, send, so[P] * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "all-to-all staging");
   if (ctx->h_alltoallv(ctx->h_a2a_user, hs, scount, hr, rcount) != 0)
-    return set_error(PB_ERR_COMM, "host alltoallv callback failed");
+    return comm_fail(ctx, "host alltoallv callback failed");
   PB_HIP(hipMemcpyAsync(recv, hr, ro[P] * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "all-to-all staging");
   return PB_OK;
 }
 
 int ctx_scratch(pb_ctx* ctx, size_t n, double** out) {
   if (n > ctx->scratch_len) {
-    PB_HIP(hipStreamSynchronize(ctx->stream));  // previous users of the old buffer are done
+    PB_SYNC(ctx, "scratch");  // previous users of the old buffer are done
     if (ctx->scratch) PB_HIP(hipFree(ctx->scratch));
     ctx->scratch = nullptr;
     ctx->scratch_len = 0;
@@ -252,16 +334,17 @@ int ctx_scratch(pb_ctx* ctx, size_t n, double** out) {
 
 int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
   if (!ctx->split) return PB_OK;
+  PB_COMM_OK(ctx);
   ScopedTimer tm(ctx, "allreduce");
   if (ctx->h_allreduce) {
     PB_HIP(hipMemcpyAsync(ctx->h_scalars + 16, d_vals, count * sizeof(double), hipMemcpyDeviceToHost,
                           ctx->stream));
-    PB_HIP(hipStreamSynchronize(ctx->stream));
+    PB_SYNC(ctx, "allreduce staging");
     if (ctx->h_allreduce(ctx->h_user, ctx->h_scalars + 16, count) != 0)
-      return set_error(PB_ERR_COMM, "host allreduce callback failed");
+      return comm_fail(ctx, "host allreduce callback failed");
     PB_HIP(hipMemcpyAsync(d_vals, ctx->h_scalars + 16, count * sizeof(double), hipMemcpyHostToDevice,
                           ctx->stream));
-    PB_HIP(hipStreamSynchronize(ctx->stream));  // staging buffer is reused by the next call
+    PB_SYNC(ctx, "allreduce staging");  // staging buffer is reused by the next call
     return PB_OK;
   }
   PB_NCCL(ncclAllReduce(d_vals, d_vals, (size_t)count, ncclDouble, ncclSum, ctx->comm, ctx->stream));
@@ -342,6 +425,7 @@ int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb
       cus > 0)
     ctx->num_cus = cus;
   ctx->roctx = env_int("PB_ROCTX", 0) != 0;
+  ctx->comm_timeout_ms = std::max(1, env_int("PB_COMM_TIMEOUT_MS", 180000));
   PB_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
   PB_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
   PB_HIP(hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming));
@@ -391,25 +475,32 @@ int pb_ctx_get_rank(const pb_ctx* ctx, int* rank, int* nranks) {
 
 int pb_ctx_sync(pb_ctx* ctx) {
   PB_CHECK_ARG(ctx, "ctx is NULL");
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "pb_ctx_sync");
   return PB_OK;
 }
 
 int pb_ctx_barrier(pb_ctx* ctx) {
   PB_CHECK_ARG(ctx, "ctx is NULL");
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "pb_ctx_barrier");
   if (ctx->split) {
     PB_TRY(allreduce_device(ctx, ctx->d_scalars + 32, 1));
-    PB_HIP(hipStreamSynchronize(ctx->stream));
+    PB_SYNC(ctx, "pb_ctx_barrier");
   }
+  return PB_OK;
+}
+
+int pb_ctx_comm_status(const pb_ctx* ctx, int* failed) {
+  PB_CHECK_ARG(ctx && failed, "bad args");
+  *failed = ctx->comm_failed ? 1 : 0;
   return PB_OK;
 }
 
 int pb_ctx_destroy(pb_ctx* ctx) {
   if (!ctx) return PB_OK;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
-  timers_collect(ctx);
+  (void)wait_stream(ctx, ctx->stream, "pb_ctx_destroy");
+  (void)wait_stream(ctx, ctx->comm_stream, "pb_ctx_destroy");
+  if (!ctx->comm_failed) timers_collect(ctx);
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
@@ -417,7 +508,6 @@ int pb_ctx_destroy(pb_ctx* ctx) {
   (void)hipFree(ctx->d_partials);
   (void)hipFree(ctx->d_scalars);
   (void)hipHostFree(ctx->h_scalars);
-  (void)hipStreamSynchronize(ctx->comm_stream);
   (void)hipEventDestroy(ctx->ev_ready);
   (void)hipEventDestroy(ctx->ev_done);
   (void)hipStreamDestroy(ctx->comm_stream);
@@ -518,7 +608,7 @@ int pb_grid_get_info(const pb_grid* g, int64_t n[3], double h[3], int64_t* nloca
 
 int pb_grid_destroy(pb_grid* g) {
   if (!g) return PB_OK;
-  (void)hipStreamSynchronize(g->ctx->stream);
+  (void)wait_stream(g->ctx, g->ctx->stream, "pb_grid_destroy");
   (void)hipFree(g->ghost_lo);
   if (g->ghost2) (void)hipFree(g->ghost2);
   if (g->h_stage) (void)hipHostFree(g->h_stage);
@@ -553,7 +643,7 @@ int pb_vec_duplicate(const pb_vec* v, pb_vec** out) {
 
 int pb_vec_destroy(pb_vec* v) {
   if (!v) return PB_OK;
-  (void)hipStreamSynchronize(v->grid->ctx->stream);
+  (void)wait_stream(v->grid->ctx, v->grid->ctx->stream, "pb_vec_destroy");
   (void)hipFree(v->d);
   delete v;
   return PB_OK;
@@ -614,7 +704,7 @@ int pb_vec_set_values_host(pb_vec* v, const double* owned) {
   // stream-ordered after any pending work on the vector (e.g. the zero fill at creation)
   hipStream_t s = v->grid->ctx->stream;
   PB_HIP(hipMemcpyAsync(v->d, owned, (size_t)v->nlocal * sizeof(double), hipMemcpyHostToDevice, s));
-  PB_HIP(hipStreamSynchronize(s));
+  PB_TRY(wait_stream(v->grid->ctx, s, "pb_vec_set_values_host"));
   return PB_OK;
 }
 
@@ -622,7 +712,7 @@ int pb_vec_get_values_host(const pb_vec* v, double* owned) {
   PB_CHECK_ARG(v && owned, "bad get_values args");
   hipStream_t s = v->grid->ctx->stream;
   PB_HIP(hipMemcpyAsync(owned, v->d, (size_t)v->nlocal * sizeof(double), hipMemcpyDeviceToHost, s));
-  PB_HIP(hipStreamSynchronize(s));
+  PB_TRY(wait_stream(v->grid->ctx, s, "pb_vec_get_values_host"));
   return PB_OK;
 }
 

@@ -136,7 +136,7 @@ int pb_op_get_diagonal(const pb_op* op, double* diag) {
 int pb_op_destroy(pb_op* op) {
   if (!op) return PB_OK;
   if (op->work) {
-    (void)hipStreamSynchronize(op->grid->ctx->stream);
+    (void)wait_stream(op->grid->ctx, op->grid->ctx->stream, "pb_op_destroy");
     (void)hipFree(op->work);
   }
   delete op;
@@ -270,7 +270,7 @@ static int ensure_done_cap(pb_ksp* k, int64_t need) {
   PB_HIP(hipHostMalloc(&h, (size_t)cap * sizeof(int), hipHostMallocMapped));
   memset(h, 0, (size_t)cap * sizeof(int));
   if (k->h_done) {
-    PB_HIP(hipStreamSynchronize(k->A->grid->ctx->stream));
+    PB_TRY(wait_stream(k->A->grid->ctx, k->A->grid->ctx->stream, "KSP flag buffer"));
     memcpy(h, k->h_done, (size_t)k->done_cap * sizeof(int));
     (void)hipHostFree(k->h_done);
   }
@@ -334,7 +334,7 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
     PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->pb[0], k->d_st, st.dinv, k->d_hist,
                           k->h_done_dev));
   }
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "pb_ksp_begin");
   k->b = b;
   k->x = x;
   k->host_iter = 0;
@@ -448,7 +448,7 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
     // lagged, rank-consistent poll: decide on the flag of iteration hi + 1 - C only
     if ((hi + 1) % C == 0 && hi + 1 >= C) {
       const int64_t j = hi + 1 - C;
-      PB_HIP(hipEventSynchronize(k->ring[j % R]));
+      PB_TRY(wait_event(ctx, k->ring[j % R], "KSP convergence poll"));
       if (k->h_done[j + 1]) k->stopped = true;
     }
   }
@@ -473,15 +473,15 @@ int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
   PB_CHECK_ARG(k, "ksp is NULL");
   if (!k->begun) return set_error(PB_ERR_STATE, "pb_ksp_end before pb_ksp_begin");
   pb_ctx* ctx = k->A->grid->ctx;
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "pb_ksp_end");
   CgState st;
   PB_HIP(hipMemcpyAsync(&st, k->d_st, sizeof(st), hipMemcpyDeviceToHost, ctx->stream));
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "pb_ksp_end");
   if (st.pend_iter >= 0) {  // apply the still-deferred alpha_m p_m (p_m lives in pb[(m+1) % ns])
     const int ns = k->pslots();
     for (int64_t m = 0; m < st.pend_count; ++m)
       PB_TRY(launch_cg_flush(k->A->grid, k->x->d, k->pb[(st.pend_iter + m + 1) % ns], st.pa[m]));
-    PB_HIP(hipStreamSynchronize(ctx->stream));
+    PB_SYNC(ctx, "pb_ksp_end");
   }
   if (res) {
     res->reason = st.reason;
@@ -496,7 +496,7 @@ int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
   if (nh > 0) {
     PB_HIP(hipMemcpyAsync(hist.data(), k->d_hist, (size_t)nh * sizeof(double), hipMemcpyDeviceToHost,
                           ctx->stream));
-    PB_HIP(hipStreamSynchronize(ctx->stream));
+    PB_SYNC(ctx, "pb_ksp_end");
   }
   if (history && cap > 0) memcpy(history, hist.data(), (size_t)std::min(nh, cap) * sizeof(double));
   if (ctx->rank == 0) {
@@ -527,7 +527,7 @@ int pb_ksp_solve(pb_ksp* k, const pb_vec* b, pb_vec* x, pb_ksp_result* res, doub
 
 int pb_ksp_destroy(pb_ksp* k) {
   if (!k) return PB_OK;
-  (void)hipStreamSynchronize(k->A->grid->ctx->stream);
+  (void)wait_stream(k->A->grid->ctx, k->A->grid->ctx->stream, "pb_ksp_destroy");
   (void)hipFree(k->r);
   for (double* p : k->pb)
     if (p) (void)hipFree(p);
@@ -555,7 +555,7 @@ int pb_ksp_pc_apply(pb_ksp* k, const pb_vec* r, pb_vec* z) {
     if (k->opts.pc_type == PB_PC_JACOBI)
       PB_TRY(vec_update(ctx, 2, z->d, nullptr, g->nlocal, 1.0 / k->P->cc));
   }
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "pb_ksp_pc_apply");
   return PB_OK;
 }
 

@@ -120,7 +120,7 @@ int vec_reduce(pb_ctx* ctx, int kind, const double* x, const double* y, int64_t 
   PB_TRY(reduce_partials(ctx, ctx->d_partials, nb, 1, dsum));
   PB_TRY(allreduce_device(ctx, dsum, 1));
   PB_HIP(hipMemcpyAsync(ctx->h_scalars, dsum, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-  PB_HIP(hipStreamSynchronize(ctx->stream));
+  PB_SYNC(ctx, "vector reduction");
   *out = ctx->h_scalars[0];
   return PB_OK;
 }

@@ -7,9 +7,17 @@
   send the first owned plane to rank-1 and the last to rank+1, receive the plane below / above).
   Used by tests to run N processes on one GPU (RCCL refuses two ranks on one device) and on CPU.
 """
+import datetime
 import os
 
 import numpy as np
+
+
+def comm_timeout_s():
+    """Per-operation bound of the host transport (PB_COMM_TIMEOUT_MS, as the library's own
+    waits): a peer that died or stalls surfaces as an exception, which the transport callback
+    turns into PB_ERR_COMM, instead of a hang."""
+    return int(os.environ.get("PB_COMM_TIMEOUT_MS", "180000")) / 1000.0
 
 
 def env_world():
@@ -37,13 +45,18 @@ def broadcast_uid(dist, rank, make_uid):
 class GlooTransport:
     """sendrecv(lo, hi) -> (recv_lo, recv_hi); allreduce(vals) -> summed vals (float64)."""
 
-    def __init__(self, dist, group=None):
+    def __init__(self, dist, group=None, timeout_s=None):
         import torch
         self.torch = torch
         self.dist = dist
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.timeout = datetime.timedelta(seconds=timeout_s if timeout_s else comm_timeout_s())
+
+    def _wait(self, reqs):
+        for q in reqs:
+            q.wait(self.timeout)  # raises on timeout / peer failure
 
     def sendrecv(self, lo, hi):
         t = self.torch
@@ -57,13 +70,12 @@ class GlooTransport:
                 self.dist.isend(t.from_numpy(np.ascontiguousarray(hi)), up, self.group, tag=2),
                 self.dist.irecv(r_hi, up, self.group, tag=1),
                 self.dist.irecv(r_lo, down, self.group, tag=2)]
-        for q in reqs:
-            q.wait()
+        self._wait(reqs)
         return r_lo.numpy(), r_hi.numpy()
 
     def allreduce(self, vals):
         v = self.torch.from_numpy(np.ascontiguousarray(vals, dtype=np.float64).copy())
-        self.dist.all_reduce(v, group=self.group)
+        self._wait([self.dist.all_reduce(v, group=self.group, async_op=True)])
         return v.numpy()
 
     def alltoallv(self, blocks, recv_sizes):
@@ -82,8 +94,7 @@ class GlooTransport:
             if len(blocks[p]):
                 reqs.append(self.dist.isend(t.from_numpy(np.ascontiguousarray(blocks[p])), p,
                                             self.group, tag=3))
-        for q in reqs:
-            q.wait()
+        self._wait(reqs)
         for p, b in bufs.items():
             out[p] = b.numpy()
         return out

@@ -177,3 +177,31 @@ def test_gloo_alltoallv_protocol(world):
     for rank, got in enumerate(res):
         for p in range(world):
             assert got[p] == [10.0 * p + rank] * (rank + 1 + p)
+
+
+def _stalled_peer(rank, world, tr):
+    """Rank 1 never joins the exchange (a dead or stalled peer); rank 0's transport calls must
+    raise within their timeout, not hang. Both ranks meet again over the store afterwards."""
+    import time
+    import torch.distributed as dist
+    from poissbox_amd.dist import GlooTransport
+    res = "no error"
+    if rank == 0:
+        t = GlooTransport(dist, timeout_s=2.0)
+        t0 = time.perf_counter()
+        for op in (lambda: t.sendrecv(np.zeros(4), np.zeros(4)),
+                   lambda: t.allreduce(np.ones(3))):
+            try:
+                op()
+            except Exception as e:  # noqa: BLE001 - any transport error is the expected outcome
+                res = f"raised after {time.perf_counter() - t0:.1f} s: {type(e).__name__}"
+                break
+    else:
+        time.sleep(6.0)
+    return res
+
+
+def test_gloo_transport_times_out_on_stalled_peer():
+    out = _run(2, _stalled_peer)
+    assert out[0].startswith("raised"), out[0]
+    assert float(out[0].split()[2]) < 10.0, out[0]

@@ -1,0 +1,80 @@
+"""GPU tier: communication failures on split (multi-rank) contexts surface as PB_ERR_COMM instead
+of hangs (include/poissbox_gpu.h pb_ctx_comm_status). The reference's MPI path has no such
+handling (src/poissbox.f90:104-105 DMGlobalToLocal blocks forever on a dead peer); here every host
+wait is bounded and a failed context refuses further communication.
+
+Both cases run one process as rank 0 of a 2-rank context over a loop-back host transport, so no
+RCCL communicator is involved (aborting one with kernels still queued is left to real failures)."""
+import os
+
+import numpy as np
+import pytest
+
+import poissbox_amd as pb
+from poissbox_amd._lib import PbError
+
+PB_ERR_COMM = 3
+
+
+def _split_ctx(sendrecv, allreduce):
+    ctx = pb.Context(0, 0, 2)
+    ctx.set_host_transport(sendrecv, allreduce)
+    return ctx
+
+
+@pytest.mark.gpu
+def test_failing_host_callback_is_an_error_and_poisons_the_context():
+    calls = {"n": 0}
+
+    def bad_sendrecv(lo, hi):
+        calls["n"] += 1
+        raise ConnectionError("peer gone")
+
+    ctx = _split_ctx(bad_sendrecv, lambda v: v)
+    try:
+        da = pb.initialise_grid(ctx, (32, 32, 16))
+        x, y = pb.Vec(da), pb.Vec(da)
+        A = pb.Mat(da, pb.STAR7)
+        with pytest.raises(PbError) as e:
+            A.mult(x, y)
+        assert e.value.code == PB_ERR_COMM and "sendrecv" in str(e.value)
+        assert ctx.comm_failed
+        with pytest.raises(PbError) as e2:  # no further collective traffic on a failed context
+            A.mult(x, y)
+        assert e2.value.code == PB_ERR_COMM and calls["n"] == 1
+        for o in (A, x, y, da):
+            o.destroy()
+    finally:
+        ctx.destroy()
+
+
+@pytest.mark.gpu
+def test_wait_timeout_is_an_error(monkeypatch):
+    """PB_COMM_TIMEOUT_MS bounds every wait of a split context: with 1 ms, waiting for a queue of
+    512x512x256-slab CG iterations (~0.7 ms each) must fail with PB_ERR_COMM, not block."""
+    monkeypatch.setenv("PB_COMM_TIMEOUT_MS", "1")
+    loop = lambda lo, hi: (hi.copy(), lo.copy())  # noqa: E731 - loop-back halo
+    ctx = _split_ctx(loop, lambda v: v)
+    try:
+        da = pb.initialise_grid(ctx, (512, 512, 512))
+        P, A, x, b = pb.initialise_linear_system(da, da.spacing)
+        b.set_random(1)
+        opts = pb.ksp_options(["-ksp_type", "cg", "-pc_type", "jacobi"], rtol=0.0, atol=0.0,
+                              dtol=1e300, max_it=200)
+        ksp = pb.KSP(A, P, opts)
+        with pytest.raises(PbError) as e:
+            ksp.begin(b, x)
+            ksp.iterate(200)
+            ksp.end()
+        assert e.value.code == PB_ERR_COMM and "PB_COMM_TIMEOUT_MS" in str(e.value)
+        assert ctx.comm_failed
+        for o in (ksp, A, P, x, b, da):
+            o.destroy()
+    finally:
+        ctx.destroy()
+    # a fresh context is unaffected
+    c2 = pb.Context(0)
+    try:
+        assert not c2.comm_failed
+    finally:
+        c2.destroy()
