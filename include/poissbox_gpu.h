@@ -127,6 +127,11 @@ enum pb_op_kind {
   PB_OP_COMPACT = 1,     /* 6th-order compact lapl = div(grad f), compact_schemes.f90:17-37  */
   PB_OP_ASSEMBLED27 = 2  /* assembled BOX AIJ P (coefficients.f90:50-113), 27-entry rows     */
 };
+/* PB_OP_ASSEMBLED27 applies P x with PETSc's AIJ row sums: stored columns ascending on one rank
+ * (MatMult_SeqAIJ), owned columns then off-rank columns on several (MatMult_MPIAIJ) -- so rows on
+ * the periodic seams and slab boundaries differ from PB_OP_STAR7 at rounding level, and
+ * src/example.f90:235-261's ||A x - P x|| is the reference's rounding-level value, not 0. As a
+ * KSP operator (A = P, src/example.f90:62-64) it runs the unfused CG iteration. */
 int pb_op_create(pb_grid* grid, int kind, const double deltas[3], pb_op** op);
 int pb_op_apply(pb_op* op, const pb_vec* x, pb_vec* y); /* ≙ MatMult(A, x, y) */
 int pb_op_get_diagonal(const pb_op* op, double* diag);  /* constant diagonal of the 7-pt P */

@@ -87,10 +87,11 @@ def stencil_slab(x, n_local, h, ghost_lo, ghost_hi):
     return y
 
 
-def assembled(x, n, h):
+def assembled(x, n, h, nranks=1):
+    """MatMult of the assembled 27-entry P (AIJ row order; MPIAIJ block order on nranks z-slabs)."""
     x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
     y = np.empty_like(x)
-    lib().pbo_assembled_apply(_n3(n), _h3(h), _p(x), _p(y))
+    lib().pbo_assembled_apply(_n3(n), _h3(h), C.c_int(nranks), _p(x), _p(y))
     return y
 
 
@@ -110,7 +111,10 @@ def cg_solve(b, n, h, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi"
     x = np.empty_like(b)
     hist = np.zeros(int(max_it) + 2)
     its, nlog = C.c_int64(0), C.c_int64(0)
-    kind = 2 if op == "compact" else (1 if faithful else 0)
+    if op == "assembled":  # A = P (src/example.f90:62-64), MatMult in AIJ order on nranks slabs
+        kind = 2 + max(1, nranks)
+    else:
+        kind = 2 if op == "compact" else (1 if faithful else 0)
     o = KspOpts(rtol, atol, dtol, max_it, PC_CODES[pc], int(nullspace), kind, nthreads,
                 mg_levels, mg_coarse_its, omega, nranks)
     reason = lib().pbo_cg_solve(_n3(n), _h3(h), C.byref(o), _p(b), _p(x), _p(hist), C.byref(its),

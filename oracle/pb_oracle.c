@@ -156,27 +156,49 @@ static int cmp_i64(const void* a, const void* b) {
 }
 
 /* src/coefficients.f90:50-113 assemble_laplacian: one MatSetValuesStencil row of the 27 box
- * entries (20 explicit zeros) per DoF, INSERT_VALUES; MatMult over an AIJ row sums the stored
- * entries in ascending global column order (natural ordering on one rank). Requires n >= 3 in
- * every direction so that the 27 columns are distinct. */
-void pbo_assembled_apply(const int64_t n[3], const double h[3], const double* x, double* y) {
+ * entries (20 explicit zeros) per DoF, INSERT_VALUES. MatMult sums a row's stored entries in
+ * ascending column order: on one rank (SeqAIJ) ascending global column (natural ordering); on
+ * `nranks` z-slabs (MPIAIJ, MatMult_MPIAIJ) first the diagonal block -- the columns this rank owns,
+ * ascending -- then the off-diagonal block added onto it (MatMultAdd), columns ascending by global
+ * index. The slabs follow pbo-side slab_partition (remainder planes on the low ranks, as
+ * pb_slab_partition / README.md:30-32). Requires n >= 3 in every direction so the 27 columns are
+ * distinct. 0 * x products of the explicit zeros leave every partial sum unchanged. */
+static void slab_of(int64_t nz, int nranks, int r, int64_t* k0, int64_t* nk) {
+  const int64_t q = nz / nranks, rem = nz % nranks;
+  *nk = q + (r < rem ? 1 : 0);
+  *k0 = r * q + (r < rem ? r : rem);
+}
+
+void pbo_assembled_apply(const int64_t n[3], const double h[3], int nranks, const double* x,
+                         double* y) {
   const int64_t nx = n[0], ny = n[1], nz = n[2];
+  const int64_t plane = nx * ny;
+  if (nranks < 1) nranks = 1;
   double c[27];
   pbo_lapl_star_coeffs(h[0], h[1], h[2], c);
-  for (int64_t k = 0; k < nz; ++k)
-    for (int64_t j = 0; j < ny; ++j)
-      for (int64_t i = 0; i < nx; ++i) {
-        int64_t key[27][2];
-        for (int m = 0; m < 27; ++m) {
-          int ii = m % 3, jj = (m / 3) % 3, kk = m / 9;
-          key[m][0] = IDX(wrap(i + ii - 1, nx), wrap(j + jj - 1, ny), wrap(k + kk - 1, nz), nx, ny);
-          key[m][1] = m;
+  for (int r = 0; r < nranks; ++r) {
+    int64_t k0, nk;
+    slab_of(nz, nranks, r, &k0, &nk);
+    const int64_t lo = k0 * plane, hi = (k0 + nk) * plane; /* owned rows / columns */
+    for (int64_t k = k0; k < k0 + nk; ++k)
+      for (int64_t j = 0; j < ny; ++j)
+        for (int64_t i = 0; i < nx; ++i) {
+          int64_t key[27][2];
+          for (int m = 0; m < 27; ++m) {
+            int ii = m % 3, jj = (m / 3) % 3, kk = m / 9;
+            const int64_t col =
+                IDX(wrap(i + ii - 1, nx), wrap(j + jj - 1, ny), wrap(k + kk - 1, nz), nx, ny);
+            const int64_t off = (nranks > 1 && (col < lo || col >= hi)) ? 1 : 0;
+            key[m][0] = (off << 62) | col;
+            key[m][1] = m;
+          }
+          qsort(key, 27, sizeof(key[0]), cmp_i64);
+          double s = 0.0;
+          for (int m = 0; m < 27; ++m)
+            s += c[key[m][1]] * x[key[m][0] & (((int64_t)1 << 62) - 1)];
+          y[IDX(i, j, k, nx, ny)] = s;
         }
-        qsort(key, 27, sizeof(key[0]), cmp_i64);
-        double s = 0.0;
-        for (int m = 0; m < 27; ++m) s += c[key[m][1]] * x[key[m][0]];
-        y[IDX(i, j, k, nx, ny)] = s;
-      }
+  }
 }
 
 /* ---------------------------------------------------------------------------------------------
@@ -423,6 +445,8 @@ static void op_apply(const int64_t n[3], const double h[3], const double* x, dou
     stencil27_mt(n, h, x, y, nt); /* faithful operator; one core = one reference MPI rank */
   else if (kind == 2)
     pbo_lapl(n, x, h, y); /* compact A; P (Jacobi diag) stays the 7-point */
+  else if (kind >= 3)
+    pbo_assembled_apply(n, h, kind - 2, x, y); /* A = P assembled, MatMult on kind-2 z-slabs */
   else
     pbo_stencil_apply7(n, h, x, y, nt);
 }

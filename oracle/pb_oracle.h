@@ -38,7 +38,8 @@ void pbo_stencil_slab(const int64_t n[3], const double h[3], const double* x, co
                       const double* ghi, double* y);
 /* assembled P (src/coefficients.f90:50-113) applied as a 27-point BOX SpMV, row-wise sum over
  * the 27 stored entries in MatSetValuesStencil column order */
-void pbo_assembled_apply(const int64_t n[3], const double h[3], const double* x, double* y);
+void pbo_assembled_apply(const int64_t n[3], const double h[3], int nranks, const double* x,
+                         double* y);
 double pbo_diag(const double h[3]);
 
 /* ---- synthetic input ---- */
@@ -52,7 +53,8 @@ typedef struct {
   int64_t max_it;
   int pc_type;       /* 0 = none, 1 = jacobi */
   int nullspace;     /* 1 = remove constant mode after every PCApply */
-  int op_kind;       /* 0 = 7-term stencil, 1 = faithful 27-term (slow), 2 = compact lapl */
+  int op_kind;       /* 0 = 7-term stencil, 1 = faithful 27-term (slow), 2 = compact lapl,
+                        3 + (R-1) = assembled P (AIJ MatMult order on R z-slabs) */
   int nthreads;      /* OpenMP threads for the 7-term operator/vector ops (1 = serial sums) */
   int mg_levels;     /* pc 3: multigrid levels (0 = automatic), pc 2 = one symmetric RB-SOR sweep */
   int mg_coarse_its; /* symmetric red-black sweeps on the coarsest level */

@@ -214,6 +214,10 @@ struct StencilPlanes {
 enum { PLANES_ALL = 0, PLANES_INTERIOR = 1, PLANES_BOUNDARY = 2 };
 int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
                        const StencilPlanes& gp, int mode);
+// assembled P (pb_assembled.hip): re-sum the seam and slab-boundary rows of y = P x in PETSc AIJ
+// order after the stencil engine produced y (glo / ghi: x's ghost planes, nullptr on one rank)
+int launch_aij_seams(pb_grid* g, const Star& s, const double* x, const double* glo,
+                     const double* ghi, double* y);
 // red-black SOR half-sweep in place (first = 1: zero-start red + black fused, x written from b)
 // and the multigrid residual, on the stencil engine (pb_mg.hip)
 struct CgState;

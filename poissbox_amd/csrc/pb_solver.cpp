@@ -19,7 +19,9 @@ int compact_lapl(pb_grid* g, const double dx[3], const double* f, double* out, d
 int64_t compact_work_len(const pb_grid* g);
 }
 
-static bool fused_kind(int kind) { return kind == PB_OP_STAR7 || kind == PB_OP_ASSEMBLED27; }
+// the fused CG passes evaluate A p inside the stencil engine (reference order); the assembled P
+// (AIJ order at the seams) runs the unfused iteration around its own MatMult
+static bool fused_kind(int kind) { return kind == PB_OP_STAR7; }
 
 struct pb_ksp {
   pb_op* A = nullptr;
@@ -78,11 +80,9 @@ int pb_op_create(pb_grid* g, int kind, const double deltas[3], pb_op** out) {
   return PB_OK;
 }
 
-static int op_apply_raw(pb_op* op, const double* x, double* y) {
+static int star7_apply(pb_op* op, const double* x, double* y) {
   pb_grid* g = op->grid;
   Star s{op->cx, op->cy, op->cz, op->cc};
-  if (op->kind == PB_OP_COMPACT) return compact_lapl_fast(g, op->deltas, x, y, op->work);
-  // STAR7 and ASSEMBLED27 (the assembled BOX matrix has the same 7 non-zeros per row)
   StencilPlanes gp;
   if (!g->ctx->split) {
     gp.ghost_lo = x + (g->nzl - 1) * g->plane;  // periodic wrap: no copy
@@ -102,6 +102,18 @@ static int op_apply_raw(pb_op* op, const double* x, double* y) {
   PB_TRY(launch_star7_apply(g, s, x, y, gp, PLANES_INTERIOR));
   PB_TRY(halo_end(g));
   return launch_star7_apply(g, s, x, y, gp, PLANES_BOUNDARY);
+}
+
+static int op_apply_raw(pb_op* op, const double* x, double* y) {
+  pb_grid* g = op->grid;
+  if (op->kind == PB_OP_COMPACT) return compact_lapl_fast(g, op->deltas, x, y, op->work);
+  PB_TRY(star7_apply(op, x, y));
+  if (op->kind != PB_OP_ASSEMBLED27) return PB_OK;
+  // assembled P: same 7 non-zeros; re-sum the seam / slab-boundary rows in AIJ order (the
+  // ghost planes hold x's halo after the apply on a split grid)
+  Star s{op->cx, op->cy, op->cz, op->cc};
+  const bool split = g->ctx->split;
+  return launch_aij_seams(g, s, x, split ? g->ghost_lo : nullptr, split ? g->ghost_hi : nullptr, y);
 }
 
 int pb_op_apply(pb_op* op, const pb_vec* x, pb_vec* y) {

@@ -50,25 +50,26 @@ def test_failing_host_callback_is_an_error_and_poisons_the_context():
 
 @pytest.mark.gpu
 def test_wait_timeout_is_an_error(monkeypatch):
-    """PB_COMM_TIMEOUT_MS bounds every wait of a split context: with 1 ms, waiting for a queue of
-    512x512x256-slab CG iterations (~0.7 ms each) must fail with PB_ERR_COMM, not block."""
+    """PB_COMM_TIMEOUT_MS bounds every wait of a split context: with 1 ms, waiting for ~1000
+    queued vector updates of a 512x512x128 slab (~0.15 ms each) must fail with PB_ERR_COMM
+    instead of blocking, and the failed context refuses further collectives."""
     monkeypatch.setenv("PB_COMM_TIMEOUT_MS", "1")
     loop = lambda lo, hi: (hi.copy(), lo.copy())  # noqa: E731 - loop-back halo
     ctx = _split_ctx(loop, lambda v: v)
     try:
-        da = pb.initialise_grid(ctx, (512, 512, 512))
-        P, A, x, b = pb.initialise_linear_system(da, da.spacing)
-        b.set_random(1)
-        opts = pb.ksp_options(["-ksp_type", "cg", "-pc_type", "jacobi"], rtol=0.0, atol=0.0,
-                              dtol=1e300, max_it=200)
-        ksp = pb.KSP(A, P, opts)
+        da = pb.initialise_grid(ctx, (512, 512, 256))
+        x, y = pb.Vec(da), pb.Vec(da)
+        y.set_random(1)
+        for _ in range(1000):
+            x.axpy(1e-3, y)
         with pytest.raises(PbError) as e:
-            ksp.begin(b, x)
-            ksp.iterate(200)
-            ksp.end()
+            ctx.sync()
         assert e.value.code == PB_ERR_COMM and "PB_COMM_TIMEOUT_MS" in str(e.value)
         assert ctx.comm_failed
-        for o in (ksp, A, P, x, b, da):
+        with pytest.raises(PbError) as e2:
+            x.norm()
+        assert e2.value.code == PB_ERR_COMM
+        for o in (x, y, da):
             o.destroy()
     finally:
         ctx.destroy()

@@ -76,11 +76,11 @@ def test_stencil_bit_exact(ctx, n):
     y = yv.get_values()
     ref = O.stencil(x, n, h, faithful=N <= 40000)
     assert np.array_equal(y, ref), np.max(np.abs(y - ref))
-    # assembled-P kind applies the same 7 non-zeros (this second apply marches the other z
-    # direction: consecutive applies alternate, so both directions are checked)
+    # assembled P: the same 7 non-zeros, summed in AIJ order on the seams (this second apply
+    # marches the other z direction: consecutive applies alternate, so both are checked)
     P = pb.Mat(da, pb.ASSEMBLED27)
     P.mult(xv, yv)
-    assert np.array_equal(yv.get_values(), ref)
+    assert np.array_equal(yv.get_values(), O.assembled(x, n, h))
     for o in (A, P, xv, yv):
         o.destroy()
     da.destroy()
@@ -309,6 +309,71 @@ def run_ranks(nranks, body):
     if errors:
         raise errors[0]
     return results
+
+
+def test_assembled_check_matrices(ctx):
+    """src/example.f90:235-261 check_matrices: ||A x - P x|| is a rounding-level number (the seam
+    rows sum in AIJ column order), and the GPU reproduces P x bit for bit, so the printed value
+    is the reference's own."""
+    n = (64, 48, 40)
+    h = tuple(1.0 / m for m in n)
+    x = O.fill_random(int(np.prod(n)), SEED)
+    da, xv = grid_vec(ctx, n, x)
+    ya, yp = pb.Vec(da), pb.Vec(da)
+    A, P = pb.Mat(da, pb.STAR7), pb.Mat(da, pb.ASSEMBLED27)
+    A.mult(xv, ya)
+    P.mult(xv, yp)
+    ref_a, ref_p = O.stencil(x, n, h), O.assembled(x, n, h)
+    assert np.array_equal(ya.get_values(), ref_a) and np.array_equal(yp.get_values(), ref_p)
+    ya.axpy(-1.0, yp)
+    d_gpu, d_ref = ya.norm(), float(np.sqrt(np.sum((ref_a - ref_p) ** 2)))
+    assert d_ref > 0 and abs(d_gpu - d_ref) <= 1e-12 * d_ref
+    for o in (A, P, xv, ya, yp):
+        o.destroy()
+    da.destroy()
+
+
+@pytest.mark.parametrize("n", [(16, 12, 10), (31, 12, 10)])
+def test_cg_assembled_operator(ctx, n):
+    """A = P (the demo's assembled branch, src/example.f90:62-64): CG runs on the AIJ-order
+    MatMult and matches the oracle's restatement of the same sums."""
+    h = tuple(1.0 / m for m in n)
+    N = int(np.prod(n))
+    b = O.assembled(O.fill_random(N, SEED), n, h)
+    xo, ro, itso, ho = O.cg_solve(b, n, h, rtol=1e-10, op="assembled")
+    da = pb.DA(ctx, n)
+    P = pb.Mat(da, pb.ASSEMBLED27, h)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(P, P, x, bv, ["-ksp_rtol", "1e-10"])
+    assert (reason, its) == (ro, itso)
+    check_history(hist, ho)
+    check_x(x.get_values(), xo)
+    for o in (P, x, bv):
+        o.destroy()
+    da.destroy()
+
+
+@pytest.mark.parametrize("nranks,n", [(2, (16, 12, 10)), (3, (20, 16, 7)), (4, (12, 10, 5)),
+                                      (3, (64, 32, 40))])
+def test_multirank_assembled_aij_order(nranks, n):
+    """MatMult_MPIAIJ order on z-slabs: owned columns first, then the off-rank (halo) columns --
+    bit-exact against the oracle on every rank, including 1-plane slabs."""
+    N = int(np.prod(n))
+    x = O.fill_random(N, SEED + 1)
+    h = tuple(1.0 / m for m in n)
+    ref = O.assembled(x, n, h, nranks=nranks).reshape(n[2], -1)
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        xv, yv = pb.Vec(da), pb.Vec(da)
+        xv.set_values(x.reshape(n[2], -1)[k0:k0 + nk])
+        pb.Mat(da, pb.ASSEMBLED27).mult(xv, yv)
+        return k0, nk, yv.get_values()
+
+    for k0, nk, y in run_ranks(nranks, body):
+        assert np.array_equal(y, ref[k0:k0 + nk].reshape(-1))
 
 
 @pytest.mark.parametrize("nranks,n", [(2, (16, 12, 10)), (3, (20, 16, 7)), (4, (32, 32, 8))])

@@ -150,6 +150,59 @@ def test_assembled_equals_stencil_interior():
     assert np.max(np.abs(y1 - y2)) <= 1e-12 * np.max(np.abs(y1))
 
 
+def _aij_rows_numpy(x, n, h, nranks):
+    """Independent numpy statement of MatMult on the assembled P: per row, the 27 (col, coeff)
+    pairs of src/coefficients.f90:50-113, sorted as MatMult_SeqAIJ / MatMult_MPIAIJ sums them
+    (owned columns ascending, then off-rank columns ascending), accumulated from 0.0."""
+    nx, ny, nz = n
+    c = O.star_coeffs(h)
+    y = np.empty(nx * ny * nz)
+    bounds = [O_slab(nz, nranks, r) for r in range(nranks)]
+    for r, (k0, nk) in enumerate(bounds):
+        lo, hi = k0 * nx * ny, (k0 + nk) * nx * ny
+        for k in range(k0, k0 + nk):
+            for j in range(ny):
+                for i in range(nx):
+                    ent = []
+                    for m in range(27):
+                        ii, jj, kk = m % 3, (m // 3) % 3, m // 9
+                        col = ((i + ii - 1) % nx) + nx * (((j + jj - 1) % ny) + ny * ((k + kk - 1) % nz))
+                        off = nranks > 1 and not (lo <= col < hi)
+                        ent.append((off, col, c[m]))
+                    s = 0.0
+                    for off, col, cv in sorted(ent):
+                        s += cv * x[col]
+                    y[i + nx * (j + ny * k)] = s
+    return y
+
+
+def O_slab(nz, nranks, r):
+    q, rem = divmod(nz, nranks)
+    return r * q + min(r, rem), q + (1 if r < rem else 0)
+
+
+@pytest.mark.parametrize("n,nranks", [((5, 4, 3), 1), ((4, 3, 7), 1), ((4, 5, 7), 2),
+                                      ((3, 4, 8), 3), ((4, 4, 5), 5)])
+def test_assembled_aij_order(n, nranks):
+    """The oracle's assembled MatMult equals the independent sorted-row statement bit for bit;
+    rows away from every seam equal the 7-point stencil bit for bit."""
+    h = (1 / n[0], 1 / n[1], 1 / n[2])
+    x = O.fill_random(n[0] * n[1] * n[2], 17)
+    y = O.assembled(x, n, h, nranks=nranks)
+    assert np.array_equal(y, _aij_rows_numpy(x, n, h, nranks))
+    ys = O.stencil(x, n, h)
+    assert np.max(np.abs(y - ys)) <= 1e-13 * np.max(np.abs(ys))
+
+
+def test_assembled_interior_rows_equal_stencil():
+    n = (16, 16, 16)
+    h = (1 / 16,) * 3
+    x = O.fill_random(16 ** 3, 5)
+    y, ys = O.assembled(x, n, h).reshape(16, 16, 16), O.stencil(x, n, h).reshape(16, 16, 16)
+    assert np.array_equal(y[1:-1, 1:-1, 1:-1], ys[1:-1, 1:-1, 1:-1])
+    assert not np.array_equal(y, ys)  # the seam rows sum in another order
+
+
 def test_cg_restatement_converges():
     for n, its_rtol5 in ((32, 57), (64, 75)):
         N = n ** 3
