@@ -219,8 +219,10 @@ int pb_pcr_alpha_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_st
                          int64_t elem_stride, double alpha, double* d);
 
 /* ---- compact schemes (replace src/compact_schemes.f90:9-13 public API) ----
- * 3-D fields on the grid (single rank: the grid must not be split across ranks yet).
- * grad/div take 3-component vectors as three pb_vec. stagger: -1 cell->vertex, +1 vertex->cell */
+ * 3-D fields on the grid; grad/div take 3-component vectors as three pb_vec. stagger: -1
+ * cell->vertex, +1 vertex->cell. Reference operation order (bit-identical to the reference). On a
+ * split grid the Z steps run on y-slabs with complete z-lines (all-to-all transposes, as
+ * pb_compact_lapl_fast), so every rank's result is bit-identical to the single-domain one. */
 int pb_compact_grad(pb_grid* grid, const double dx[3], const pb_vec* f, pb_vec* const df[3]);
 int pb_compact_div(pb_grid* grid, const double dx[3], const pb_vec* const f[3], pb_vec* df);
 int pb_compact_interp(pb_grid* grid, int stagger, const pb_vec* f, pb_vec* fi);

@@ -258,30 +258,69 @@ static int launch_line(pb_ctx* ctx, int kind, int stagger, double dx, int64_t n,
   return PB_OK;
 }
 
-// direction d of an nx*ny*nz field
-static LineMap dir_map(const pb_grid* g, int d) {
-  const int64_t nx = g->n[0], ny = g->n[1];
+// direction d of an n0*n1*n2 box (the owned slab: n2 = nzl; or a y-slab with complete z-lines)
+static LineMap dir_map(const int64_t b[3], int d) {
+  const int64_t nx = b[0], ny = b[1];
   if (d == 0) return LineMap{ny, nx, nx * ny, 1};
   if (d == 1) return LineMap{nx, 1, nx * ny, nx};
   return LineMap{nx * ny, 1, 0, nx * ny};
 }
-static int64_t nlines(const pb_grid* g, int d) { return g->nlocal / g->n[d]; }
 
 enum { K_GRAD = 0, K_INTERP = 1 };
 
-static int line3(pb_grid* g, int d, int kind, int stagger, double dx, const double* in,
-                 double* out, const double* in2 = nullptr, const double* addend = nullptr) {
-  return launch_line(g->ctx, kind, stagger, dx, g->n[d], nlines(g, d), dir_map(g, d), in, in2,
-                     addend, out);
+static int line_box(pb_ctx* ctx, const int64_t b[3], int d, int kind, int stagger, double dx,
+                    const double* in, double* out, const double* in2 = nullptr,
+                    const double* addend = nullptr) {
+  return launch_line(ctx, kind, stagger, dx, b[d], b[0] * b[1] * b[2] / b[d], dir_map(b, d), in,
+                     in2, addend, out);
 }
 
-// src/compact_schemes.f90:42-88 grad; scratch 5N
+// x and y lines are complete in every z-slab; z lines too on one rank
+static int line3(pb_grid* g, int d, int kind, int stagger, double dx, const double* in,
+                 double* out, const double* in2 = nullptr, const double* addend = nullptr) {
+  const int64_t b[3] = {g->n[0], g->n[1], g->nzl};
+  return line_box(g->ctx, b, d, kind, stagger, dx, in, out, in2, addend);
+}
+
+// Z steps on a split grid run on y-slabs (complete z-lines; pb_compact_dist.hip transposes):
+// same line kernels, same per-line operation order => bit-identical to one rank. Scratch for
+// them: 4 y-slab fields + the transpose aux space.
+static int64_t zsplit_len(const pb_grid* g) {
+  return g->ctx->split ? 4 * yslab_len(g) + yslab_aux_len(g) : 0;
+}
+
+struct ZSplit {
+  YSlabPlan p;
+  double* y[4];
+  int64_t b[3];
+};
+static int zsplit_begin(pb_grid* g, double* ws, ZSplit* z) {
+  const int64_t L = yslab_len(g);
+  for (int i = 0; i < 4; ++i) z->y[i] = ws + i * L;
+  PB_TRY(yslab_begin(g, ws + 4 * L, &z->p));
+  z->b[0] = g->n[0];
+  z->b[1] = z->p.ny_me;
+  z->b[2] = g->n[2];
+  return PB_OK;
+}
+
+// src/compact_schemes.f90:42-88 grad; scratch 5N (+ zsplit_len)
 static int grad3(pb_grid* g, const double dx[3], const double* f, double* df1, double* df2,
                  double* df3, double* ws) {
   const int64_t N = g->nlocal;
   double *dff1 = ws, *dff3 = ws + N, *dfe1 = ws + 2 * N, *dfe2 = ws + 3 * N, *dfe3 = ws + 4 * N;
-  PB_TRY(line3(g, 2, K_INTERP, -1, 0.0, f, dff1));      // :61
-  PB_TRY(line3(g, 2, K_GRAD, -1, dx[2], f, dff3));      // :63  (dff2 = dff1, :62)
+  if (!g->ctx->split) {
+    PB_TRY(line3(g, 2, K_INTERP, -1, 0.0, f, dff1));    // :61
+    PB_TRY(line3(g, 2, K_GRAD, -1, dx[2], f, dff3));    // :63  (dff2 = dff1, :62)
+  } else {
+    ZSplit z;
+    PB_TRY(zsplit_begin(g, ws + 5 * N, &z));
+    PB_TRY(yslab_to(g, z.p, f, z.y[0]));
+    PB_TRY(line_box(g->ctx, z.b, 2, K_INTERP, -1, 0.0, z.y[0], z.y[1]));
+    PB_TRY(line_box(g->ctx, z.b, 2, K_GRAD, -1, dx[2], z.y[0], z.y[2]));
+    PB_TRY(yslab_from(g, z.p, z.y[1], dff1));
+    PB_TRY(yslab_from(g, z.p, z.y[2], dff3));
+  }
   PB_TRY(line3(g, 1, K_INTERP, -1, 0.0, dff1, dfe1));   // :71
   PB_TRY(line3(g, 1, K_GRAD, -1, dx[1], dff1, dfe2));   // :72
   PB_TRY(line3(g, 1, K_INTERP, -1, 0.0, dff3, dfe3));   // :73
@@ -291,7 +330,7 @@ static int grad3(pb_grid* g, const double dx[3], const double* f, double* df1, d
   return PB_OK;
 }
 
-// src/compact_schemes.f90:207-257 div; scratch 6N
+// src/compact_schemes.f90:207-257 div; scratch 6N (+ zsplit_len)
 static int div3(pb_grid* g, const double dx[3], const double* f1, const double* f2,
                 const double* f3, double* out, double* ws) {
   const int64_t N = g->nlocal;
@@ -303,15 +342,25 @@ static int div3(pb_grid* g, const double dx[3], const double* f1, const double* 
   PB_TRY(line3(g, 1, K_INTERP, +1, 0.0, dfe1, dff1));   // :237
   PB_TRY(line3(g, 1, K_GRAD, +1, dx[1], dfe2, dff2));   // :238
   PB_TRY(line3(g, 1, K_INTERP, +1, 0.0, dfe3, dff3));   // :239
-  double* dfc = dfe1;
-  PB_TRY(line3(g, 2, K_INTERP, +1, 0.0, dff1, dfc, dff2));       // :248 interp(dff1 + dff2)
-  PB_TRY(line3(g, 2, K_GRAD, +1, dx[2], dff3, out, nullptr, dfc));  // :249-250
-  return PB_OK;
+  if (!g->ctx->split) {
+    double* dfc = dfe1;
+    PB_TRY(line3(g, 2, K_INTERP, +1, 0.0, dff1, dfc, dff2));          // :248 interp(dff1 + dff2)
+    PB_TRY(line3(g, 2, K_GRAD, +1, dx[2], dff3, out, nullptr, dfc));  // :249-250
+    return PB_OK;
+  }
+  ZSplit z;
+  PB_TRY(zsplit_begin(g, ws + 6 * N, &z));
+  PB_TRY(yslab_to(g, z.p, dff1, z.y[0]));
+  PB_TRY(yslab_to(g, z.p, dff2, z.y[1]));
+  PB_TRY(yslab_to(g, z.p, dff3, z.y[2]));
+  PB_TRY(line_box(g->ctx, z.b, 2, K_INTERP, +1, 0.0, z.y[0], z.y[3], z.y[1]));
+  PB_TRY(line_box(g->ctx, z.b, 2, K_GRAD, +1, dx[2], z.y[2], z.y[0], nullptr, z.y[3]));
+  return yslab_from(g, z.p, z.y[0], out);
 }
 
-int64_t compact_work_len(const pb_grid* g) { return 9 * g->nlocal; }
+int64_t compact_work_len(const pb_grid* g) { return 9 * g->nlocal + zsplit_len(g); }
 
-// src/compact_schemes.f90:17-37 lapl = div(grad f); work: 9N
+// src/compact_schemes.f90:17-37 lapl = div(grad f); work: 9N (+ zsplit_len)
 int compact_lapl(pb_grid* g, const double dx[3], const double* f, double* out, double* work) {
   ScopedTimer tm(g->ctx, "compact_lapl");
   const int64_t N = g->nlocal;
@@ -427,26 +476,18 @@ int pb_compact_1d_batched(pb_ctx* ctx, int kind, int stagger, double dx, int64_t
                      nullptr, out);
 }
 
-static int single_rank(const pb_grid* g) {
-  return g->ctx->nranks == 1
-             ? PB_OK
-             : set_error(PB_ERR_UNSUPPORTED, "compact operators on a split grid: not yet");
-}
-
 int pb_compact_grad(pb_grid* g, const double dx[3], const pb_vec* f, pb_vec* const df[3]) {
   PB_CHECK_ARG(g && dx && f && df && df[0] && df[1] && df[2], "bad grad args");
-  PB_TRY(single_rank(g));
   double* ws = nullptr;
-  PB_TRY(ctx_scratch(g->ctx, (size_t)(5 * g->nlocal), &ws));
+  PB_TRY(ctx_scratch(g->ctx, (size_t)(5 * g->nlocal + zsplit_len(g)), &ws));
   int rc = grad3(g, dx, f->d, df[0]->d, df[1]->d, df[2]->d, ws);
   return rc;
 }
 
 int pb_compact_div(pb_grid* g, const double dx[3], const pb_vec* const f[3], pb_vec* df) {
   PB_CHECK_ARG(g && dx && f && f[0] && f[1] && f[2] && df, "bad div args");
-  PB_TRY(single_rank(g));
   double* ws = nullptr;
-  PB_TRY(ctx_scratch(g->ctx, (size_t)(6 * g->nlocal), &ws));
+  PB_TRY(ctx_scratch(g->ctx, (size_t)(6 * g->nlocal + zsplit_len(g)), &ws));
   int rc = div3(g, dx, f[0]->d, f[1]->d, f[2]->d, df->d, ws);
   return rc;
 }
@@ -454,11 +495,19 @@ int pb_compact_div(pb_grid* g, const double dx[3], const pb_vec* const f[3], pb_
 int pb_compact_interp(pb_grid* g, int stagger, const pb_vec* f, pb_vec* fi) {
   PB_CHECK_ARG(g && f && fi && f != fi, "bad interp args");
   PB_CHECK_ARG(stagger == -1 || stagger == 1, "stagger must be -1 or +1");
-  PB_TRY(single_rank(g));
   double* ws = nullptr;
   const int64_t N = g->nlocal;
-  PB_TRY(ctx_scratch(g->ctx, (size_t)(2 * N), &ws));
-  int rc = line3(g, 2, K_INTERP, stagger, 0.0, f->d, ws);           // :238
+  PB_TRY(ctx_scratch(g->ctx, (size_t)(2 * N + zsplit_len(g)), &ws));
+  int rc = PB_OK;
+  if (!g->ctx->split) {
+    rc = line3(g, 2, K_INTERP, stagger, 0.0, f->d, ws);             // :238
+  } else {  // the Z step on y-slabs
+    ZSplit z;
+    rc = zsplit_begin(g, ws + 2 * N, &z);
+    if (!rc) rc = yslab_to(g, z.p, f->d, z.y[0]);
+    if (!rc) rc = line_box(g->ctx, z.b, 2, K_INTERP, stagger, 0.0, z.y[0], z.y[1]);
+    if (!rc) rc = yslab_from(g, z.p, z.y[1], ws);
+  }
   if (!rc) rc = line3(g, 1, K_INTERP, stagger, 0.0, ws, ws + N);    // :246
   if (!rc) rc = line3(g, 0, K_INTERP, stagger, 0.0, ws + N, fi->d); // :254
   return rc;
@@ -466,7 +515,6 @@ int pb_compact_interp(pb_grid* g, int stagger, const pb_vec* f, pb_vec* fi) {
 
 int pb_compact_lapl(pb_grid* g, const double dx[3], const pb_vec* f, pb_vec* out) {
   PB_CHECK_ARG(g && dx && f && out && f != out, "bad lapl args");
-  PB_TRY(single_rank(g));
   double* ws = nullptr;
   PB_TRY(ctx_scratch(g->ctx, (size_t)compact_work_len(g), &ws));
   int rc = compact_lapl(g, dx, f->d, out->d, ws);

@@ -38,78 +38,98 @@ __global__ __launch_bounds__(256) void slab_transpose_kernel(double* zs, double*
   }
 }
 
-struct DistPlan {
-  std::vector<int64_t> k0, nzl, j0, nyl;
-  int64_t ny_me = 0;
-};
-
-static DistPlan make_plan(const pb_grid* g) {
+static void make_plan(const pb_grid* g, YSlabPlan* d) {
   const int P = g->ctx->nranks;
-  DistPlan d;
-  d.k0.resize(P);
-  d.nzl.resize(P);
-  d.j0.resize(P);
-  d.nyl.resize(P);
+  d->k0.resize(P);
+  d->nzl.resize(P);
+  d->j0.resize(P);
+  d->nyl.resize(P);
   for (int r = 0; r < P; ++r) {
-    pb_slab_partition(g->n[2], P, r, &d.k0[r], &d.nzl[r]);
-    pb_slab_partition(g->n[1], P, r, &d.j0[r], &d.nyl[r]);
+    pb_slab_partition(g->n[2], P, r, &d->k0[r], &d->nzl[r]);
+    pb_slab_partition(g->n[1], P, r, &d->j0[r], &d->nyl[r]);
   }
-  d.ny_me = d.nyl[g->ctx->rank];
-  return d;
+  d->ny_me = d->nyl[g->ctx->rank];
+  d->ny_slab = g->n[0] * d->ny_me * g->n[2];
 }
 
-// y-slab fields fy, uy, vy (3 * nx * nyl * nz), staging (max of the two slab sizes), and the
-// small rank tables (j -> rank, j0, nyl) as doubles-sized slots
-int64_t compact_dist_work_len(const pb_grid* g) {
-  const DistPlan d = make_plan(g);
-  const int64_t ny_slab = g->n[0] * d.ny_me * g->n[2];
+int64_t yslab_len(const pb_grid* g) {
+  YSlabPlan d;
+  make_plan(g, &d);
+  return d.ny_slab;
+}
+
+// staging (max of the two slab sizes) and the small rank tables (j -> rank, j0, nyl) as
+// doubles-sized slots
+int64_t yslab_aux_len(const pb_grid* g) {
   const int64_t tables = (g->n[1] + 2 * g->ctx->nranks + 1) / 2 + 1;
-  return 3 * ny_slab + std::max<int64_t>(ny_slab, g->nlocal) + tables;
+  return std::max<int64_t>(yslab_len(g), g->nlocal) + tables;
 }
 
-int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double* v, double* work) {
+int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p) {
   pb_ctx* ctx = g->ctx;
-  const int P = ctx->nranks, me = ctx->rank;
-  if (g->n[1] < P) return set_error(PB_ERR_UNSUPPORTED, "compact operator: ny < ranks");
-  const DistPlan d = make_plan(g);
-  const int64_t nx = g->n[0], ny = g->n[1], nz = g->n[2];
-  const int64_t ny_slab = nx * d.ny_me * nz;
-  double* fy = work;
-  double* uy = fy + ny_slab;
-  double* vy = uy + ny_slab;
-  double* stage = vy + ny_slab;
-  int* tab = (int*)(stage + std::max<int64_t>(ny_slab, g->nlocal));
+  const int P = ctx->nranks;
+  if (g->n[1] < P) return set_error(PB_ERR_UNSUPPORTED, "compact operators: ny < ranks");
+  make_plan(g, p);
+  const int64_t nx = g->n[0], ny = g->n[1];
+  p->stage = aux;
+  p->tab = (int*)(aux + std::max<int64_t>(p->ny_slab, g->nlocal));
   // rank tables (tiny, uploaded per call on the stream)
   std::vector<int> htab(ny + 2 * P);
   for (int r = 0; r < P; ++r) {
-    for (int64_t j = d.j0[r]; j < d.j0[r] + d.nyl[r]; ++j) htab[j] = r;
-    htab[ny + r] = (int)d.j0[r];
-    htab[ny + P + r] = (int)d.nyl[r];
+    for (int64_t j = p->j0[r]; j < p->j0[r] + p->nyl[r]; ++j) htab[j] = r;
+    htab[ny + r] = (int)p->j0[r];
+    htab[ny + P + r] = (int)p->nyl[r];
   }
-  PB_HIP(hipMemcpyAsync(tab, htab.data(), htab.size() * sizeof(int), hipMemcpyHostToDevice,
+  PB_HIP(hipMemcpyAsync(p->tab, htab.data(), htab.size() * sizeof(int), hipMemcpyHostToDevice,
                         ctx->stream));
-  std::vector<int64_t> zc(P), yc(P);  // z-slab block for rank p; y-slab block from rank p
-  for (int p = 0; p < P; ++p) {
-    zc[p] = g->nzl * nx * d.nyl[p];
-    yc[p] = d.nzl[p] * nx * d.ny_me;
-  }
-  const int nb = (int)std::min<int64_t>((g->nlocal + 255) / 256, (int64_t)ctx->num_cus * 16);
-  hipLaunchKernelGGL(slab_transpose_kernel, dim3(nb), dim3(256), 0, ctx->stream,
-                     const_cast<double*>(f), stage, (int)nx, (int)ny, (int)g->nzl, tab, tab + ny,
-                     tab + ny + P, 0);
-  PB_HIP(hipGetLastError());
   PB_SYNC(ctx, "compact transpose");  // htab stays valid until the copy is done
-  PB_TRY(alltoallv_device(ctx, stage, zc.data(), fy, yc.data()));
-  const int64_t dy[3] = {nx, d.ny_me, nz};
-  PB_TRY(compact_pass_z(ctx, dy, h, fy, uy, vy));
-  for (int f2 = 0; f2 < 2; ++f2) {
-    PB_TRY(alltoallv_device(ctx, f2 ? vy : uy, yc.data(), stage, zc.data()));
-    hipLaunchKernelGGL(slab_transpose_kernel, dim3(nb), dim3(256), 0, ctx->stream, f2 ? v : u,
-                       stage, (int)nx, (int)ny, (int)g->nzl, tab, tab + ny, tab + ny + P, 1);
-    PB_HIP(hipGetLastError());
+  p->zc.resize(P);  // z-slab block for rank q; y-slab block from rank q
+  p->yc.resize(P);
+  for (int q = 0; q < P; ++q) {
+    p->zc[q] = g->nzl * nx * p->nyl[q];
+    p->yc[q] = p->nzl[q] * nx * p->ny_me;
   }
-  (void)me;
+  p->nb = (int)std::min<int64_t>((g->nlocal + 255) / 256, (int64_t)ctx->num_cus * 16);
   return PB_OK;
+}
+
+int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy) {
+  pb_ctx* ctx = g->ctx;
+  const int64_t ny = g->n[1];
+  const int P = ctx->nranks;
+  hipLaunchKernelGGL(slab_transpose_kernel, dim3(p.nb), dim3(256), 0, ctx->stream,
+                     const_cast<double*>(f), p.stage, (int)g->n[0], (int)ny, (int)g->nzl, p.tab,
+                     p.tab + ny, p.tab + ny + P, 0);
+  PB_HIP(hipGetLastError());
+  return alltoallv_device(ctx, p.stage, p.zc.data(), fy, p.yc.data());
+}
+
+int yslab_from(pb_grid* g, const YSlabPlan& p, const double* fy, double* f) {
+  pb_ctx* ctx = g->ctx;
+  const int64_t ny = g->n[1];
+  const int P = ctx->nranks;
+  PB_TRY(alltoallv_device(ctx, fy, p.yc.data(), p.stage, p.zc.data()));
+  hipLaunchKernelGGL(slab_transpose_kernel, dim3(p.nb), dim3(256), 0, ctx->stream, f, p.stage,
+                     (int)g->n[0], (int)ny, (int)g->nzl, p.tab, p.tab + ny, p.tab + ny + P, 1);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+// y-slab fields fy, uy, vy and the transpose aux space
+int64_t compact_dist_work_len(const pb_grid* g) { return 3 * yslab_len(g) + yslab_aux_len(g); }
+
+int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double* v, double* work) {
+  const int64_t ny_slab = yslab_len(g);
+  double* fy = work;
+  double* uy = fy + ny_slab;
+  double* vy = uy + ny_slab;
+  YSlabPlan p;
+  PB_TRY(yslab_begin(g, vy + ny_slab, &p));
+  PB_TRY(yslab_to(g, p, f, fy));
+  const int64_t dy[3] = {g->n[0], p.ny_me, g->n[2]};
+  PB_TRY(compact_pass_z(g->ctx, dy, h, fy, uy, vy));
+  PB_TRY(yslab_from(g, p, uy, u));
+  return yslab_from(g, p, vy, v);
 }
 
 }  // namespace pb

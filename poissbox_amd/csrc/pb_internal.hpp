@@ -298,6 +298,20 @@ int compact_pass_x(pb_ctx* ctx, const int64_t d[3], double h, const double* s, c
 // ---- multi-rank Z pass: z-slab <-> y-slab all-to-all transposes (compact_dist.cpp) ----
 int64_t compact_dist_work_len(const pb_grid* g);
 int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double* v, double* work);
+// z-slab <-> y-slab transposes (rank r holds rows [j0_r, j0_r + nyl_r) of every plane: complete
+// z-lines) for line operations along z on a split grid; pb_compact_dist.hip
+struct YSlabPlan {
+  std::vector<int64_t> k0, nzl, j0, nyl, zc, yc;
+  int64_t ny_me = 0, ny_slab = 0;  // this rank's y rows; doubles of one y-slab field
+  double* stage = nullptr;
+  int* tab = nullptr;
+  int nb = 0;
+};
+int64_t yslab_len(const pb_grid* g);
+int64_t yslab_aux_len(const pb_grid* g);
+int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p);  // aux: yslab_aux_len doubles
+int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy);
+int yslab_from(pb_grid* g, const YSlabPlan& p, const double* fy, double* f);
 // all-to-all with per-peer counts; blocks are contiguous in rank order on both sides
 int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,
                      const int64_t* rcount);

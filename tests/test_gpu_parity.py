@@ -794,6 +794,47 @@ def test_multirank_mg_bit_exact_and_cg(monkeypatch, kern, nranks, n):
 # ---------------------------------------------------------------------------------------------
 # compact Laplacian / compact CG on a split grid (z-slab <-> y-slab all-to-all transposes)
 # ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("op", ["grad", "div", "interp", "interp_div", "lapl"])
+@pytest.mark.parametrize("nranks,n", [(2, (16, 12, 10)), (3, (12, 9, 7)), (4, (8, 8, 13))])
+def test_multirank_compact_reference_order(nranks, n, op):
+    """src/compact_schemes.f90:17-257 in the reference's operation order on a split grid: the Z
+    steps run on y-slabs (complete z-lines), so every rank's slab is bit-identical to the
+    oracle's single-domain result (itself bit-exact against the flang-built reference)."""
+    N = int(np.prod(n))
+    h = tuple(2 * np.pi / m for m in n)
+    f = O.fill_random(3 * N if op == "div" else N, 91)
+    if op == "grad":
+        ref = O.grad(f, n, h).reshape(3, n[2], -1)
+    elif op == "div":
+        ref = O.div(f, n, h).reshape(1, n[2], -1)
+    elif op == "lapl":
+        ref = O.lapl(f, n, h).reshape(1, n[2], -1)
+    else:
+        ref = O.interp(f, n, -1 if op == "interp" else 1).reshape(1, n[2], -1)
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n, (2 * np.pi,) * 3)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        comps = f.reshape(-1, n[2], n[1] * n[0])
+        ins = [pb.Vec(da) for _ in range(comps.shape[0])]
+        for c, v in enumerate(ins):
+            v.set_values(comps[c, k0:k0 + nk])
+        outs = [pb.Vec(da) for _ in range(3 if op == "grad" else 1)]
+        if op == "grad":
+            pb.compact_grad(da, h, ins[0], outs)
+        elif op == "div":
+            pb.compact_div(da, h, ins, outs[0])
+        elif op == "lapl":
+            pb.compact_lapl(da, h, ins[0], outs[0])
+        else:
+            pb.compact_interp(da, -1 if op == "interp" else 1, ins[0], outs[0])
+        return k0, nk, [o.get_values() for o in outs]
+
+    for k0, nk, got in run_ranks(nranks, body):
+        for c, y in enumerate(got):
+            assert np.array_equal(y, ref[c, k0:k0 + nk].reshape(-1)), (op, c, k0)
+
+
 @pytest.mark.parametrize("nranks,n", [(2, (64, 32, 128)), (3, (64, 48, 64)), (4, (32, 16, 20))])
 def test_multirank_compact_lapl(nranks, n):
     N = int(np.prod(n))
