@@ -47,6 +47,10 @@ typedef struct pb_ksp pb_ksp;   /* KSP analogue                                 
 
 const char* pb_last_error(void);
 int pb_version(int* major, int* minor);
+/* src/coefficients.f90:22-48: lapl_1d_coeffs (c = [1, -2, 1] / dx^2) and lapl_star_coeffs (the
+ * 3x3x3 box, column-major, of the 7-point star) -- the coefficients every operator here uses. */
+int pb_lapl_1d_coeffs(double dx, double c[3]);
+int pb_lapl_star_coeffs(double dx, double dy, double dz, double c[27]);
 
 /* ---- context / communicator (replaces MPI_Init + PetscInitialize, src/example.f90:43-47) ---- */
 /* 128-byte RCCL unique id; rank 0 creates it and the caller broadcasts it (any channel). */
@@ -71,6 +75,20 @@ typedef int (*pb_alltoallv_fn)(void* user, const double* send, const int64_t* se
                                double* recv, const int64_t* recv_counts);
 int pb_ctx_set_host_alltoallv(pb_ctx* ctx, pb_alltoallv_fn alltoallv, void* user);
 int pb_ctx_get_rank(const pb_ctx* ctx, int* rank, int* nranks);
+/* Launcher-agnostic start (≙ MPI_Init + MPI_Comm_rank/size, src/example.f90:43-47): the rank
+ * layout comes from RANK/WORLD_SIZE/LOCAL_RANK (torchrun --no-python), OMPI_COMM_WORLD_* (mpirun)
+ * or PMI_RANK/PMI_SIZE; one process = rank 0 of 1 on `device` (-1: LOCAL_RANK). Several ranks
+ * take GPU LOCAL_RANK mod visible GPUs (PB_DEVICE overrides) and connect over
+ *   PB_TRANSPORT=rccl (default when every rank has its own GPU): rank 0's unique id is passed in
+ *     a file PB_RENDEZVOUS_DIR/pb_uid_<job> (default /tmp; job = PB_JOB_ID, else MASTER_PORT),
+ *     removed once the communicator is up;
+ *   PB_TRANSPORT=shm (default when ranks outnumber GPUs): a built-in POSIX shared-memory host
+ *     transport (halo planes and scalar sums; ranks may share one GPU; no all-to-all, so the
+ *     compact operators need RCCL or a host alltoallv callback on a split grid). */
+int pb_ctx_create_from_env(int device, pb_ctx** ctx);
+/* In-place SUM over all ranks of `count` (<= 32) host doubles (≙ MPI_Allreduce(MPI_SUM) of the
+ * reference driver's checks, src/example.f90:108,137-147,194). */
+int pb_ctx_allreduce_host(pb_ctx* ctx, double* vals, int count);
 int pb_ctx_sync(pb_ctx* ctx);  /* stream synchronize (≙ MPI_Barrier for device work) */
 int pb_ctx_barrier(pb_ctx* ctx); /* synchronize + all ranks rendezvous */
 /* Failure handling on multi-rank contexts (the reference's MPI calls would hang or abort): every
@@ -134,6 +152,9 @@ enum pb_op_kind {
  * KSP operator (A = P, src/example.f90:62-64) it runs the unfused CG iteration. */
 int pb_op_create(pb_grid* grid, int kind, const double deltas[3], pb_op** op);
 int pb_op_apply(pb_op* op, const pb_vec* x, pb_vec* y); /* ≙ MatMult(A, x, y) */
+/* ≙ assemble_laplacian(da, dx, dy, dz, M) (src/coefficients.f90:50-113): (re)set the spacings
+ * the operator's coefficients are built from (lapl_star_coeffs). */
+int pb_op_set_deltas(pb_op* op, const double deltas[3]);
 int pb_op_get_diagonal(const pb_op* op, double* diag);  /* constant diagonal of the 7-pt P */
 int pb_op_destroy(pb_op* op);
 /* ≙ MatGetOwnershipRange / VecGetOwnershipRange (src/example.f90:137-147): global row range
@@ -213,6 +234,11 @@ int pb_solve(pb_op* A, pb_op* P, const pb_ksp_opts* opts, const pb_vec* b, pb_ve
 int pb_tdma_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
                     int64_t elem_stride, const double* a, double* b, const double* c, double* d,
                     int periodic);
+/* fwd_sweep (which = 1: a, b, c, d -> modified b, d) or bwd_sweep (which = 2: b, c, d -> x in d;
+ * a unused) alone, src/tridsol.f90:76-115 (exported by the reference for its tests). */
+int pb_tdma_sweeps_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                           int64_t elem_stride, const double* a, double* b, const double* c,
+                           double* d, int which);
 /* Constant-coefficient periodic (alpha, 1, alpha) systems -- the compact-scheme solves
  * (src/compact_schemes.f90:197,312) -- by parallel cyclic reduction, in place on d. */
 int pb_pcr_alpha_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
@@ -236,6 +262,30 @@ int pb_compact_lapl_fast(pb_grid* grid, const double dx[3], const pb_vec* f, pb_
 int pb_compact_1d_batched(pb_ctx* ctx, int kind, int stagger, double dx, int64_t n,
                           int64_t nbatch, int64_t line_stride, int64_t elem_stride,
                           const double* f, double* out);
+
+/* ---- host-array forms of the module procedures (src/tridsol.f90:16-18, compact_schemes.f90:9-13):
+ * the reference works on process-local Fortran arrays, so these take host pointers, stage them
+ * through device memory, run the kernels above and copy back (synchronous). The Fortran modules
+ * `tridsol` and `compact_schemes` in poissbox_amd/fortran wrap them with the reference's
+ * assumed-shape signatures. 3-D fields are whole arrays of shape n (never split, whatever the
+ * context); vector fields are (nx, ny, nz, 3) with the component slowest. ---- */
+int pb_tdma_batched_host(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                         int64_t elem_stride, const double* a, double* b, const double* c,
+                         double* d, int periodic);
+int pb_tdma_sweeps_batched_host(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                                int64_t elem_stride, const double* a, double* b, const double* c,
+                                double* d, int which);
+int pb_compact_1d_batched_host(pb_ctx* ctx, int kind, int stagger, double dx, int64_t n,
+                               int64_t nbatch, int64_t line_stride, int64_t elem_stride,
+                               const double* f, double* out);
+int pb_compact_grad_host(pb_ctx* ctx, const int64_t n[3], const double dx[3], const double* f,
+                         double* df);
+int pb_compact_div_host(pb_ctx* ctx, const int64_t n[3], const double dx[3], const double* f,
+                        double* df);
+int pb_compact_interp_host(pb_ctx* ctx, const int64_t n[3], int stagger, const double* f,
+                           double* fi);
+int pb_compact_lapl_host(pb_ctx* ctx, const int64_t n[3], const double dx[3], const double* f,
+                         double* out);
 
 #ifdef __cplusplus
 }

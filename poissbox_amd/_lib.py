@@ -44,6 +44,8 @@ ALLTOALLV_FN = C.CFUNCTYPE(C.c_int, c_p, P_d, P_i64, P_d, P_i64)
 _SIGS = {
     "pb_last_error": [],
     "pb_version": [C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "pb_lapl_1d_coeffs": [c_d, P_d],
+    "pb_lapl_star_coeffs": [c_d, c_d, c_d, P_d],
     "pb_comm_unique_id": [C.c_char_p],
     "pb_ctx_create": [C.c_int, C.c_int, C.c_int, C.c_char_p, C.POINTER(c_p)],
     "pb_ctx_set_host_transport": [c_p, SENDRECV_FN, ALLREDUCE_FN, c_p],
@@ -52,6 +54,8 @@ _SIGS = {
     "pb_ctx_sync": [c_p],
     "pb_ctx_barrier": [c_p],
     "pb_ctx_comm_status": [c_p, C.POINTER(C.c_int)],
+    "pb_ctx_create_from_env": [C.c_int, C.POINTER(c_p)],
+    "pb_ctx_allreduce_host": [c_p, P_d, C.c_int],
     "pb_ctx_destroy": [c_p],
     "pb_ctx_set_timing": [c_p, C.c_int],
     "pb_ctx_get_timing": [c_p, C.c_char_p, P_d, P_i64],
@@ -78,6 +82,7 @@ _SIGS = {
     "pb_vec_device_ptr": [c_p, C.POINTER(c_p), P_i64],
     "pb_op_create": [c_p, C.c_int, P_d, C.POINTER(c_p)],
     "pb_op_apply": [c_p, c_p, c_p],
+    "pb_op_set_deltas": [c_p, P_d],
     "pb_op_get_diagonal": [c_p, P_d],
     "pb_op_destroy": [c_p],
     "pb_op_get_ownership_range": [c_p, P_i64, P_i64],
@@ -101,6 +106,16 @@ _SIGS = {
     "pb_compact_lapl": [c_p, P_d, c_p, c_p],
     "pb_compact_lapl_fast": [c_p, P_d, c_p, c_p],
     "pb_compact_1d_batched": [c_p, C.c_int, C.c_int, c_d, c_i64, c_i64, c_i64, c_i64, c_p, c_p],
+    "pb_tdma_sweeps_batched": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, C.c_int],
+    "pb_tdma_sweeps_batched_host": [c_p, c_i64, c_i64, c_i64, c_i64, P_d, P_d, P_d, P_d,
+                                    C.c_int],
+    "pb_tdma_batched_host": [c_p, c_i64, c_i64, c_i64, c_i64, P_d, P_d, P_d, P_d, C.c_int],
+    "pb_compact_1d_batched_host": [c_p, C.c_int, C.c_int, c_d, c_i64, c_i64, c_i64, c_i64, P_d,
+                                   P_d],
+    "pb_compact_grad_host": [c_p, P_i64, P_d, P_d, P_d],
+    "pb_compact_div_host": [c_p, P_i64, P_d, P_d, P_d],
+    "pb_compact_interp_host": [c_p, P_i64, C.c_int, P_d, P_d],
+    "pb_compact_lapl_host": [c_p, P_i64, P_d, P_d, P_d],
 }
 _RESTYPES = {"pb_last_error": C.c_char_p}
 

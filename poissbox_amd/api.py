@@ -65,6 +65,26 @@ class Context:
         self.rank, self.nranks = rank, nranks
         self._keep = []
 
+    @classmethod
+    def from_env(cls, device=-1):
+        """pb_ctx_create_from_env: rank layout from the launcher's environment (torchrun / mpirun /
+        PMI), RCCL or the built-in shared-memory transport (PB_TRANSPORT)."""
+        self = cls.__new__(cls)
+        h = C.c_void_p()
+        L.call("pb_ctx_create_from_env", int(device), C.byref(h))
+        self.h = h
+        r, n = C.c_int(), C.c_int()
+        L.call("pb_ctx_get_rank", h, C.byref(r), C.byref(n))
+        self.rank, self.nranks = r.value, n.value
+        self._keep = []
+        return self
+
+    def allreduce_sum(self, vals):
+        """SUM over ranks of a few host doubles (MPI_Allreduce of the reference's checks)."""
+        a = np.ascontiguousarray(vals, dtype=np.float64).reshape(-1).copy()
+        L.call("pb_ctx_allreduce_host", self.h, _dptr(a), a.size)
+        return a
+
     def set_host_transport(self, sendrecv, allreduce, alltoallv=None):
         """sendrecv(send_lo, send_hi) -> (recv_lo, recv_hi) numpy arrays; allreduce(vals) -> vals;
         alltoallv(list of per-rank send blocks, list of per-rank receive sizes) -> list of
@@ -397,6 +417,30 @@ def compact_interp(da, stagger, f, fi):
 
 def compact_lapl(da, dx, f, out):
     L.call("pb_compact_lapl", da.h, _d_3(dx), f.h, out.h)
+
+
+# host-array forms (the reference's module procedures on process-local arrays)
+def tdma_host(ctx, a, b, c, d, periodic=False):
+    """tdma / tdma_periodic (src/tridsol.f90:22-74) on host arrays, batched over leading axes:
+    the last axis is the line. b and d are updated in place like the reference."""
+    for v in (a, b, c, d):
+        assert v.dtype == np.float64 and v.flags.c_contiguous and v.shape == d.shape
+    n = d.shape[-1]
+    L.call("pb_tdma_batched_host", ctx.h, n, d.size // n, n, 1, _dptr(a), _dptr(b), _dptr(c),
+           _dptr(d), int(bool(periodic)))
+
+
+def compact_host(ctx, op, f, n, dx=(1.0, 1.0, 1.0), stagger=-1):
+    """grad / div / interp / lapl (src/compact_schemes.f90) on whole host arrays (C order
+    [c][k][j][i] == Fortran (i, j, k, c)); returns the result array."""
+    f = np.ascontiguousarray(f, dtype=np.float64).reshape(-1)
+    N = int(np.prod(n))
+    out = np.empty(3 * N if op == "grad" else N)
+    if op == "interp":
+        L.call("pb_compact_interp_host", ctx.h, _i64_3(n), int(stagger), _dptr(f), _dptr(out))
+    else:
+        L.call(f"pb_compact_{op}_host", ctx.h, _i64_3(n), _d_3(dx), _dptr(f), _dptr(out))
+    return out
 
 
 def compact_lapl_fast(da, dx, f, out):

@@ -62,6 +62,37 @@ __global__ __launch_bounds__(64) void tdma_kernel(int64_t n, int64_t nb, LineMap
   }
 }
 
+// fwd_sweep (:76-96) or bwd_sweep (:98-115) alone (the reference exports both for its tests)
+__global__ __launch_bounds__(64) void tdma_sweep_kernel(int64_t n, int64_t nb, LineMap lm,
+                                                        const double* __restrict__ a,
+                                                        double* __restrict__ b,
+                                                        const double* __restrict__ c,
+                                                        double* __restrict__ d, int which) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= nb) return;
+  const int64_t o = lm.base(l), es = lm.es;
+  if (which == 1) {
+    double bp = b[o], cp = c[o], dp = d[o];
+    for (int64_t i = 1; i < n; ++i) {
+      const int64_t e = o + i * es;
+      const double w = a[e] / bp;
+      bp = b[e] - w * cp;
+      dp = d[e] - w * dp;
+      cp = c[e];
+      b[e] = bp;
+      d[e] = dp;
+    }
+    return;
+  }
+  double xn = d[o + (n - 1) * es] / b[o + (n - 1) * es];
+  d[o + (n - 1) * es] = xn;
+  for (int64_t i = n - 2; i >= 0; --i) {
+    const int64_t e = o + i * es;
+    xn = (d[e] - c[e] * xn) / b[e];
+    d[e] = xn;
+  }
+}
+
 // tdma_periodic :34-74; the two auxiliary Thomas solves share one forward elimination of bmod
 // (the reference recomputes bmod identically for the second solve). scratch: 2*n per line,
 // element i of line l at [i*nb + l] (coalesced across lines).
@@ -286,7 +317,7 @@ static int line3(pb_grid* g, int d, int kind, int stagger, double dx, const doub
 // same line kernels, same per-line operation order => bit-identical to one rank. Scratch for
 // them: 4 y-slab fields + the transpose aux space.
 static int64_t zsplit_len(const pb_grid* g) {
-  return g->ctx->split ? 4 * yslab_len(g) + yslab_aux_len(g) : 0;
+  return grid_split(g) ? 4 * yslab_len(g) + yslab_aux_len(g) : 0;
 }
 
 struct ZSplit {
@@ -309,7 +340,7 @@ static int grad3(pb_grid* g, const double dx[3], const double* f, double* df1, d
                  double* df3, double* ws) {
   const int64_t N = g->nlocal;
   double *dff1 = ws, *dff3 = ws + N, *dfe1 = ws + 2 * N, *dfe2 = ws + 3 * N, *dfe3 = ws + 4 * N;
-  if (!g->ctx->split) {
+  if (!grid_split(g)) {
     PB_TRY(line3(g, 2, K_INTERP, -1, 0.0, f, dff1));    // :61
     PB_TRY(line3(g, 2, K_GRAD, -1, dx[2], f, dff3));    // :63  (dff2 = dff1, :62)
   } else {
@@ -342,7 +373,7 @@ static int div3(pb_grid* g, const double dx[3], const double* f1, const double* 
   PB_TRY(line3(g, 1, K_INTERP, +1, 0.0, dfe1, dff1));   // :237
   PB_TRY(line3(g, 1, K_GRAD, +1, dx[1], dfe2, dff2));   // :238
   PB_TRY(line3(g, 1, K_INTERP, +1, 0.0, dfe3, dff3));   // :239
-  if (!g->ctx->split) {
+  if (!grid_split(g)) {
     double* dfc = dfe1;
     PB_TRY(line3(g, 2, K_INTERP, +1, 0.0, dff1, dfc, dff2));          // :248 interp(dff1 + dff2)
     PB_TRY(line3(g, 2, K_GRAD, +1, dx[2], dff3, out, nullptr, dfc));  // :249-250
@@ -443,6 +474,20 @@ int pb_tdma_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
   return PB_OK;
 }
 
+int pb_tdma_sweeps_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                           int64_t elem_stride, const double* a, double* b, const double* c,
+                           double* d, int which) {
+  PB_CHECK_ARG(ctx && b && c && d && (which == 2 || a), "bad sweep args");
+  PB_CHECK_ARG(which == 1 || which == 2, "which: 1 = fwd_sweep, 2 = bwd_sweep");
+  PB_CHECK_ARG(n >= 2 && nbatch >= 1, "bad sweep sizes");
+  LineMap lm{nbatch, line_stride, 0, elem_stride};
+  ScopedTimer tm(ctx, "tdma");
+  hipLaunchKernelGGL(tdma_sweep_kernel, dim3((unsigned)((nbatch + 63) / 64)), dim3(64), 0,
+                     ctx->stream, n, nbatch, lm, a, b, c, d, which);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
 int pb_pcr_alpha_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
                          int64_t elem_stride, double alpha, double* d) {
   PB_CHECK_ARG(ctx && d, "bad pcr args");
@@ -499,7 +544,7 @@ int pb_compact_interp(pb_grid* g, int stagger, const pb_vec* f, pb_vec* fi) {
   const int64_t N = g->nlocal;
   PB_TRY(ctx_scratch(g->ctx, (size_t)(2 * N + zsplit_len(g)), &ws));
   int rc = PB_OK;
-  if (!g->ctx->split) {
+  if (!grid_split(g)) {
     rc = line3(g, 2, K_INTERP, stagger, 0.0, f->d, ws);             // :238
   } else {  // the Z step on y-slabs
     ZSplit z;
@@ -519,6 +564,155 @@ int pb_compact_lapl(pb_grid* g, const double dx[3], const pb_vec* f, pb_vec* out
   PB_TRY(ctx_scratch(g->ctx, (size_t)compact_work_len(g), &ws));
   int rc = compact_lapl(g, dx, f->d, out->d, ws);
   return rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host-array forms: the reference's module procedures (src/tridsol.f90:16-18,
+// src/compact_schemes.f90:9-13) take plain process-local Fortran arrays. These stage them through
+// device memory, run the same kernels and copy back (synchronous; convenience, not the fast path).
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct DevBuf {
+  double* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+int stage_in(pb_ctx* ctx, DevBuf& b, size_t n, const double* host) {
+  if (hipMalloc(&b.p, std::max<size_t>(n, 1) * sizeof(double)) != hipSuccess)
+    return set_error(PB_ERR_ALLOC, "host-array staging of %zu doubles: out of device memory", n);
+  if (host)
+    PB_HIP(hipMemcpyAsync(b.p, host, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  return PB_OK;
+}
+int stage_out(pb_ctx* ctx, const DevBuf& b, size_t n, double* host) {
+  PB_HIP(hipMemcpyAsync(host, b.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  PB_SYNC(ctx, "host-array copy-out");
+  return PB_OK;
+}
+int64_t extent(int64_t n, int64_t nbatch, int64_t ls, int64_t es) {
+  return (nbatch - 1) * ls + (n - 1) * es + 1;
+}
+// a process-local grid of the array's shape (never split, whatever the context)
+struct LocalGrid {
+  pb_grid* g = nullptr;
+  ~LocalGrid() {
+    if (g) pb_grid_destroy(g);
+  }
+};
+int local_grid(pb_ctx* ctx, const int64_t n[3], LocalGrid& lg) {
+  for (int d = 0; d < 3; ++d) PB_CHECK_ARG(n[d] >= 3, "compact operators need n >= 3");
+  PB_TRY(grid_create_part(ctx, n, nullptr, 0, n[2], &lg.g));
+  lg.g->whole = true;
+  return PB_OK;
+}
+}  // namespace
+
+int pb_tdma_batched_host(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                         int64_t elem_stride, const double* a, double* b, const double* c,
+                         double* d, int periodic) {
+  PB_CHECK_ARG(ctx && a && b && c && d && line_stride >= 0 && elem_stride >= 1, "bad tdma args");
+  PB_CHECK_ARG(n >= 2 && nbatch >= 1, "bad tdma sizes");
+  const size_t E = (size_t)extent(n, nbatch, line_stride, elem_stride);
+  DevBuf da, db, dc, dd;
+  PB_TRY(stage_in(ctx, da, E, a));
+  PB_TRY(stage_in(ctx, db, E, b));
+  PB_TRY(stage_in(ctx, dc, E, c));
+  PB_TRY(stage_in(ctx, dd, E, d));
+  PB_TRY(pb_tdma_batched(ctx, n, nbatch, line_stride, elem_stride, da.p, db.p, dc.p, dd.p,
+                         periodic));
+  if (!periodic) PB_TRY(stage_out(ctx, db, E, b));  // tdma overwrites b (src/tridsol.f90:22-32)
+  return stage_out(ctx, dd, E, d);
+}
+
+int pb_tdma_sweeps_batched_host(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
+                                int64_t elem_stride, const double* a, double* b, const double* c,
+                                double* d, int which) {
+  PB_CHECK_ARG(ctx && b && c && d && (which == 2 || a) && line_stride >= 0 && elem_stride >= 1,
+               "bad sweep args");
+  PB_CHECK_ARG(n >= 2 && nbatch >= 1, "bad sweep sizes");
+  const size_t E = (size_t)extent(n, nbatch, line_stride, elem_stride);
+  DevBuf da, db, dc, dd;
+  if (which == 1) PB_TRY(stage_in(ctx, da, E, a));
+  PB_TRY(stage_in(ctx, db, E, b));
+  PB_TRY(stage_in(ctx, dc, E, c));
+  PB_TRY(stage_in(ctx, dd, E, d));
+  PB_TRY(pb_tdma_sweeps_batched(ctx, n, nbatch, line_stride, elem_stride, da.p, db.p, dc.p, dd.p,
+                                which));
+  if (which == 1) PB_TRY(stage_out(ctx, db, E, b));
+  return stage_out(ctx, dd, E, d);
+}
+
+int pb_compact_1d_batched_host(pb_ctx* ctx, int kind, int stagger, double dx, int64_t n,
+                               int64_t nbatch, int64_t line_stride, int64_t elem_stride,
+                               const double* f, double* out) {
+  PB_CHECK_ARG(ctx && f && out && line_stride >= 0 && elem_stride >= 1, "bad compact_1d args");
+  PB_CHECK_ARG(n >= 3 && nbatch >= 1, "compact_1d: n >= 3");
+  const size_t E = (size_t)extent(n, nbatch, line_stride, elem_stride);
+  DevBuf df, dout;
+  PB_TRY(stage_in(ctx, df, E, f));
+  PB_TRY(stage_in(ctx, dout, E, out));  // untouched gaps of a strided layout keep their values
+  PB_TRY(pb_compact_1d_batched(ctx, kind, stagger, dx, n, nbatch, line_stride, elem_stride, df.p,
+                               dout.p));
+  return stage_out(ctx, dout, E, out);
+}
+
+int pb_compact_grad_host(pb_ctx* ctx, const int64_t n[3], const double dx[3], const double* f,
+                         double* df) {
+  PB_CHECK_ARG(ctx && n && dx && f && df, "bad grad args");
+  LocalGrid lg;
+  PB_TRY(local_grid(ctx, n, lg));
+  const size_t N = (size_t)lg.g->nlocal;
+  DevBuf d, o, w;
+  PB_TRY(stage_in(ctx, d, N, f));
+  PB_TRY(stage_in(ctx, o, 3 * N, nullptr));
+  PB_TRY(stage_in(ctx, w, 5 * N, nullptr));
+  PB_TRY(grad3(lg.g, dx, d.p, o.p, o.p + N, o.p + 2 * N, w.p));
+  return stage_out(ctx, o, 3 * N, df);  // df(nx, ny, nz, 3): component slowest
+}
+
+int pb_compact_div_host(pb_ctx* ctx, const int64_t n[3], const double dx[3], const double* f,
+                        double* df) {
+  PB_CHECK_ARG(ctx && n && dx && f && df, "bad div args");
+  LocalGrid lg;
+  PB_TRY(local_grid(ctx, n, lg));
+  const size_t N = (size_t)lg.g->nlocal;
+  DevBuf d, o, w;
+  PB_TRY(stage_in(ctx, d, 3 * N, f));  // f(nx, ny, nz, 3)
+  PB_TRY(stage_in(ctx, o, N, nullptr));
+  PB_TRY(stage_in(ctx, w, 6 * N, nullptr));
+  PB_TRY(div3(lg.g, dx, d.p, d.p + N, d.p + 2 * N, o.p, w.p));
+  return stage_out(ctx, o, N, df);
+}
+
+int pb_compact_interp_host(pb_ctx* ctx, const int64_t n[3], int stagger, const double* f,
+                           double* fi) {
+  PB_CHECK_ARG(ctx && n && f && fi, "bad interp args");
+  PB_CHECK_ARG(stagger == -1 || stagger == 1, "stagger must be -1 or +1");
+  LocalGrid lg;
+  PB_TRY(local_grid(ctx, n, lg));
+  const size_t N = (size_t)lg.g->nlocal;
+  DevBuf d, w;
+  PB_TRY(stage_in(ctx, d, N, f));
+  PB_TRY(stage_in(ctx, w, 2 * N, nullptr));
+  PB_TRY(line3(lg.g, 2, K_INTERP, stagger, 0.0, d.p, w.p));          // :122-127
+  PB_TRY(line3(lg.g, 1, K_INTERP, stagger, 0.0, w.p, w.p + N));      // :130-135
+  PB_TRY(line3(lg.g, 0, K_INTERP, stagger, 0.0, w.p + N, d.p));      // :139-143
+  return stage_out(ctx, d, N, fi);
+}
+
+int pb_compact_lapl_host(pb_ctx* ctx, const int64_t n[3], const double dx[3], const double* f,
+                         double* out) {
+  PB_CHECK_ARG(ctx && n && dx && f && out, "bad lapl args");
+  LocalGrid lg;
+  PB_TRY(local_grid(ctx, n, lg));
+  const size_t N = (size_t)lg.g->nlocal;
+  DevBuf d, o, w;
+  PB_TRY(stage_in(ctx, d, N, f));
+  PB_TRY(stage_in(ctx, o, N, nullptr));
+  PB_TRY(stage_in(ctx, w, (size_t)compact_work_len(lg.g), nullptr));
+  PB_TRY(compact_lapl(lg.g, dx, d.p, o.p, w.p));
+  return stage_out(ctx, o, N, out);
 }
 
 }  // extern "C"

@@ -73,6 +73,7 @@ struct pb_ctx {
   // later collective call returns PB_ERR_COMM at once
   int64_t comm_timeout_ms = 180000;
   bool comm_failed = false;
+  void* shm = nullptr;  // built-in shared-memory host transport (pb_transport.cpp), if attached
   // host transport (tests)
   pb_sendrecv_fn h_sendrecv = nullptr;
   pb_allreduce_fn h_allreduce = nullptr;
@@ -123,7 +124,11 @@ struct pb_grid {
   // ghost2 = [planes -2, -1 | nzl, nzl+1], h_stage2 = host staging (8 planes)
   double* ghost2 = nullptr;
   double* h_stage2 = nullptr;
+  // the whole domain on this rank even on a multi-rank context (host-array compact entry points:
+  // the reference's module procedures work on process-local arrays)
+  bool whole = false;
 };
+inline bool grid_split(const pb_grid* g) { return g->ctx->split && !g->whole; }
 
 struct pb_vec {
   pb_grid* grid = nullptr;
@@ -186,6 +191,8 @@ int halo_begin(pb_grid* g, const double* lo, const double* hi);
 int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, double* rlo,
                     double* rhi);
 int halo_end(pb_grid* g);
+// release the shared-memory transport of a context (pb_transport.cpp)
+void transport_destroy(pb_ctx* ctx);
 // In-place SUM allreduce of `count` device doubles (stream ordered).
 int allreduce_device(pb_ctx* ctx, double* d_vals, int count);
 // Bounded host waits. One rank without a communicator: plain hipStream/EventSynchronize. Split

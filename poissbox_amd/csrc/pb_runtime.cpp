@@ -391,6 +391,31 @@ extern "C" {
 
 const char* pb_last_error(void) { return g_err; }
 
+// src/coefficients.f90:22-35 (invdx2 = 1/dx**2; [invdx2, -2 invdx2, invdx2])
+int pb_lapl_1d_coeffs(double dx, double c[3]) {
+  PB_CHECK_ARG(c, "c is NULL");
+  const double inv = 1.0 / (dx * dx);
+  c[0] = inv;
+  c[1] = -2.0 * inv;
+  c[2] = inv;
+  return PB_OK;
+}
+
+// src/coefficients.f90:38-48: the 3x3x3 box (column-major, i fastest), zero but for the three
+// 1-D lines through the centre, each added onto the box in x, y, z order
+int pb_lapl_star_coeffs(double dx, double dy, double dz, double c[27]) {
+  PB_CHECK_ARG(c, "c is NULL");
+  double l[3][3];
+  pb_lapl_1d_coeffs(dx, l[0]);
+  pb_lapl_1d_coeffs(dy, l[1]);
+  pb_lapl_1d_coeffs(dz, l[2]);
+  for (int m = 0; m < 27; ++m) c[m] = 0.0;
+  for (int t = 0; t < 3; ++t) c[t + 3 * 1 + 9 * 1] = c[t + 3 * 1 + 9 * 1] + l[0][t];
+  for (int t = 0; t < 3; ++t) c[1 + 3 * t + 9 * 1] = c[1 + 3 * t + 9 * 1] + l[1][t];
+  for (int t = 0; t < 3; ++t) c[1 + 3 * 1 + 9 * t] = c[1 + 3 * 1 + 9 * t] + l[2][t];
+  return PB_OK;
+}
+
 int pb_version(int* major, int* minor) {
   if (major) *major = PB_VERSION_MAJOR;
   if (minor) *minor = PB_VERSION_MINOR;
@@ -505,6 +530,7 @@ int pb_ctx_destroy(pb_ctx* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->h_a2a) (void)hipHostFree(ctx->h_a2a);
+  transport_destroy(ctx);
   (void)hipFree(ctx->d_partials);
   (void)hipFree(ctx->d_scalars);
   (void)hipHostFree(ctx->h_scalars);

@@ -116,6 +116,17 @@ static int op_apply_raw(pb_op* op, const double* x, double* y) {
   return launch_aij_seams(g, s, x, split ? g->ghost_lo : nullptr, split ? g->ghost_hi : nullptr, y);
 }
 
+int pb_op_set_deltas(pb_op* op, const double deltas[3]) {
+  PB_CHECK_ARG(op && deltas, "bad args");
+  for (int d = 0; d < 3; ++d) op->deltas[d] = deltas[d];
+  Star s = star_coeffs(op->deltas);
+  op->cx = s.cx;
+  op->cy = s.cy;
+  op->cz = s.cz;
+  op->cc = s.cc;
+  return PB_OK;
+}
+
 int pb_op_apply(pb_op* op, const pb_vec* x, pb_vec* y) {
   PB_CHECK_ARG(op && x && y, "bad apply args");
   PB_CHECK_ARG(x->grid == op->grid && y->grid == op->grid, "vector/operator grid mismatch");

@@ -1,8 +1,11 @@
-!! poissbox_demo.f90 -- the reference demo flow (src/example.f90) on one MI355X.
+!! poissbox_demo.f90 -- the reference demo flow (src/example.f90) on 1..N MI355X ranks.
 !
 ! Same sequence of steps as poissbox_example (src/example.f90:55-84): grid + check_grid, linear
-! system, x = random in [-1,1], b = A x, check_lapl (A x vs pointwise stencil), check_matrices
-! (A x vs P x), KSP solve from PETSc-style options, final residual ||A x - b||_2.
+! system + check_linear_system, assemble_laplacian, x = random in [-1,1], b = A x, check_lapl
+! (A x vs pointwise stencil), check_matrices (A x vs P x), KSP solve from PETSc-style options,
+! final residual ||A x - b||_2. One process per rank, started by any launcher
+! (`torchrun --no-python --nproc-per-node N poissbox_demo ...`, mpirun, or RANK/WORLD_SIZE set by
+! hand): the per-rank lines reproduce README.md:25-33 (64^3 on 3 ranks: 90112/86016/86016).
 ! Usage: poissbox_demo [-n N] [-ksp_rtol 1e-10] [-ksp_monitor] [-ksp_converged_reason] ...
 program poissbox_demo
 
@@ -11,7 +14,7 @@ program poissbox_demo
 
   implicit none
 
-  integer :: ierr, n1, its, reason
+  integer :: ierr, n1, its, reason, irank, nproc
   integer, dimension(3) :: n
   real(pb_dp), dimension(3) :: h
   real(pb_dp) :: error, rnorm
@@ -26,8 +29,10 @@ program poissbox_demo
 
   call PoissboxInitialize(0, ierr)
   if (ierr /= 0) stop 1
-  print *, "Running poissbox on ", 1, " ranks"
-  print *, "Hello from ", 0
+  call PoissboxCommRank(irank, nproc, ierr)
+  if (irank == 0) print *, "Running poissbox on ", nproc, " ranks"
+  call PoissboxBarrier(ierr)
+  print *, "Hello from ", irank
 
   call initialise_grid(n, da, ierr)
   call check_grid(n, da)
@@ -37,6 +42,7 @@ program poissbox_demo
   call initialise_linear_system(da, ctx, P, A, x, b, ierr)
   if (ierr /= 0) stop 1
   call check_linear_system(n, P, x, b)
+  call assemble_laplacian(da, h(1), h(2), h(3), P)
 
   call set_solution(da, x)
   print *, "Calling MatMult"
@@ -76,14 +82,16 @@ contains
     end do
   end function arg_int
 
-  !! src/example.f90:92-116: owned DoF vs global DoF
+  !! src/example.f90:92-116: owned DoF vs global DoF (sum over ranks)
   subroutine check_grid(nglobal, da)
     integer, dimension(3), intent(in) :: nglobal
     type(tDM), intent(in) :: da
-    integer :: istart, jstart, kstart, ni, nj, nk, ierr
+    integer :: istart, jstart, kstart, ni, nj, nk, ierr, nloc, nglob
     call DMDAGetCorners(da, istart, jstart, kstart, ni, nj, nk, ierr)
-    print *, "(DMDA): Rank ", 0, " has ", ni * nj * nk, " of ", ni * nj * nk, &
-         " expected: ", product(nglobal)
+    nloc = ni * nj * nk
+    nglob = nloc
+    call PoissboxAllreduceSum(nglob, ierr)
+    print *, "(DMDA): Rank ", irank, " has ", nloc, " of ", nglob, " expected: ", product(nglobal)
   end subroutine check_grid
 
   !! src/example.f90:118-152: row ownership of P, x and b against the global DoF count
@@ -91,20 +99,26 @@ contains
     integer, dimension(3), intent(in) :: nglobal
     type(tMat), intent(in) :: M
     type(tVec), intent(in) :: x, b
-    integer :: myrow, nextrow, ierr
+    integer :: myrow, nextrow, ierr, nloc, nglob
     call MatGetOwnershipRange(M, myrow, nextrow, ierr)
-    print *, "(M): Rank ", 0, " has ", nextrow - myrow, " rows of ", nextrow - myrow, &
-         " expected: ", product(nglobal)
+    nloc = nextrow - myrow
+    nglob = nloc
+    call PoissboxAllreduceSum(nglob, ierr)
+    print *, "(M): Rank ", irank, " has ", nloc, " rows of ", nglob, " expected: ", product(nglobal)
     call VecGetOwnershipRange(x, myrow, nextrow, ierr)
-    print *, "(x): Rank ", 0, " has ", nextrow - myrow, " rows of ", nextrow - myrow, &
-         " expected: ", product(nglobal)
+    nloc = nextrow - myrow
+    nglob = nloc
+    call PoissboxAllreduceSum(nglob, ierr)
+    print *, "(x): Rank ", irank, " has ", nloc, " rows of ", nglob, " expected: ", product(nglobal)
     call VecGetOwnershipRange(b, myrow, nextrow, ierr)
-    print *, "(b): Rank ", 0, " has ", nextrow - myrow, " rows of ", nextrow - myrow, &
-         " expected: ", product(nglobal)
+    nloc = nextrow - myrow
+    nglob = nloc
+    call PoissboxAllreduceSum(nglob, ierr)
+    print *, "(b): Rank ", irank, " has ", nloc, " rows of ", nglob, " expected: ", product(nglobal)
   end subroutine check_linear_system
 
   !! src/example.f90:154-199: x = 2(0.5 - U) on the owned block; the sum computed directly over
-  !! the owned values (host loop, as the reference's xsum) against VecSum (device reduction)
+  !! the owned values (host loop, as the reference's xsum, summed over ranks) against VecSum
   subroutine set_solution(da, x)
     type(tDM), intent(in) :: da
     type(tVec), intent(inout) :: x
@@ -125,7 +139,8 @@ contains
     end do
     deallocate(xdof)
     call VecSum(x, xsum_v, ierr)
-    print *, "Rank ", 0, "Delta of XSUM norms computed directly and from X: ", xsum_v - xs, &
+    call PoissboxAllreduceSum(xs, ierr)
+    print *, "Rank ", irank, "Delta of XSUM norms computed directly and from X: ", xsum_v - xs, &
          xsum_v, xs
   end subroutine set_solution
 
@@ -142,7 +157,7 @@ contains
     call compute_lapl_pointwise(da, h, x, c, ierr)
     call VecAXPY(b2, -1.0_pb_dp, c, ierr)
     call VecNorm(b2, residual, ierr)
-    print *, "Rank ", 0, "Delta between b=Mx and pointwise calculation: ", residual
+    print *, "Rank ", irank, "Delta between b=Mx and pointwise calculation: ", residual
     call VecDestroy(b2, ierr)
     call VecDestroy(c, ierr)
   end subroutine check_lapl

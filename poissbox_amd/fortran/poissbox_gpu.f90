@@ -10,17 +10,25 @@
 !   compute_lapl_pointwise(da, grid_deltas, x, b) (:84-126)          -> same
 !   DMDAGetCorners, VecDuplicate, VecCopy, VecAXPY, VecNorm, VecSum, VecSet, VecDestroy,
 !   DMDAVecGetArrayF90 (copy-out form: VecGetValues / VecSetValues)
+!   MPI_Init / MPI_Comm_rank / MPI_Comm_size / MPI_Allreduce(SUM) / MPI_Barrier
+!     (src/example.f90:43-52,108,137-147,194) -> PoissboxInitialize (launcher environment:
+!     torchrun --no-python, mpirun, PMI), PoissboxCommRank, PoissboxAllreduceSum, PoissboxBarrier
+!   assemble_laplacian(da, dx, dy, dz, M) (src/coefficients.f90:50-113) -> same
+! The module procedures of src/tridsol.f90 and src/compact_schemes.f90 keep their own module
+! names (poissbox_modules.f90: modules tridsol, compact_schemes, coefficients; constants in
+! poissbox_constants.f90); the device-pointer C entry points are bound here as c_pb_*.
 ! Every routine returns ierr (0 = success) as the last argument, PETSc style; unlike the
 ! reference, ierr is always set.
 module poissbox_gpu
 
   use iso_c_binding
+  use constants, only: pb_dp
 
   implicit none
 
   private
 
-  integer, parameter, public :: pb_dp = c_double
+  public :: pb_dp
 
   type, public :: tDM
      type(c_ptr) :: h = c_null_ptr
@@ -65,6 +73,19 @@ module poissbox_gpu
   public :: DMDAGetCorners, MatMult, MatDestroy, MatGetOwnershipRange, VecGetOwnershipRange
   public :: VecDuplicate, VecCopy, VecAXPY, VecNorm, VecSum, VecSet, VecDestroy
   public :: VecSetRandom, VecGetValues, VecSetValues, pb_error_string
+  public :: PoissboxContext, PoissboxCommRank, PoissboxAllreduceSum, PoissboxBarrier
+  public :: assemble_laplacian
+  public :: CompactGrad, CompactDiv, CompactInterp, CompactLapl, CompactLaplFast
+  ! C entry points on device pointers / host arrays (batched line solvers, compact operators)
+  public :: c_pb_comm_unique_id, c_pb_tdma_batched, c_pb_tdma_sweeps_batched
+  public :: c_pb_pcr_alpha_batched, c_pb_compact_1d_batched
+  public :: c_pb_tdma_batched_host, c_pb_tdma_sweeps_batched_host, c_pb_compact_1d_batched_host
+  public :: c_pb_compact_grad_host, c_pb_compact_div_host, c_pb_compact_interp_host
+  public :: c_pb_compact_lapl_host, c_pb_lapl_1d_coeffs, c_pb_lapl_star_coeffs
+
+  interface PoissboxAllreduceSum  ! ≙ MPI_Allreduce(..., MPI_SUM, MPI_COMM_WORLD)
+     module procedure allreduce_sum_int, allreduce_sum_real
+  end interface PoissboxAllreduceSum
 
   interface
      integer(c_int) function c_pb_ctx_create(device, rank, nranks, uid, ctx) bind(C, name="pb_ctx_create")
@@ -72,6 +93,166 @@ module poissbox_gpu
        integer(c_int), value :: device, rank, nranks
        type(c_ptr), value :: uid
        type(c_ptr) :: ctx
+     end function
+     integer(c_int) function c_pb_ctx_create_from_env(device, ctx) &
+          bind(C, name="pb_ctx_create_from_env")
+       import :: c_int, c_ptr
+       integer(c_int), value :: device
+       type(c_ptr) :: ctx
+     end function
+     integer(c_int) function c_pb_ctx_get_rank(ctx, rank, nranks) bind(C, name="pb_ctx_get_rank")
+       import :: c_int, c_ptr
+       type(c_ptr), value :: ctx
+       integer(c_int) :: rank, nranks
+     end function
+     integer(c_int) function c_pb_ctx_allreduce_host(ctx, vals, count) &
+          bind(C, name="pb_ctx_allreduce_host")
+       import :: c_int, c_ptr, c_double
+       type(c_ptr), value :: ctx
+       real(c_double), dimension(*) :: vals
+       integer(c_int), value :: count
+     end function
+     integer(c_int) function c_pb_ctx_barrier(ctx) bind(C, name="pb_ctx_barrier")
+       import :: c_int, c_ptr
+       type(c_ptr), value :: ctx
+     end function
+     integer(c_int) function c_pb_comm_unique_id(uid) bind(C, name="pb_comm_unique_id")
+       import :: c_int, c_char
+       character(kind=c_char), dimension(128) :: uid
+     end function
+     integer(c_int) function c_pb_op_set_deltas(op, deltas) bind(C, name="pb_op_set_deltas")
+       import :: c_int, c_ptr, c_double
+       type(c_ptr), value :: op
+       real(c_double), dimension(3) :: deltas
+     end function
+     ! src/tridsol.f90 on device pointers (element e of line l at ptr[l*line_stride + e*elem_stride])
+     integer(c_int) function c_pb_tdma_batched(ctx, n, nbatch, ls, es, a, b, c, d, periodic) &
+          bind(C, name="pb_tdma_batched")
+       import :: c_int, c_ptr, c_int64_t
+       type(c_ptr), value :: ctx, a, b, c, d
+       integer(c_int64_t), value :: n, nbatch, ls, es
+       integer(c_int), value :: periodic
+     end function
+     integer(c_int) function c_pb_tdma_sweeps_batched(ctx, n, nbatch, ls, es, a, b, c, d, which) &
+          bind(C, name="pb_tdma_sweeps_batched")
+       import :: c_int, c_ptr, c_int64_t
+       type(c_ptr), value :: ctx, a, b, c, d
+       integer(c_int64_t), value :: n, nbatch, ls, es
+       integer(c_int), value :: which
+     end function
+     integer(c_int) function c_pb_pcr_alpha_batched(ctx, n, nbatch, ls, es, alpha, d) &
+          bind(C, name="pb_pcr_alpha_batched")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx, d
+       integer(c_int64_t), value :: n, nbatch, ls, es
+       real(c_double), value :: alpha
+     end function
+     integer(c_int) function c_pb_compact_1d_batched(ctx, kind, stagger, dx, n, nbatch, ls, es, &
+          f, out) bind(C, name="pb_compact_1d_batched")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx, f, out
+       integer(c_int), value :: kind, stagger
+       real(c_double), value :: dx
+       integer(c_int64_t), value :: n, nbatch, ls, es
+     end function
+     ! the same on host arrays (copied through device memory)
+     integer(c_int) function c_pb_tdma_batched_host(ctx, n, nbatch, ls, es, a, b, c, d, periodic) &
+          bind(C, name="pb_tdma_batched_host")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx
+       integer(c_int64_t), value :: n, nbatch, ls, es
+       real(c_double), dimension(*) :: a, b, c, d
+       integer(c_int), value :: periodic
+     end function
+     integer(c_int) function c_pb_tdma_sweeps_batched_host(ctx, n, nbatch, ls, es, a, b, c, d, &
+          which) bind(C, name="pb_tdma_sweeps_batched_host")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx
+       integer(c_int64_t), value :: n, nbatch, ls, es
+       real(c_double), dimension(*) :: a, b, c, d
+       integer(c_int), value :: which
+     end function
+     integer(c_int) function c_pb_compact_1d_batched_host(ctx, kind, stagger, dx, n, nbatch, ls, &
+          es, f, out) bind(C, name="pb_compact_1d_batched_host")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx
+       integer(c_int), value :: kind, stagger
+       real(c_double), value :: dx
+       integer(c_int64_t), value :: n, nbatch, ls, es
+       real(c_double), dimension(*) :: f, out
+     end function
+     integer(c_int) function c_pb_compact_grad_host(ctx, n, dx, f, df) &
+          bind(C, name="pb_compact_grad_host")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx
+       integer(c_int64_t), dimension(3) :: n
+       real(c_double), dimension(3) :: dx
+       real(c_double), dimension(*) :: f, df
+     end function
+     integer(c_int) function c_pb_compact_div_host(ctx, n, dx, f, df) &
+          bind(C, name="pb_compact_div_host")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx
+       integer(c_int64_t), dimension(3) :: n
+       real(c_double), dimension(3) :: dx
+       real(c_double), dimension(*) :: f, df
+     end function
+     integer(c_int) function c_pb_compact_interp_host(ctx, n, stagger, f, fi) &
+          bind(C, name="pb_compact_interp_host")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx
+       integer(c_int64_t), dimension(3) :: n
+       integer(c_int), value :: stagger
+       real(c_double), dimension(*) :: f, fi
+     end function
+     integer(c_int) function c_pb_compact_lapl_host(ctx, n, dx, f, out) &
+          bind(C, name="pb_compact_lapl_host")
+       import :: c_int, c_ptr, c_int64_t, c_double
+       type(c_ptr), value :: ctx
+       integer(c_int64_t), dimension(3) :: n
+       real(c_double), dimension(3) :: dx
+       real(c_double), dimension(*) :: f, out
+     end function
+     pure integer(c_int) function c_pb_lapl_1d_coeffs(dx, c) bind(C, name="pb_lapl_1d_coeffs")
+       import :: c_int, c_double
+       real(c_double), value, intent(in) :: dx
+       real(c_double), dimension(3), intent(out) :: c
+     end function
+     pure integer(c_int) function c_pb_lapl_star_coeffs(dx, dy, dz, c) &
+          bind(C, name="pb_lapl_star_coeffs")
+       import :: c_int, c_double
+       real(c_double), value, intent(in) :: dx, dy, dz
+       real(c_double), dimension(27), intent(out) :: c
+     end function
+     ! compact operators on grid vectors (z-slab split grids included)
+     integer(c_int) function c_pb_compact_grad(grid, dx, f, df) bind(C, name="pb_compact_grad")
+       import :: c_int, c_ptr, c_double
+       type(c_ptr), value :: grid, f
+       real(c_double), dimension(3) :: dx
+       type(c_ptr), dimension(3) :: df
+     end function
+     integer(c_int) function c_pb_compact_div(grid, dx, f, df) bind(C, name="pb_compact_div")
+       import :: c_int, c_ptr, c_double
+       type(c_ptr), value :: grid, df
+       real(c_double), dimension(3) :: dx
+       type(c_ptr), dimension(3) :: f
+     end function
+     integer(c_int) function c_pb_compact_interp(grid, stagger, f, fi) &
+          bind(C, name="pb_compact_interp")
+       import :: c_int, c_ptr
+       type(c_ptr), value :: grid, f, fi
+       integer(c_int), value :: stagger
+     end function
+     integer(c_int) function c_pb_compact_lapl(grid, dx, f, out) bind(C, name="pb_compact_lapl")
+       import :: c_int, c_ptr, c_double
+       type(c_ptr), value :: grid, f, out
+       real(c_double), dimension(3) :: dx
+     end function
+     integer(c_int) function c_pb_compact_lapl_fast(grid, dx, f, out) &
+          bind(C, name="pb_compact_lapl_fast")
+       import :: c_int, c_ptr, c_double
+       type(c_ptr), value :: grid, f, out
+       real(c_double), dimension(3) :: dx
      end function
      integer(c_int) function c_pb_ctx_destroy(ctx) bind(C, name="pb_ctx_destroy")
        import :: c_int, c_ptr
@@ -213,13 +394,149 @@ contains
     if (ierr /= 0) print *, "poissbox_gpu: ", where, " failed (", ierr, "): ", pb_error_string()
   end subroutine check
 
-  !! ≙ MPI_Init + PetscInitialize (src/example.f90:43-47); one GPU per process
+  !! ≙ MPI_Init + PetscInitialize (src/example.f90:43-47). One process: rank 0 of 1 on GPU
+  !! `device`. Under a launcher (torchrun --no-python, mpirun, PMI) every process is one rank on
+  !! GPU LOCAL_RANK, connected over RCCL, or over the built-in shared-memory transport when ranks
+  !! outnumber GPUs (PB_TRANSPORT, include/poissbox_gpu.h pb_ctx_create_from_env).
   subroutine PoissboxInitialize(device, ierr)
     integer, intent(in) :: device
     integer, intent(out) :: ierr
-    ierr = c_pb_ctx_create(int(device, c_int), 0_c_int, 1_c_int, c_null_ptr, g_ctx)
+    ierr = c_pb_ctx_create_from_env(int(device, c_int), g_ctx)
     call check(ierr, "PoissboxInitialize")
   end subroutine PoissboxInitialize
+
+  !! the process's context; created on first use (GPU LOCAL_RANK) when a program calls a module
+  !! procedure without PoissboxInitialize (the reference's compact / tridiagonal routines need no
+  !! set-up either)
+  function PoissboxContext() result(ctx)
+    type(c_ptr) :: ctx
+    integer :: ierr
+    if (.not. c_associated(g_ctx)) then
+       ierr = c_pb_ctx_create_from_env(-1_c_int, g_ctx)
+       if (ierr /= 0) then
+          call check(ierr, "PoissboxContext")
+          error stop 1
+       end if
+    end if
+    ctx = g_ctx
+  end function PoissboxContext
+
+  !! ≙ MPI_Comm_rank + MPI_Comm_size on MPI_COMM_WORLD
+  subroutine PoissboxCommRank(rank, nranks, ierr)
+    integer, intent(out) :: rank, nranks, ierr
+    integer(c_int) :: r, n
+    ierr = c_pb_ctx_get_rank(PoissboxContext(), r, n)
+    rank = int(r)
+    nranks = int(n)
+  end subroutine PoissboxCommRank
+
+  !! ≙ MPI_Barrier(MPI_COMM_WORLD)
+  subroutine PoissboxBarrier(ierr)
+    integer, intent(out) :: ierr
+    ierr = c_pb_ctx_barrier(PoissboxContext())
+    call check(ierr, "PoissboxBarrier")
+  end subroutine PoissboxBarrier
+
+  subroutine allreduce_sum_real(v, ierr)
+    real(pb_dp), intent(inout) :: v
+    integer, intent(out) :: ierr
+    real(c_double), dimension(1) :: t
+    t(1) = v
+    ierr = c_pb_ctx_allreduce_host(PoissboxContext(), t, 1_c_int)
+    call check(ierr, "PoissboxAllreduceSum")
+    v = t(1)
+  end subroutine allreduce_sum_real
+
+  subroutine allreduce_sum_int(v, ierr)  ! exact for |sum| < 2**53
+    integer, intent(inout) :: v
+    integer, intent(out) :: ierr
+    real(c_double), dimension(1) :: t
+    t(1) = real(v, c_double)
+    ierr = c_pb_ctx_allreduce_host(PoissboxContext(), t, 1_c_int)
+    call check(ierr, "PoissboxAllreduceSum")
+    v = nint(t(1))
+  end subroutine allreduce_sum_int
+
+  !! src/coefficients.f90:50-113: the operator's coefficients from the spacings (the 27-entry
+  !! BOX rows are implicit: PB_OP_ASSEMBLED27 sums them in PETSc AIJ order)
+  subroutine assemble_laplacian(da, dx, dy, dz, M)
+    type(tDM), intent(in) :: da
+    real(pb_dp), intent(in) :: dx, dy, dz
+    type(tMat), intent(inout) :: M
+    real(c_double), dimension(3) :: d
+    integer :: ierr
+    d = [dx, dy, dz]
+    if (.not. c_associated(M%h)) then
+       ierr = c_pb_op_create(da%h, PB_OP_ASSEMBLED27, d, M%h)
+    else
+       ierr = c_pb_op_set_deltas(M%h, d)
+    end if
+    call check(ierr, "assemble_laplacian")
+  end subroutine assemble_laplacian
+
+  !! compact operators on grid vectors (src/compact_schemes.f90:17-257), split grids included
+  subroutine CompactGrad(da, dx, f, df, ierr)
+    type(tDM), intent(in) :: da
+    real(pb_dp), dimension(3), intent(in) :: dx
+    type(tVec), intent(in) :: f
+    type(tVec), dimension(3), intent(inout) :: df
+    integer, intent(out) :: ierr
+    real(c_double), dimension(3) :: d
+    type(c_ptr), dimension(3) :: h
+    d = dx
+    h = [df(1)%h, df(2)%h, df(3)%h]
+    ierr = c_pb_compact_grad(da%h, d, f%h, h)
+    call check(ierr, "CompactGrad")
+  end subroutine CompactGrad
+
+  subroutine CompactDiv(da, dx, f, df, ierr)
+    type(tDM), intent(in) :: da
+    real(pb_dp), dimension(3), intent(in) :: dx
+    type(tVec), dimension(3), intent(in) :: f
+    type(tVec), intent(inout) :: df
+    integer, intent(out) :: ierr
+    real(c_double), dimension(3) :: d
+    type(c_ptr), dimension(3) :: h
+    d = dx
+    h = [f(1)%h, f(2)%h, f(3)%h]
+    ierr = c_pb_compact_div(da%h, d, h, df%h)
+    call check(ierr, "CompactDiv")
+  end subroutine CompactDiv
+
+  subroutine CompactInterp(da, stagger, f, fi, ierr)
+    type(tDM), intent(in) :: da
+    integer, intent(in) :: stagger
+    type(tVec), intent(in) :: f
+    type(tVec), intent(inout) :: fi
+    integer, intent(out) :: ierr
+    ierr = c_pb_compact_interp(da%h, int(stagger, c_int), f%h, fi%h)
+    call check(ierr, "CompactInterp")
+  end subroutine CompactInterp
+
+  subroutine CompactLapl(da, dx, f, out, ierr)
+    type(tDM), intent(in) :: da
+    real(pb_dp), dimension(3), intent(in) :: dx
+    type(tVec), intent(in) :: f
+    type(tVec), intent(inout) :: out
+    integer, intent(out) :: ierr
+    real(c_double), dimension(3) :: d
+    d = dx
+    ierr = c_pb_compact_lapl(da%h, d, f%h, out%h)
+    call check(ierr, "CompactLapl")
+  end subroutine CompactLapl
+
+  !! the 3-pass factorised compact Laplacian (what PB_OP_COMPACT applies)
+  subroutine CompactLaplFast(da, dx, f, out, ierr)
+    type(tDM), intent(in) :: da
+    real(pb_dp), dimension(3), intent(in) :: dx
+    type(tVec), intent(in) :: f
+    type(tVec), intent(inout) :: out
+    integer, intent(out) :: ierr
+    real(c_double), dimension(3) :: d
+    d = dx
+    ierr = c_pb_compact_lapl_fast(da%h, d, f%h, out%h)
+    call check(ierr, "CompactLaplFast")
+  end subroutine CompactLaplFast
 
   subroutine PoissboxFinalize(ierr)
     integer, intent(out) :: ierr
@@ -236,7 +553,7 @@ contains
     real(c_double), dimension(3) :: L
     n = int(nglobal, c_int64_t)
     L = 1.0_c_double
-    ierr = c_pb_grid_create(g_ctx, n, L, da%h)
+    ierr = c_pb_grid_create(PoissboxContext(), n, L, da%h)
     call check(ierr, "initialise_grid")
   end subroutine initialise_grid
 

@@ -15,10 +15,14 @@ FLANG = "/opt/rocm/lib/llvm/bin/flang"
 
 @pytest.mark.skipif(not os.path.exists(FLANG), reason="flang not in this image")
 def test_fortran_module_compiles(tmp_path):
-    out = subprocess.run([FLANG, "-c", os.path.join(FDIR, "poissbox_gpu.f90")], cwd=tmp_path,
-                         capture_output=True, text=True)
-    assert out.returncode == 0, out.stderr
-    assert (tmp_path / "poissbox_gpu.mod").exists()
+    for src in ("poissbox_constants.f90", "poissbox_gpu.f90", "poissbox_modules.f90"):
+        out = subprocess.run([FLANG, "-c", os.path.join(FDIR, src)], cwd=tmp_path,
+                             capture_output=True, text=True)
+        assert out.returncode == 0, out.stderr
+    # the reference's module names (src/constants.f90, coefficients.f90, tridsol.f90,
+    # compact_schemes.f90) next to the boundary module
+    for mod in ("constants", "poissbox_gpu", "coefficients", "tridsol", "compact_schemes"):
+        assert (tmp_path / f"{mod}.mod").exists(), mod
 
 
 @pytest.mark.gpu
@@ -56,3 +60,77 @@ def test_fortran_demo_matches_oracle():
     assert m and int(m.group(1)) == its
     res = float(re.search(r"Solution residual \(L2 norm\):\s+(\S+)", txt).group(1))
     assert res < 1e-4 * np.linalg.norm(b)
+
+
+def _launch(nranks, args, extra_env=None, timeout=300):
+    """Start nranks demo processes as a launcher would (RANK / WORLD_SIZE / LOCAL_RANK), here on
+    one GPU through the built-in shared-memory transport."""
+    job = f"pytest{os.getpid()}"
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(nranks), LOCAL_RANK=str(r),
+                   PB_JOB_ID=job, PB_TRANSPORT="shm", PB_DEVICE="0", PB_COMM_TIMEOUT_MS="120000")
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen([DEMO] + args, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, env=env))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, o, e))
+    return outs
+
+
+@pytest.mark.gpu
+def test_fortran_demo_three_ranks_readme():
+    """README.md:25-33: `mpirun -np 3` on 64^3 gives 90112 / 86016 / 86016 DoF per rank. The demo
+    runs as 3 processes (one rank each, shared-memory transport on this one-GPU box), prints the
+    reference's per-rank lines, and its CG solve matches the oracle's iteration count."""
+    from oracle import oracle as O
+    if not os.path.exists(DEMO):
+        subprocess.run(["make", "-s", "-C", FDIR], check=True)
+    outs = _launch(3, ["-n", "64", "-ksp_rtol", "1e-8", "-ksp_converged_reason"])
+    for rc, o, e in outs:
+        assert rc == 0, o + e
+    txt = "".join(o for _, o, _ in outs)
+    assert re.search(r"Running poissbox on\s+3\s+ranks", txt)
+    for r, dof in enumerate((90112, 86016, 86016)):
+        assert re.search(r"Hello from\s+%d\b" % r, txt)
+        assert re.search(r"\(DMDA\): Rank\s+%d\s+has\s+%d\s+of\s+262144\s+expected:\s+262144" % (r, dof), txt)
+        for tag in ("M", "x", "b"):
+            assert re.search(r"\(%s\): Rank\s+%d\s+has\s+%d\s+rows of\s+262144\s+expected:\s+262144"
+                             % (tag, r, dof), txt)
+    # check_lapl on every rank: the operator and the pointwise evaluation are one kernel
+    lap = re.findall(r"Rank\s+(\d+)\s*Delta between b=Mx and pointwise calculation:\s+(\S+)", txt)
+    assert sorted(int(r) for r, _ in lap) == [0, 1, 2] and all(float(v) == 0.0 for _, v in lap)
+    # x summed directly over all ranks vs VecSum: equal up to summation order
+    for m in re.finditer(r"Delta of XSUM norms computed directly and from X:\s+(\S+)", txt):
+        assert abs(float(m.group(1))) <= 1e-9 * 262144
+    n3 = (64, 64, 64)
+    h = (1 / 64,) * 3
+    b = O.stencil(O.fill_random(64 ** 3, 20231015), n3, h)
+    _, reason, its, _ = O.cg_solve(b, n3, h, rtol=1e-8)
+    m = re.findall(r"converged due to CONVERGED_RTOL iterations (\d+)", txt)
+    assert m and all(int(v) == its for v in m)
+
+
+@pytest.mark.gpu
+def test_fortran_demo_dead_peer_is_an_error():
+    """A rank that never arrives (only 2 of 3 processes started) must end the others with an
+    error within PB_COMM_TIMEOUT_MS, not hang them."""
+    if not os.path.exists(DEMO):
+        subprocess.run(["make", "-s", "-C", FDIR], check=True)
+    job = f"pytestdead{os.getpid()}"
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="3", LOCAL_RANK=str(r), PB_JOB_ID=job,
+                   PB_TRANSPORT="shm", PB_DEVICE="0", PB_COMM_TIMEOUT_MS="3000")
+        procs.append(subprocess.Popen([DEMO, "-n", "32"], stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, env=env))
+    for p in procs:
+        o, e = p.communicate(timeout=120)
+        assert p.returncode != 0, o + e
