@@ -164,7 +164,10 @@ int pb_vec_get_ownership_range(const pb_vec* v, int64_t* first, int64_t* next);
 
 /* ---- KSP (replaces solve(P, A, x, b), src/poissbox.f90:269-298 -> KSPSolve) ---- */
 enum pb_ksp_type { PB_KSP_CG = 0 };
-enum pb_pc_type { PB_PC_NONE = 0, PB_PC_JACOBI = 1, PB_PC_SOR = 2, PB_PC_MG = 3 };
+/* PB_PC_FFT (-pc_type fft): z = P^+ r by separable Hartley transforms with P's symbol (the compact
+ * operator's when P is PB_OP_COMPACT, else the 7-point star's); periodic, power-of-two extents in
+ * 64..1024. Not in the reference: the spectrally exact PC for config 5. */
+enum pb_pc_type { PB_PC_NONE = 0, PB_PC_JACOBI = 1, PB_PC_SOR = 2, PB_PC_MG = 3, PB_PC_FFT = 4 };
 /* PETSc KSPConvergedReason values */
 enum pb_ksp_reason {
   PB_KSP_ITERATING = 0, PB_KSP_CONVERGED_RTOL = 2, PB_KSP_CONVERGED_ATOL = 3,

@@ -40,9 +40,10 @@ class KspOpts(C.Structure):
     _fields_ = [("rtol", C.c_double), ("atol", C.c_double), ("dtol", C.c_double),
                 ("max_it", C.c_int64), ("pc_type", C.c_int), ("nullspace", C.c_int),
                 ("op_kind", C.c_int), ("nthreads", C.c_int), ("mg_levels", C.c_int),
-                ("mg_coarse_its", C.c_int), ("omega", C.c_double), ("nranks", C.c_int)]
+                ("mg_coarse_its", C.c_int), ("omega", C.c_double), ("nranks", C.c_int),
+                ("pc_compact", C.c_int)]
 
-PC_CODES = {"none": 0, "jacobi": 1, "sor": 2, "mg": 3}
+PC_CODES = {"none": 0, "jacobi": 1, "sor": 2, "mg": 3, "fft": 4}
 
 
 def _p(a):
@@ -103,8 +104,9 @@ def fill_random(count, seed, g0=0):
 
 def cg_solve(b, n, h, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
              nullspace=True, faithful=False, nthreads=1, op="star7", mg_levels=0,
-             mg_coarse_its=8, omega=1.0, nranks=1):
-    """KSPSolve(-ksp_type cg -pc_type jacobi|none|sor|mg) with the constant null space.
+             mg_coarse_its=8, omega=1.0, nranks=1, pc_compact=None):
+    """KSPSolve(-ksp_type cg -pc_type jacobi|none|sor|mg|fft) with the constant null space.
+    pc_compact: the fft PC inverts the compact operator's symbol (default: when op is compact).
     Returns (x, reason, its, history): the norms KSPLogResidualHistory logged (its + 1 of them,
     its after a breakdown exit)."""
     b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1)
@@ -115,8 +117,10 @@ def cg_solve(b, n, h, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi"
         kind = 2 + max(1, nranks)
     else:
         kind = 2 if op == "compact" else (1 if faithful else 0)
+    if pc_compact is None:
+        pc_compact = op == "compact"
     o = KspOpts(rtol, atol, dtol, max_it, PC_CODES[pc], int(nullspace), kind, nthreads,
-                mg_levels, mg_coarse_its, omega, nranks)
+                mg_levels, mg_coarse_its, omega, nranks, int(pc_compact))
     reason = lib().pbo_cg_solve(_n3(n), _h3(h), C.byref(o), _p(b), _p(x), _p(hist), C.byref(its),
                                 C.byref(nlog))
     return x, reason, its.value, hist[:nlog.value].copy()
@@ -132,6 +136,14 @@ def mg_apply(r, n, h, pc="mg", levels=0, coarse_its=8, omega=1.0, nranks=1):
     z = np.empty_like(r)
     lib().pbo_mg_apply(_n3(n), _h3(h), C.c_int(PC_CODES[pc]), C.c_int(levels),
                        C.c_int(coarse_its), C.c_double(omega), C.c_int(nranks), _p(r), _p(z))
+    return z
+
+
+def fft_pc_apply(r, n, h, compact=False):
+    """z = P^+ r, the spectral preconditioner (pb_fft.hip restatement by naive Hartley sums)."""
+    r = np.ascontiguousarray(r, dtype=np.float64).reshape(-1)
+    z = np.empty_like(r)
+    lib().pbo_fft_pc_apply(_n3(n), _h3(h), C.c_int(int(compact)), _p(r), _p(z))
     return z
 
 

@@ -426,6 +426,100 @@ void pbo_mg_apply(const int64_t n[3], const double h[3], int pc_type, int levels
   free(lv);
 }
 
+/* ---- spectral preconditioner (-pc_type fft): restates pb_fft.hip's definition, not its FFT ----
+ * Both P's are sums of products of 1-D circulants with real even symbols, so the separable
+ * Hartley transform H (H_d[j][k] = cas(2 pi j k / n_d), H_d H_d = n_d I) diagonalises them:
+ *   P^+ = H diag(1 / (N lambda)) H.
+ * 7-point star (src/coefficients.f90:22-48): lambda = sum_d (2 cos t_d - 2) / h_d^2.
+ * compact lapl (src/compact_schemes.f90:17-37, coefficients :188-190 / :303-305):
+ *   lambda = Lx Jy Jz + Jx Ly Jz + Jx Jy Lz,
+ *   L(t) = -4 (a_d sin(t/2) + b_d sin(3t/2))^2 / (1 + 2 al_d cos t)^2   (D+ D-),
+ *   J(t) =  4 (a_i cos(t/2) + b_i cos(3t/2))^2 / (1 + 2 al_i cos t)^2   (I+ I-).
+ * Pinned by tests/test_oracle.py: P (pbo_stencil_apply7 / pbo_lapl, themselves pinned to the
+ * reference) applied to z gives r minus its null-mode part, and a numpy complex-FFT statement of
+ * the same definition agrees. */
+static void fft_axis_symbols(int compact, int64_t n, double h, double* L, double* J) {
+  const long double pi = 3.14159265358979323846264338327950288L;
+  const long double a_d = 63.0L / 62.0L / h, b_d = 17.0L / 62.0L / (3.0L * h), al_d = 9.0L / 62.0L;
+  const long double a_i = 0.75L, b_i = 1.0L / 20.0L, al_i = 3.0L / 10.0L;
+  for (int64_t k = 0; k < n; ++k) {
+    const long double t = 2.0L * pi * (long double)k / (long double)n;
+    if (!compact) {
+      L[k] = (double)((2.0L * cosl(t) - 2.0L) / ((long double)h * (long double)h));
+      J[k] = 1.0;
+    } else {
+      const long double sd = a_d * sinl(t / 2) + b_d * sinl(1.5L * t), td = 1 + 2 * al_d * cosl(t);
+      const long double si = a_i * cosl(t / 2) + b_i * cosl(1.5L * t), ti = 1 + 2 * al_i * cosl(t);
+      L[k] = (double)(-4.0L * sd * sd / (td * td));
+      J[k] = (double)(4.0L * si * si / (ti * ti));
+    }
+  }
+}
+
+/* in place: u[e] over lines of axis d (n = extent, stride) <- sum_j u[j] cas(2 pi j e / n) */
+static void dht_axis_naive(const int64_t n[3], int d, double* u) {
+  const long double pi = 3.14159265358979323846264338327950288L;
+  const int64_t m = n[d], stride = d == 0 ? 1 : (d == 1 ? n[0] : n[0] * n[1]);
+  double* cas = (double*)malloc(sizeof(double) * m);
+  for (int64_t q = 0; q < m; ++q) {
+    const long double t = 2.0L * pi * (long double)q / (long double)m;
+    cas[q] = (double)(cosl(t) + sinl(t));
+  }
+  const int64_t N = n[0] * n[1] * n[2], lines = N / m;
+#pragma omp parallel
+  {
+    double* in = (double*)malloc(sizeof(double) * m);
+#pragma omp for schedule(static)
+    for (int64_t l = 0; l < lines; ++l) {
+      /* line l: base = (l % stride) + (l / stride) * stride * m */
+      const int64_t base = (l % stride) + (l / stride) * stride * m;
+      for (int64_t j = 0; j < m; ++j) in[j] = u[base + j * stride];
+      for (int64_t e = 0; e < m; ++e) {
+        double acc = 0.0;
+        for (int64_t j = 0; j < m; ++j) acc += in[j] * cas[(j * e) % m];
+        u[base + e * stride] = acc;
+      }
+    }
+    free(in);
+  }
+  free(cas);
+}
+
+void pbo_fft_pc_apply(const int64_t n[3], const double h[3], int compact, const double* r,
+                      double* z) {
+  const int64_t N = n[0] * n[1] * n[2];
+  double* L[3];
+  double* J[3];
+  double bound = 0.0, lmax[3], jmax[3];
+  for (int d = 0; d < 3; ++d) {
+    L[d] = (double*)malloc(sizeof(double) * n[d]);
+    J[d] = (double*)malloc(sizeof(double) * n[d]);
+    fft_axis_symbols(compact, n[d], h[d], L[d], J[d]);
+    lmax[d] = jmax[d] = 0.0;
+    for (int64_t k = 0; k < n[d]; ++k) {
+      lmax[d] = fmax(lmax[d], fabs(L[d][k]));
+      jmax[d] = fmax(jmax[d], J[d][k]);
+    }
+  }
+  bound = lmax[0] * jmax[1] * jmax[2] + jmax[0] * lmax[1] * jmax[2] + jmax[0] * jmax[1] * lmax[2];
+  const double thr = 1e-10 * bound, scale = 1.0 / ((double)n[0] * (double)n[1] * (double)n[2]);
+  memcpy(z, r, sizeof(double) * N);
+  for (int d = 0; d < 3; ++d) dht_axis_naive(n, d, z);
+  for (int64_t k = 0; k < n[2]; ++k)
+    for (int64_t j = 0; j < n[1]; ++j)
+      for (int64_t i = 0; i < n[0]; ++i) {
+        const double lam = (L[0][i] * J[1][j] + J[0][i] * L[1][j]) * J[2][k] +
+                           J[0][i] * J[1][j] * L[2][k];
+        const int64_t id = i + n[0] * (j + n[1] * k);
+        z[id] = fabs(lam) > thr ? z[id] * (scale / lam) : 0.0;
+      }
+  for (int d = 0; d < 3; ++d) dht_axis_naive(n, d, z);
+  for (int d = 0; d < 3; ++d) {
+    free(L[d]);
+    free(J[d]);
+  }
+}
+
 /* KSP_PCApply = PCApply_Jacobi (z = diag^-1 .* r, PETSc stores the reciprocal) followed by
  * KSP_RemoveNullSpace -> MatNullSpaceRemove(has_cnst): z += VecSum(z) / (-N). */
 static void pc_apply(int64_t N, const double* r, double* z, double dinv, int pc, int nsp, int nt) {
@@ -452,13 +546,17 @@ static void op_apply(const int64_t n[3], const double h[3], const double* x, dou
 }
 
 /* PCApply for every pc_type: Jacobi / none as above; SOR (2) and MG (3) through pbo_mg_apply,
+ * FFT (4) through pbo_fft_pc_apply,
  * followed by the same null-space removal */
 static void pc_apply_any(const int64_t n[3], const double h[3], const pbo_ksp_opts* o,
                          const double* r, double* z, double dinv, int nt) {
   const int64_t N = n[0] * n[1] * n[2];
-  if (o->pc_type == 2 || o->pc_type == 3) {
-    pbo_mg_apply(n, h, o->pc_type, o->mg_levels, o->mg_coarse_its, o->omega,
-                 o->nranks > 0 ? o->nranks : 1, r, z);
+  if (o->pc_type == 2 || o->pc_type == 3 || o->pc_type == 4) {
+    if (o->pc_type == 4)
+      pbo_fft_pc_apply(n, h, o->pc_compact, r, z);
+    else
+      pbo_mg_apply(n, h, o->pc_type, o->mg_levels, o->mg_coarse_its, o->omega,
+                   o->nranks > 0 ? o->nranks : 1, r, z);
     if (o->nullspace) {
       double shift = vsum(N, z, nt) / (-1.0 * (double)N);
       for (int64_t t = 0; t < N; ++t) z[t] += shift;

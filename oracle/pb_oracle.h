@@ -60,6 +60,8 @@ typedef struct {
   int mg_coarse_its; /* symmetric red-black sweeps on the coarsest level */
   double omega;      /* SOR relaxation */
   int nranks;        /* slab count the GPU run uses (only changes the automatic level count) */
+  int pc_compact;    /* pc 4 (fft): invert the compact operator's symbol (P = compact), else the
+                        7-point star's */
 } pbo_ksp_opts;
 
 /* ---- red-black SOR / geometric multigrid preconditioner (our GPU design, poissbox_amd/csrc/
@@ -69,6 +71,13 @@ int pbo_mg_plan_levels(const int64_t n[3], int nranks, int levels_req);
 /* z = M^-1 r from a zero initial guess; pc_type 2 (SOR) or 3 (MG) */
 void pbo_mg_apply(const int64_t n[3], const double h[3], int pc_type, int levels, int coarse_its,
                   double omega, int nranks, const double* r, double* z);
+
+/* spectral preconditioner (our design, poissbox_amd/csrc/pb_fft.hip; not in the reference):
+ * z = P^+ r for the periodic operator P (7-point star, or compact lapl when compact != 0), by a
+ * naive separable discrete Hartley transform (O(n) per element per axis, cas tables in long
+ * double) and the operator's Fourier symbol; 1/lambda := 0 where |lambda| <= 1e-10 * bound. */
+void pbo_fft_pc_apply(const int64_t n[3], const double h[3], int compact, const double* r,
+                      double* z);
 
 /* Returns PETSc KSPConvergedReason; history[0..nlog) = ||z_k||_2 (capacity max_it+1): the
  * entries KSPLogResidualHistory wrote -- its+1 normally, its after a breakdown exit (beta = 0,

@@ -21,7 +21,7 @@ import numpy as np
 from . import _lib as L
 
 STAR7, COMPACT, ASSEMBLED27 = 0, 1, 2
-PC_NONE, PC_JACOBI, PC_SOR, PC_MG = 0, 1, 2, 3
+PC_NONE, PC_JACOBI, PC_SOR, PC_MG, PC_FFT = 0, 1, 2, 3, 4
 
 REASONS = {0: "CONVERGED_ITERATING", 2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL",
            4: "CONVERGED_ITS", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",

@@ -1,0 +1,436 @@
+// pb_fft.hip -- spectral preconditioner (-pc_type fft): z = P^+ r for the periodic
+// constant-coefficient operators of this library, by separable discrete Hartley transforms.
+//
+// Every operator here is a sum of products of 1-D circulant operators with real, even symbols:
+//   7-point star (src/coefficients.f90:22-48):   lambda = sum_d (2 cos t_d - 2) / h_d^2
+//   compact lapl (src/compact_schemes.f90:17-37): lambda = Lx Jy Jz + Jx Ly Jz + Jx Jy Lz, with
+//     J(t) = (I+ I-)(t) = 4 (a_i cos(t/2) + b_i cos(3t/2))^2 / (1 + 2 alpha_i cos t)^2
+//     L(t) = (D+ D-)(t) = -4 (a_d sin(t/2) + b_d sin(3t/2))^2 / (1 + 2 alpha_d cos t)^2
+//     (coefficients :188-190, :303-305; D+ = -D-^T, I+ = I-^T, so lambda is real and <= 0)
+// A symbol even in each t_d separately is diagonalised by the separable real Hartley transform
+// H = Hx Hy Hz (H_d: cas(2 pi j k / n_d) = cos + sin, H_d H_d = n_d I), so
+//   P^+ = H diag(1 / (N lambda)) H,  1/lambda := 0 on the null modes (|lambda| <= 1e-10 max|lambda|:
+//   the constants, and for the compact operator every mode with two or more Nyquist components --
+//   the near-null modes that stall Jacobi- or 7-point-MG-preconditioned CG on config 5).
+// CG with this PC converges in a handful of iterations on any grid size.
+//
+// Passes (5 line passes, 16 B/DoF each, in place after the first): X forward (r -> z), Y forward,
+// Z forward * 1/(N lambda) * Z inverse (one kernel), Y inverse, X inverse. On a split grid the Z
+// pass runs on y-slabs with complete z-lines (the compact operators' z-slab <-> y-slab transposes).
+//
+// Line kernel: a block loads a tile of TL lines into LDS (coalesced rows), each wave takes two
+// real lines x, y and runs ONE complex FFT of z = x + i y of length n = 64*C: C-point DFTs in
+// registers (lane owns elements lane + 64 m), twiddles, then a 64-point DFT across the lanes by six
+// radix-2 decimation-in-frequency stages over wave shuffles (output in bit-reversed lane order);
+// the two Hartley spectra follow from Z(k) and Z(-k) (one more shuffle), and go back to LDS in
+// natural order for the coalesced store. Twiddles come from a per-axis table exp(-2 pi i k / n).
+#include <cmath>
+#include <vector>
+
+#include "pb_internal.hpp"
+
+namespace pb {
+
+namespace {
+
+struct DhtPass {
+  const double* in;   // tile source (X forward: r), else == out
+  double* out;
+  int64_t li, lo, es;  // element e of line (outer, inner) at outer*lo + inner*li + e*es
+  int ninner, nouter, ntiles_inner;
+  const double* w;    // twiddles of the line axis: (re, im) of exp(-2 pi i k / n), k < n
+  const double* tab;  // [Lx | Jx | Ly | Jy | Lz | Jz] (SCALE only)
+  int nx, ny, j0;     // global x / y sizes, global y of the box's row 0 (SCALE only)
+  double scale, thr;  // 1 / (nx ny nz) and the null-mode threshold (SCALE only)
+};
+
+struct cplx {
+  double re, im;
+};
+__device__ __forceinline__ cplx cmul(cplx a, cplx b) {
+  return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+__device__ __forceinline__ cplx tw(const double* w, int k) { return {w[2 * k], w[2 * k + 1]}; }
+
+__host__ __device__ constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v >> 1); }
+__host__ __device__ constexpr int bitrev(int v, int bits) {
+  int r = 0;
+  for (int b = 0; b < bits; ++b) r |= ((v >> b) & 1) << (bits - 1 - b);
+  return r;
+}
+
+// z (lane owns elements lane + 64 m, m < C) -> spectrum: lane L holds Z[k2 + C bitrev6(L)] in
+// z[k2]. n = 64 C, w = exp(-2 pi i k / n).
+template <int C>
+__device__ __forceinline__ void fft_wave(cplx (&z)[C], const double* w, int lane) {
+  constexpr int n = 64 * C, LB = ilog2(C);
+  // (1) C-point DFT over m in registers (radix-2 DIT, bit-reversed input order)
+  cplx t[C];
+#pragma unroll
+  for (int i = 0; i < C; ++i) t[i] = z[bitrev(i, LB)];
+#pragma unroll
+  for (int len = 2; len <= C; len <<= 1)
+#pragma unroll
+    for (int i = 0; i < C; i += len)
+#pragma unroll
+      for (int j = 0; j < len / 2; ++j) {
+        const cplx u = t[i + j], v = cmul(t[i + j + len / 2], tw(w, j * (n / len)));
+        t[i + j] = {u.re + v.re, u.im + v.im};
+        t[i + j + len / 2] = {u.re - v.re, u.im - v.im};
+      }
+  // (2) twiddles exp(-2 pi i lane k2 / n)
+#pragma unroll
+  for (int k2 = 0; k2 < C; ++k2) z[k2] = k2 ? cmul(t[k2], tw(w, (lane * k2) & (n - 1))) : t[k2];
+  // (3) 64-point DFT across lanes: radix-2 DIF, partner lane ^ h
+#pragma unroll
+  for (int h = 32; h >= 1; h >>= 1) {
+    const cplx wh = tw(w, (lane & (h - 1)) * (n / (2 * h)));
+    const bool upper = lane & h;
+#pragma unroll
+    for (int k2 = 0; k2 < C; ++k2) {
+      const cplx p = {__shfl_xor(z[k2].re, h, 64), __shfl_xor(z[k2].im, h, 64)};
+      if (upper)
+        z[k2] = cmul({p.re - z[k2].re, p.im - z[k2].im}, wh);
+      else
+        z[k2] = {z[k2].re + p.re, z[k2].im + p.im};
+    }
+  }
+}
+
+// Hartley spectra of the two real lines packed in z (spectrum layout of fft_wave): hx, hy at
+// k = k2 + C bitrev6(lane)
+template <int C>
+__device__ __forceinline__ void hartley_split(const cplx (&z)[C], double (&hx)[C], double (&hy)[C],
+                                              int lane) {
+  const int k1 = bitrev(lane, 6);
+#pragma unroll
+  for (int k2 = 0; k2 < C; ++k2) {
+    // partner -k mod n: k2 = 0 -> (0, -k1 mod 64); else (C - k2, 63 - k1)
+    const int k2p = k2 == 0 ? 0 : C - k2;
+    const int k1p = k2 == 0 ? ((64 - k1) & 63) : 63 - k1;
+    const int src = bitrev(k1p, 6);
+    const cplx m = {__shfl(z[k2p].re, src, 64), __shfl(z[k2p].im, src, 64)};
+    hx[k2] = 0.5 * ((z[k2].re + m.re) - (z[k2].im - m.im));
+    hy[k2] = 0.5 * ((z[k2].im + m.im) + (z[k2].re - m.re));
+  }
+}
+
+template <int C>
+struct DhtTile {
+  static constexpr int n = 64 * C;
+  static constexpr int TL = C >= 16 ? 8 : 16;  // lines per tile (LDS: TL * (n + 1) doubles)
+  static constexpr int NW = TL / 2;            // waves: two lines each
+  static constexpr int NT = 64 * NW;
+  static constexpr int LP = n + 1;             // odd line pitch: column writes spread over banks
+};
+
+// one DHT of the wave's two lines (pair p) in LDS, in place; SCALE: multiply by s(k) before the
+// write-back (callers run the inverse transform again afterwards)
+template <int C, bool SCALE>
+__device__ __forceinline__ void dht_pair(double* lds, int l0, const DhtPass& p, int lane,
+                                         int64_t outer, int inner0) {
+  using T = DhtTile<C>;
+  cplx z[C];
+#pragma unroll
+  for (int m = 0; m < C; ++m) z[m] = {lds[l0 * T::LP + lane + 64 * m], lds[(l0 + 1) * T::LP + lane + 64 * m]};
+  fft_wave<C>(z, p.w, lane);
+  double hx[C], hy[C];
+  hartley_split<C>(z, hx, hy, lane);
+  const int k1 = bitrev(lane, 6);
+  if constexpr (SCALE) {  // Z pass: line (i, j) -> kx = i, ky = j; element -> kz
+    const int nx = p.nx, ny = p.ny;
+    const int i0 = inner0 + l0, j = p.j0 + (int)outer;
+    const double* Lx = p.tab;
+    const double* Jx = Lx + nx;
+    const double* Ly = Jx + nx;
+    const double* Jy = Ly + ny;
+    const double* Lz = Jy + ny;
+    const double* Jz = Lz + T::n;
+    const double ly = Ly[j], jy = Jy[j];
+    const double a0 = Lx[i0] * jy + Jx[i0] * ly, c0 = Jx[i0] * jy;
+    const double a1 = Lx[i0 + 1] * jy + Jx[i0 + 1] * ly, c1 = Jx[i0 + 1] * jy;
+#pragma unroll
+    for (int k2 = 0; k2 < C; ++k2) {
+      const int k = k2 + C * k1;
+      const double lam0 = a0 * Jz[k] + c0 * Lz[k], lam1 = a1 * Jz[k] + c1 * Lz[k];
+      hx[k2] = fabs(lam0) > p.thr ? hx[k2] * (p.scale / lam0) : 0.0;
+      hy[k2] = fabs(lam1) > p.thr ? hy[k2] * (p.scale / lam1) : 0.0;
+    }
+  }
+#pragma unroll
+  for (int k2 = 0; k2 < C; ++k2) {
+    const int k = k2 + C * k1;
+    lds[l0 * T::LP + k] = hx[k2];
+    lds[(l0 + 1) * T::LP + k] = hy[k2];
+  }
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LAYOUT 0: the tile's lines are adjacent (li = 1), elements strided (rows of TL doubles);
+// LAYOUT 1: lines contiguous (es = 1). MODE 0: one DHT; MODE 1: DHT, 1/(N lambda), DHT.
+template <int C, int LAYOUT, int MODE>
+__global__ __launch_bounds__(DhtTile<C>::NT) void dht_lines_kernel(DhtPass p, const int* skip) {
+  using T = DhtTile<C>;
+  constexpr int n = T::n, TL = T::TL, NT = T::NT, LP = T::LP;
+  if (skip && *skip) return;  // CG's device convergence flag (uniform)
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int tile = blockIdx.x;
+  const int64_t outer = tile / p.ntiles_inner;
+  const int inner0 = (tile % p.ntiles_inner) * TL;
+  const int64_t base = outer * p.lo + (int64_t)inner0 * p.li;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  typedef double dv2 __attribute__((ext_vector_type(2)));
+  // tile -> LDS (16-byte pairs along the contiguous direction)
+  constexpr int NP = TL * n / 2;
+#pragma unroll 4
+  for (int f = threadIdx.x; f < NP; f += NT) {
+    int l, e;
+    if (LAYOUT == 0) {
+      l = (f % (TL / 2)) * 2;
+      e = f / (TL / 2);
+    } else {
+      l = f / (n / 2);
+      e = (f % (n / 2)) * 2;
+    }
+    const dv2 v = __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es));
+    if (LAYOUT == 0) {
+      lds[l * LP + e] = v.x;
+      lds[(l + 1) * LP + e] = v.y;
+    } else {
+      lds[l * LP + e] = v.x;
+      lds[l * LP + e + 1] = v.y;
+    }
+  }
+  __syncthreads();
+  const int l0 = 2 * wave;
+  if (l0 < p.ninner - inner0) {
+    dht_pair<C, MODE == 1>(lds, l0, p, lane, outer, inner0);
+    if (MODE == 1) {
+      wave_sync_lds();
+      dht_pair<C, false>(lds, l0, p, lane, outer, inner0);
+    }
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int f = threadIdx.x; f < NP; f += NT) {
+    int l, e;
+    if (LAYOUT == 0) {
+      l = (f % (TL / 2)) * 2;
+      e = f / (TL / 2);
+    } else {
+      l = f / (n / 2);
+      e = (f % (n / 2)) * 2;
+    }
+    dv2 v;
+    if (LAYOUT == 0) {
+      v.x = lds[l * LP + e];
+      v.y = lds[(l + 1) * LP + e];
+    } else {
+      v.x = lds[l * LP + e];
+      v.y = lds[l * LP + e + 1];
+    }
+    __builtin_nontemporal_store(v, (dv2*)(p.out + base + l * p.li + e * p.es));
+  }
+}
+
+template <int C, int LAYOUT, int MODE>
+int launch_dht_c(pb_ctx* ctx, DhtPass& p, const int* skip) {
+  using T = DhtTile<C>;
+  p.ntiles_inner = (p.ninner + T::TL - 1) / T::TL;
+  const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
+  const size_t lds = (size_t)T::TL * T::LP * sizeof(double);
+  auto kern = dht_lines_kernel<C, LAYOUT, MODE>;
+  static bool attr = false;
+  if (!attr) {
+    PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(T::NT), lds, ctx->stream, p, skip);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+template <int LAYOUT, int MODE>
+int launch_dht(pb_ctx* ctx, int64_t n, DhtPass& p, const int* skip) {
+  switch (n) {
+    case 64: return launch_dht_c<1, LAYOUT, MODE>(ctx, p, skip);
+    case 128: return launch_dht_c<2, LAYOUT, MODE>(ctx, p, skip);
+    case 256: return launch_dht_c<4, LAYOUT, MODE>(ctx, p, skip);
+    case 512: return launch_dht_c<8, LAYOUT, MODE>(ctx, p, skip);
+    case 1024: return launch_dht_c<16, LAYOUT, MODE>(ctx, p, skip);
+  }
+  return set_error(PB_ERR_UNSUPPORTED, "fft pc: line length %lld (64..1024, power of two)",
+                   (long long)n);
+}
+
+bool dht_length_ok(int64_t n) { return n >= 64 && n <= 1024 && (n & (n - 1)) == 0; }
+
+}  // namespace
+
+struct FftPc {
+  pb_grid* g = nullptr;
+  double* dev = nullptr;  // twiddles (2 nx | 2 ny | 2 nz) then symbol tables (2 nx | 2 ny | 2 nz)
+  double* tw[3] = {nullptr, nullptr, nullptr};
+  double* tab = nullptr;
+  double* ybuf = nullptr;  // split grids: one y-slab field + the transpose aux space
+  double thr = 0.0;
+};
+
+// per-axis symbol factors (L, J) of the operator kind at wavenumber t = 2 pi k / n
+static void axis_symbols(int compact, int64_t n, double h, double* L, double* J) {
+  const double a_d = 63.0 / 62.0 / h, b_d = 17.0 / 62.0 / (3.0 * h), al_d = 9.0 / 62.0;
+  const double a_i = 0.75, b_i = 1.0 / 20.0, al_i = 3.0 / 10.0;
+  for (int64_t k = 0; k < n; ++k) {
+    const long double t = 2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
+    if (!compact) {
+      L[k] = (double)((2.0L * cosl(t) - 2.0L) / ((long double)h * (long double)h));
+      J[k] = 1.0;
+      continue;
+    }
+    const long double sd = a_d * sinl(t / 2) + b_d * sinl(1.5L * t);
+    const long double td = 1.0L + 2.0L * al_d * cosl(t);
+    const long double si = a_i * cosl(t / 2) + b_i * cosl(1.5L * t);
+    const long double ti = 1.0L + 2.0L * al_i * cosl(t);
+    L[k] = (double)(-4.0L * sd * sd / (td * td));
+    J[k] = (double)(4.0L * si * si / (ti * ti));
+  }
+}
+
+int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
+  for (int d = 0; d < 3; ++d)
+    if (!dht_length_ok(g->n[d]))
+      return set_error(PB_ERR_UNSUPPORTED,
+                       "-pc_type fft: every grid extent must be a power of two in 64..1024 "
+                       "(got %lld x %lld x %lld)",
+                       (long long)g->n[0], (long long)g->n[1], (long long)g->n[2]);
+  if (grid_split(g) && g->n[1] < g->ctx->nranks)
+    return set_error(PB_ERR_UNSUPPORTED, "-pc_type fft: ny < ranks");
+  FftPc* f = new FftPc();
+  f->g = g;
+  const int64_t nsum = g->n[0] + g->n[1] + g->n[2];
+  std::vector<double> host(4 * nsum);
+  double* ht = host.data();
+  double* hs = host.data() + 2 * nsum;
+  double lmax[3], jmax[3];
+  int64_t off = 0;
+  for (int d = 0; d < 3; ++d) {
+    const int64_t n = g->n[d];
+    for (int64_t k = 0; k < n; ++k) {
+      const long double t = -2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
+      ht[2 * (off + k)] = (double)cosl(t);
+      ht[2 * (off + k) + 1] = (double)sinl(t);
+    }
+    double* L = hs + 2 * off;
+    double* J = L + n;
+    axis_symbols(compact, n, deltas[d], L, J);
+    lmax[d] = jmax[d] = 0.0;
+    for (int64_t k = 0; k < n; ++k) {
+      lmax[d] = std::max(lmax[d], std::fabs(L[k]));
+      jmax[d] = std::max(jmax[d], J[k]);
+    }
+    off += n;
+  }
+  // |lambda| <= sum_d max|L_d| prod_{e != d} max J_e
+  const double bound = lmax[0] * jmax[1] * jmax[2] + jmax[0] * lmax[1] * jmax[2] +
+                       jmax[0] * jmax[1] * lmax[2];
+  f->thr = 1e-10 * bound;
+  if (hipMalloc(&f->dev, host.size() * sizeof(double)) != hipSuccess) {
+    delete f;
+    return set_error(PB_ERR_ALLOC, "fft pc tables: out of device memory");
+  }
+  pb_ctx* ctx = g->ctx;
+  PB_HIP(hipMemcpyAsync(f->dev, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice,
+                        ctx->stream));
+  PB_SYNC(ctx, "fft pc tables");
+  f->tw[0] = f->dev;
+  f->tw[1] = f->dev + 2 * g->n[0];
+  f->tw[2] = f->dev + 2 * (g->n[0] + g->n[1]);
+  f->tab = f->dev + 2 * nsum;
+  if (grid_split(g)) {
+    const int64_t len = yslab_len(g) + yslab_aux_len(g);
+    if (hipMalloc(&f->ybuf, (size_t)len * sizeof(double)) != hipSuccess) {
+      (void)hipFree(f->dev);
+      delete f;
+      return set_error(PB_ERR_ALLOC, "fft pc y-slab buffer: out of device memory");
+    }
+  }
+  *out = f;
+  return PB_OK;
+}
+
+// one DHT along an axis of the box b (b[2] = planes), in place or from `in`
+static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, const double* in,
+                    double* out, const int* skip, int j0 = 0) {
+  DhtPass p{};
+  p.in = in;
+  p.out = out;
+  p.w = f->tw[axis];
+  const int64_t nx = b[0], ny = b[1], nz = b[2];
+  if (axis == 0) {  // contiguous lines: inner = j, outer = k
+    p.li = nx;
+    p.lo = nx * ny;
+    p.es = 1;
+    p.ninner = (int)ny;
+    p.nouter = (int)nz;
+    return launch_dht<1, 0>(ctx, nx, p, skip);
+  }
+  if (axis == 1) {  // inner = i, outer = k, elements along j
+    p.li = 1;
+    p.lo = nx * ny;
+    p.es = nx;
+    p.ninner = (int)nx;
+    p.nouter = (int)nz;
+    return launch_dht<0, 0>(ctx, ny, p, skip);
+  }
+  // axis 2 with the scaling: inner = i, outer = j, elements along k
+  p.li = 1;
+  p.lo = nx;
+  p.es = nx * ny;
+  p.ninner = (int)nx;
+  p.nouter = (int)ny;
+  p.tab = f->tab;
+  p.nx = (int)f->g->n[0];
+  p.ny = (int)f->g->n[1];
+  p.j0 = j0;
+  p.scale = 1.0 / ((double)f->g->n[0] * (double)f->g->n[1] * (double)f->g->n[2]);
+  p.thr = f->thr;
+  return launch_dht<0, 1>(ctx, nz, p, skip);
+}
+
+int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip) {
+  pb_grid* g = f->g;
+  pb_ctx* ctx = g->ctx;
+  ScopedTimer tm(ctx, "pc_fft");
+  const int64_t b[3] = {g->n[0], g->n[1], g->nzl};
+  PB_TRY(dht_axis(ctx, f, b, 0, r, z, skip));
+  PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
+  if (!grid_split(g)) {
+    PB_TRY(dht_axis(ctx, f, b, 2, z, z, skip));
+  } else {
+    YSlabPlan yp;
+    double* fy = f->ybuf;
+    PB_TRY(yslab_begin(g, fy + yslab_len(g), &yp));
+    PB_TRY(yslab_to(g, yp, z, fy));
+    const int64_t by[3] = {g->n[0], yp.ny_me, g->n[2]};
+    PB_TRY(dht_axis(ctx, f, by, 2, fy, fy, skip, (int)yp.j0[ctx->rank]));
+    PB_TRY(yslab_from(g, yp, fy, z));
+  }
+  PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
+  return dht_axis(ctx, f, b, 0, z, z, skip);
+}
+
+void fftpc_destroy(FftPc* f) {
+  if (!f) return;
+  (void)wait_stream(f->g->ctx, f->g->ctx->stream, "fftpc_destroy");
+  if (f->dev) (void)hipFree(f->dev);
+  if (f->ybuf) (void)hipFree(f->ybuf);
+  delete f;
+}
+
+}  // namespace pb

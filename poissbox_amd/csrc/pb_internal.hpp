@@ -363,6 +363,13 @@ void mg_destroy(Mg* mg);
 // deterministic level count for a global grid split over nranks z-slabs (every rank agrees)
 int mg_plan_levels(const int64_t n[3], int nranks, int levels_req);
 
+// ---- spectral preconditioner (pb_fft.hip): z = P^+ r by separable Hartley transforms ----
+struct FftPc;
+// compact: invert the compact operator's symbol (else the 7-point star's); power-of-two extents
+int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out);
+int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip = nullptr);
+void fftpc_destroy(FftPc* f);
+
 // ---- context scratch: at least n doubles, valid until the next call on this context ----
 int ctx_scratch(pb_ctx* ctx, size_t n, double** out);
 

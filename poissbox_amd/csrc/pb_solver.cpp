@@ -34,6 +34,8 @@ struct pb_ksp {
   double* w = nullptr;   // generic (unfused) path only
   double* z = nullptr;   // generic path only
   pb::Mg* mg = nullptr;  // SOR / multigrid preconditioner (PB_PC_SOR, PB_PC_MG)
+  pb::FftPc* fft = nullptr;  // spectral preconditioner (PB_PC_FFT)
+  bool stored_z() const { return mg || fft; }  // PCs whose z = M^-1 r is stored (not Jacobi)
   CgState* d_st = nullptr;
   double* d_hist = nullptr;
   int64_t nhist = 0;
@@ -201,6 +203,7 @@ int pb_ksp_opts_parse(pb_ksp_opts* o, int argc, const char* const* argv) {
       else if (!strcmp(v, "jacobi")) o->pc_type = PB_PC_JACOBI;
       else if (!strcmp(v, "sor")) o->pc_type = PB_PC_SOR;
       else if (!strcmp(v, "mg") || !strcmp(v, "gamg")) o->pc_type = PB_PC_MG;
+      else if (!strcmp(v, "fft")) o->pc_type = PB_PC_FFT;
       else return set_error(PB_ERR_UNSUPPORTED, "-pc_type %s", v);
       ++i;
     } else if (!strcmp(a, "-ksp_rtol") && v) {
@@ -246,11 +249,13 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   if (opts) k->opts = *opts;
   else pb_ksp_opts_default(&k->opts);
   if (k->opts.check_every < 1) k->opts.check_every = 8;
-  // SOR / MG iterations are expensive and few: poll the device flag more often
-  if ((k->opts.pc_type == PB_PC_SOR || k->opts.pc_type == PB_PC_MG) && k->opts.check_every > 2)
+  // SOR / MG / FFT iterations are expensive and few: poll the device flag more often
+  if ((k->opts.pc_type == PB_PC_SOR || k->opts.pc_type == PB_PC_MG ||
+       k->opts.pc_type == PB_PC_FFT) && k->opts.check_every > 2)
     k->opts.check_every = 2;
   const int pc = k->opts.pc_type;
-  if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG) {
+  if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG &&
+      pc != PB_PC_FFT) {
     delete k;
     return set_error(PB_ERR_UNSUPPORTED, "unknown pc_type %d", pc);
   }
@@ -269,14 +274,23 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
       return rc;
     }
   }
+  if (pc == PB_PC_FFT) {
+    // the symbol of P: the compact operator (config 5: A = P = compact) or the 7-point star
+    const int rc = fftpc_create(g, P->deltas, P->kind == PB_OP_COMPACT, &k->fft);
+    if (rc != PB_OK) {
+      delete k;
+      return rc;
+    }
+  }
   if (field_alloc(&k->r, vb) != hipSuccess || field_alloc(&k->pb[0], vb) != hipSuccess ||
       field_alloc(&k->pb[1], vb) != hipSuccess) {
     delete k;
     return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
   }
-  if (!fused_kind(A->kind) || k->mg) {
+  if (!fused_kind(A->kind) || k->stored_z()) {
     if (field_alloc(&k->w, vb) != hipSuccess || field_alloc(&k->z, vb) != hipSuccess) {
       if (k->mg) mg_destroy(k->mg);
+      fftpc_destroy(k->fft);
       delete k;
       return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
     }
@@ -301,6 +315,14 @@ static int ensure_done_cap(pb_ksp* k, int64_t need) {
   PB_HIP(hipHostGetDevicePointer((void**)&k->h_done_dev, h, 0));
   k->done_cap = cap;
   return PB_OK;
+}
+
+// z = M^-1 r for the stored-z preconditioners; *np = residual-sum partial blocks written by the
+// PC itself (MG's last sweep), 0 if the caller must take the sums
+static int pc_apply_dev(pb_ksp* k, const double* r, double* z, const int* skip, int* np) {
+  *np = 0;
+  if (k->fft) return fftpc_apply(k->fft, r, z, skip);
+  return mg_apply(k->mg, r, z, skip, k->d_st, np);
 }
 
 int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
@@ -343,14 +365,14 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
       return set_error(PB_ERR_ALLOC, "CG direction buffers: out of device memory");
   }
   PB_HIP(hipMemcpyAsync(k->d_st, &st, sizeof(st), hipMemcpyHostToDevice, ctx->stream));
-  if (k->mg) {
+  if (k->stored_z()) {
     // r = b, x = 0, p = 0; z = M^-1 r; sums of z (KSPSolve_CG setup, PC_LEFT)
     const size_t vb = (size_t)g->nlocal * sizeof(double);
     PB_HIP(hipMemcpyAsync(k->r, b->d, vb, hipMemcpyDeviceToDevice, ctx->stream));
     PB_HIP(hipMemsetAsync(x->d, 0, vb, ctx->stream));
     PB_HIP(hipMemsetAsync(k->pb[0], 0, vb, ctx->stream));
     int np = 0;
-    PB_TRY(mg_apply(k->mg, k->r, k->z, nullptr, k->d_st, &np));
+    PB_TRY(pc_apply_dev(k, k->r, k->z, nullptr, &np));
     if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
     PB_TRY(cg_finalize_init(ctx, np, k->d_st, k->d_hist, k->h_done_dev));
   } else {
@@ -393,13 +415,14 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
   PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
   PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, k->r, k->d_st));
-  PB_TRY(mg_apply(k->mg, k->r, k->z, &k->d_st->done, k->d_st, &np));
+  PB_TRY(pc_apply_dev(k, k->r, k->z, &k->d_st->done, &np));
   if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
 }
 
 static int enqueue_iteration(pb_ksp* k) {
-  if (!fused_kind(k->A->kind)) return k->mg ? enqueue_pc_iteration(k) : enqueue_generic_iteration(k);
+  if (!fused_kind(k->A->kind))
+    return k->stored_z() ? enqueue_pc_iteration(k) : enqueue_generic_iteration(k);
   pb_grid* g = k->A->grid;
   pb_ctx* ctx = g->ctx;
   Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};
@@ -410,7 +433,7 @@ static int enqueue_iteration(pb_ksp* k) {
   // p of iterations i-1, i-2, i-3 (depth-4 deferral reads all three at i % 4 == 3)
   const double* p_prev[3] = {p_old, k->pb[(i + ns - 1) % ns], k->pb[(i + ns - 2) % ns]};
   // Jacobi: pass A builds z = dinv*r - mu on the fly; SOR / MG: z is stored (dinv = 1)
-  const double* zsrc = k->mg ? k->z : k->r;
+  const double* zsrc = k->stored_z() ? k->z : k->r;
   StencilPlanes gp;
   int nparts = 0;
   if (!ctx->split) {
@@ -440,10 +463,10 @@ static int enqueue_iteration(pb_ksp* k) {
   }
   PB_TRY(cg_finalize_pass_a(ctx, nparts, k->d_st));
   PB_TRY(launch_cg_pass_b(g, s, p_new, p_prev, k->x->d, k->r, gp, k->d_st, k->d_hist,
-                          k->h_done_dev, i, k->defer_x, !k->mg));
-  if (k->mg) {  // z = M^-1 r, then the residual sums over z
+                          k->h_done_dev, i, k->defer_x, !k->stored_z()));
+  if (k->stored_z()) {  // z = M^-1 r, then the residual sums over z
     int np = 0;
-    PB_TRY(mg_apply(k->mg, k->r, k->z, &k->d_st->done, k->d_st, &np));
+    PB_TRY(pc_apply_dev(k, k->r, k->z, &k->d_st->done, &np));
     if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
     PB_TRY(cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, i));
   }
@@ -557,6 +580,7 @@ int pb_ksp_destroy(pb_ksp* k) {
   if (k->w) (void)hipFree(k->w);
   if (k->z) (void)hipFree(k->z);
   if (k->mg) mg_destroy(k->mg);
+  fftpc_destroy(k->fft);
   (void)hipFree(k->d_st);
   if (k->d_hist) (void)hipFree(k->d_hist);
   if (k->h_done) (void)hipHostFree(k->h_done);
@@ -572,6 +596,8 @@ int pb_ksp_pc_apply(pb_ksp* k, const pb_vec* r, pb_vec* z) {
   pb_ctx* ctx = g->ctx;
   if (k->mg) {
     PB_TRY(mg_apply(k->mg, r->d, z->d));
+  } else if (k->fft) {
+    PB_TRY(fftpc_apply(k->fft, r->d, z->d));
   } else {
     PB_HIP(hipMemcpyAsync(z->d, r->d, (size_t)g->nlocal * sizeof(double),
                           hipMemcpyDeviceToDevice, ctx->stream));

@@ -1,4 +1,4 @@
-"""Full KSPSolve to rtol 1e-10 (SURVEY.md §8d timing (iii)) with -pc_type jacobi | sor | mg on one
+"""Full KSPSolve to rtol 1e-10 (SURVEY.md §8d timing (iii)) with -pc_type jacobi | sor | mg | fft on one
 GPU: iterations, wall time of the solve (inputs resident, HIP-synchronised), per-iteration time,
 and the multigrid V-cycle time. One JSON line per (n, pc). The oracle's CPU solve is timed at 64^3
 beside it (1 core).
@@ -41,7 +41,8 @@ def main():
             if pc == "sor" and n > 256:
                 continue
             opts = pb.ksp_options(["-pc_type", pc, "-ksp_rtol", "1e-10"])
-            k = pb.KSP(A, P, opts)
+            # fft: the PC inverts P's symbol, so config 5 takes P = A = the compact operator
+            k = pb.KSP(A, A if pc == "fft" else P, opts)
             k.solve(b, x)  # warm-up (allocations, first-touch)
             ctx.sync()
             ctx.set_timing(True)
@@ -50,7 +51,7 @@ def main():
             reason, its, hist = k.solve(b, x)
             ctx.sync()
             dt = time.perf_counter() - t0
-            mg_ms, mg_cnt = ctx.timing("mg_apply")
+            mg_ms, mg_cnt = ctx.timing("pc_fft" if pc == "fft" else "mg_apply")
             parts = {}
             for nm in ("mg_fine_smooth_first", "mg_fine_resid_restrict", "mg_fine_prolong_post",
                        "mg_coarse_levels", "cg_pass_a", "cg_pass_b", "cg_pass_b_even",
@@ -65,7 +66,7 @@ def main():
             out = {"n": n, "op": op, "pc": pc, "reason": int(reason), "its": int(its), "solve_ms": dt * 1e3,
                    "ms_per_it": dt * 1e3 / max(its, 1), "levels": k.pc_levels,
                    "rel_residual": r.norm() / b.norm(),
-                   "mg_apply_ms": (mg_ms / mg_cnt) if mg_cnt else None,
+                   "pc_apply_ms": (mg_ms / mg_cnt) if mg_cnt else None,
                    "per_apply_ms": parts}
             print(json.dumps(out), flush=True)
             r.destroy()

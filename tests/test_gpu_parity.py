@@ -792,6 +792,98 @@ def test_multirank_mg_bit_exact_and_cg(monkeypatch, kern, nranks, n):
 
 
 # ---------------------------------------------------------------------------------------------
+# spectral preconditioner (-pc_type fft, pb_fft.hip): z = P^+ r by separable Hartley transforms;
+# against the oracle's naive-sum restatement (tests/test_oracle.py pins that to the reference
+# operators). FFT and naive sums round differently: measured differences ~1e-14 of max|z|.
+# ---------------------------------------------------------------------------------------------
+FFT_PC_RTOL = 1e-11
+
+
+def _fft_case(n3, compact):
+    h = tuple(2 * np.pi / m for m in n3) if compact else tuple(1.0 / m for m in n3)
+    return h, (pb.COMPACT if compact else pb.STAR7)
+
+
+@pytest.mark.parametrize("compact", [False, True])
+@pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 256), (256, 128, 64), (1024, 64, 64),
+                                (64, 1024, 64), (64, 64, 512)])
+def test_fft_pc_apply_vs_oracle(ctx, n3, compact):
+    N = int(np.prod(n3))
+    h, kind = _fft_case(n3, compact)
+    r = O.fill_random(N, 17)
+    ref = O.fft_pc_apply(r, n3, h, compact)
+    da = pb.DA(ctx, n3)
+    P = pb.Mat(da, kind, h)
+    k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
+    rv, zv = pb.Vec(da), pb.Vec(da)
+    rv.set_values(r)
+    k.pc_apply(rv, zv)
+    z = zv.get_values()
+    assert np.isfinite(z).all()
+    err = float(np.max(np.abs(z - ref)) / np.max(np.abs(ref)))
+    assert err < FFT_PC_RTOL, err
+    k.destroy()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+@pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 128)])
+def test_cg_fft_pc_matches_oracle(ctx, n3, compact):
+    """CG + the spectral PC: A = P (7-point star, or config 5's compact operator). One iteration
+    reaches rounding level, so after ||z_0|| the logged norms are rounding noise: they are checked
+    against ||z_0|| (absolute), reason / its / x against the oracle."""
+    N = int(np.prod(n3))
+    h, kind = _fft_case(n3, compact)
+    x0 = O.fill_random(N, SEED)
+    b = O.lapl(x0, n3, h) if compact else O.stencil(x0, n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-10, pc="fft",
+                                  op="compact" if compact else "star7", nthreads=8)
+    assert ro == 2 and itso <= 3
+    da = pb.DA(ctx, n3)
+    A = pb.Mat(da, kind, h)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(A, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "1e-10"])
+    assert (reason, its) == (ro, itso)
+    assert abs(hist[0] - ho[0]) / ho[0] < 1e-12
+    assert np.max(np.abs(np.asarray(hist[1:]) - ho[1:])) / ho[0] < 1e-10
+    check_x(x.get_values(), xo)
+
+
+@pytest.mark.parametrize("compact", [False, True])
+@pytest.mark.parametrize("nranks,n3", [(2, (64, 64, 64)), (4, (128, 64, 64)), (3, (64, 64, 64))])
+def test_multirank_fft_pc(nranks, n3, compact):
+    """Split grid: the Z pass runs on y-slabs (z-slab <-> y-slab transposes); per-rank result
+    equals the single-grid oracle."""
+    N = int(np.prod(n3))
+    h, kind = _fft_case(n3, compact)
+    r = O.fill_random(N, 23)
+    ref = O.fft_pc_apply(r, n3, h, compact).reshape(n3[2], -1)
+    scale = float(np.max(np.abs(ref)))
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n3)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        P = pb.Mat(da, kind, h)
+        k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
+        rv, zv = pb.Vec(da), pb.Vec(da)
+        rv.set_values(r.reshape(n3[2], -1)[k0:k0 + nk])
+        k.pc_apply(rv, zv)
+        return k0, nk, zv.get_values()
+
+    for k0, nk, z in run_ranks(nranks, body):
+        err = float(np.max(np.abs(z - ref[k0:k0 + nk].reshape(-1)))) / scale
+        assert err < FFT_PC_RTOL, err
+
+
+def test_fft_pc_rejects_bad_extents(ctx):
+    for n3 in [(48, 64, 64), (64, 32, 64), (64, 64, 2048)]:
+        da = pb.DA(ctx, n3)
+        P = pb.Mat(da, pb.STAR7, tuple(1.0 / m for m in n3))
+        with pytest.raises(pb.PbError):
+            pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
+
+
+# ---------------------------------------------------------------------------------------------
 # compact Laplacian / compact CG on a split grid (z-slab <-> y-slab all-to-all transposes)
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("op", ["grad", "div", "interp", "interp_div", "lapl"])
