@@ -267,6 +267,19 @@ int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* c
                      double* x, double* r, const StencilPlanes& gp, CgState* st, double* hist,
                      int* h_done, int64_t host_iter, int defer, bool finalize = true);
 int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
+// Folded single-rank Jacobi iteration (finalize in the passes' prologues, pb_stencil.hip): state
+// in two slots st2[0..1]; pass A of iteration host_iter >= 1 runs stage 2 of host_iter - 1
+// (st2[1] -> st2[0], history and done flag as finalize's), pass B stage 1 (st2[0] -> st2[1]);
+// cg_fold_tail completes the last iteration of a batch and leaves the state in st2[0].
+int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const double* p_old,
+                            double* p_new, const StencilPlanes& gp, CgState* st2, int nparts_b,
+                            double* hist, int* h_done, int64_t host_iter, int* nblocks);
+int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
+                            const double* const* p_prev, double* x, double* r,
+                            const StencilPlanes& gp, CgState* st2, int nparts_a, int64_t host_iter,
+                            int defer, int* nparts_b);
+int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_done,
+                 int64_t host_iter);
 
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----
 int64_t compact_fast_work_len(const pb_grid* g);
@@ -279,11 +292,11 @@ inline int env_int(const char* name, int dflt) {
 // Field-sized device allocations (vectors, KSP work vectors). PB_ALLOC_CONTIGUOUS=1 asks for
 // physically contiguous memory (hipDeviceMallocContiguous): fewer translation misses when a
 // kernel streams many 1 GiB arrays at once (A/B knob for the x-update pass).
-inline hipError_t field_alloc(void** p, size_t bytes) {
-  static const int contiguous = env_int("PB_ALLOC_CONTIGUOUS", 0);
-  if (contiguous) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
-  return hipMalloc(p, bytes);
-}
+// PB_ALLOC_STAGGER=b: the n-th field starts (n % 8) * b bytes into its allocation (b a multiple
+// of 256), so arrays a kernel streams at the same offsets do not hit the same HBM channel / bank
+// at the same time (A/B knob). Free with field_free.
+hipError_t field_alloc(void** p, size_t bytes);
+void field_free(void* p);
 template <class T>
 inline hipError_t field_alloc(T** p, size_t bytes) {
   return field_alloc(reinterpret_cast<void**>(p), bytes);

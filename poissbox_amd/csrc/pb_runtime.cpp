@@ -7,10 +7,48 @@
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "pb_internal.hpp"
 
 namespace pb {
+
+// ---- field allocations (pb_internal.hpp) ----
+namespace {
+std::mutex g_field_mu;
+std::unordered_map<void*, void*> g_field_base;  // staggered pointer -> allocation base
+unsigned g_field_count = 0;
+}  // namespace
+
+hipError_t field_alloc(void** p, size_t bytes) {
+  static const int contiguous = env_int("PB_ALLOC_CONTIGUOUS", 0);
+  static const size_t stagger = (size_t)std::max(0, env_int("PB_ALLOC_STAGGER", 0)) & ~(size_t)255;
+  std::lock_guard<std::mutex> lk(g_field_mu);
+  const size_t off = stagger * (g_field_count++ % 8);
+  void* base = nullptr;
+  const hipError_t e = contiguous
+                           ? hipExtMallocWithFlags(&base, bytes + off, hipDeviceMallocContiguous)
+                           : hipMalloc(&base, bytes + off);
+  if (e != hipSuccess) return e;
+  *p = static_cast<char*>(base) + off;
+  if (off) g_field_base[*p] = base;
+  return hipSuccess;
+}
+
+void field_free(void* p) {
+  if (!p) return;
+  void* base = p;
+  {
+    std::lock_guard<std::mutex> lk(g_field_mu);
+    auto it = g_field_base.find(p);
+    if (it != g_field_base.end()) {
+      base = it->second;
+      g_field_base.erase(it);
+    }
+  }
+  (void)hipFree(base);
+}
 
 static thread_local char g_err[1024] = "";
 
@@ -670,7 +708,7 @@ int pb_vec_duplicate(const pb_vec* v, pb_vec** out) {
 int pb_vec_destroy(pb_vec* v) {
   if (!v) return PB_OK;
   (void)wait_stream(v->grid->ctx, v->grid->ctx->stream, "pb_vec_destroy");
-  (void)hipFree(v->d);
+  field_free(v->d);
   delete v;
   return PB_OK;
 }

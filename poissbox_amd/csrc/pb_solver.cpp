@@ -35,6 +35,7 @@ struct pb_ksp {
   double* z = nullptr;   // generic path only
   pb::Mg* mg = nullptr;  // SOR / multigrid preconditioner (PB_PC_SOR, PB_PC_MG)
   pb::FftPc* fft = nullptr;  // spectral preconditioner (PB_PC_FFT)
+  int fold_nparts_b = 0;     // partial-sum blocks of the last folded pass B
   bool stored_z() const { return mg || fft; }  // PCs whose z = M^-1 r is stored (not Jacobi)
   CgState* d_st = nullptr;
   double* d_hist = nullptr;
@@ -295,7 +296,7 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
       return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
     }
   }
-  PB_HIP(hipMalloc(&k->d_st, sizeof(CgState)));
+  PB_HIP(hipMalloc(&k->d_st, 2 * sizeof(CgState)));  // [1]: the folded iteration's second slot
   *out = k;
   return PB_OK;
 }
@@ -420,7 +421,9 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
 }
 
-static int enqueue_iteration(pb_ksp* k) {
+// fold: the finalize steps run in the passes' prologues (one rank, Jacobi; fold_a = pass A also
+// folds, i.e. this is not the first iteration of the batch)
+static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
   if (!fused_kind(k->A->kind))
     return k->stored_z() ? enqueue_pc_iteration(k) : enqueue_generic_iteration(k);
   pb_grid* g = k->A->grid;
@@ -436,6 +439,17 @@ static int enqueue_iteration(pb_ksp* k) {
   const double* zsrc = k->stored_z() ? k->z : k->r;
   StencilPlanes gp;
   int nparts = 0;
+  if (fold) {
+    gp.ghost_lo = gp.ghost_hi = nullptr;
+    gp.wrap = true;
+    if (fold_a)
+      PB_TRY(launch_cg_pass_a_folded(g, s, zsrc, p_old, p_new, gp, k->d_st, k->fold_nparts_b,
+                                     k->d_hist, k->h_done_dev, i, &nparts));
+    else
+      PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
+    return launch_cg_pass_b_folded(g, s, p_new, p_prev, k->x->d, k->r, gp, k->d_st, nparts, i,
+                                   k->defer_x, &k->fold_nparts_b);
+  }
   if (!ctx->split) {
     // periodic wrap read in place: pass A combines r, p_old of the wrap planes itself and pass B
     // reads p_new's wrap planes (no boundary-plane kernel on one rank)
@@ -487,17 +501,26 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
     }
   }
   PB_TRY(ensure_done_cap(k, k->host_iter + iters + 2));
-  for (int64_t n = 0; n < iters && !k->stopped; ++n) {
-    PB_TRY(enqueue_iteration(k));
+  // one rank, Jacobi, fused operator: the finalize steps ride in the passes' prologues
+  // (PB_CG_FOLD=0 keeps the separate finalize launches)
+  const bool fold = C >= 2 && !ctx->split && fused_kind(k->A->kind) && !k->stored_z() &&
+                    env_int("PB_CG_FOLD", 1) != 0;
+  int64_t n = 0;
+  for (; n < iters && !k->stopped; ++n) {
+    PB_TRY(enqueue_iteration(k, fold, fold && n > 0));
     const int64_t hi = k->host_iter++;
     PB_HIP(hipEventRecord(k->ring[hi % R], ctx->stream));
-    // lagged, rank-consistent poll: decide on the flag of iteration hi + 1 - C only
+    // lagged, rank-consistent poll: decide on the flag of iteration hi + 1 - C only (folded:
+    // that flag is written by the next iteration's pass A, so wait for that iteration's event)
     if ((hi + 1) % C == 0 && hi + 1 >= C) {
       const int64_t j = hi + 1 - C;
-      PB_TRY(wait_event(ctx, k->ring[j % R], "KSP convergence poll"));
+      PB_TRY(wait_event(ctx, k->ring[(fold ? j + 1 : j) % R], "KSP convergence poll"));
       if (k->h_done[j + 1]) k->stopped = true;
     }
   }
+  if (fold && n > 0)
+    PB_TRY(cg_fold_tail(ctx, k->fold_nparts_b, k->d_st, k->d_hist, k->h_done_dev,
+                        k->host_iter - 1));
   return PB_OK;
 }
 
@@ -574,11 +597,10 @@ int pb_ksp_solve(pb_ksp* k, const pb_vec* b, pb_vec* x, pb_ksp_result* res, doub
 int pb_ksp_destroy(pb_ksp* k) {
   if (!k) return PB_OK;
   (void)wait_stream(k->A->grid->ctx, k->A->grid->ctx->stream, "pb_ksp_destroy");
-  (void)hipFree(k->r);
-  for (double* p : k->pb)
-    if (p) (void)hipFree(p);
-  if (k->w) (void)hipFree(k->w);
-  if (k->z) (void)hipFree(k->z);
+  field_free(k->r);
+  for (double* p : k->pb) field_free(p);
+  field_free(k->w);
+  field_free(k->z);
   if (k->mg) mg_destroy(k->mg);
   fftpc_destroy(k->fft);
   (void)hipFree(k->d_st);

@@ -61,10 +61,12 @@ struct CombineLoad {
   const double* __restrict__ p;
   const CgState* st;
   double dinv, shift, bb;
-  __device__ __forceinline__ void prepare() {
-    dinv = st->dinv;
-    shift = -st->mu;
-    bb = cg_bb(st);
+  __device__ __forceinline__ void prepare() { prepare_from(*st); }
+  template <class S>
+  __device__ __forceinline__ void prepare_from(const S& s) {
+    dinv = s.dinv;
+    shift = -s.mu;
+    bb = s.it == 0 ? 0.0 : s.beta / s.betaold;
   }
   __device__ __forceinline__ const double* src(int a) const { return a == 0 ? r : p; }
   __device__ __forceinline__ double f(double rv, double pv) const {
@@ -140,7 +142,19 @@ struct PassB {
   const double* __restrict__ p_m3;
   const CgState* st;
   double alpha, alpha_prev, dinv, mu, a2, a3;
-  __device__ __forceinline__ void prepare();
+  __device__ __forceinline__ void prepare() { prepare_from(*st); }
+  template <class S>
+  __device__ __forceinline__ void prepare_from(const S& s) {
+    alpha = s.alpha;
+    alpha_prev = s.alpha_prev;
+    dinv = s.dinv;
+    mu = s.mu;
+    if constexpr (XU == 3) {  // pending alphas of iterations i-3, i-2, i-1
+      a3 = s.pa[0];
+      a2 = s.pa[1];
+      alpha_prev = s.pa[2];
+    }
+  }
   __device__ __forceinline__ const double* src(int a) const {
     return a == 0 ? r : (a == 1 ? x : (a == 2 ? p_prev : (a == 3 ? p_m2 : p_m3)));
   }
@@ -185,6 +199,38 @@ struct PassB {
 };
 
 // ---------------------------------------------------------------------------------------------
+// Finalize folded into the next pass's prologue (one rank, Jacobi CG): EVERY WAVE reduces the
+// previous pass's partials in the finalize kernel's fixed order (lane-strided sums, xor
+// butterfly: bit-identical in every lane) and runs the PETSc scalar step (stage 1 before pass B,
+// stage 2 of the previous iteration before pass A) on a register copy of the state -- no LDS, no
+// barrier; lane 0 of block 0 stores the result into the OTHER state slot, so the slot this launch
+// reads is never written while it runs. Removes the two finalize launches (and their kernel
+// boundaries) from every iteration.
+// ---------------------------------------------------------------------------------------------
+struct Fold {
+  int stage = 0;                  // 0: no fold; 1: stage 1 (pass B); 2: stage 2 (pass A)
+  int nparts = 0, width = 1;      // partials of the previous pass
+  const double* parts = nullptr;
+  const CgState* in = nullptr;    // state slot read
+  CgState* out = nullptr;         // state slot written (block 0)
+  double* hist = nullptr;         // stage 2: history / host-mapped done flags, as finalize's
+  int* h_done = nullptr;
+  int64_t host_iter = 0;          // stage 2: the iteration whose stage 2 this is
+};
+__device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st);
+
+// Load / Epi structs that read CG scalars have prepare_from(state): fed the register copy
+template <class T>
+__device__ __forceinline__ auto prepare_state(T& t, const CgState& s, int)
+    -> decltype(t.prepare_from(s), void()) {
+  t.prepare_from(s);
+}
+template <class T>
+__device__ __forceinline__ void prepare_state(T& t, const CgState&, long) {
+  t.prepare();
+}
+
+// ---------------------------------------------------------------------------------------------
 // The stencil engine
 // ---------------------------------------------------------------------------------------------
 template <int V, int TY, class Load, class Epi>
@@ -193,12 +239,20 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
                                                          const double* __restrict__ ghost_lo,
                                                          const double* __restrict__ ghost_hi,
                                                          Epi ep0, double* parts,
-                                                         const int* __restrict__ skip) {
-  if (skip && *skip) return;  // device-side convergence flag (uniform)
+                                                         const int* __restrict__ skip, Fold fold) {
   Load ld = ld0;
-  ld.prepare();
   Epi ep = ep0;
-  ep.prepare();
+  if (fold.stage) {
+    CgState sst;  // register copy
+    fold_prologue(fold, sst);
+    if (sst.done) return;  // uniform: every wave computed the same state
+    prepare_state(ld, sst, 0);
+    prepare_state(ep, sst, 0);
+  } else {
+    if (skip && *skip) return;  // device-side convergence flag (uniform)
+    ld.prepare();
+    ep.prepare();
+  }
   constexpr int NS = Epi::NS, NR = Load::NR;
   constexpr int NE = Epi::NE > 0 ? Epi::NE : 1;
   double acc[NS > 0 ? NS : 1];
@@ -471,7 +525,7 @@ static int pick_ty(int ny) {
 template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                     const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev,
-                    int wgcu) {
+                    int wgcu, const Fold& fold) {
   Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU);
   geo.wrap = gp.wrap && !g->ctx->split ? 1 : 0;
   const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
@@ -481,7 +535,7 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
                      (long long)nblocks);
   hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads), 0,
                      g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
-                     g->ctx->d_partials + (int64_t)part_off * NS, skip);
+                     g->ctx->d_partials + (int64_t)part_off * NS, skip, fold);
   PB_HIP(hipGetLastError());
   if (nb_out) *nb_out = (int)nblocks;
   return PB_OK;
@@ -502,7 +556,8 @@ struct TallOf<E, std::void_t<decltype(E::TALL)>> {
 template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                       const Epi& ep, const int* skip, int mode = PLANES_ALL, int part_off = 0,
-                      int* nb_out = nullptr, int rev = 0, int wgcu = 0) {
+                      int* nb_out = nullptr, int rev = 0, int wgcu = 0,
+                      const Fold& fold = Fold{}) {
   const bool vec2 = (g->n[0] % 2) == 0;
   const int ty = pick_ty((int)g->n[1]);
   if constexpr (TallOf<Epi>::v) {
@@ -511,19 +566,19 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
     if (vec2 && ty == 4 && tall && !getenv("PB_STENCIL_TY") && g->n[1] % 8 == 0 &&
         g->plane >= tall_min)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev,
-                            wgcu > 0 ? wgcu : 1);
+                            wgcu > 0 ? wgcu : 1, fold);
   }
   if (vec2) {
     switch (ty) {
-      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
-      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
-      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
+      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
+      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
+      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
     }
   }
   switch (ty) {
-    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
-    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
-    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu);
+    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
+    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
+    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
   }
 }
 
@@ -670,18 +725,6 @@ __device__ __forceinline__ void SorHalfT<SUMS>::prepare() {
   if constexpr (SUMS) mu = st->mu;
 }
 
-template <int XU>
-__device__ __forceinline__ void PassB<XU>::prepare() {
-  alpha = st->alpha;
-  alpha_prev = st->alpha_prev;
-  dinv = st->dinv;
-  mu = st->mu;
-  if constexpr (XU == 3) {  // pending alphas of iterations i-3, i-2, i-1
-    a3 = st->pa[0];
-    a2 = st->pa[1];
-    alpha_prev = st->pa[2];
-  }
-}
 
 // r = b, x = 0, p = 0 and the sums of s = dinv*r (t = s - 0)
 __global__ __launch_bounds__(256) void cg_init_kernel(const double* __restrict__ b,
@@ -723,187 +766,232 @@ __global__ __launch_bounds__(256) void cg_boundary_kernel(const double* __restri
 }
 
 // ---------------------------------------------------------------------------------------------
-// Finalize: deterministic fixed-order reduction of the per-block partials, then the PETSc CG
-// scalar logic (KSPSolve_CG + KSPConvergedDefault) on the device. mode bit 1 = reduce partials
-// into sums[], bit 2 = update the state from sums[] (split around the RCCL allreduce).
-// stage 0 = after init, 1 = after pass A (p.w), 2 = after pass B (residual sums).
+// CG scalar logic (PETSc KSPSolve_CG + KSPConvergedDefault), shared by the finalize kernel and
+// the folded pass prologues
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool finite(double v) { return v == v && v - v == 0.0; }
 
-__global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restrict__ parts,
-                                                          int nparts, int width, double* sums,
-                                                          int mode, int stage, CgState* st,
-                                                          double* hist, int* h_done,
-                                                          int64_t host_iter) {
-  __shared__ double red[256][4];
-  if (mode & 1) {
-    for (int s = 0; s < width; ++s) {
-      double v = 0.0;
-      for (int b = threadIdx.x; b < nparts; b += 256) v += parts[(int64_t)b * width + s];
-      red[threadIdx.x][s] = v;
-    }
-    __syncthreads();
-    for (int off = 128; off >= 1; off >>= 1) {
-      if ((int)threadIdx.x < off)
-        for (int s = 0; s < width; ++s) red[threadIdx.x][s] += red[threadIdx.x + off][s];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0)
-      for (int s = 0; s < width; ++s) sums[s] = red[0][s];
+// fixed-order reduction of nparts x width partials by ONE wave: lane l sums blocks l, l+64, ...
+// in order, then an xor butterfly (every lane ends with the same bits). Used by the finalize
+// kernel (wave 0) and by every wave of a folded pass prologue, so both paths round alike.
+__device__ __forceinline__ void wave_reduce_parts(const double* __restrict__ parts, int nparts,
+                                                  int width, double* S) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    double v = 0.0;
+    if (s < width)
+      for (int b = lane; b < nparts; b += 64) v += parts[(int64_t)b * width + s];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    S[s] = v;
   }
-  if (!(mode & 2) || threadIdx.x != 0) return;
-  double S[4];
-  for (int s = 0; s < 4; ++s) S[s] = s < width ? sums[s] : 0.0;
-  const double N = st->ntot;
-  if (stage == 0) {
-    double mu = 0.0, zz = S[1], zr = S[2];
-    if (st->nullspace) {
-      const double delta = S[0] / N;
-      mu = delta;
-      zz = S[1] - N * delta * delta;
-      zr = S[2] - delta * S[3];
-    }
-    const double dp = sqrt(zz > 0.0 ? zz : 0.0);
-    st->mu = mu;
-    st->dp = dp;
-    st->rnorm0 = dp;
-    st->it = 0;
-    st->its = 0;
-    st->dpi = 0.0;
-    st->alpha = 0.0;
-    st->alpha_prev = 0.0;
-    st->pend_iter = -1;
-    st->pend_count = 0;
-    st->reason = 0;
-    st->done = 0;
-    if (st->nhist > 0) hist[0] = dp;
-    st->nlog = st->nhist > 0 ? 1 : 0;
-    if (!finite(dp)) {
-      st->reason = PB_KSP_DIVERGED_NANORINF;
-      st->done = 1;
+}
+
+// stage 0 (after init / the first PC apply): S = (sum t, sum t^2, sum t.r, sum r)
+__device__ __forceinline__ void cg_stage0(CgState& st, const double* S, double* hist,
+                                          int* h_done) {
+  const double N = st.ntot;
+  double mu = 0.0, zz = S[1], zr = S[2];
+  if (st.nullspace) {
+    const double delta = S[0] / N;
+    mu = delta;
+    zz = S[1] - N * delta * delta;
+    zr = S[2] - delta * S[3];
+  }
+  const double dp = sqrt(zz > 0.0 ? zz : 0.0);
+  st.mu = mu;
+  st.dp = dp;
+  st.rnorm0 = dp;
+  st.it = 0;
+  st.its = 0;
+  st.dpi = 0.0;
+  st.alpha = 0.0;
+  st.alpha_prev = 0.0;
+  st.pend_iter = -1;
+  st.pend_count = 0;
+  st.reason = 0;
+  st.done = 0;
+  if (st.nhist > 0 && hist) hist[0] = dp;
+  st.nlog = st.nhist > 0 ? 1 : 0;
+  if (!finite(dp)) {
+    st.reason = PB_KSP_DIVERGED_NANORINF;
+    st.done = 1;
+  } else {
+    st.ttol = fmax(st.rtol * dp, st.atol);
+    if (dp <= st.ttol) {
+      st.reason = dp < st.atol ? PB_KSP_CONVERGED_ATOL : PB_KSP_CONVERGED_RTOL;
+      st.done = 1;
     } else {
-      st->ttol = fmax(st->rtol * dp, st->atol);
-      if (dp <= st->ttol) {
-        st->reason = dp < st->atol ? PB_KSP_CONVERGED_ATOL : PB_KSP_CONVERGED_RTOL;
-        st->done = 1;
-      } else {
-        st->beta = zr;
-        if (!finite(zr)) {
-          st->reason = PB_KSP_DIVERGED_NANORINF;
-          st->done = 1;
-        } else if (zr == 0.0) {
-          st->its = 1;
-          st->reason = PB_KSP_CONVERGED_ATOL;
-          st->done = 1;
-        } else if (st->max_it <= 0) {
-          st->reason = PB_KSP_DIVERGED_ITS;
-          st->done = 1;
-        }
+      st.beta = zr;
+      if (!finite(zr)) {
+        st.reason = PB_KSP_DIVERGED_NANORINF;
+        st.done = 1;
+      } else if (zr == 0.0) {
+        st.its = 1;
+        st.reason = PB_KSP_CONVERGED_ATOL;
+        st.done = 1;
+      } else if (st.max_it <= 0) {
+        st.reason = PB_KSP_DIVERGED_ITS;
+        st.done = 1;
       }
     }
-    if (h_done) h_done[0] = st->done;
-    return;
   }
-  if (stage == 1) {
-    if (st->done) return;
-    const int64_t i = st->it;
-    const double dpi = S[0];
-    const double sp = (double)((dpi > 0) - (dpi < 0)), so = (double)((st->dpi > 0) - (st->dpi < 0));
-    if (!finite(dpi)) {
-      st->its = i + 1;
-      st->reason = PB_KSP_DIVERGED_NANORINF;
-      st->done = 1;
-    } else if (dpi == 0.0 || (i > 0 && sp * so < 0.0)) {
-      st->its = i + 1;
-      st->reason = PB_KSP_DIVERGED_INDEFINITE_MAT;
-      st->done = 1;
-    } else {
-      st->dpiold = st->dpi;
-      st->dpi = dpi;
-      st->betaold = st->beta;
-      st->alpha_prev = st->alpha;
-      st->alpha = st->beta / dpi;
-    }
-    return;
+  if (h_done) h_done[0] = st.done;
+}
+
+// stage 1 (after pass A): dpi = p.w -> alpha, or an INDEFINITE_MAT / NaN exit
+__device__ __forceinline__ void cg_stage1(CgState& st, double dpi) {
+  if (st.done) return;
+  const int64_t i = st.it;
+  const double sp = (double)((dpi > 0) - (dpi < 0)), so = (double)((st.dpi > 0) - (st.dpi < 0));
+  if (!finite(dpi)) {
+    st.its = i + 1;
+    st.reason = PB_KSP_DIVERGED_NANORINF;
+    st.done = 1;
+  } else if (dpi == 0.0 || (i > 0 && sp * so < 0.0)) {
+    st.its = i + 1;
+    st.reason = PB_KSP_DIVERGED_INDEFINITE_MAT;
+    st.done = 1;
+  } else {
+    st.dpiold = st.dpi;
+    st.dpi = dpi;
+    st.betaold = st.beta;
+    st.alpha_prev = st.alpha;
+    st.alpha = st.beta / dpi;
   }
-  // stage 2
-  if (!st->done) {
-    const int64_t i = st->it;
-    double mu = st->mu, zz = S[1], zr = S[2];
-    if (st->nullspace) {
+}
+
+// stage 2 (after pass B / the PC apply): residual sums -> norm, convergence tests, next beta
+__device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* hist, int* h_done,
+                                          int64_t host_iter) {
+  if (!st.done) {
+    const double N = st.ntot;
+    const int64_t i = st.it;
+    double mu = st.mu, zz = S[1], zr = S[2];
+    if (st.nullspace) {
       const double delta = S[0] / N;
-      mu = st->mu + delta;
+      mu = st.mu + delta;
       zz = S[1] - N * delta * delta;
       zr = S[2] - delta * S[3];
     }
     const double dp = sqrt(zz > 0.0 ? zz : 0.0);
     // iterations i % D < D-1 leave alpha_i p_i pending in x; the last of each D applied them all
     // (PassB<XU>)
-    const int D = st->defer_x;
+    const int D = st.defer_x;
     const int m = D > 0 ? (int)(i % D) : 0;
     if (D > 0 && m < D - 1) {
-      st->pa[m] = st->alpha;
-      st->pend_iter = i - m;
-      st->pend_count = m + 1;
+      // (value selects, no computed index: st may be a register copy)
+      st.pa[0] = m == 0 ? st.alpha : st.pa[0];
+      st.pa[1] = m == 1 ? st.alpha : st.pa[1];
+      st.pa[2] = m == 2 ? st.alpha : st.pa[2];
+      st.pend_iter = i - m;
+      st.pend_count = m + 1;
     } else {
-      st->pend_iter = -1;
-      st->pend_count = 0;
+      st.pend_iter = -1;
+      st.pend_count = 0;
     }
-    st->dp = dp;
-    st->its = i + 1;
-    if (i + 1 < st->nhist) {
-      hist[i + 1] = dp;
-      st->nlog = i + 2;
+    st.dp = dp;
+    st.its = i + 1;
+    if (i + 1 < st.nhist) {
+      if (hist) hist[i + 1] = dp;
+      st.nlog = i + 2;
     }
     if (!finite(dp)) {
-      st->reason = PB_KSP_DIVERGED_NANORINF;
-      st->done = 1;
-    } else if (dp <= st->ttol) {
-      st->reason = dp < st->atol ? PB_KSP_CONVERGED_ATOL : PB_KSP_CONVERGED_RTOL;
-      st->done = 1;
-    } else if (dp >= st->dtol * st->rnorm0) {
-      st->reason = PB_KSP_DIVERGED_DTOL;
-      st->done = 1;
+      st.reason = PB_KSP_DIVERGED_NANORINF;
+      st.done = 1;
+    } else if (dp <= st.ttol) {
+      st.reason = dp < st.atol ? PB_KSP_CONVERGED_ATOL : PB_KSP_CONVERGED_RTOL;
+      st.done = 1;
+    } else if (dp >= st.dtol * st.rnorm0) {
+      st.reason = PB_KSP_DIVERGED_DTOL;
+      st.done = 1;
     } else {
-      st->beta = zr;
-      st->mu = mu;
-      st->it = i + 1;
+      st.beta = zr;
+      st.mu = mu;
+      st.it = i + 1;
       if (!finite(zr)) {
-        st->reason = PB_KSP_DIVERGED_NANORINF;
-        st->done = 1;
-      } else if (st->it >= st->max_it) {
-        st->reason = PB_KSP_DIVERGED_ITS;
-        st->done = 1;
+        st.reason = PB_KSP_DIVERGED_NANORINF;
+        st.done = 1;
+      } else if (st.it >= st.max_it) {
+        st.reason = PB_KSP_DIVERGED_ITS;
+        st.done = 1;
       } else if (zr == 0.0) {
-        st->its = st->it + 1;
-        st->reason = PB_KSP_CONVERGED_ATOL;
-        st->done = 1;
-      } else if (zr * st->betaold < 0.0) {
+        st.its = st.it + 1;
+        st.reason = PB_KSP_CONVERGED_ATOL;
+        st.done = 1;
+      } else if (zr * st.betaold < 0.0) {
         // PETSc KSPSolve_CG, top of iteration i+1 (real scalars): beta*betaold < 0 -> the
         // preconditioner is indefinite (betaold = the beta iteration i used, stage 1)
-        st->its = st->it + 1;
-        st->reason = PB_KSP_DIVERGED_INDEFINITE_PC;
-        st->done = 1;
+        st.its = st.it + 1;
+        st.reason = PB_KSP_DIVERGED_INDEFINITE_PC;
+        st.done = 1;
       }
     }
   }
-  if (h_done) h_done[host_iter + 1] = st->done;
+  if (h_done) h_done[host_iter + 1] = st.done;
+}
+
+// Finalize: deterministic fixed-order reduction of the per-block partials, then the PETSc CG
+// scalar logic (KSPSolve_CG + KSPConvergedDefault) on the device. mode bit 1 = reduce partials
+// into sums[], bit 2 = update the state from sums[] (split around the RCCL allreduce).
+// stage 0 = after init, 1 = after pass A (p.w), 2 = after pass B (residual sums).
+__global__ __launch_bounds__(64) void cg_finalize_kernel(const double* __restrict__ parts,
+                                                          int nparts, int width, double* sums,
+                                                          int mode, int stage, CgState* st,
+                                                          double* hist, int* h_done,
+                                                          int64_t host_iter) {
+  if (threadIdx.x >= 64) return;  // one wave
+  double S[4];
+  if (mode & 1) {
+    wave_reduce_parts(parts, nparts, width, S);
+    if (threadIdx.x == 0)
+      for (int s = 0; s < width; ++s) sums[s] = S[s];
+  }
+  if (!(mode & 2) || threadIdx.x != 0) return;
+  for (int s = 0; s < 4; ++s) S[s] = s < width ? sums[s] : 0.0;
+  if (stage == 0) cg_stage0(*st, S, hist, h_done);
+  else if (stage == 1) cg_stage1(*st, S[0]);
+  else cg_stage2(*st, S, hist, h_done, host_iter);
+}
+
+// field-wise copy (an aggregate copy becomes a memcpy that pins the register copy in scratch)
+__device__ __forceinline__ void cg_copy(CgState& d, const CgState& s) {
+  d.beta = s.beta, d.betaold = s.betaold, d.dpi = s.dpi, d.dpiold = s.dpiold;
+  d.alpha = s.alpha, d.alpha_prev = s.alpha_prev, d.mu = s.mu, d.dp = s.dp, d.ttol = s.ttol;
+  d.rnorm0 = s.rnorm0, d.pa[0] = s.pa[0], d.pa[1] = s.pa[1], d.pa[2] = s.pa[2];
+  d.rtol = s.rtol, d.atol = s.atol, d.dtol = s.dtol, d.dinv = s.dinv, d.ntot = s.ntot;
+  d.it = s.it, d.its = s.its, d.max_it = s.max_it, d.nhist = s.nhist, d.pend_iter = s.pend_iter;
+  d.pend_count = s.pend_count, d.nlog = s.nlog;
+  d.reason = s.reason, d.done = s.done, d.pc = s.pc, d.nullspace = s.nullspace;
+  d.defer_x = s.defer_x;
+}
+static_assert(sizeof(CgState) == 224, "cg_copy lists every CgState field");
+
+__device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st) {
+  double S[4];
+  cg_copy(st, *f.in);
+  wave_reduce_parts(f.parts, f.nparts, f.width, S);  // (garbage if done: the stages ignore it)
+  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+  if (f.stage == 1) cg_stage1(st, S[0]);
+  else cg_stage2(st, S, lead ? f.hist : nullptr, lead ? f.h_done : nullptr, f.host_iter);
+  if (lead) cg_copy(*f.out, st);
 }
 
 static int cg_reduce_update(pb_ctx* ctx, int stage, int nparts, int width, CgState* st,
                             double* hist, int* h_done, int64_t host_iter) {
   double* sums = ctx->d_scalars;
   if (!ctx->split) {
-    hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+    hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->d_partials,
                        nparts, width, sums, 3, stage, st, hist, h_done, host_iter);
     PB_HIP(hipGetLastError());
     return PB_OK;
   }
-  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->d_partials,
                      nparts, width, sums, 1, stage, st, hist, h_done, host_iter);
   PB_HIP(hipGetLastError());
   PB_TRY(allreduce_device(ctx, sums, width));
-  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->d_partials,
                      nparts, width, sums, 2, stage, st, hist, h_done, host_iter);
   PB_HIP(hipGetLastError());
   return PB_OK;
@@ -948,6 +1036,30 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
                     &st->done, mode, part_off, nblocks);
 }
 
+// Folded iteration (one rank, Jacobi): partial sums of pass A at block 0, of pass B at
+// fold_parts_b_off(); state slots st2[0] (read by pass B, written by pass A) and st2[1].
+static int64_t fold_parts_b_off(const pb_ctx* ctx) { return ctx->partials_cap / 8; }
+
+int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const double* p_old,
+                            double* p_new, const StencilPlanes& gp, CgState* st2, int nparts_b,
+                            double* hist, int* h_done, int64_t host_iter, int* nblocks) {
+  ScopedTimer tm(g->ctx, "cg_pass_a");
+  pb_ctx* ctx = g->ctx;
+  Fold f;
+  f.stage = 2;
+  f.nparts = nparts_b;
+  f.width = 4;
+  f.parts = ctx->d_partials + fold_parts_b_off(ctx) * 4;
+  f.in = st2 + 1;
+  f.out = st2;
+  f.hist = hist;
+  f.h_done = h_done;
+  f.host_iter = host_iter - 1;  // stage 2 of the previous iteration
+  const int nt_p = env_int("PB_PASSA_NT", 1);
+  return launch_any(g, s, CombineLoad{r, p_old, nullptr, 0.0, 0.0, 0.0}, gp, PassA{p_new, nt_p},
+                    nullptr, PLANES_ALL, 0, nblocks, 0, 0, f);
+}
+
 int cg_finalize_init(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done) {
   return cg_reduce_update(ctx, 0, nparts, 4, st, hist, h_done, -1);
 }
@@ -961,36 +1073,71 @@ int cg_finalize_stage2(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* 
   return cg_reduce_update(ctx, 2, nparts, 4, st, hist, h_done, host_iter);
 }
 
+// pass B variants by the x-update position; fold.stage = 1: stage 1 in the prologue (partials
+// of pass A at block 0, state st2[0] -> st2[1]) and the partials written at fold_parts_b_off()
+static int pass_b_launch(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
+                         double* x, double* r, const StencilPlanes& gp, CgState* st,
+                         int64_t host_iter, int defer, const Fold& f, int* nparts) {
+  const double* pp = p_prev[0];
+  const int* skip = f.stage ? nullptr : &st->done;
+  const int off = f.stage ? (int)fold_parts_b_off(g->ctx) : 0;
+  if (defer == 0) {
+    ScopedTimer tm(g->ctx, "cg_pass_b");
+    return launch_any(g, s, PlainLoad{p}, gp,
+                      PassB<2>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                      skip, PLANES_ALL, off, nparts, 1, 0, f);
+  }
+  if (host_iter % defer != defer - 1) {
+    ScopedTimer tm(g->ctx, "cg_pass_b_even");
+    return launch_any(g, s, PlainLoad{p}, gp,
+                      PassB<0>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                      skip, PLANES_ALL, off, nparts, 1, 0, f);
+  }
+  if (defer == 2) {
+    ScopedTimer tm(g->ctx, "cg_pass_b_odd");
+    return launch_any(g, s, PlainLoad{p}, gp,
+                      PassB<1>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                      skip, PLANES_ALL, off, nparts, 1, 0, f);
+  }
+  ScopedTimer tm(g->ctx, "cg_pass_b_x4");
+  return launch_any(g, s, PlainLoad{p}, gp,
+                    PassB<3>{x, r, pp, p_prev[1], p_prev[2], st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
+                    skip, PLANES_ALL, off, nparts, 1, 0, f);
+}
+
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
                      double* x, double* r, const StencilPlanes& gp, CgState* st, double* hist,
                      int* h_done, int64_t host_iter, int defer, bool finalize) {
   int nparts = 0;
-  {
-    const double* pp = p_prev[0];
-    if (defer == 0) {
-      ScopedTimer tm(g->ctx, "cg_pass_b");
-      PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<2>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-                        &st->done, PLANES_ALL, 0, &nparts, 1));
-    } else if (host_iter % defer != defer - 1) {
-      ScopedTimer tm(g->ctx, "cg_pass_b_even");
-      PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<0>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-                        &st->done, PLANES_ALL, 0, &nparts, 1));
-    } else if (defer == 2) {
-      ScopedTimer tm(g->ctx, "cg_pass_b_odd");
-      PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<1>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-                        &st->done, PLANES_ALL, 0, &nparts, 1));
-    } else {
-      ScopedTimer tm(g->ctx, "cg_pass_b_x4");
-      PB_TRY(launch_any(g, s, PlainLoad{p}, gp,
-                        PassB<3>{x, r, pp, p_prev[1], p_prev[2], st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-                        &st->done, PLANES_ALL, 0, &nparts, 1));
-    }
-  }
+  PB_TRY(pass_b_launch(g, s, p, p_prev, x, r, gp, st, host_iter, defer, Fold{}, &nparts));
   if (!finalize) return PB_OK;  // preconditioned path: the sums come from z = M^-1 r later
   return cg_reduce_update(g->ctx, 2, nparts, 4, st, hist, h_done, host_iter);
+}
+
+int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
+                            const double* const* p_prev, double* x, double* r,
+                            const StencilPlanes& gp, CgState* st2, int nparts_a, int64_t host_iter,
+                            int defer, int* nparts_b) {
+  Fold f;
+  f.stage = 1;
+  f.nparts = nparts_a;
+  f.width = 1;
+  f.parts = g->ctx->d_partials;
+  f.in = st2;
+  f.out = st2 + 1;
+  return pass_b_launch(g, s, p, p_prev, x, r, gp, nullptr, host_iter, defer, f, nparts_b);
+}
+
+// after the last folded iteration of a pb_ksp_iterate call: its stage 2 (in place on st2[1]),
+// then st2[0] = st2[1], so the unfolded entry points find the complete state in slot 0
+int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_done,
+                 int64_t host_iter) {
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(64), 0, ctx->stream,
+                     ctx->d_partials + fold_parts_b_off(ctx) * 4, nparts_b, 4, ctx->d_scalars, 3,
+                     2, st2 + 1, hist, h_done, host_iter);
+  PB_HIP(hipGetLastError());
+  PB_HIP(hipMemcpyAsync(st2, st2 + 1, sizeof(CgState), hipMemcpyDeviceToDevice, ctx->stream));
+  return PB_OK;
 }
 
 // x += alpha * p (the pending half of the deferred solution update)

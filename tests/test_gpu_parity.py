@@ -229,6 +229,53 @@ def test_cg_deferred_x_update(ctx, monkeypatch, defer, max_it):
     check_x(x.get_values(), xo, bar=1e-12)
 
 
+@pytest.mark.parametrize("case", ["rtol", "rtol_tight", "max_it1", "max_it2", "max_it9",
+                                  "split_iterate", "check1"])
+def test_cg_folded_finalize_bit_identical(ctx, monkeypatch, case):
+    """One-rank Jacobi CG with the finalize steps folded into the passes' prologues (default)
+    against the separate finalize launches (PB_CG_FOLD=0): same reason, iteration count,
+    history and x, bit for bit -- stopping at every kind of place (rtol inside a poll interval,
+    max_it 1 / 2 / 9, a begin / iterate(3) / iterate(n) / end sequence, check_every 1 which
+    cannot fold)."""
+    n3 = (64, 32, 16)
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(N, SEED), n3, h)
+    opts = {"rtol": ["-ksp_rtol", "1e-5"], "rtol_tight": ["-ksp_rtol", "1e-11"],
+            "max_it1": ["-ksp_rtol", "0", "-ksp_max_it", "1"],
+            "max_it2": ["-ksp_rtol", "0", "-ksp_max_it", "2"],
+            "max_it9": ["-ksp_rtol", "0", "-ksp_max_it", "9"],
+            "split_iterate": ["-ksp_rtol", "1e-7"], "check1": ["-ksp_rtol", "1e-6"]}[case]
+    out = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("PB_CG_FOLD", fold)
+        da = pb.DA(ctx, n3)
+        P, A, x, bv = pb.initialise_linear_system(da, h)
+        bv.set_values(b)
+        if case == "split_iterate":
+            k = pb.KSP(A, P, pb.ksp_options(opts))
+            k.begin(bv, x)
+            k.iterate(3)
+            k.iterate(5)
+            k.iterate(1000)
+            reason, its, hist = k.end()
+            k.destroy()
+        elif case == "check1":
+            k = pb.KSP(A, P, pb.ksp_options(opts, check_every=1))
+            reason, its, hist = k.solve(bv, x)
+            k.destroy()
+        else:
+            reason, its, hist = pb.solve(P, A, x, bv, opts)
+        out[fold] = (reason, its, np.asarray(hist), x.get_values())
+    (r1, i1, h1, x1), (r0, i0, h0, x0) = out["1"], out["0"]
+    assert (r1, i1) == (r0, i0)
+    assert np.array_equal(h1, h0) and np.array_equal(x1, x0)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, **({"rtol": float(opts[1])} if opts[1] != "0" else
+                                                {"rtol": 0.0, "max_it": int(opts[3])}))
+    assert (r1, i1) == (ro, itso)
+    check_history(h1, ho)
+
+
 def test_cg_zero_rhs_converges_immediately(ctx):
     n3 = (8, 8, 8)
     da = pb.DA(ctx, n3)
