@@ -52,6 +52,51 @@ __device__ __forceinline__ void store_row(double* p, int64_t idx, const double (
   }
 }
 
+// Row-element address split into a wave-uniform row offset (elements) and the lane's byte
+// offset inside the row (32-bit): the loads/stores then take an SGPR base and ONE shared VGPR
+// offset instead of a 64-bit VGPR address per row (fewer VGPRs, no spills in the tall kernels).
+struct RowIx {
+  int64_t row;    // uniform
+  unsigned boff;  // lane byte offset
+};
+template <int V>
+__device__ __forceinline__ void load_row(const double* __restrict__ p, RowIx ix, double (&v)[V]) {
+  const char* q = reinterpret_cast<const char*>(p + ix.row) + ix.boff;
+  if constexpr (V == 2) {
+    const dv2 t = *reinterpret_cast<const dv2*>(q);
+    v[0] = t.x;
+    v[1] = t.y;
+  } else {
+    v[0] = *reinterpret_cast<const double*>(q);
+  }
+}
+template <int V>
+__device__ __forceinline__ void load_row_nt(const double* __restrict__ p, RowIx ix,
+                                            double (&v)[V]) {
+  const char* q = reinterpret_cast<const char*>(p + ix.row) + ix.boff;
+  if constexpr (V == 2) {
+    const dv2 t = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(q));
+    v[0] = t.x;
+    v[1] = t.y;
+  } else {
+    v[0] = __builtin_nontemporal_load(reinterpret_cast<const double*>(q));
+  }
+}
+template <int V>
+__device__ __forceinline__ void store_row(double* p, RowIx ix, const double (&v)[V], int nt) {
+  char* q = reinterpret_cast<char*>(p + ix.row) + ix.boff;
+  if constexpr (V == 2) {
+    dv2 t;
+    t.x = v[0];
+    t.y = v[1];
+    if (nt) __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(q));
+    else *reinterpret_cast<dv2*>(q) = t;
+  } else {
+    if (nt) __builtin_nontemporal_store(v[0], reinterpret_cast<double*>(q));
+    else *reinterpret_cast<double*>(q) = v[0];
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Cross-lane helpers (DPP wave shifts: VALU only, no LDS traffic)
 // ---------------------------------------------------------------------------------------------

@@ -91,7 +91,7 @@ struct StoreY {
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ const double* src(int) const { return nullptr; }
   template <int V>
-  __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
+  __device__ __forceinline__ void put(RowIx idx, const double (&c)[V], const double (&w)[V],
                                       double (&)[1][V], double*, int nt) const {
     store_row<V>(y, idx, w, nt);
     (void)c;
@@ -110,7 +110,7 @@ struct PassA {
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ const double* src(int) const { return nullptr; }
   template <int V>
-  __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
+  __device__ __forceinline__ void put(RowIx idx, const double (&c)[V], const double (&w)[V],
                                       double (&)[1][V], double* acc, int nt) const {
     store_row<V>(p_new, idx, c, nt && nt_p);
 #pragma unroll
@@ -159,7 +159,7 @@ struct PassB {
     return a == 0 ? r : (a == 1 ? x : (a == 2 ? p_prev : (a == 3 ? p_m2 : p_m3)));
   }
   template <int V>
-  __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
+  __device__ __forceinline__ void put(RowIx idx, const double (&c)[V], const double (&w)[V],
                                       double (&op)[NE][V], double* acc, int nt) const {
     double rv[V];
 #pragma unroll
@@ -259,7 +259,8 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 #pragma unroll
   for (int s = 0; s < (NS > 0 ? NS : 1); ++s) acc[s] = 0.0;
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wave index as a scalar: row addresses are wave-uniform (SGPR base + one lane offset, RowIx)
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // XCD-aware remap (speed only): the dispatcher deals blocks round-robin over the 8 XCDs, so
   // give each XCD a contiguous range of logical tiles -- y/x-neighbouring tiles then share the
   // XCD's L2 and their halo rows hit there. Bijective for any grid size.
@@ -287,8 +288,10 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   const bool edge_lane = edge_row < TY;
   const int edge_i = lane < 32 ? (seg0 == 0 ? nx - 1 : seg0 - 1) : (seg_end >= nx ? 0 : seg_end);
   const int64_t edge_off = (int64_t)(j0 + (edge_lane ? edge_row : 0)) * nx + edge_i;
-  const int64_t off_dn = (int64_t)(j0 == 0 ? g.ny - 1 : j0 - 1) * nx + ic;
-  const int64_t off_up = (int64_t)((j0 + TY >= g.ny) ? 0 : j0 + TY) * nx + ic;
+  const unsigned boff = (unsigned)ic * 8u;  // lane byte offset inside a row
+  const int64_t row_dn = (int64_t)(j0 == 0 ? g.ny - 1 : j0 - 1) * nx;
+  const int64_t row_up = (int64_t)((j0 + TY >= g.ny) ? 0 : j0 + TY) * nx;
+  auto rix = [&](int64_t row) { return RowIx{row, boff}; };
 
   if (wave_on) {
     // combined z-queue (planes k-1, k, k+1) and raw prefetch of plane k+2
@@ -300,20 +303,20 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
     double hdn_r[NR][V], hup_r[NR][V], edge_r[NR];
     double opc[TY][NE][V], opn[Epi::PREFETCH ? TY : 1][NE][V];
 
+    // Every load below is issued unconditionally (ghost planes by a uniform pointer select, the
+    // chunk's last step re-loading valid planes): no branch around a load, so the compiler keeps
+    // the prefetch registers stable instead of copying them at control-flow joins -- such copies
+    // must wait for the loads and serialised the software pipeline (pass A ran ~10 % slower).
     auto issue_zrow = [&](int kk) {  // raw rows of plane kk in [-1, nzl] -> zr
       if (g.wrap) kk = kk < 0 ? kk + g.nzl : (kk >= g.nzl ? kk - g.nzl : kk);
       zr_ghost = kk < 0 || kk >= g.nzl;
-      if (zr_ghost) {
-        const double* gp = kk < 0 ? ghost_lo : ghost_hi;
+      const double* gp = kk < 0 ? ghost_lo : ghost_hi;
+      const int64_t base = zr_ghost ? 0 : (int64_t)kk * g.plane;
 #pragma unroll
-        for (int t = 0; t < TY; ++t) load_row<V>(gp, (int64_t)(j0 + t) * nx + ic, zr[0][t]);
-      } else {
-        const int64_t base = (int64_t)kk * g.plane;
+      for (int a = 0; a < NR; ++a) {
+        const double* src = zr_ghost ? gp : ld.src(a);
 #pragma unroll
-        for (int a = 0; a < NR; ++a)
-#pragma unroll
-          for (int t = 0; t < TY; ++t)
-            load_row<V>(ld.src(a), base + (int64_t)(j0 + t) * nx + ic, zr[a][t]);
+        for (int t = 0; t < TY; ++t) load_row<V>(src, rix(base + (int64_t)(j0 + t) * nx), zr[a][t]);
       }
     };
     auto take_zrow = [&](double (&q)[TY][V]) {  // combine zr into q
@@ -332,15 +335,15 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 #pragma unroll
       for (int a = 0; a < NR; ++a) {
 #ifdef PB_ABLATE_HALO  // timing experiments only (wrong results): y-halo rows from own rows
-        load_row<V>(ld.src(a), base + (int64_t)j0 * nx + ic, hdn_r[a]);
-        load_row<V>(ld.src(a), base + (int64_t)(j0 + TY - 1) * nx + ic, hup_r[a]);
+        load_row<V>(ld.src(a), rix(base + (int64_t)j0 * nx), hdn_r[a]);
+        load_row<V>(ld.src(a), rix(base + (int64_t)(j0 + TY - 1) * nx), hup_r[a]);
 #else
-        load_row<V>(ld.src(a), base + off_dn, hdn_r[a]);
-        load_row<V>(ld.src(a), base + off_up, hup_r[a]);
+        load_row<V>(ld.src(a), rix(base + row_dn), hdn_r[a]);
+        load_row<V>(ld.src(a), rix(base + row_up), hup_r[a]);
 #endif
         edge_r[a] = 0.0;
 #ifndef PB_ABLATE_EDGES  // timing experiments only (wrong results): no segment-edge loads
-        if (edge_lane) edge_r[a] = ld.src(a)[base + edge_off];
+        edge_r[a] = ld.src(a)[base + edge_off];  // (all lanes: valid address, only edge lanes read)
 #endif
       }
       if constexpr (Epi::NE > 0 && Epi::PREFETCH) {
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         for (int t = 0; t < TY; ++t)
 #pragma unroll
           for (int a = 0; a < Epi::NE; ++a)
-            load_row_nt<V>(ep.src(a), base + (int64_t)(j0 + t) * nx + ic, opn[t][a]);
+            load_row_nt<V>(ep.src(a), rix(base + (int64_t)(j0 + t) * nx), opn[t][a]);
       }
     };
     auto issue_ops_now = [&](int kk) {  // operands without prefetch: plane kk straight to opc
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         for (int t = 0; t < TY; ++t)
 #pragma unroll
           for (int a = 0; a < Epi::NE; ++a)
-            load_row_nt<V>(ep.src(a), base + (int64_t)(j0 + t) * nx + ic, opc[t][a]);
+            load_row_nt<V>(ep.src(a), rix(base + (int64_t)(j0 + t) * nx), opc[t][a]);
       }
     };
     auto take_plane_ops = [&]() {
@@ -401,8 +404,8 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
       take_zrow(q2);                    // plane k+dir (in flight since the previous step)
       take_plane_ops();                 // halo/edges/operands of plane k
       issue_ops_now(k);
-      if (m + 2 <= nk) issue_zrow(k + 2 * dir);
-      if (m + 1 < nk) issue_plane_ops(k + dir);
+      issue_zrow(m + 2 <= nk ? k + 2 * dir : k + dir);  // (last step: a valid plane, unused)
+      issue_plane_ops(m + 1 < nk ? k + dir : k);
       const int64_t base = (int64_t)k * g.plane;
 #pragma unroll
       for (int t = 0; t < TY; ++t) {
@@ -424,7 +427,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
             nzp[e] = g.rev ? q0[t][e] : q2[t][e];
           }
           if (active)
-            ep.template put_raw<V>(base + (int64_t)(j0 + t) * nx + i0, i0 + j0 + t + g.k0 + k,
+            ep.template put_raw<V>(rix(base + (int64_t)(j0 + t) * nx), i0 + j0 + t + g.k0 + k,
                                    nzm, nym, nxm, q1[t], nxp, nyp, nzp, opc[t], acc, g.nt);
         } else {
           double w[V];
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
             w[e] = s;
           }
           if (active)
-            ep.template put<V>(base + (int64_t)(j0 + t) * nx + i0, q1[t], w, opc[t], acc, g.nt);
+            ep.template put<V>(rix(base + (int64_t)(j0 + t) * nx), q1[t], w, opc[t], acc, g.nt);
         }
       }
 #pragma unroll
@@ -640,7 +643,7 @@ struct SorHalfT {
   __device__ __forceinline__ void prepare();
   __device__ __forceinline__ const double* src(int) const { return b; }
   template <int V>
-  __device__ __forceinline__ void put_raw(int64_t idx, int par, const double (&zm)[V],
+  __device__ __forceinline__ void put_raw(RowIx idx, int par, const double (&zm)[V],
                                           const double (&ym)[V], const double (&xm)[V],
                                           const double (&c)[V], const double (&xp)[V],
                                           const double (&yp)[V], const double (&zp)[V],
@@ -683,7 +686,7 @@ struct ResidEpi {
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ const double* src(int) const { return b; }
   template <int V>
-  __device__ __forceinline__ void put(int64_t idx, const double (&c)[V], const double (&w)[V],
+  __device__ __forceinline__ void put(RowIx idx, const double (&c)[V], const double (&w)[V],
                                       double (&op)[1][V], double*, int nt) const {
     double o[V];
 #pragma unroll

@@ -33,4 +33,5 @@ for rep in range(reps):
         d = json.loads(p.stdout.strip().splitlines()[-1])
         ks = {k: round(v["avg_ms"], 4) for k, v in d.get("kernels", {}).items()}
         print(json.dumps({"cfg": cfg, "rep": rep, "ms_per_step": round(d["ms_per_step"], 4),
-                          "frac": round(d["roofline"]["frac"], 4), "kernels": ks}), flush=True)
+                          "frac": round(d["roofline"]["frac"], 4), "kernels": ks,
+                          "ksp": d.get("ksp_state", {}).get("reason")}), flush=True)
