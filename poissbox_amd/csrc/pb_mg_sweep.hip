@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
   if (skip && *skip) return;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const double mu = SUMS ? st->mu : 0.0;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int bid = xcd_block(g.remap);
   const int seg = bid % g.nseg;
   bid /= g.nseg;
@@ -73,16 +73,18 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
   const int o = seg * kSegOut + 2 * (lane - kSegLead);  // output pair
   const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
   if (j0 < ny && kb < nz) {
-    int64_t ro[kRW];
+    int64_t ro[kRW];  // wave-uniform row offsets; the lane's pair is the byte offset boff
     int par_row[kRW];  // (i + j) parity base of each row for element 0
 #pragma unroll
     for (int r = 0; r < kRW; ++r) {
       int j = j0 - 2 + r;
       if (j < 0) j += ny;
       if (j >= ny) j -= ny;
-      ro[r] = (int64_t)j * nx + ip;
+      ro[r] = (int64_t)j * nx;
       par_row[r] = (ip + j) & 1;
     }
+    const unsigned boff = (unsigned)ip * 8u;
+    auto rix = [&](int64_t row) { return RowIx{row, boff}; };
     // one rank: periodic plane offsets into xin / b; N ranks: own planes or the ghost planes
     auto pl = [&](int kk) -> int64_t {
       if constexpr (!SPLIT) kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
@@ -109,22 +111,22 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
       if constexpr (SPLIT) {
         const double* P = xplane(kk);
 #pragma unroll
-        for (int r = 0; r < kRW; ++r) load_row<2>(P, ro[r], dst[r]);
+        for (int r = 0; r < kRW; ++r) load_row<2>(P, rix(ro[r]), dst[r]);
       } else {
         const int64_t base = pl(kk);
 #pragma unroll
-        for (int r = 0; r < kRW; ++r) load_row<2>(xin, base + ro[r], dst[r]);
+        for (int r = 0; r < kRW; ++r) load_row<2>(xin, rix(base + ro[r]), dst[r]);
       }
     };
     auto ldb = [&](double (&dst)[kRW][2], int kk) {
       if constexpr (SPLIT) {
         const double* P = bplane(kk);
 #pragma unroll
-        for (int r = 1; r < kRW - 1; ++r) load_row<2>(P, ro[r], dst[r]);
+        for (int r = 1; r < kRW - 1; ++r) load_row<2>(P, rix(ro[r]), dst[r]);
       } else {
         const int64_t base = pl(kk);
 #pragma unroll
-        for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, base + ro[r], dst[r]);
+        for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
       }
     };
     // M = 1: b values of plane kk -> the x of the zero-start red half-sweep (red: w D^-1 b,
@@ -206,10 +208,10 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
     }
     for (int k = kb; k < ke; ++k) {
       const bool more = k + 1 < ke;
-      if (more) {
-        ldx(xn, k + 3);
-        ldb(bn, k + 2);
-      }
+      // unconditional (the chunk's last step re-loads valid planes, unused): a load under a
+      // branch made the compiler copy the prefetch registers at the join, waiting for the loads
+      ldx(xn, more ? k + 3 : k + 2);
+      ldb(bn, more ? k + 2 : k + 1);
       half1(xq[0], xq[1], xq[2], bq[1], k + 1, s1[2]);  // S1 at plane k+1
       // second half-sweep at plane k, own rows 2 .. 2+TY2-1
       const int kp = kpar(k);
@@ -234,8 +236,8 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
             rv[e] = bq[0][r][e] - a;
           }
           if (out_ok && j0 + r - 2 < ny) {
-            store_row<2>(xout, base + ro[r], s1[1][r], g.nt);
-            store_row<2>(res, base + ro[r], rv, g.nt);
+            store_row<2>(xout, rix(base + ro[r]), s1[1][r], g.nt);
+            store_row<2>(res, rix(base + ro[r]), rv, g.nt);
           }
           continue;
         }
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
         ov[0] = a1 ? s1[1][r][0] : v;
         ov[1] = a1 ? v : s1[1][r][1];
         if (out_ok && j0 + r - 2 < ny) {  // rows past ny (last tile) would wrap: not ours
-          store_row<2>(xout, base + ro[r], ov, g.nt);
+          store_row<2>(xout, rix(base + ro[r]), ov, g.nt);
           if constexpr (SUMS) {
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
