@@ -24,6 +24,7 @@
 // radix-2 decimation-in-frequency stages over wave shuffles (output in bit-reversed lane order);
 // the two Hartley spectra follow from Z(k) and Z(-k) (one more shuffle), and go back to LDS in
 // natural order for the coalesced store. Twiddles come from a per-axis table exp(-2 pi i k / n).
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -59,10 +60,81 @@ __host__ __device__ constexpr int bitrev(int v, int bits) {
   return r;
 }
 
+// ---- lane exchanges without LDS: value of lane ^ H (H = 1..32) and of lane ^ 63 ----
+// H = 1, 2: DPP quad_perm; 4, 8: DPP row shifts up / down and a select; 16, 32: the gfx950
+// permlane swaps. All VALU: no LDS round trip per FFT stage (the r02 first cut used
+// __shfl_xor = ds_bpermute, twice per double).
+template <int CTRL>
+__device__ __forceinline__ int dpp32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int H>
+__device__ __forceinline__ int xor_lane32(int v, int lane) {
+  if constexpr (H == 1) return dpp32<0xB1>(v);  // quad_perm [1, 0, 3, 2]
+  else if constexpr (H == 2) return dpp32<0x4E>(v);  // quad_perm [2, 3, 0, 1]
+  else if constexpr (H == 4 || H == 8) {
+    const int up = dpp32<0x100 + H>(v);  // row_shl:H -> lane + H
+    const int dn = dpp32<0x110 + H>(v);  // row_shr:H -> lane - H
+    return (lane & H) ? dn : up;
+  } else if constexpr (H == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? (int)r[0] : (int)r[1];
+  } else {
+    static_assert(H == 32, "xor_lane32: H in {1, 2, 4, 8, 16, 32}");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane & 32) ? (int)r[0] : (int)r[1];
+  }
+}
+template <int H>
+__device__ __forceinline__ double xor_lane(double v, int lane) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = xor_lane32<H>((int)b, lane), hi = xor_lane32<H>((int)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+// lane ^ 63 = row_mirror (lane ^ 15), then ^ 16, ^ 32
+__device__ __forceinline__ double mirror_lane(double v, int lane) {
+  const long long b = __builtin_bit_cast(long long, v);
+  int lo = dpp32<0x140>((int)b), hi = dpp32<0x140>((int)(b >> 32));
+  lo = xor_lane32<32>(xor_lane32<16>(lo, lane), lane);
+  hi = xor_lane32<32>(xor_lane32<16>(hi, lane), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// lane-dependent twiddles of fft_wave, loaded once per wave before the tile arrives
+template <int C>
+struct WaveTw {
+  cplx t2[C];   // exp(-2 pi i lane k2 / n), k2 >= 1
+  cplx st[6];   // stage h = 32 >> s: exp(-2 pi i (lane & (h-1)) n / (2h) / n)
+  __device__ __forceinline__ void load(const double* w, int lane) {
+    constexpr int n = 64 * C;
+#pragma unroll
+    for (int k2 = 1; k2 < C; ++k2) t2[k2] = tw(w, (lane * k2) & (n - 1));
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int h = 32 >> s;
+      st[s] = tw(w, (lane & (h - 1)) * (n / (2 * h)));
+    }
+  }
+};
+
+template <int H, int C>
+__device__ __forceinline__ void dif_stage(cplx (&z)[C], const cplx wh, int lane) {
+  const bool upper = lane & H;
+#pragma unroll
+  for (int k2 = 0; k2 < C; ++k2) {
+    const cplx p = {xor_lane<H>(z[k2].re, lane), xor_lane<H>(z[k2].im, lane)};
+    if (upper)
+      z[k2] = cmul({p.re - z[k2].re, p.im - z[k2].im}, wh);
+    else
+      z[k2] = {z[k2].re + p.re, z[k2].im + p.im};
+  }
+}
+
 // z (lane owns elements lane + 64 m, m < C) -> spectrum: lane L holds Z[k2 + C bitrev6(L)] in
 // z[k2]. n = 64 C, w = exp(-2 pi i k / n).
 template <int C>
-__device__ __forceinline__ void fft_wave(cplx (&z)[C], const double* w, int lane) {
+__device__ __forceinline__ void fft_wave(cplx (&z)[C], const double* w, const WaveTw<C>& T,
+                                         int lane) {
   constexpr int n = 64 * C, LB = ilog2(C);
   // (1) C-point DFT over m in registers (radix-2 DIT, bit-reversed input order)
   cplx t[C];
@@ -80,21 +152,14 @@ __device__ __forceinline__ void fft_wave(cplx (&z)[C], const double* w, int lane
       }
   // (2) twiddles exp(-2 pi i lane k2 / n)
 #pragma unroll
-  for (int k2 = 0; k2 < C; ++k2) z[k2] = k2 ? cmul(t[k2], tw(w, (lane * k2) & (n - 1))) : t[k2];
+  for (int k2 = 0; k2 < C; ++k2) z[k2] = k2 ? cmul(t[k2], T.t2[k2]) : t[k2];
   // (3) 64-point DFT across lanes: radix-2 DIF, partner lane ^ h
-#pragma unroll
-  for (int h = 32; h >= 1; h >>= 1) {
-    const cplx wh = tw(w, (lane & (h - 1)) * (n / (2 * h)));
-    const bool upper = lane & h;
-#pragma unroll
-    for (int k2 = 0; k2 < C; ++k2) {
-      const cplx p = {__shfl_xor(z[k2].re, h, 64), __shfl_xor(z[k2].im, h, 64)};
-      if (upper)
-        z[k2] = cmul({p.re - z[k2].re, p.im - z[k2].im}, wh);
-      else
-        z[k2] = {z[k2].re + p.re, z[k2].im + p.im};
-    }
-  }
+  dif_stage<32>(z, T.st[0], lane);
+  dif_stage<16>(z, T.st[1], lane);
+  dif_stage<8>(z, T.st[2], lane);
+  dif_stage<4>(z, T.st[3], lane);
+  dif_stage<2>(z, T.st[4], lane);
+  dif_stage<1>(z, T.st[5], lane);
 }
 
 // Hartley spectra of the two real lines packed in z (spectrum layout of fft_wave): hx, hy at
@@ -105,35 +170,42 @@ __device__ __forceinline__ void hartley_split(const cplx (&z)[C], double (&hx)[C
   const int k1 = bitrev(lane, 6);
 #pragma unroll
   for (int k2 = 0; k2 < C; ++k2) {
-    // partner -k mod n: k2 = 0 -> (0, -k1 mod 64); else (C - k2, 63 - k1)
+    // partner -k mod n: k2 = 0 -> (0, -k1 mod 64), lane bitrev6((64 - k1) & 63) (a bpermute);
+    // else (C - k2, 63 - k1), lane bitrev6(63 - k1) = lane ^ 63
     const int k2p = k2 == 0 ? 0 : C - k2;
-    const int k1p = k2 == 0 ? ((64 - k1) & 63) : 63 - k1;
-    const int src = bitrev(k1p, 6);
-    const cplx m = {__shfl(z[k2p].re, src, 64), __shfl(z[k2p].im, src, 64)};
+    cplx m;
+    if (k2 == 0) {
+      const int src = bitrev((64 - k1) & 63, 6);
+      m = {__shfl(z[0].re, src, 64), __shfl(z[0].im, src, 64)};
+    } else {
+      m = {mirror_lane(z[k2p].re, lane), mirror_lane(z[k2p].im, lane)};
+    }
     hx[k2] = 0.5 * ((z[k2].re + m.re) - (z[k2].im - m.im));
     hy[k2] = 0.5 * ((z[k2].im + m.im) + (z[k2].re - m.re));
   }
 }
 
-template <int C>
+template <int C, int TL_>
 struct DhtTile {
   static constexpr int n = 64 * C;
-  static constexpr int TL = C >= 16 ? 8 : 16;  // lines per tile (LDS: TL * (n + 1) doubles)
-  static constexpr int NW = TL / 2;            // waves: two lines each
+  static constexpr int TL = TL_;       // lines per tile (LDS: TL * (n + 1) doubles)
+  static constexpr int NW = TL / 2;    // waves: two lines each
   static constexpr int NT = 64 * NW;
-  static constexpr int LP = n + 1;             // odd line pitch: column writes spread over banks
+  static constexpr int LP = n + 1;     // odd line pitch: column writes spread over banks
+  static constexpr size_t LDS = (size_t)TL * LP * sizeof(double);
 };
 
 // one DHT of the wave's two lines (pair p) in LDS, in place; SCALE: multiply by s(k) before the
 // write-back (callers run the inverse transform again afterwards)
 template <int C, bool SCALE>
-__device__ __forceinline__ void dht_pair(double* lds, int l0, const DhtPass& p, int lane,
-                                         int64_t outer, int inner0) {
-  using T = DhtTile<C>;
+__device__ __forceinline__ void dht_pair(double* lds, int l0, const DhtPass& p, const WaveTw<C>& T,
+                                         int lane, int64_t outer, int inner0) {
+  constexpr int LP = 64 * C + 1;
+  constexpr int n = 64 * C;
   cplx z[C];
 #pragma unroll
-  for (int m = 0; m < C; ++m) z[m] = {lds[l0 * T::LP + lane + 64 * m], lds[(l0 + 1) * T::LP + lane + 64 * m]};
-  fft_wave<C>(z, p.w, lane);
+  for (int m = 0; m < C; ++m) z[m] = {lds[l0 * LP + lane + 64 * m], lds[(l0 + 1) * LP + lane + 64 * m]};
+  fft_wave<C>(z, p.w, T, lane);
   double hx[C], hy[C];
   hartley_split<C>(z, hx, hy, lane);
   const int k1 = bitrev(lane, 6);
@@ -145,7 +217,7 @@ __device__ __forceinline__ void dht_pair(double* lds, int l0, const DhtPass& p, 
     const double* Ly = Jx + nx;
     const double* Jy = Ly + ny;
     const double* Lz = Jy + ny;
-    const double* Jz = Lz + T::n;
+    const double* Jz = Lz + n;
     const double ly = Ly[j], jy = Jy[j];
     const double a0 = Lx[i0] * jy + Jx[i0] * ly, c0 = Jx[i0] * jy;
     const double a1 = Lx[i0 + 1] * jy + Jx[i0 + 1] * ly, c1 = Jx[i0 + 1] * jy;
@@ -160,8 +232,8 @@ __device__ __forceinline__ void dht_pair(double* lds, int l0, const DhtPass& p, 
 #pragma unroll
   for (int k2 = 0; k2 < C; ++k2) {
     const int k = k2 + C * k1;
-    lds[l0 * T::LP + k] = hx[k2];
-    lds[(l0 + 1) * T::LP + k] = hy[k2];
+    lds[l0 * LP + k] = hx[k2];
+    lds[(l0 + 1) * LP + k] = hy[k2];
   }
 }
 
@@ -173,10 +245,12 @@ __device__ __forceinline__ void wave_sync_lds() {
 
 // LAYOUT 0: the tile's lines are adjacent (li = 1), elements strided (rows of TL doubles);
 // LAYOUT 1: lines contiguous (es = 1). MODE 0: one DHT; MODE 1: DHT, 1/(N lambda), DHT.
-template <int C, int LAYOUT, int MODE>
-__global__ __launch_bounds__(DhtTile<C>::NT) void dht_lines_kernel(DhtPass p, const int* skip) {
-  using T = DhtTile<C>;
-  constexpr int n = T::n, TL = T::TL, NT = T::NT, LP = T::LP;
+// One tile per block (a persistent form that prefetched the next tile into registers during the
+// transforms measured 10-30 % slower: twice the VGPRs, half the resident waves).
+template <int C, int TL, int LAYOUT, int MODE>
+__global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int* skip) {
+  using T = DhtTile<C, TL>;
+  constexpr int n = T::n, NT = T::NT, LP = T::LP;
   if (skip && *skip) return;  // CG's device convergence flag (uniform)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int tile = blockIdx.x;
@@ -184,6 +258,8 @@ __global__ __launch_bounds__(DhtTile<C>::NT) void dht_lines_kernel(DhtPass p, co
   const int inner0 = (tile % p.ntiles_inner) * TL;
   const int64_t base = outer * p.lo + (int64_t)inner0 * p.li;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  WaveTw<C> twv;
+  twv.load(p.w, lane);  // in flight while the tile loads
   typedef double dv2 __attribute__((ext_vector_type(2)));
   // tile -> LDS (16-byte pairs along the contiguous direction)
   constexpr int NP = TL * n / 2;
@@ -209,10 +285,10 @@ __global__ __launch_bounds__(DhtTile<C>::NT) void dht_lines_kernel(DhtPass p, co
   __syncthreads();
   const int l0 = 2 * wave;
   if (l0 < p.ninner - inner0) {
-    dht_pair<C, MODE == 1>(lds, l0, p, lane, outer, inner0);
+    dht_pair<C, MODE == 1>(lds, l0, p, twv, lane, outer, inner0);
     if (MODE == 1) {
       wave_sync_lds();
-      dht_pair<C, false>(lds, l0, p, lane, outer, inner0);
+      dht_pair<C, false>(lds, l0, p, twv, lane, outer, inner0);
     }
   }
   __syncthreads();
@@ -238,22 +314,43 @@ __global__ __launch_bounds__(DhtTile<C>::NT) void dht_lines_kernel(DhtPass p, co
   }
 }
 
-template <int C, int LAYOUT, int MODE>
-int launch_dht_c(pb_ctx* ctx, DhtPass& p, const int* skip) {
-  using T = DhtTile<C>;
-  p.ntiles_inner = (p.ninner + T::TL - 1) / T::TL;
+template <int C, int TL, int LAYOUT, int MODE>
+int launch_dht_tl(pb_ctx* ctx, DhtPass& p, const int* skip) {
+  using T = DhtTile<C, TL>;
+  p.ntiles_inner = p.ninner / TL;
   const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
-  const size_t lds = (size_t)T::TL * T::LP * sizeof(double);
-  auto kern = dht_lines_kernel<C, LAYOUT, MODE>;
+  auto kern = dht_lines_kernel<C, TL, LAYOUT, MODE>;
   static bool attr = false;
   if (!attr) {
     PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)lds));
+                               (int)T::LDS));
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(T::NT), lds, ctx->stream, p, skip);
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(T::NT), T::LDS, ctx->stream, p, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
+}
+
+// lines per tile by pass (PB_FFT_TL_X / _Y / _Z; default 16, 8 for the Z pass -- measured at
+// 512^3: X/Y 16 vs 8 vs 32 lines 0.52 / 0.57 / 0.66 ms, Z 8 lines 1.43 ms vs 1.64 with 16 --
+// and 8 for 1024-long lines): a power of two dividing ninner (>= 64)
+template <int C, int LAYOUT, int MODE>
+int launch_dht_c(pb_ctx* ctx, DhtPass& p, const int* skip) {
+  const char* knob = LAYOUT == 1 ? "PB_FFT_TL_X" : (MODE == 1 ? "PB_FFT_TL_Z" : "PB_FFT_TL_Y");
+  int tl = env_int(knob, (LAYOUT == 0 && MODE == 1) ? 8 : 16);
+  if (C >= 16 && tl > 8) tl = 8;
+  while (tl > 4 && p.ninner % tl) tl /= 2;
+  if (p.ninner % tl)
+    return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines do not tile", p.ninner);
+  switch (tl) {
+    case 32:
+      if constexpr (C < 16) return launch_dht_tl<C, 32, LAYOUT, MODE>(ctx, p, skip);
+      break;
+    case 16: return launch_dht_tl<C, 16, LAYOUT, MODE>(ctx, p, skip);
+    case 8: return launch_dht_tl<C, 8, LAYOUT, MODE>(ctx, p, skip);
+    default: return launch_dht_tl<C, 4, LAYOUT, MODE>(ctx, p, skip);
+  }
+  return launch_dht_tl<C, 8, LAYOUT, MODE>(ctx, p, skip);
 }
 
 template <int LAYOUT, int MODE>

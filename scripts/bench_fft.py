@@ -1,0 +1,43 @@
+"""Spectral PC apply time (pb_ksp_pc_apply, -pc_type fft) per grid; one JSON line per grid with
+the knobs in the environment (PB_FFT_TL_X / _Y / _Z). usage: python scripts/bench_fft.py [n ...]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import poissbox_amd as pb  # noqa: E402
+
+
+def main():
+    sizes = [int(a) for a in sys.argv[1:]] or [512]
+    ctx = pb.Context(0)
+    for n in sizes:
+        n3 = (n, n, n)
+        h = (2 * np.pi / n,) * 3
+        da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+        P = pb.Mat(da, pb.COMPACT, h)
+        k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
+        r, z = pb.Vec(da), pb.Vec(da)
+        r.set_random(7)
+        for _ in range(3):
+            k.pc_apply(r, z)
+        ctx.sync()
+        reps = 20
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            k.pc_apply(r, z)
+        ctx.sync()
+        ms = (time.perf_counter() - t0) * 1e3 / reps
+        cfg = {kk: v for kk, v in os.environ.items() if kk.startswith("PB_FFT")}
+        print(json.dumps({"n": n, "pc_apply_ms": ms, "GBps_80B": 80 * n ** 3 / ms / 1e6,
+                          "cfg": cfg}), flush=True)
+        for o in (k, r, z, P):
+            o.destroy()
+        da.destroy()
+
+
+if __name__ == "__main__":
+    main()
