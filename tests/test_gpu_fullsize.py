@@ -136,6 +136,29 @@ def test_cg_full_solve_512(ctx, pc, rtol):
     da.destroy()
 
 
+def test_config5_compact_fft_solve_512(ctx):
+    """BASELINE config 5 at full size on one GPU: the compact-scheme Laplacian (A = P = compact,
+    src/compact_schemes.f90:17-37) in CG with the spectral preconditioner built from it, to the
+    north-star rtol 1e-10 (r01: 7-point MG stalled, 10,000 iterations, DIVERGED_ITS). The compact
+    operator's null space holds every mode with two or more Nyquist components, so x_true is
+    recovered only up to it: the bar is the true residual."""
+    n = (512, 512, 512)
+    h = tuple(2 * np.pi / m for m in n)
+    da = pb.DA(ctx, n, (2 * np.pi,) * 3)
+    A = pb.Mat(da, pb.COMPACT, h)
+    x, b, xt = pb.Vec(da), pb.Vec(da), pb.Vec(da)
+    xt.set_random(SEED)
+    A.mult(xt, b)
+    reason, its, hist = pb.solve(A, A, x, b, ["-ksp_type", "cg", "-pc_type", "fft",
+                                              "-ksp_rtol", "1e-10"])
+    assert reason == 2 and its <= 3
+    assert hist[-1] <= 1e-10 * hist[0]
+    assert _true_residual(A, x, b) < 1e-12
+    for o in (A, x, b, xt):
+        o.destroy()
+    da.destroy()
+
+
 def test_mg_pc_apply_512_bit_exact(ctx):
     """One V-cycle (8 levels, fused sweeps on the 512^3 and 256^3 levels) bit-identical to the
     oracle's over the whole grid."""

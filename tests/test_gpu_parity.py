@@ -922,6 +922,33 @@ def test_multirank_fft_pc(nranks, n3, compact):
         assert err < FFT_PC_RTOL, err
 
 
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_multirank_cg_compact_fft(nranks):
+    """Config 5 decomposed: compact A = P on z-slabs (Z passes on y-slabs via all-to-all
+    transposes), spectral PC, CG to rtol 1e-10 -- reason / its equal to the single-grid oracle,
+    x within the CG bar on every rank."""
+    n3 = (64, 64, 64)
+    N = int(np.prod(n3))
+    h = tuple(2 * np.pi / m for m in n3)
+    b = O.lapl(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-10, pc="fft", op="compact", nthreads=8)
+    assert ro == 2
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        A = pb.Mat(da, pb.COMPACT, h)
+        x, bv = pb.Vec(da), pb.Vec(da)
+        bv.set_values(b.reshape(n3[2], -1)[k0:k0 + nk])
+        reason, its, hist = pb.solve(A, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "1e-10"])
+        return k0, nk, reason, its, hist, x.get_values()
+
+    for k0, nk, reason, its, hist, xs in run_ranks(nranks, body):
+        assert (reason, its) == (ro, itso)
+        assert abs(hist[0] - ho[0]) / ho[0] < 1e-12
+        check_x(xs, xo.reshape(n3[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
+
+
 def test_fft_pc_rejects_bad_extents(ctx):
     for n3 in [(48, 64, 64), (64, 32, 64), (64, 64, 2048)]:
         da = pb.DA(ctx, n3)
