@@ -297,6 +297,197 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
   if constexpr (SUMS) block_partials<4>(acc, parts);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Pre-smoothing from x = 0 fused with the residual, slim form of sor_sweep2_kernel<.., 1, ..>:
+// after the zero-start red half-sweep every pair holds ONE non-zero (its red point, w b / c), and
+// the black half-sweep reads only red values -- so the x queue keeps one double per pair (the red
+// value) instead of two, and b is loaded once per plane (the red values are formed from the raw
+// rows that also serve as the b operand). Same per-point operations as sor_sweep2_kernel M = 1
+// (Red0Load + SorHalf, then ResidEpi's order): bit-identical. 42 fewer VGPRs -> two waves per SIMD
+// instead of one.
+// ---------------------------------------------------------------------------------------------
+template <bool SPLIT>
+__global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
+    Sweep2Geo g, double cx, double cy, double cz, double cc, double omega,
+    const double* __restrict__ b, double* __restrict__ xout, double* __restrict__ res,
+    const int* skip) {
+  if (skip && *skip) return;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bid = xcd_block(g.remap);
+  const int seg = bid % g.nseg;
+  bid /= g.nseg;
+  const int tile = bid % g.ntile;
+  const int chunk = bid / g.ntile;
+  const int j0 = (tile * kWaves + wid) * kTY2;
+  const int kb = chunk * g.kc;
+  const int ke = min(kb + g.kc, g.nzl);
+  const int nx = g.nx, ny = g.ny, nz = g.nzl;
+  int ip = seg * kSegOut + 2 * (lane - kSegLead);
+  if (ip < 0) ip += nx;
+  if (ip >= nx) ip -= nx;
+  const int o = seg * kSegOut + 2 * (lane - kSegLead);
+  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
+  if (!(j0 < ny && kb < nz)) return;
+  int64_t ro[kRW];
+  int par_row[kRW];
+#pragma unroll
+  for (int r = 0; r < kRW; ++r) {
+    int j = j0 - 2 + r;
+    if (j < 0) j += ny;
+    if (j >= ny) j -= ny;
+    ro[r] = (int64_t)j * nx;
+    par_row[r] = (ip + j) & 1;
+  }
+  const unsigned boff = (unsigned)ip * 8u;
+  auto rix = [&](int64_t row) { return RowIx{row, boff}; };
+  auto kpar = [&](int kk) -> int {
+    if constexpr (!SPLIT) kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
+    return (g.k0 + kk) & 1;
+  };
+  // b plane kk in [-2, nzl+1]: own planes or (N ranks) the two-deep ghosts of b
+  auto bplane = [&](int kk) -> const double* {
+    if constexpr (!SPLIT) {
+      kk = kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk);
+      return b + (int64_t)kk * g.plane;
+    } else {
+      if (kk >= 0 && kk < nz) return b + (int64_t)kk * g.plane;
+      return g.xg + (int64_t)(kk < 0 ? kk + 2 : kk - nz + 2) * g.plane;
+    }
+  };
+  auto ldraw = [&](double (&dst)[kRW][2], int kk) {
+    const double* P = bplane(kk);
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) load_row<2>(P, rix(ro[r]), dst[r]);
+  };
+  // raw b rows of plane kk -> the red value of each pair (Red0Load's arithmetic)
+  auto redv = [&](const double (&v)[kRW][2], int kk, double (&red)[kRW]) {
+    const int kp = kpar(kk);
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) {
+      const long long m = -(long long)(((par_row[r] + kp) & 1) != 0);  // red point is element 1
+      const double bv = __builtin_bit_cast(
+          double, (__builtin_bit_cast(long long, v[r][1]) & m) |
+                      (__builtin_bit_cast(long long, v[r][0]) & ~m));  // (see half1)
+      const double t = (bv - 0.0) / cc;
+      red[r] = (1.0 - omega) * 0.0 + omega * t;
+    }
+  };
+  auto keepb = [&](const double (&v)[kRW][2], double (&bb)[kRW][2]) {
+#pragma unroll
+    for (int r = 1; r < kRW - 1; ++r) {
+      bb[r][0] = v[r][0];
+      bb[r][1] = v[r][1];
+    }
+  };
+  // black half-sweep at plane kk (rows 1 .. kRW-2) from the red values of planes kk-1, kk, kk+1:
+  // the pair's full values (red, new black) -> out. sor_sweep2's half1 with c1 = 1, x_old = 0.
+  auto half1 = [&](const double (&rm)[kRW], const double (&rc)[kRW], const double (&rp)[kRW],
+                   const double (&bb)[kRW][2], int kk, double (&out)[kRW][2]) {
+    const int kp = kpar(kk);
+#pragma unroll
+    for (int r = 1; r < kRW - 1; ++r) {
+      const bool a1 = ((par_row[r] + kp) & 1) != 1;  // the black point is element 1
+      const double lo = dpp_from_lower(rc[r]);
+      const double hi = dpp_from_upper(rc[r]);
+      const double xl = a1 ? rc[r] : lo;
+      const double xr = a1 ? hi : rc[r];
+      double nb = cz * rm[r];
+      nb = nb + cy * rc[r - 1];
+      nb = nb + cx * xl;
+      nb = nb + cx * xr;
+      nb = nb + cy * rc[r + 1];
+      nb = nb + cz * rp[r];
+      // (bitwise select: a `?:` on the two array elements became a computed address, which put
+      // the array in scratch)
+      const long long m = -(long long)a1;
+      const double bv = __builtin_bit_cast(
+          double, (__builtin_bit_cast(long long, bb[r][1]) & m) |
+                      (__builtin_bit_cast(long long, bb[r][0]) & ~m));
+      const double t = (bv - nb) / cc;
+      const double v = (1.0 - omega) * 0.0 + omega * t;
+      out[r][0] = a1 ? rc[r] : v;
+      out[r][1] = a1 ? v : rc[r];
+    }
+  };
+  double rq[3][kRW];      // red values, planes k, k+1, k+2
+  double nraw[kRW][2];    // prefetch: raw b, plane k+3
+  double s1[3][kRW][2];   // S1 planes k-1, k, k+1 (rows 1 .. kRW-2)
+  double bq[3][kRW][2];   // raw b planes k, k+1, k+2 (rows 1 .. kRW-2)
+  {
+    double raw[kRW][2] = {}, ra[kRW] = {};
+    ldraw(raw, kb - 2);
+    redv(raw, kb - 2, ra);
+    ldraw(raw, kb - 1);
+    redv(raw, kb - 1, rq[0]);
+    double bm[kRW][2] = {};
+    keepb(raw, bm);
+    ldraw(raw, kb);
+    redv(raw, kb, rq[1]);
+    keepb(raw, bq[0]);
+    half1(ra, rq[0], rq[1], bm, kb - 1, s1[0]);
+    ldraw(raw, kb + 1);
+    redv(raw, kb + 1, rq[2]);
+    keepb(raw, bq[1]);
+    half1(rq[0], rq[1], rq[2], bq[0], kb, s1[1]);
+    // queue to (kb, kb+1, kb+2)
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) {
+      rq[0][r] = rq[1][r];
+      rq[1][r] = rq[2][r];
+    }
+    ldraw(raw, kb + 2);
+    redv(raw, kb + 2, rq[2]);
+    keepb(raw, bq[2]);
+  }
+  for (int k = kb; k < ke; ++k) {
+    const bool more = k + 1 < ke;
+    ldraw(nraw, more ? k + 3 : k + 2);  // unconditional: see sor_sweep2_kernel
+    half1(rq[0], rq[1], rq[2], bq[1], k + 1, s1[2]);  // S1 at plane k+1
+    // x = S1; res = b - A S1 at plane k (z-, y-, x-, c, x+, y+, z+)
+    const int64_t base = (int64_t)k * g.plane;
+#pragma unroll
+    for (int r = 2; r < 2 + kTY2; ++r) {
+      const double lo = dpp_from_lower(s1[1][r][1]);
+      const double hi = dpp_from_upper(s1[1][r][0]);
+      double rv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const double xl = e == 0 ? lo : s1[1][r][0];
+        const double xr = e == 1 ? hi : s1[1][r][1];
+        double a = cz * s1[0][r][e];
+        a = a + cy * s1[1][r - 1][e];
+        a = a + cx * xl;
+        a = a + cc * s1[1][r][e];
+        a = a + cx * xr;
+        a = a + cy * s1[1][r + 1][e];
+        a = a + cz * s1[2][r][e];
+        rv[e] = bq[0][r][e] - a;
+      }
+      if (out_ok && j0 + r - 2 < ny) {
+        store_row<2>(xout, rix(base + ro[r]), s1[1][r], g.nt);
+        store_row<2>(res, rix(base + ro[r]), rv, g.nt);
+      }
+    }
+    // rotate: red (k+1, k+2, k+3), b (k+1, k+2, k+3), S1 (k, k+1, .)
+    double rn[kRW];
+    redv(nraw, k + 3, rn);
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) {
+      rq[0][r] = rq[1][r];
+      rq[1][r] = rq[2][r];
+      rq[2][r] = rn[r];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        s1[0][r][e] = s1[1][r][e];
+        s1[1][r][e] = s1[2][r][e];
+        bq[0][r][e] = bq[1][r][e];
+        bq[1][r][e] = bq[2][r][e];
+      }
+    }
+    keepb(nraw, bq[2]);
+  }
+}
+
 // even extents, nx >= 128, >= 4 planes per rank: the fused sweep applies (else two half-sweeps)
 bool sor_sweep2_supported(const pb_grid* g) {
   return g->n[0] >= 128 && g->n[0] % 2 == 0 && g->n[1] % 2 == 0 && g->n[1] >= 8 &&
@@ -379,10 +570,16 @@ int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double
   Sweep2Geo geo;
   const int64_t nblocks = sweep2_geo(g, geo);
   PB_TRY(sweep2_ghosts(g, b, b, geo));
-  auto kern = geo.split ? sor_sweep2_kernel<false, 1, true> : sor_sweep2_kernel<false, 1, false>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
-                     g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, 1, b, b, x, res,
-                     (const CgState*)nullptr, (double*)nullptr, skip);
+  if (env_int("PB_MG_PRESMOOTH_SLIM", 1)) {  // one double per pair in the x queue
+    auto kern = geo.split ? presmooth_resid_kernel<true> : presmooth_resid_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0, g->ctx->stream, geo,
+                       s.cx, s.cy, s.cz, s.cc, omega, b, x, res, skip);
+  } else {
+    auto kern = geo.split ? sor_sweep2_kernel<false, 1, true> : sor_sweep2_kernel<false, 1, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
+                       g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, 1, b, b, x, res,
+                       (const CgState*)nullptr, (double*)nullptr, skip);
+  }
   PB_HIP(hipGetLastError());
   return PB_OK;
 }

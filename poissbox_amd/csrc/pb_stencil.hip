@@ -774,6 +774,10 @@ __global__ __launch_bounds__(256) void cg_boundary_kernel(const double* __restri
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool finite(double v) { return v == v && v - v == 0.0; }
 
+// partial counts up to which the finalize kernel reduces with one wave in this order (the CG
+// passes: one workgroup per CU); beyond it, a 256-thread tree (a lone wave took 29 us over the
+// 2048 partials of the elementwise kernels of the preconditioned CG)
+static constexpr int kFoldMaxParts = 1024;
 // fixed-order reduction of nparts x width partials by ONE wave: lane l sums blocks l, l+64, ...
 // in order, then an xor butterfly (every lane ends with the same bits). Used by the finalize
 // kernel (wave 0) and by every wave of a folded pass prologue, so both paths round alike.
@@ -939,14 +943,31 @@ __device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* 
 // scalar logic (KSPSolve_CG + KSPConvergedDefault) on the device. mode bit 1 = reduce partials
 // into sums[], bit 2 = update the state from sums[] (split around the RCCL allreduce).
 // stage 0 = after init, 1 = after pass A (p.w), 2 = after pass B (residual sums).
-__global__ __launch_bounds__(64) void cg_finalize_kernel(const double* __restrict__ parts,
+__global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restrict__ parts,
                                                           int nparts, int width, double* sums,
                                                           int mode, int stage, CgState* st,
                                                           double* hist, int* h_done,
                                                           int64_t host_iter) {
-  if (threadIdx.x >= 64) return;  // one wave
   double S[4];
-  if (mode & 1) {
+  if ((mode & 1) && nparts > kFoldMaxParts) {
+    // many partials (elementwise / multigrid kernels): 256-thread fixed-order tree
+    __shared__ double red[256][4];
+    for (int s = 0; s < width; ++s) {
+      double v = 0.0;
+      for (int b = threadIdx.x; b < nparts; b += 256) v += parts[(int64_t)b * width + s];
+      red[threadIdx.x][s] = v;
+    }
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+      if ((int)threadIdx.x < off)
+        for (int s = 0; s < width; ++s) red[threadIdx.x][s] += red[threadIdx.x + off][s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0)
+      for (int s = 0; s < width; ++s) sums[s] = red[0][s];
+  } else if (mode & 1) {
+    // up to kFoldMaxParts: one wave, the folded prologues' order (folded == unfolded bits)
+    if (threadIdx.x >= 64) return;
     wave_reduce_parts(parts, nparts, width, S);
     if (threadIdx.x == 0)
       for (int s = 0; s < width; ++s) sums[s] = S[s];
@@ -985,16 +1006,16 @@ static int cg_reduce_update(pb_ctx* ctx, int stage, int nparts, int width, CgSta
                             double* hist, int* h_done, int64_t host_iter) {
   double* sums = ctx->d_scalars;
   if (!ctx->split) {
-    hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->d_partials,
+    hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
                        nparts, width, sums, 3, stage, st, hist, h_done, host_iter);
     PB_HIP(hipGetLastError());
     return PB_OK;
   }
-  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->d_partials,
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
                      nparts, width, sums, 1, stage, st, hist, h_done, host_iter);
   PB_HIP(hipGetLastError());
   PB_TRY(allreduce_device(ctx, sums, width));
-  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(64), 0, ctx->stream, ctx->d_partials,
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
                      nparts, width, sums, 2, stage, st, hist, h_done, host_iter);
   PB_HIP(hipGetLastError());
   return PB_OK;
@@ -1135,7 +1156,7 @@ int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
 // then st2[0] = st2[1], so the unfolded entry points find the complete state in slot 0
 int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_done,
                  int64_t host_iter) {
-  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(64), 0, ctx->stream,
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream,
                      ctx->d_partials + fold_parts_b_off(ctx) * 4, nparts_b, 4, ctx->d_scalars, 3,
                      2, st2 + 1, hist, h_done, host_iter);
   PB_HIP(hipGetLastError());
