@@ -116,15 +116,10 @@ __device__ __forceinline__ double red0(double b, const Star& s, double omega) {
 // mode 0: one red-black SOR half-sweep over `color` (x holds the current iterate).
 // mode 1: the first two half-sweeps from x = 0 fused: red = w D^-1 b, then black from those red
 //         values, computed from b directly (lo / hi are then b's ghost planes).
-__global__ __launch_bounds__(256) void mg_smooth_kernel(MgGeo G, double* x,
-                                                        const double* __restrict__ b,
-                                                        const double* lo, const double* hi, Star s,
-                                                        double omega, int color, int mode,
-                                                        const int* skip) {
-  if (skip && *skip) return;
+__device__ __forceinline__ void mg_smooth_body(MgGeo G, double* x, const double* __restrict__ b, const double* lo, const double* hi, Star s, double omega, int color, int mode, int64_t t0, int64_t ts) {
   const int64_t npairs = G.nlocal >> 1;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npairs;
-       q += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t q = t0; q < npairs;
+       q += ts) {
     const PairPos P = pair_pos(G, q);
     const int64_t row = P.idx - P.i0;
     if (mode == 1) {
@@ -174,17 +169,21 @@ __global__ __launch_bounds__(256) void mg_smooth_kernel(MgGeo G, double* x,
     *(dv2*)(x + P.idx) = o;
   }
 }
+__global__ __launch_bounds__(256) void mg_smooth_kernel(MgGeo G, double* x,
+                                                        const double* __restrict__ b,
+                                                        const double* lo, const double* hi, Star s,
+                                                        double omega, int color, int mode,
+                                                        const int* skip) {
+  if (skip && *skip) return;
+  mg_smooth_body(G, x, b, lo, hi, s, omega, color, mode, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                  (int64_t)gridDim.x * blockDim.x);
+}
 
 // res = b - A x for both points of the pair (the reference operator's summation order)
-__global__ __launch_bounds__(256) void mg_residual_kernel(MgGeo G, const double* __restrict__ x,
-                                                          const double* __restrict__ b,
-                                                          const double* __restrict__ lo,
-                                                          const double* __restrict__ hi, Star s,
-                                                          double* __restrict__ res, const int* skip) {
-  if (skip && *skip) return;
+__device__ __forceinline__ void mg_residual_body(MgGeo G, const double* __restrict__ x, const double* __restrict__ b, const double* __restrict__ lo, const double* __restrict__ hi, Star s, double* __restrict__ res, int64_t t0, int64_t ts) {
   const int64_t npairs = G.nlocal >> 1;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npairs;
-       q += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t q = t0; q < npairs;
+       q += ts) {
     const PairPos P = pair_pos(G, q);
     const int64_t row = P.idx - P.i0;
     const dv2 xc = *(const dv2*)(x + P.idx);
@@ -216,6 +215,15 @@ __global__ __launch_bounds__(256) void mg_residual_kernel(MgGeo G, const double*
     *(dv2*)(res + P.idx) = o;
   }
 }
+__global__ __launch_bounds__(256) void mg_residual_kernel(MgGeo G, const double* __restrict__ x,
+                                                          const double* __restrict__ b,
+                                                          const double* __restrict__ lo,
+                                                          const double* __restrict__ hi, Star s,
+                                                          double* __restrict__ res, const int* skip) {
+  if (skip && *skip) return;
+  mg_residual_body(G, x, b, lo, hi, s, res, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                  (int64_t)gridDim.x * blockDim.x);
+}
 
 __device__ __forceinline__ void mg_ijk(const MgGeo& G, int64_t idx, int& i, int& j, int& k) {
   const uint32_t u = (uint32_t)idx, nx = (uint32_t)G.nx;
@@ -226,14 +234,10 @@ __device__ __forceinline__ void mg_ijk(const MgGeo& G, int64_t idx, int& i, int&
 }
 
 // b_c = R res_f, R = P^T / 8: 4 x 4 x 4 fine cells (2I-1 .. 2I+2 per direction)
-__global__ __launch_bounds__(256) void mg_restrict_kernel(MgGeo F, const double* __restrict__ rf,
-                                                          const double* __restrict__ lo,
-                                                          const double* __restrict__ hi, MgGeo Cg,
-                                                          double* __restrict__ bc, const int* skip) {
-  if (skip && *skip) return;
+__device__ __forceinline__ void mg_restrict_body(MgGeo F, const double* __restrict__ rf, const double* __restrict__ lo, const double* __restrict__ hi, MgGeo Cg, double* __restrict__ bc, int64_t t0, int64_t ts) {
   const double w[4] = {0.125, 0.375, 0.375, 0.125};
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < Cg.nlocal;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t idx = t0; idx < Cg.nlocal;
+       idx += ts) {
     int I, J, K;
     mg_ijk(Cg, idx, I, J, K);
     const int xl = wrapm(2 * I - 1, F.nx), xr = wrapm(2 * I + 2, F.nx);
@@ -257,6 +261,14 @@ __global__ __launch_bounds__(256) void mg_restrict_kernel(MgGeo F, const double*
     }
     bc[idx] = sz;
   }
+}
+__global__ __launch_bounds__(256) void mg_restrict_kernel(MgGeo F, const double* __restrict__ rf,
+                                                          const double* __restrict__ lo,
+                                                          const double* __restrict__ hi, MgGeo Cg,
+                                                          double* __restrict__ bc, const int* skip) {
+  if (skip && *skip) return;
+  mg_restrict_body(F, rf, lo, hi, Cg, bc, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                  (int64_t)gridDim.x * blockDim.x);
 }
 
 // The same restriction, one thread per coarse (I, J) column marching over a chunk of coarse
@@ -314,15 +326,10 @@ __global__ __launch_bounds__(256) void mg_restrict_z_kernel(MgGeo F, const doubl
 }
 
 // x_f += P x_c for both points of the pair (trilinear, cell-centred: near parent 3/4, far 1/4)
-__global__ __launch_bounds__(256) void mg_prolong_kernel(MgGeo F, double* __restrict__ xf, MgGeo Cg,
-                                                         const double* __restrict__ xc,
-                                                         const double* __restrict__ lo,
-                                                         const double* __restrict__ hi,
-                                                         const int* skip) {
-  if (skip && *skip) return;
+__device__ __forceinline__ void mg_prolong_body(MgGeo F, double* __restrict__ xf, MgGeo Cg, const double* __restrict__ xc, const double* __restrict__ lo, const double* __restrict__ hi, int64_t t0, int64_t ts) {
   const int64_t npairs = F.nlocal >> 1;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < npairs;
-       q += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t q = t0; q < npairs;
+       q += ts) {
     const PairPos P = pair_pos(F, q);
     const int I = P.i0 >> 1, J = P.j >> 1, K = P.k >> 1;
     const int fI0 = wrapm(I - 1, Cg.nx), fI1 = wrapm(I + 1, Cg.nx);
@@ -346,20 +353,23 @@ __global__ __launch_bounds__(256) void mg_prolong_kernel(MgGeo F, double* __rest
     *(dv2*)(xf + P.idx) = o;
   }
 }
+__global__ __launch_bounds__(256) void mg_prolong_kernel(MgGeo F, double* __restrict__ xf, MgGeo Cg,
+                                                         const double* __restrict__ xc,
+                                                         const double* __restrict__ lo,
+                                                         const double* __restrict__ hi,
+                                                         const int* skip) {
+  if (skip && *skip) return;
+  mg_prolong_body(F, xf, Cg, xc, lo, hi, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                  (int64_t)gridDim.x * blockDim.x);
+}
 
 // The same prolongation, one thread per coarse cell: its 2 x 2 x 2 fine children from the
 // 3 x 3 x 3 coarse neighbourhood (each child by the formula above, same operation order), so a
 // fine row pair is read and written with 16-byte accesses and each coarse value is fetched
 // ~27/8 times per fine point instead of 6.
-__global__ __launch_bounds__(256) void mg_prolong_cell_kernel(MgGeo F, double* __restrict__ xf,
-                                                              MgGeo Cg,
-                                                              const double* __restrict__ xc,
-                                                              const double* __restrict__ lo,
-                                                              const double* __restrict__ hi,
-                                                              const int* skip) {
-  if (skip && *skip) return;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < Cg.nlocal;
-       idx += (int64_t)gridDim.x * blockDim.x) {
+__device__ __forceinline__ void mg_prolong_cell_body(MgGeo F, double* __restrict__ xf, MgGeo Cg, const double* __restrict__ xc, const double* __restrict__ lo, const double* __restrict__ hi, int64_t t0, int64_t ts) {
+  for (int64_t idx = t0; idx < Cg.nlocal;
+       idx += ts) {
     int I, J, K;
     mg_ijk(Cg, idx, I, J, K);
     const int Im = wrapm(I - 1, Cg.nx), Ip = wrapm(I + 1, Cg.nx);
@@ -389,6 +399,16 @@ __global__ __launch_bounds__(256) void mg_prolong_cell_kernel(MgGeo F, double* _
       }
     }
   }
+}
+__global__ __launch_bounds__(256) void mg_prolong_cell_kernel(MgGeo F, double* __restrict__ xf,
+                                                              MgGeo Cg,
+                                                              const double* __restrict__ xc,
+                                                              const double* __restrict__ lo,
+                                                              const double* __restrict__ hi,
+                                                              const int* skip) {
+  if (skip && *skip) return;
+  mg_prolong_cell_body(F, xf, Cg, xc, lo, hi, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
+                  (int64_t)gridDim.x * blockDim.x);
 }
 
 // The same prolongation, one thread per coarse (I, J) column marching over a chunk of coarse
@@ -470,6 +490,73 @@ __global__ __launch_bounds__(256) void mg_prolong_z_kernel(MgGeo F, const double
       for (int dj = 0; dj < 2; ++dj) *(dv2*)(xout + q[dk][dj]) = ov[dk][dj];
     cm = c0;
     c0 = cp;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The coarse tail of the V-cycle in ONE launch (one rank): every level of at most
+// PB_MG_TAIL_MAX points (16^3 at 512^3: the 16^3, 8^3 and 4^3 levels) -- down-legs, the coarsest
+// level's sweeps and the up-legs -- run by one workgroup, step after step with a barrier between
+// them, through the same per-point bodies as the per-level kernels (same operations, bit for bit).
+// Replaces ~28 launches of a few microseconds each per V-cycle.
+// ---------------------------------------------------------------------------------------------
+struct TailLevel {
+  MgGeo G;
+  double* x;
+  double* b;
+  double* res;
+  Star s;
+};
+static constexpr int kTailMax = 12;
+struct TailArgs {
+  TailLevel lv[kTailMax];
+  int nl;           // levels in the tail; lv[nl-1] is the coarsest
+  int coarse_its;
+  int prolong_cell;
+  double omega;
+};
+
+__device__ __forceinline__ const double* wrap_lo(const MgGeo& G, const double* v) {
+  return v + (int64_t)(G.nzl - 1) * G.plane;  // one rank: plane -1 is the last plane
+}
+
+__global__ __launch_bounds__(512) void mg_tail_kernel(TailArgs A, const int* skip) {
+  if (skip && *skip) return;
+  const int64_t t0 = threadIdx.x, ts = blockDim.x;
+  const double w = A.omega;
+  auto smooth = [&](const TailLevel& L, int color, int mode) {
+    const double* v = mode == 1 ? L.b : L.x;
+    mg_smooth_body(L.G, L.x, L.b, wrap_lo(L.G, v), v, L.s, w, color, mode, t0, ts);
+    __syncthreads();
+  };
+  for (int t = 0; t + 1 < A.nl; ++t) {  // down: pre-smooth, residual, restrict
+    const TailLevel& F = A.lv[t];
+    smooth(F, 0, 1);
+    mg_residual_body(F.G, F.x, F.b, wrap_lo(F.G, F.x), F.x, F.s, F.res, t0, ts);
+    __syncthreads();
+    mg_restrict_body(F.G, F.res, wrap_lo(F.G, F.res), F.res, A.lv[t + 1].G, A.lv[t + 1].b, t0,
+                     ts);
+    __syncthreads();
+  }
+  {  // coarsest: `coarse_its` symmetric red-black sweeps from zero (coarse_solve's order)
+    const TailLevel& L = A.lv[A.nl - 1];
+    smooth(L, 0, 1);
+    smooth(L, 0, 0);
+    for (int it = 1; it < A.coarse_its; ++it) {
+      smooth(L, 1, 0);
+      smooth(L, 0, 0);
+    }
+  }
+  for (int t = A.nl - 2; t >= 0; --t) {  // up: prolongate + correct, post-smooth
+    const TailLevel& F = A.lv[t];
+    const TailLevel& Cl = A.lv[t + 1];
+    if (A.prolong_cell)
+      mg_prolong_cell_body(F.G, F.x, Cl.G, Cl.x, wrap_lo(Cl.G, Cl.x), Cl.x, t0, ts);
+    else
+      mg_prolong_body(F.G, F.x, Cl.G, Cl.x, wrap_lo(Cl.G, Cl.x), Cl.x, t0, ts);
+    __syncthreads();
+    smooth(F, 1, 0);
+    smooth(F, 0, 0);
   }
 }
 
@@ -647,7 +734,16 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
   mg->lv[0].b = const_cast<double*>(r);
   mg->lv[0].x = z;
   pb_ctx* ctx = mg->ctx;
-  for (int l = 0; l < L - 1; ++l) {  // down: pre-smooth (red, black), residual, restrict
+  // the coarse tail in one launch (one rank): levels Lt .. L-1 of <= PB_MG_TAIL_MAX points
+  int Lt = L;
+  if (!ctx->split && env_int("PB_MG_TAIL", 1)) {
+    const int64_t tail_max = env_int("PB_MG_TAIL_MAX", 8192);
+    Lt = L - 1;
+    while (Lt > 1 && mg->lv[Lt - 1].g->nlocal <= tail_max) --Lt;
+    if (Lt < 1 || mg->lv[Lt].g->nlocal > tail_max || L - Lt > kTailMax) Lt = L;
+  }
+  const int Ldown = Lt < L ? Lt : L - 1;  // host down-legs l < Ldown
+  for (int l = 0; l < Ldown; ++l) {  // down: pre-smooth (red, black), residual, restrict
     MgLevel& F = mg->lv[l];
     MgLevel& Cl = mg->lv[l + 1];
     // large level: zero-start red + black half-sweeps and the residual in one pass
@@ -689,11 +785,25 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     }
     PB_HIP(hipGetLastError());
   }
-  {
+  if (Lt < L) {
+    ScopedTimer t3(ctx, "mg_coarse_levels");
+    TailArgs A{};
+    A.nl = L - Lt;
+    A.coarse_its = mg->coarse_its;
+    A.prolong_cell = mg->prolong_cell;
+    A.omega = mg->omega;
+    for (int t = 0; t < A.nl; ++t) {
+      const MgLevel& lv = mg->lv[Lt + t];
+      A.lv[t] = TailLevel{lv.geo(), lv.x, lv.b, lv.res, lv.s};
+    }
+    hipLaunchKernelGGL(mg_tail_kernel, dim3(1), dim3(512), 0, ctx->stream, A, mg->skip);
+    PB_HIP(hipGetLastError());
+  } else {
     ScopedTimer t3(ctx, L > 1 ? "mg_coarse_levels" : "mg_fine_smooth_first");
     PB_TRY(coarse_solve(mg, mg->lv[L - 1], L == 1 ? sums_st : nullptr, nparts));
   }
-  for (int l = L - 2; l >= 0; --l) {  // up: prolongate + correct, post-smooth (black, red)
+  // up: prolongate + correct, post-smooth; with a tail, the first host up-leg prolongates from Lt
+  for (int l = Lt < L ? Lt - 1 : L - 2; l >= 0; --l) {
     MgLevel& F = mg->lv[l];
     MgLevel& Cl = mg->lv[l + 1];
     ScopedTimer t4(ctx, l == 0 ? "mg_fine_prolong_post" : "mg_coarse_levels");

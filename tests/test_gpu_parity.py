@@ -672,7 +672,11 @@ MG_KERNELS = {"default": {},
               "legacy": {"PB_MG_ENGINE_MIN_PLANE": "1000000000", "PB_MG_RESTRICT_Z": "0",
                          "PB_MG_PROLONG_CELL": "0"},
               "unfused": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_SWEEP2": "0",
-                          "PB_MG_PRESMOOTH_FUSED": "0"}}
+                          "PB_MG_PRESMOOTH_FUSED": "0"},
+              # per-level launches for the coarse tail, and the pre-r02 pre-smoothing kernel
+              "notail": {"PB_MG_TAIL": "0", "PB_MG_PRESMOOTH_SLIM": "0"},
+              # a longer one-launch tail (every level up to 32^3)
+              "bigtail": {"PB_MG_TAIL_MAX": "40000"}}
 
 
 @pytest.mark.parametrize("kern", sorted(MG_KERNELS))
