@@ -307,29 +307,32 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
     // chunk's last step re-loading valid planes): no branch around a load, so the compiler keeps
     // the prefetch registers stable instead of copying them at control-flow joins -- such copies
     // must wait for the loads and serialised the software pipeline (pass A ran ~10 % slower).
-    auto issue_zrow = [&](int kk) {  // raw rows of plane kk in [-1, nzl] -> zr
+    // raw rows of plane kk in [-1, nzl] -> dst (ghost: the plane is a ghost buffer)
+    auto issue_rows = [&](int kk, double (&dst)[NR][TY][V], bool& ghost) {
       if (g.wrap) kk = kk < 0 ? kk + g.nzl : (kk >= g.nzl ? kk - g.nzl : kk);
-      zr_ghost = kk < 0 || kk >= g.nzl;
+      ghost = kk < 0 || kk >= g.nzl;
       const double* gp = kk < 0 ? ghost_lo : ghost_hi;
-      const int64_t base = zr_ghost ? 0 : (int64_t)kk * g.plane;
+      const int64_t base = ghost ? 0 : (int64_t)kk * g.plane;
 #pragma unroll
       for (int a = 0; a < NR; ++a) {
-        const double* src = zr_ghost ? gp : ld.src(a);
+        const double* src = ghost ? gp : ld.src(a);
 #pragma unroll
-        for (int t = 0; t < TY; ++t) load_row<V>(src, rix(base + (int64_t)(j0 + t) * nx), zr[a][t]);
+        for (int t = 0; t < TY; ++t) load_row<V>(src, rix(base + (int64_t)(j0 + t) * nx), dst[a][t]);
       }
     };
-    auto take_zrow = [&](double (&q)[TY][V]) {  // combine zr into q
+    auto take_rows = [&](const double (&src)[NR][TY][V], bool ghost, double (&q)[TY][V]) {
 #pragma unroll
       for (int t = 0; t < TY; ++t)
 #pragma unroll
         for (int e = 0; e < V; ++e) {
           double raw[NR];
 #pragma unroll
-          for (int a = 0; a < NR; ++a) raw[a] = zr[a][t][e];
-          q[t][e] = (zr_ghost && !Load::GHOST_RAW) ? zr[0][t][e] : ld.value(raw);
+          for (int a = 0; a < NR; ++a) raw[a] = src[a][t][e];
+          q[t][e] = (ghost && !Load::GHOST_RAW) ? src[0][t][e] : ld.value(raw);
         }
     };
+    auto issue_zrow = [&](int kk) { issue_rows(kk, zr, zr_ghost); };
+    auto take_zrow = [&](double (&q)[TY][V]) { take_rows(zr, zr_ghost, q); };
     auto issue_plane_ops = [&](int kk) {  // halo rows, edges, epilogue operands of own plane kk
       const int64_t base = (int64_t)kk * g.plane;
 #pragma unroll
@@ -393,12 +396,25 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
     const int dir = g.rev ? -1 : 1;
     const int kf = g.rev ? ke - 1 : kb;
     const int nk = ke - kb;
-    issue_zrow(kf - dir);
-    take_zrow(q0);
-    issue_zrow(kf);
-    take_zrow(q1);
-    issue_plane_ops(kf);
-    issue_zrow(kf + dir);
+    // The first planes' loads go out together (one wait instead of one per plane; the
+    // prologue is ~10 % of a 32-plane chunk): one array through the queue -- planes kf-dir, kf,
+    // kf+dir and plane kf's operands all in flight; two -- kf-dir and kf, then the rest.
+    {
+      double r0[NR][TY][V], r1[NR][TY][V];
+      bool g0 = false, g1 = false;
+      issue_rows(kf - dir, r0, g0);
+      issue_rows(kf, r1, g1);
+      if constexpr (NR == 1) {
+        issue_plane_ops(kf);
+        issue_zrow(kf + dir);
+      }
+      take_rows(r0, g0, q0);
+      take_rows(r1, g1, q1);
+      if constexpr (NR != 1) {
+        issue_plane_ops(kf);
+        issue_zrow(kf + dir);
+      }
+    }
     for (int m = 0; m < nk; ++m) {
       const int k = kf + m * dir;
       take_zrow(q2);                    // plane k+dir (in flight since the previous step)
