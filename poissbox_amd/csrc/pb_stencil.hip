@@ -585,7 +585,7 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
     if (vec2 && ty == 4 && tall && !getenv("PB_STENCIL_TY") && g->n[1] % 8 == 0 &&
         g->plane >= tall_min)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev,
-                            wgcu > 0 ? wgcu : 1, fold);
+                            wgcu > 0 ? wgcu : env_int("PB_TALL_WGCU", 1), fold);
   }
   if (vec2) {
     switch (ty) {
