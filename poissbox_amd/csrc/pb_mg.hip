@@ -42,6 +42,9 @@ struct MgLevel {
   double* x = nullptr;    // correction (level 0: the PC output z)
   double* b = nullptr;    // right-hand side (level 0: the PC input r)
   double* res = nullptr;  // residual scratch
+  // fused post-smoothing (one rank, large levels): the pre-smoothed x, kept apart from x so that
+  // the prolongation + both half-sweeps can read it and write x in one pass
+  double* xs = nullptr;
   MgGeo geo() const {
     return MgGeo{(int)g->n[0], (int)g->n[1], (int)g->nzl, g->plane, g->nlocal, g->k0};
   }
@@ -679,6 +682,12 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
   mg->coarse_its = pc_type == PB_PC_MG ? std::max(1, coarse_its) : 1;
   mg->lv.resize(L);
   int64_t total = 0;
+  // levels that take the fused post-smoothing (PB_MG_POST_FUSED, one rank): an xs array each
+  const bool want_post = !ctx->split && env_int("PB_MG_POST_FUSED", 1) != 0;
+  const int64_t post_min_plane = env_int("PB_MG_ENGINE_MIN_PLANE", 256 * 256);
+  auto takes_post = [&](const MgLevel& lv, int l) {
+    return want_post && l < L - 1 && lv.g->plane >= post_min_plane && sor_sweep2_supported(lv.g);
+  };
   for (int l = 0; l < L; ++l) {
     MgLevel& lv = mg->lv[l];
     for (int d = 0; d < 3; ++d) {
@@ -698,6 +707,7 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
       total += 2 * lv.g->nlocal;  // x, b
     }
     if (l < L - 1) total += lv.g->nlocal;  // residual
+    if (takes_post(lv, l)) total += lv.g->nlocal;
   }
   if (total > 0 && hipMalloc(&mg->mem, (size_t)total * sizeof(double)) != hipSuccess) {
     mg_destroy(mg);
@@ -716,9 +726,25 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
       lv.res = p;
       p += lv.g->nlocal;
     }
+    if (takes_post(lv, l)) {
+      lv.xs = p;
+      p += lv.g->nlocal;
+    }
   }
   *out = mg;
   return PB_OK;
+}
+
+// level l pre-smooths into xs and post-smooths with the fused prolongation kernel: it has an xs
+// array (mg_create), the fused pre-smoothing applies, and so does the marching prolongation
+static bool post_fused(const Mg* mg, int l) {
+  const MgLevel& F = mg->lv[l];
+  if (!F.xs || l + 1 >= (int)mg->lv.size() || F.g->plane < mg->engine_min_plane ||
+      !env_int("PB_MG_PRESMOOTH_FUSED", 1) || !env_int("PB_MG_POST_FUSED", 1) ||
+      mg->prolong_cell != 2)
+    return false;
+  const MgLevel& C = mg->lv[l + 1];
+  return C.g->n[0] * C.g->n[1] >= mg->restrict_z_min_cols;
 }
 
 int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState* sums_st,
@@ -752,7 +778,8 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     {
       ScopedTimer t1(ctx, l == 0 ? "mg_fine_smooth_first" : "mg_coarse_levels");
       if (fused)
-        PB_TRY(launch_presmooth_residual(F.g, F.s, F.b, F.x, F.res, mg->omega, mg->skip));
+        PB_TRY(launch_presmooth_residual(F.g, F.s, F.b, post_fused(mg, l) ? F.xs : F.x, F.res,
+                                         mg->omega, mg->skip));
       else
         PB_TRY(smooth(mg, F, 0, 1));  // red from zero + black
     }
@@ -807,6 +834,12 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     MgLevel& F = mg->lv[l];
     MgLevel& Cl = mg->lv[l + 1];
     ScopedTimer t4(ctx, l == 0 ? "mg_fine_prolong_post" : "mg_coarse_levels");
+    if (post_fused(mg, l)) {
+      // prolongation + correction + both post-smoothing half-sweeps in one pass, xs -> x
+      PB_TRY(launch_post_sweep(F.g, F.s, Cl.g, F.xs, Cl.x, F.b, F.x, mg->omega, mg->skip,
+                               l == 0 ? sums_st : nullptr, l == 0 ? nparts : nullptr));
+      continue;
+    }
     const double *lo, *hi;
     PB_TRY(ghosts(Cl, Cl.x, &lo, &hi));
     const MgGeo G = F.geo(), CG = Cl.geo();

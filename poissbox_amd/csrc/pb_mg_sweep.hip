@@ -4,6 +4,7 @@
 // the residual. Same per-point arithmetic as the half-sweep / residual kernels (SorHalf, ResidEpi
 // in pb_stencil.hip, restated in oracle/pb_oracle.c pbo_mg_apply), hence bit-identical results.
 #include <algorithm>
+#include <type_traits>
 
 #include "pb_device.hpp"
 
@@ -488,6 +489,274 @@ __global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Post-smoothing with the prolongation folded in (one rank): the sweep's input
+// xin = x_s + P x_c is formed as the planes arrive -- x_s (the pre-smoothed iterate) and the
+// coarse correction x_c are read, the prolongated input is never stored. Then both half-sweeps
+// (c1 = 1 first, then the other colour) out of place into xout, CG's residual sums optional.
+// Per fine point: read x_s and b, write xout (+ 1/8 of a coarse value): 24 B/DoF instead of the
+// prolongation pass's 16 plus the sweep's 24. Arithmetic: mg_prolong_z_kernel's interpolation
+// (x-stage, then y, then z, same operation order) and sor_sweep2_kernel's half-sweeps, so the
+// result is bit-identical. The first-half queue keeps only the c1 value of each pair (the
+// second half-sweep reads only c1 points; the c2 values are the input's), which pays for the
+// coarse-value prefetch in registers.
+// ---------------------------------------------------------------------------------------------
+struct PostGeo {
+  int ncx, ncy, ncz;   // coarse extents (one rank: the whole coarse grid)
+  int64_t cplane;
+};
+
+// v[1] if e1 else v[0], as bit operations: a `?:` between two elements of a register array can
+// become a computed address, which moves the whole array to scratch
+__device__ __forceinline__ double pick(bool e1, const double (&v)[2]) {
+  const long long m = -(long long)e1;
+  return __builtin_bit_cast(double, (__builtin_bit_cast(long long, v[1]) & m) |
+                                        (__builtin_bit_cast(long long, v[0]) & ~m));
+}
+
+template <bool SUMS>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void post_sweep_kernel(
+    Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
+    const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
+    double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
+  if (skip && *skip) return;
+  constexpr int c1 = 1;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const double mu = SUMS ? st->mu : 0.0;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bid = xcd_block(g.remap);
+  const int seg = bid % g.nseg;
+  bid /= g.nseg;
+  const int tile = bid % g.ntile;
+  const int chunk = bid / g.ntile;
+  const int j0 = (tile * kWaves + wid) * kTY2;
+  const int kb = chunk * g.kc;
+  const int ke = min(kb + g.kc, g.nzl);
+  const int nx = g.nx, ny = g.ny, nz = g.nzl;
+  int ip = seg * kSegOut + 2 * (lane - kSegLead);
+  if (ip < 0) ip += nx;
+  if (ip >= nx) ip -= nx;
+  const int o = seg * kSegOut + 2 * (lane - kSegLead);
+  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
+  if (j0 < ny && kb < nz) {
+    int64_t ro[kRW];
+    int par_row[kRW];
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) {
+      int j = j0 - 2 + r;
+      if (j < 0) j += ny;
+      if (j >= ny) j -= ny;
+      ro[r] = (int64_t)j * nx;
+      par_row[r] = (ip + j) & 1;
+    }
+    const unsigned boff = (unsigned)ip * 8u;
+    auto rix = [&](int64_t row) { return RowIx{row, boff}; };
+    auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+    auto pl = [&](int kk) -> int64_t { return (int64_t)wrapk(kk) * g.plane; };
+    auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
+    // coarse rows Jb .. Jb+5 cover the 7 fine rows j0-2 .. j0+4 and their far rows
+    const int p0 = j0 & 1;
+    const int Jb = ((j0 - 2) >> 1) - 1;
+    int64_t crow[6];
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      int J = Jb + t;
+      if (J < 0) J += cgeo.ncy;
+      if (J >= cgeo.ncy) J -= cgeo.ncy;
+      crow[t] = (int64_t)J * cgeo.ncx;
+    }
+    const unsigned cboff = (unsigned)(ip >> 1) * 8u;  // coarse column I = ip / 2
+    // fine plane kk: raw x_s rows and the coarse rows of its near / far coarse planes
+    auto ldx = [&](double (&dst)[kRW][2], double (&cv)[2][6], int kk) {
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 0; r < kRW; ++r) load_row<2>(xs, rix(base + ro[r]), dst[r]);
+      const int kw = wrapk(kk);
+      const int K = kw >> 1;
+      int fK = (kw & 1) ? K + 1 : K - 1;
+      if (fK < 0) fK += cgeo.ncz;
+      if (fK >= cgeo.ncz) fK -= cgeo.ncz;
+      const double* cn = xc + (int64_t)K * cgeo.cplane;
+      const double* cf = xc + (int64_t)fK * cgeo.cplane;
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        cv[0][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cn + crow[t]) + cboff);
+        cv[1][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cf + crow[t]) + cboff);
+      }
+    };
+    // x_s + P x_c (mg_prolong_z_kernel's operation order); P0 = j0 parity (wave-uniform)
+    auto prolong_p = [&](auto P0c, double (&v)[kRW][2], const double (&cv)[2][6]) {
+      constexpr int P0 = decltype(P0c)::value;
+#pragma unroll
+      for (int r = 0; r < kRW; ++r) {
+        // fine row j0-2+r: coarse row J at index tJ, far row (J-1 even / J+1 odd) at tf
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int odd = (P0 + r) & 1;
+        const int tJ = 1 + ((P0 + r) >> 1);
+        const int tf = odd ? tJ + 1 : tJ - 1;
+        const double cnn = cv[0][tJ], cnf = cv[0][tf], cfn = cv[1][tJ], cff = cv[1][tf];
+        const double lnn = dpp_from_lower(cnn), lnf = dpp_from_lower(cnf);
+        const double lfn = dpp_from_lower(cfn), lff = dpp_from_lower(cff);
+        const double unn = dpp_from_upper(cnn), unf = dpp_from_upper(cnf);
+        const double ufn = dpp_from_upper(cfn), uff = dpp_from_upper(cff);
+        // element 0: far column I-1; element 1: I+1
+        const double vn0 = 0.75 * (0.75 * cnn + 0.25 * lnn) + 0.25 * (0.75 * cnf + 0.25 * lnf);
+        const double vf0 = 0.75 * (0.75 * cfn + 0.25 * lfn) + 0.25 * (0.75 * cff + 0.25 * lff);
+        const double vn1 = 0.75 * (0.75 * cnn + 0.25 * unn) + 0.25 * (0.75 * cnf + 0.25 * unf);
+        const double vf1 = 0.75 * (0.75 * cfn + 0.25 * ufn) + 0.25 * (0.75 * cff + 0.25 * uff);
+        v[r][0] = v[r][0] + (0.75 * vn0 + 0.25 * vf0);
+        v[r][1] = v[r][1] + (0.75 * vn1 + 0.25 * vf1);
+      }
+    };
+    auto prolong = [&](double (&v)[kRW][2], const double (&cv)[2][6]) {
+      if (p0) prolong_p(std::integral_constant<int, 1>{}, v, cv);
+      else prolong_p(std::integral_constant<int, 0>{}, v, cv);
+    };
+    auto ldb = [&](double (&dst)[kRW][2], int kk) {
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
+    };
+    // element of the c1 point in row r of plane kk (the c2 point is the other one)
+    auto ec1 = [&](int kk, int r) -> bool { return ((par_row[r] + kpar(kk)) & 1) != c1; };
+    // first half-sweep (colour c1) at plane kk, rows 1 .. kRW-2 -> the c1 value of each pair.
+    // zmv: plane kk-1's values at those points (its c2 points); xcn, xp: planes kk, kk+1 (full)
+    auto half1 = [&](const double (&zmv)[kRW], const double (&xcn)[kRW][2],
+                     const double (&xp)[kRW][2], const double (&bb)[kRW][2], int kk,
+                     double (&out)[kRW]) {
+#pragma unroll
+      for (int r = 1; r < kRW - 1; ++r) {
+        const bool a1 = ec1(kk, r);  // c1 point is element 1
+        const double lo = dpp_from_lower(xcn[r][1]);
+        const double hi = dpp_from_upper(xcn[r][0]);
+        const double xl = a1 ? xcn[r][0] : lo;
+        const double xr = a1 ? hi : xcn[r][1];
+        const double zm = zmv[r];
+        const double ym = pick(a1, xcn[r - 1]);
+        const double yp = pick(a1, xcn[r + 1]);
+        const double zp = pick(a1, xp[r]);
+        const double bv = pick(a1, bb[r]);
+        const double xo = pick(a1, xcn[r]);
+        double nb = cz * zm;
+        nb = nb + cy * ym;
+        nb = nb + cx * xl;
+        nb = nb + cx * xr;
+        nb = nb + cy * yp;
+        nb = nb + cz * zp;
+        const double t = (bv - nb) / cc;
+        out[r] = (1.0 - omega) * xo + omega * t;
+      }
+    };
+    // the c2 values of a full plane (rows 1 .. kRW-2)
+    auto c2of = [&](const double (&v)[kRW][2], int kk, double (&out)[kRW]) {
+#pragma unroll
+      for (int r = 1; r < kRW - 1; ++r) out[r] = pick(!ec1(kk, r), v[r]);
+    };
+    auto c1of = [&](const double (&v)[kRW][2], int kk, double (&out)[kRW]) {
+#pragma unroll
+      for (int r = 1; r < kRW - 1; ++r) out[r] = pick(ec1(kk, r), v[r]);
+    };
+    // second half-sweep at plane kk, own rows 2 .. 2+TY2-1: the c2 points from the c1 values
+    // around them (sor_sweep2_kernel's, M = 0). sm, sc, sp: c1 values at planes kk-1, kk, kk+1;
+    // xo, bo: the plane's c2 input values and right-hand side (bc1: b at its c1 points, sums only)
+    auto half2 = [&](int kk, const double (&sm)[kRW], const double (&sc)[kRW],
+                     const double (&sp)[kRW], const double (&xo)[kRW], const double (&bo)[kRW],
+                     const double (&bc1)[SUMS ? kRW : 1]) {
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 2; r < 2 + kTY2; ++r) {
+        const bool a1 = !ec1(kk, r);  // second-colour point is element 1
+        const double cself = sc[r];
+        const double lo = dpp_from_lower(cself);
+        const double hi = dpp_from_upper(cself);
+        const double xl = a1 ? cself : lo;
+        const double xr = a1 ? hi : cself;
+        double nb = cz * sm[r];
+        nb = nb + cy * sc[r - 1];
+        nb = nb + cx * xl;
+        nb = nb + cx * xr;
+        nb = nb + cy * sc[r + 1];
+        nb = nb + cz * sp[r];
+        const double t = (bo[r] - nb) / cc;
+        const double v = (1.0 - omega) * xo[r] + omega * t;
+        double ov[2];
+        ov[0] = a1 ? cself : v;
+        ov[1] = a1 ? v : cself;
+        if (out_ok && j0 + r - 2 < ny) {
+          store_row<2>(xout, rix(base + ro[r]), ov, g.nt);
+          if constexpr (SUMS) {
+            double rv2[2];
+            rv2[0] = a1 ? bc1[r] : bo[r];
+            rv2[1] = a1 ? bo[r] : bc1[r];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const double t2 = ov[e] - mu;
+              acc[0] += t2;
+              acc[1] += t2 * t2;
+              acc[2] += t2 * rv2[e];
+              acc[3] += rv2[e];
+            }
+          }
+        }
+      }
+    };
+    // Iteration k issues plane k+2's loads, runs the second half at plane k-1 while they are in
+    // flight, then prolongates plane k+2 and runs the first half at plane k+1. The queues keep
+    // only the c2 values of planes k-1 and k (x: the second half's old value, and the first half's
+    // z-neighbour; b: the second half's right-hand side). The loop starts two planes early
+    // (kb-2, kb-1: first halves only) so the queues fill without a separate prologue; the second
+    // half at plane ke-1 follows the loop.
+    double xm[kRW], x0[kRW];  // x input, c2 points: planes k-1, k
+    double xq1[kRW][2];       // x input, plane k+1
+    double s1[4][kRW];        // c1 values after the first half: planes k-2 .. k+1
+    double bm[kRW], b0[kRW];  // b at c2 points: planes k-1, k
+    double bm1[SUMS ? kRW : 1], b01[SUMS ? kRW : 1];  // and (sums only) at the c1 points
+    {
+      double cv[2][6];
+      ldx(xq1, cv, kb - 2);
+      prolong(xq1, cv);
+      c2of(xq1, kb - 2, x0);
+      ldx(xq1, cv, kb - 1);
+      prolong(xq1, cv);
+    }
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) {
+      xm[r] = bm[r] = b0[r] = 0.0;
+      s1[0][r] = s1[1][r] = s1[2][r] = 0.0;
+      if constexpr (SUMS) bm1[r] = b01[r] = 0.0;
+    }
+#pragma unroll 1
+    for (int k = kb - 2; k < ke; ++k) {
+      double xq2[kRW][2], bq1[kRW][2], cv[2][6];
+      ldx(xq2, cv, k + 2);
+      ldb(bq1, k + 1);
+      if (k > kb) half2(k - 1, s1[0], s1[1], s1[2], xm, bm, bm1);
+      prolong(xq2, cv);
+      half1(x0, xq1, xq2, bq1, k + 1, s1[3]);  // c1 values at plane k+1
+      // rotate: planes k-1 <- k <- k+1 (c2 values), k+1 <- k+2
+#pragma unroll
+      for (int r = 0; r < kRW; ++r) {
+        xm[r] = x0[r];
+        bm[r] = b0[r];
+        if constexpr (SUMS) bm1[r] = b01[r];
+        s1[0][r] = s1[1][r];
+        s1[1][r] = s1[2][r];
+        s1[2][r] = s1[3][r];
+      }
+      c2of(xq1, k + 1, x0);
+      c2of(bq1, k + 1, b0);
+      if constexpr (SUMS) c1of(bq1, k + 1, b01);
+#pragma unroll
+      for (int r = 0; r < kRW; ++r)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) xq1[r][e] = xq2[r][e];
+    }
+    half2(ke - 1, s1[0], s1[1], s1[2], xm, bm, bm1);
+  }
+  if constexpr (SUMS) block_partials<4>(acc, parts);
+}
+
 // even extents, nx >= 128, >= 4 planes per rank: the fused sweep applies (else two half-sweeps)
 bool sor_sweep2_supported(const pb_grid* g) {
   return g->n[0] >= 128 && g->n[0] % 2 == 0 && g->n[1] % 2 == 0 && g->n[1] >= 8 &&
@@ -557,6 +826,36 @@ int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
                        (double*)nullptr, (const CgState*)nullptr, (double*)nullptr, skip);
+  }
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double* xs,
+                      const double* xc, const double* b, double* xout, double omega,
+                      const int* skip, const CgState* sums_st, int* nparts) {
+  ScopedTimer tm(g->ctx, "mg_post_sweep");
+  if (g->ctx->split) return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: one rank only");
+  if (xs == xout) return set_error(PB_ERR_ARG, "fused post-smoothing must run out of place");
+  if (cg->n[0] * 2 != g->n[0] || cg->n[1] * 2 != g->n[1] || cg->nzl * 2 != g->nzl)
+    return set_error(PB_ERR_ARG, "fused post-smoothing: coarse grid is not half the fine one");
+  Sweep2Geo geo;
+  const int64_t nblocks = sweep2_geo(g, geo);
+  geo.split = 0;
+  geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
+  PostGeo cgeo{(int)cg->n[0], (int)cg->n[1], (int)cg->nzl, cg->plane};
+  if (sums_st) {
+    if (nblocks * 4 > g->ctx->partials_cap)
+      return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
+                       (long long)nblocks);
+    hipLaunchKernelGGL(post_sweep_kernel<true>, dim3((unsigned)nblocks), dim3(kThreads), 0,
+                       g->ctx->stream, geo, cgeo, s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout,
+                       sums_st, g->ctx->d_partials, skip);
+    if (nparts) *nparts = (int)nblocks;
+  } else {
+    hipLaunchKernelGGL(post_sweep_kernel<false>, dim3((unsigned)nblocks), dim3(kThreads), 0,
+                       g->ctx->stream, geo, cgeo, s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout,
+                       (const CgState*)nullptr, (double*)nullptr, skip);
   }
   PB_HIP(hipGetLastError());
   return PB_OK;

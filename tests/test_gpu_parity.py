@@ -676,7 +676,10 @@ MG_KERNELS = {"default": {},
               # per-level launches for the coarse tail, and the pre-r02 pre-smoothing kernel
               "notail": {"PB_MG_TAIL": "0", "PB_MG_PRESMOOTH_SLIM": "0"},
               # a longer one-launch tail (every level up to 32^3)
-              "bigtail": {"PB_MG_TAIL_MAX": "40000"}}
+              "bigtail": {"PB_MG_TAIL_MAX": "40000"},
+              # prolongation and post-smoothing as two launches (the pre-r02 up-leg)
+              "nopost": {"PB_MG_POST_FUSED": "0", "PB_MG_ENGINE_MIN_PLANE": "0",
+                         "PB_MG_RESTRICT_Z_MIN_COLS": "0"}}
 
 
 @pytest.mark.parametrize("kern", sorted(MG_KERNELS))
@@ -724,7 +727,7 @@ def test_cg_sor_mg_matches_oracle(ctx, monkeypatch, kern, pc, n):
         assert its <= 16  # h-independent V-cycle preconditioning
 
 
-@pytest.mark.parametrize("kern", ["default", "engine", "legacy", "unfused"])
+@pytest.mark.parametrize("kern", ["default", "engine", "legacy", "unfused", "nopost"])
 def test_cg_mg_fused_post_smoothing(ctx, monkeypatch, kern):
     """x extent >= 128: the V-cycle's post-smoothing runs as ONE fused two-colour pass (out of
     place, with CG's residual sums on level 0); history / solution within the CG bar, PC apply
