@@ -293,6 +293,7 @@ static int64_t wrap64(int64_t v, int64_t n) { return v < 0 ? v + n : (v >= n ? v
 
 static void mg_smooth(const mg_level* L, int color, int zero_init, double omega) {
   const int64_t nx = L->n[0], ny = L->n[1], nz = L->n[2];
+  const double icc = 1.0 / L->cc; /* the update multiplies by the inverted diagonal (MatSOR idiag) */
   for (int64_t k = 0; k < nz; ++k)
     for (int64_t j = 0; j < ny; ++j)
       for (int64_t i = 0; i < nx; ++i) {
@@ -312,7 +313,7 @@ static void mg_smooth(const mg_level* L, int color, int zero_init, double omega)
           nb = nb + L->cz * x[i + nx * (j + ny * wrap64(k + 1, nz))];
           xo = x[id];
         }
-        const double t = (L->b[id] - nb) / L->cc;
+        const double t = (L->b[id] - nb) * icc;
         L->x[id] = (1.0 - omega) * xo + omega * t;
       }
 }

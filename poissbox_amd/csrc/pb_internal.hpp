@@ -239,6 +239,9 @@ int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double
 // pre-smoothing from zero (red + black half-sweeps) fused with the residual: x, res from b
 // post-smoothing with the prolongation folded in (one rank): xout = both half-sweeps (black, red)
 // of xin = xs + P xc (cg: the coarse grid of xc), optional CG residual sums
+// pre-smoothing from zero + residual + restriction to the coarse b in one pass (one rank)
+int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, const double* b,
+                              double* xout, double* bc, double omega, const int* skip);
 int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double* xs,
                       const double* xc, const double* b, double* xout, double omega,
                       const int* skip, const CgState* sums_st = nullptr, int* nparts = nullptr);

@@ -110,9 +110,9 @@ __device__ __forceinline__ Nb4 nb4(const MgGeo& G, const double* v, const double
   return r;
 }
 
-// red value after the zero-initialised first half-sweep: (1 - w) * 0 + w * ((b - 0) / c)
+// red value after the zero-initialised first half-sweep: (1 - w) * 0 + w * ((b - 0) * (1 / c))
 __device__ __forceinline__ double red0(double b, const Star& s, double omega) {
-  const double t = (b - 0.0) / s.cc;
+  const double t = (b - 0.0) * (1.0 / s.cc);
   return (1.0 - omega) * 0.0 + omega * t;
 }
 
@@ -141,7 +141,7 @@ __device__ __forceinline__ void mg_smooth_body(MgGeo G, double* x, const double*
       nb = nb + s.cx * red0(bxp, s, omega);
       nb = nb + s.cy * red0(n4.yp, s, omega);
       nb = nb + s.cz * red0(n4.zp, s, omega);
-      const double t = (bb - nb) / s.cc;
+      const double t = (bb - nb) * (1.0 / s.cc);
       const double xb = (1.0 - omega) * 0.0 + omega * t;
       const double xr = red0(br, s, omega);
       dv2 o;
@@ -164,7 +164,7 @@ __device__ __forceinline__ void mg_smooth_body(MgGeo G, double* x, const double*
     nb = nb + s.cy * n4.yp;
     nb = nb + s.cz * n4.zp;
     const double xo = d ? xp.y : xp.x;
-    const double t = (b[id] - nb) / s.cc;
+    const double t = (b[id] - nb) * (1.0 / s.cc);
     const double xn = (1.0 - omega) * xo + omega * t;
     dv2 o = xp;
     if (d) o.y = xn;
@@ -566,8 +566,10 @@ __global__ __launch_bounds__(512) void mg_tail_kernel(TailArgs A, const int* ski
 // chunks of coarse planes for the z-marching transfer kernels: ~16 resident waves per CU, at
 // least 4 coarse planes per chunk
 static int transfer_chunk(pb_ctx* ctx, int64_t cols, int64_t nzl, int64_t* nchunk_out) {
-  int64_t nchunk = ((int64_t)ctx->num_cus * 1024 + cols - 1) / cols;
-  nchunk = std::max<int64_t>(1, std::min<int64_t>(nchunk, nzl / 4));
+  const int64_t tpc = env_int("PB_MG_TRANSFER_TPC", 1024);  // threads per CU
+  const int64_t minz = env_int("PB_MG_TRANSFER_MINZ", 4);   // coarse planes per chunk, at least
+  int64_t nchunk = ((int64_t)ctx->num_cus * tpc + cols - 1) / cols;
+  nchunk = std::max<int64_t>(1, std::min<int64_t>(nchunk, nzl / minz));
   const int kc = (int)((nzl + nchunk - 1) / nchunk);
   *nchunk_out = (nzl + kc - 1) / kc;
   return kc;
@@ -775,6 +777,15 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     // large level: zero-start red + black half-sweeps and the residual in one pass
     const bool fused = F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g) &&
                        env_int("PB_MG_PRESMOOTH_FUSED", 1);
+    // one rank: the restriction too (the residual is never stored)
+    const bool fused_r = fused && !ctx->split && F.g->nzl % 2 == 0 &&
+                         env_int("PB_MG_PRESMOOTH_RESTRICT", 1);
+    if (fused_r) {
+      ScopedTimer t1(ctx, l == 0 ? "mg_fine_smooth_first" : "mg_coarse_levels");
+      PB_TRY(launch_presmooth_restrict(F.g, F.s, Cl.g, F.b, post_fused(mg, l) ? F.xs : F.x, Cl.b,
+                                       mg->omega, mg->skip));
+      continue;
+    }
     {
       ScopedTimer t1(ctx, l == 0 ? "mg_fine_smooth_first" : "mg_coarse_levels");
       if (fused)

@@ -29,6 +29,14 @@ static constexpr int kSegOut = 112;     // outputs per wave segment (lanes 4..59
                                         // 128-B lines, so no line is written by two waves
 static constexpr int kSegLead = 4;      // halo pairs left of the outputs (>= 1 needed)
 
+// v[1] if e1 else v[0], as bit operations: a `?:` between two elements of a register array can
+// become a computed address, which moves the whole array to scratch
+__device__ __forceinline__ double pick(bool e1, const double (&v)[2]) {
+  const long long m = -(long long)e1;
+  return __builtin_bit_cast(double, (__builtin_bit_cast(long long, v[1]) & m) |
+                                        (__builtin_bit_cast(long long, v[0]) & ~m));
+}
+
 struct Sweep2Geo {
   int nx, ny, nzl;
   int64_t plane;
@@ -56,6 +64,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
                                                                const CgState* st, double* parts,
                                                                const int* skip) {
   if (skip && *skip) return;
+  const double icc = 1.0 / cc;  // SOR: multiply by the inverted diagonal
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const double mu = SUMS ? st->mu : 0.0;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -139,7 +148,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
         for (int r = 0; r < kRW; ++r) {
           // one red point per pair, at a wave-uniform element: one division per pair
           const bool red1 = ((par_row[r] + kp) & 1) != 0;  // the red point is element 1
-          const double t = ((red1 ? v[r][1] : v[r][0]) - 0.0) / cc;
+          const double t = ((red1 ? v[r][1] : v[r][0]) - 0.0) * icc;
           const double red = (1.0 - omega) * 0.0 + omega * t;
           v[r][0] = red1 ? 0.0 : red;
           v[r][1] = red1 ? red : 0.0;
@@ -174,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
         nb = nb + cx * xr;
         nb = nb + cy * yp;
         nb = nb + cz * zp;
-        const double t = (bv - nb) / cc;
+        const double t = (bv - nb) * icc;
         const double v = (1.0 - omega) * xo + omega * t;
         out[r][0] = a1 ? xc[r][0] : v;
         out[r][1] = a1 ? v : xc[r][1];
@@ -259,7 +268,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
         nb = nb + cx * xr;
         nb = nb + cy * yp;
         nb = nb + cz * zp;
-        const double t = (bv - nb) / cc;
+        const double t = (bv - nb) * icc;
         const double v = (1.0 - omega) * xo + omega * t;
         double ov[2];
         ov[0] = a1 ? s1[1][r][0] : v;
@@ -313,6 +322,7 @@ __global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
     const double* __restrict__ b, double* __restrict__ xout, double* __restrict__ res,
     const int* skip) {
   if (skip && *skip) return;
+  const double icc = 1.0 / cc;  // SOR: multiply by the inverted diagonal
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int bid = xcd_block(g.remap);
   const int seg = bid % g.nseg;
@@ -369,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
       const double bv = __builtin_bit_cast(
           double, (__builtin_bit_cast(long long, v[r][1]) & m) |
                       (__builtin_bit_cast(long long, v[r][0]) & ~m));  // (see half1)
-      const double t = (bv - 0.0) / cc;
+      const double t = (bv - 0.0) * icc;
       red[r] = (1.0 - omega) * 0.0 + omega * t;
     }
   };
@@ -404,7 +414,7 @@ __global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
       const double bv = __builtin_bit_cast(
           double, (__builtin_bit_cast(long long, bb[r][1]) & m) |
                       (__builtin_bit_cast(long long, bb[r][0]) & ~m));
-      const double t = (bv - nb) / cc;
+      const double t = (bv - nb) * icc;
       const double v = (1.0 - omega) * 0.0 + omega * t;
       out[r][0] = a1 ? rc[r] : v;
       out[r][1] = a1 ? v : rc[r];
@@ -490,6 +500,193 @@ __global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
+// Pre-smoothing from x = 0, residual AND restriction in one pass (one rank): the residual is
+// never stored -- each wave owns the two fine rows 2J, 2J+1 of one coarse row J and forms the
+// residual on the four rows 2J-1 .. 2J+2 that the restriction reads (so S1 on six rows, red values
+// on eight), then the restriction's x and y sums per fine plane and its z sum over the four planes
+// 2K-1 .. 2K+2 as the planes pass. Per fine point: read b, write x (+ 1/8 of a coarse b) --
+// 17 B/DoF instead of the pre-smoothing pass's 24 plus the restriction's 9. Arithmetic: the slim
+// pre-smoothing kernel's (red, black, residual) and mg_restrict_z_kernel's (restrict_xy, then the
+// z sum in the same order), so results are bit-identical.
+// ---------------------------------------------------------------------------------------------
+static constexpr int kTYR = 2;         // own fine rows per wave (one coarse row)
+static constexpr int kRR = kTYR + 6;   // b rows held: j0-3 .. j0+4 (red values on all of them)
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void
+presmooth_restrict_kernel(Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz,
+                          double cc, double omega, const double* __restrict__ b,
+                          double* __restrict__ xout, double* __restrict__ bc, const int* skip) {
+  if (skip && *skip) return;
+  const double icc = 1.0 / cc;  // SOR: multiply by the inverted diagonal
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bid = xcd_block(g.remap);
+  const int seg = bid % g.nseg;
+  bid /= g.nseg;
+  const int tile = bid % g.ntile;
+  const int chunk = bid / g.ntile;
+  const int j0 = (tile * kWaves + wid) * kTYR;  // even: fine rows 2J, 2J+1
+  const int kb = chunk * g.kc;                  // even (kc even)
+  const int ke = min(kb + g.kc, g.nzl);
+  const int nx = g.nx, ny = g.ny, nz = g.nzl;
+  int ip = seg * kSegOut + 2 * (lane - kSegLead);
+  if (ip < 0) ip += nx;
+  if (ip >= nx) ip -= nx;
+  const int o = seg * kSegOut + 2 * (lane - kSegLead);
+  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
+  if (!(j0 < ny && kb < nz)) return;
+  int64_t ro[kRR];
+  int par_row[kRR];
+#pragma unroll
+  for (int r = 0; r < kRR; ++r) {
+    int j = j0 - 3 + r;
+    if (j < 0) j += ny;
+    if (j >= ny) j -= ny;
+    ro[r] = (int64_t)j * nx;
+    par_row[r] = (ip + j) & 1;
+  }
+  const unsigned boff = (unsigned)ip * 8u;
+  auto rix = [&](int64_t row) { return RowIx{row, boff}; };
+  auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+  auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
+  auto ldraw = [&](double (&dst)[kRR][2], int kk) {
+    const int64_t base = (int64_t)wrapk(kk) * g.plane;
+#pragma unroll
+    for (int r = 0; r < kRR; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
+  };
+  // raw b rows -> the red value of each pair (presmooth_resid_kernel's redv)
+  auto redv = [&](const double (&v)[kRR][2], int kk, double (&red)[kRR]) {
+    const int kp = kpar(kk);
+#pragma unroll
+    for (int r = 0; r < kRR; ++r) {
+      const double bv = pick(((par_row[r] + kp) & 1) != 0, v[r]);  // red point is element 1
+      const double t = (bv - 0.0) * icc;
+      red[r] = (1.0 - omega) * 0.0 + omega * t;
+    }
+  };
+  // black half-sweep at plane kk, rows 1 .. kRR-2 (presmooth_resid_kernel's half1)
+  auto black = [&](const double (&rm)[kRR], const double (&rc)[kRR], const double (&rp)[kRR],
+                   const double (&bb)[kRR][2], int kk, double (&out)[kRR][2]) {
+    const int kp = kpar(kk);
+#pragma unroll
+    for (int r = 1; r < kRR - 1; ++r) {
+      const bool a1 = ((par_row[r] + kp) & 1) != 1;  // the black point is element 1
+      const double lo = dpp_from_lower(rc[r]);
+      const double hi = dpp_from_upper(rc[r]);
+      const double xl = a1 ? rc[r] : lo;
+      const double xr = a1 ? hi : rc[r];
+      double nb = cz * rm[r];
+      nb = nb + cy * rc[r - 1];
+      nb = nb + cx * xl;
+      nb = nb + cx * xr;
+      nb = nb + cy * rc[r + 1];
+      nb = nb + cz * rp[r];
+      const double t = (pick(a1, bb[r]) - nb) * icc;
+      const double v = (1.0 - omega) * 0.0 + omega * t;
+      out[r][0] = a1 ? rc[r] : v;
+      out[r][1] = a1 ? v : rc[r];
+    }
+  };
+  const int J = j0 >> 1;
+  const int I = o >> 1;
+  // queues at iteration k: red values of planes k, k+1; S1 of planes k-1 (rows 2..5) and k
+  // (rows 1..6); b of planes k (rows 2..5) and k+1 (rows 1..6); the z sums of coarse planes K
+  // (A) and K-1 (B) for the fine plane k in 2K-1 .. 2K
+  double rq0[kRR], rq1[kRR], rq2[kRR];  // red values, planes k, k+1, k+2
+  double s1m[kRR][2], s1c[kRR][2];
+  double bq0[kRR][2], bq1[kRR][2], bq2[kRR][2];  // b, planes k, k+1, k+2
+  double accA = 0.0, accB = 0.0;
+  {
+    double raw[kRR][2];
+    ldraw(raw, kb - 3);
+    redv(raw, kb - 3, rq0);
+    ldraw(bq1, kb - 2);
+    redv(bq1, kb - 2, rq1);
+    ldraw(bq2, kb - 1);
+    redv(bq2, kb - 1, rq2);
+  }
+#pragma unroll
+  for (int r = 0; r < kRR; ++r)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) s1m[r][e] = s1c[r][e] = bq0[r][e] = 0.0;
+  // planes kb-3, kb-2: S1 warm-up; kb-1 and ke: residual for the restriction only
+#pragma unroll 1
+  for (int k = kb - 3; k <= ke; ++k) {
+    double raw[kRR][2], s1p[kRR][2];
+    ldraw(raw, k + 3);  // in flight during this plane's sweeps (consumed at the rotation)
+    black(rq0, rq1, rq2, bq1, k + 1, s1p);  // S1 at plane k+1
+    if (k >= kb - 1) {
+      // x = S1 on the own rows; res = b - A S1 on rows 2..5 (z-, y-, x-, c, x+, y+, z+)
+      double rv[kRR][2];
+#pragma unroll
+      for (int r = 2; r < kRR - 2; ++r) {
+        const double lo = dpp_from_lower(s1c[r][1]);
+        const double hi = dpp_from_upper(s1c[r][0]);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double xl = e == 0 ? lo : s1c[r][0];
+          const double xr = e == 1 ? hi : s1c[r][1];
+          double a = cz * s1m[r][e];
+          a = a + cy * s1c[r - 1][e];
+          a = a + cx * xl;
+          a = a + cc * s1c[r][e];
+          a = a + cx * xr;
+          a = a + cy * s1c[r + 1][e];
+          a = a + cz * s1p[r][e];
+          rv[r][e] = bq0[r][e] - a;
+        }
+      }
+      if (k >= kb && k < ke && out_ok) {
+        const int64_t base = (int64_t)k * g.plane;
+#pragma unroll
+        for (int r = 3; r < 3 + kTYR; ++r) store_row<2>(xout, rix(base + ro[r]), s1c[r], g.nt);
+      }
+      // restriction: x then y sums of fine rows 2J-1 .. 2J+2 (restrict_xy's order)
+      const double w[4] = {0.125, 0.375, 0.375, 0.125};
+      double sy = 0.0;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const int r = 2 + bb;
+        const double lo = dpp_from_lower(rv[r][1]);
+        const double hi = dpp_from_upper(rv[r][0]);
+        double sx = w[0] * lo;
+        sx = sx + w[1] * rv[r][0];
+        sx = sx + w[2] * rv[r][1];
+        sx = sx + w[3] * hi;
+        sy = sy + w[bb] * sx;
+      }
+      if (k & 1) {  // k = 2K-1: third term of K-1, first of K
+        accB = accB + 0.375 * sy;
+        accA = 0.0;
+        accA = accA + 0.125 * sy;
+      } else {      // k = 2K: last term of K-1 (complete), second of K
+        accB = accB + 0.125 * sy;
+        if (k >= kb + 2 && out_ok)
+          bc[(int64_t)((k >> 1) - 1) * cplane + (int64_t)J * ncx + I] = accB;
+        accA = accA + 0.375 * sy;
+        accB = accA;
+      }
+    }
+    // rotate: red (k+1, k+2, k+3), S1 (k, k+1), b (k+1, k+2, k+3)
+    double rn[kRR];
+    redv(raw, k + 3, rn);
+#pragma unroll
+    for (int r = 0; r < kRR; ++r) {
+      rq0[r] = rq1[r];
+      rq1[r] = rq2[r];
+      rq2[r] = rn[r];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        s1m[r][e] = s1c[r][e];
+        s1c[r][e] = s1p[r][e];
+        bq0[r][e] = bq1[r][e];
+        bq1[r][e] = bq2[r][e];
+        bq2[r][e] = raw[r][e];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Post-smoothing with the prolongation folded in (one rank): the sweep's input
 // xin = x_s + P x_c is formed as the planes arrive -- x_s (the pre-smoothed iterate) and the
 // coarse correction x_c are read, the prolongated input is never stored. Then both half-sweeps
@@ -506,20 +703,13 @@ struct PostGeo {
   int64_t cplane;
 };
 
-// v[1] if e1 else v[0], as bit operations: a `?:` between two elements of a register array can
-// become a computed address, which moves the whole array to scratch
-__device__ __forceinline__ double pick(bool e1, const double (&v)[2]) {
-  const long long m = -(long long)e1;
-  return __builtin_bit_cast(double, (__builtin_bit_cast(long long, v[1]) & m) |
-                                        (__builtin_bit_cast(long long, v[0]) & ~m));
-}
-
 template <bool SUMS>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void post_sweep_kernel(
     Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
     const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
     double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
   if (skip && *skip) return;
+  const double icc = 1.0 / cc;  // SOR: multiply by the inverted diagonal
   constexpr int c1 = 1;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const double mu = SUMS ? st->mu : 0.0;
@@ -644,7 +834,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         nb = nb + cx * xr;
         nb = nb + cy * yp;
         nb = nb + cz * zp;
-        const double t = (bv - nb) / cc;
+        const double t = (bv - nb) * icc;
         out[r] = (1.0 - omega) * xo + omega * t;
       }
     };
@@ -678,7 +868,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         nb = nb + cx * xr;
         nb = nb + cy * sc[r + 1];
         nb = nb + cz * sp[r];
-        const double t = (bo[r] - nb) / cc;
+        const double t = (bo[r] - nb) * icc;
         const double v = (1.0 - omega) * xo[r] + omega * t;
         double ov[2];
         ov[0] = a1 ? cself : v;
@@ -857,6 +1047,37 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
                        g->ctx->stream, geo, cgeo, s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout,
                        (const CgState*)nullptr, (double*)nullptr, skip);
   }
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
+int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, const double* b,
+                              double* xout, double* bc, double omega, const int* skip) {
+  ScopedTimer tm(g->ctx, "mg_presmooth_restrict");
+  if (g->ctx->split) return set_error(PB_ERR_UNSUPPORTED, "fused restriction: one rank only");
+  if (b == xout) return set_error(PB_ERR_ARG, "fused pre-smoothing must run out of place");
+  if (!sor_sweep2_supported(g) || g->nzl % 2)
+    return set_error(PB_ERR_UNSUPPORTED, "fused restriction: grid not supported");
+  if (cg->n[0] * 2 != g->n[0] || cg->n[1] * 2 != g->n[1] || cg->nzl * 2 != g->nzl)
+    return set_error(PB_ERR_ARG, "fused restriction: coarse grid is not half the fine one");
+  Sweep2Geo geo;
+  sweep2_geo(g, geo);
+  geo.split = 0;
+  geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
+  geo.ntile = (geo.ny + kWaves * kTYR - 1) / (kWaves * kTYR);
+  // chunks of an even number of planes (the restriction pairs them); each chunk also forms S1 on
+  // three planes and the residual on two planes outside it, so chunks stay long
+  const int columns = geo.nseg * geo.ntile;
+  const int target = env_int("PB_PRR_WGCU", 4) * g->ctx->num_cus;
+  int nchunk = std::max(1, (target + columns - 1) / columns);
+  nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_PRR_MINZ", 32)));
+  geo.kc = (geo.nzl + nchunk - 1) / nchunk;
+  geo.kc += geo.kc & 1;
+  geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
+  const int64_t nblocks = (int64_t)columns * geo.nchunk;
+  hipLaunchKernelGGL(presmooth_restrict_kernel, dim3((unsigned)nblocks), dim3(kThreads), 0,
+                     g->ctx->stream, geo, (int)cg->n[0], cg->plane, s.cx, s.cy, s.cz, s.cc, omega,
+                     b, xout, bc, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }

@@ -628,16 +628,16 @@ int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
 // the half-sweep does not modify, so halo rows read from other waves are the same whether or not
 // those waves have stored their plane yet (the stored other-colour values are bit-identical).
 // ---------------------------------------------------------------------------------------------
-// the red values of the first half-sweep from x = 0: (1 - w) * 0 + w * ((b - 0) / c)
+// the red values of the first half-sweep from x = 0: (1 - w) * 0 + w * ((b - 0) * (1 / c))
 struct Red0Load {
   static constexpr int NR = 1;
   static constexpr bool GHOST_RAW = true;  // ghost planes are b's: transform them too
   const double* __restrict__ b;
-  double cc, omega;
+  double icc, omega;  // icc = 1 / c (the SOR update multiplies by the inverted diagonal)
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ const double* src(int) const { return b; }
   __device__ __forceinline__ double value(const double* raw) const {
-    const double t = (raw[0] - 0.0) / cc;
+    const double t = (raw[0] - 0.0) * icc;
     return (1.0 - omega) * 0.0 + omega * t;
   }
 };
@@ -651,7 +651,7 @@ struct SorHalfT {
   static constexpr int WGCU = 1;  // (the zero-start sweep overrides: 3)
   double* x;
   const double* __restrict__ b;
-  double cx, cy, cz, cc, omega;
+  double cx, cy, cz, icc, omega;  // icc = 1 / c
   int color;  // points with (i + j + k_global) % 2 == color are updated
   int first;  // 1: black half-sweep after the zero-start red one (x_old = 0, field = Red0Load)
   const CgState* st;
@@ -673,7 +673,7 @@ struct SorHalfT {
       nb = nb + cx * xp[e];
       nb = nb + cy * yp[e];
       nb = nb + cz * zp[e];
-      const double t = (op[0][e] - nb) / cc;
+      const double t = (op[0][e] - nb) * icc;
       const double xo = first ? 0.0 : c[e];
       const double xn = (1.0 - omega) * xo + omega * t;
       o[e] = ((par + e) & 1) == color ? xn : c[e];
@@ -717,12 +717,12 @@ int launch_mg_sor(pb_grid* g, const Star& s, double* x, const double* b, const S
                   int* nparts) {
   ScopedTimer tm(g->ctx, "mg_sor");
   if (sums_st) {  // partial sums -> ctx->d_partials[0 .. nparts*4)
-    SorHalfT<true> ep{x, b, s.cx, s.cy, s.cz, s.cc, omega, color, 0, sums_st, 0.0};
+    SorHalfT<true> ep{x, b, s.cx, s.cy, s.cz, 1.0 / s.cc, omega, color, 0, sums_st, 0.0};
     return launch_any(g, s, PlainLoad{x}, gp, ep, skip, PLANES_ALL, 0, nparts);
   }
-  SorHalf ep{x, b, s.cx, s.cy, s.cz, s.cc, omega, first ? 1 : color, first, nullptr, 0.0};
+  SorHalf ep{x, b, s.cx, s.cy, s.cz, 1.0 / s.cc, omega, first ? 1 : color, first, nullptr, 0.0};
   if (first)  // measured: the zero-start sweep prefers 3 workgroups per CU, the others 1
-    return launch_any(g, s, Red0Load{b, s.cc, omega}, gp, ep, skip, PLANES_ALL, 0, nullptr, 0, 3);
+    return launch_any(g, s, Red0Load{b, 1.0 / s.cc, omega}, gp, ep, skip, PLANES_ALL, 0, nullptr, 0, 3);
   return launch_any(g, s, PlainLoad{x}, gp, ep, skip);
 }
 

@@ -679,7 +679,12 @@ MG_KERNELS = {"default": {},
               "bigtail": {"PB_MG_TAIL_MAX": "40000"},
               # prolongation and post-smoothing as two launches (the pre-r02 up-leg)
               "nopost": {"PB_MG_POST_FUSED": "0", "PB_MG_ENGINE_MIN_PLANE": "0",
-                         "PB_MG_RESTRICT_Z_MIN_COLS": "0"}}
+                         "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
+              # residual stored and restricted by its own pass (the pre-r02 down-leg)
+              "norestrict": {"PB_MG_PRESMOOTH_RESTRICT": "0", "PB_MG_ENGINE_MIN_PLANE": "0"},
+              # short chunks: more z-chunk seams in the fused restriction
+              "prrchunks": {"PB_PRR_WGCU": "64", "PB_PRR_MINZ": "2",
+                            "PB_MG_ENGINE_MIN_PLANE": "0"}}
 
 
 @pytest.mark.parametrize("kern", sorted(MG_KERNELS))
@@ -727,7 +732,8 @@ def test_cg_sor_mg_matches_oracle(ctx, monkeypatch, kern, pc, n):
         assert its <= 16  # h-independent V-cycle preconditioning
 
 
-@pytest.mark.parametrize("kern", ["default", "engine", "legacy", "unfused", "nopost"])
+@pytest.mark.parametrize("kern", ["default", "engine", "legacy", "unfused", "nopost",
+                                  "norestrict"])
 def test_cg_mg_fused_post_smoothing(ctx, monkeypatch, kern):
     """x extent >= 128: the V-cycle's post-smoothing runs as ONE fused two-colour pass (out of
     place, with CG's residual sums on level 0); history / solution within the CG bar, PC apply
