@@ -98,18 +98,19 @@ __device__ __forceinline__ void store_row(double* p, RowIx ix, const double (&v)
 }
 
 // ---------------------------------------------------------------------------------------------
-// Cross-lane helpers (DPP wave shifts: VALU only, no LDS traffic)
+// Cross-lane helpers (DPP wave shifts: VALU only, no LDS traffic; bound_ctrl: the end lane
+// with no source reads 0, no old-value operand to initialise)
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ double dpp_from_lower(double v) {  // lane l <- lane l-1 (wave_shr:1)
   const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x138, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x138, 0xf, 0xf, true);
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double dpp_from_upper(double v) {  // lane l <- lane l+1 (wave_shl:1)
   const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x130, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x130, 0xf, 0xf, true);
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double readlane_d(double v, int l) {

@@ -66,7 +66,7 @@ __host__ __device__ constexpr int bitrev(int v, int bits) {
 // __shfl_xor = ds_bpermute, twice per double).
 template <int CTRL>
 __device__ __forceinline__ int dpp32(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true);  // bound_ctrl: no old operand
 }
 template <int H>
 __device__ __forceinline__ int xor_lane32(int v, int lane) {

@@ -774,29 +774,33 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) v
         cv[1][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cf + crow[t]) + cboff);
       }
     };
-    // x_s + P x_c (mg_prolong_z_kernel's operation order); P0 = j0 parity (wave-uniform)
+    // x_s + P x_c (mg_prolong_z_kernel's operation order); P0 = j0 parity (wave-uniform). The
+    // x-interpolated coarse values are formed once per coarse row and plane (each serves two or
+    // three fine rows): the same operations on the same operands, so the same results
     auto prolong_p = [&](auto P0c, double (&v)[kRW][2], const double (&cv)[2][6]) {
       constexpr int P0 = decltype(P0c)::value;
+      // element 0: far column I-1; element 1: I+1
+      double xi[2][6][2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+          const double c = cv[q][t];
+          xi[q][t][0] = 0.75 * c + 0.25 * dpp_from_lower(c);
+          xi[q][t][1] = 0.75 * c + 0.25 * dpp_from_upper(c);
+        }
 #pragma unroll
       for (int r = 0; r < kRW; ++r) {
         // fine row j0-2+r: coarse row J at index tJ, far row (J-1 even / J+1 odd) at tf
-        constexpr int dummy = 0;
-        (void)dummy;
         const int odd = (P0 + r) & 1;
         const int tJ = 1 + ((P0 + r) >> 1);
         const int tf = odd ? tJ + 1 : tJ - 1;
-        const double cnn = cv[0][tJ], cnf = cv[0][tf], cfn = cv[1][tJ], cff = cv[1][tf];
-        const double lnn = dpp_from_lower(cnn), lnf = dpp_from_lower(cnf);
-        const double lfn = dpp_from_lower(cfn), lff = dpp_from_lower(cff);
-        const double unn = dpp_from_upper(cnn), unf = dpp_from_upper(cnf);
-        const double ufn = dpp_from_upper(cfn), uff = dpp_from_upper(cff);
-        // element 0: far column I-1; element 1: I+1
-        const double vn0 = 0.75 * (0.75 * cnn + 0.25 * lnn) + 0.25 * (0.75 * cnf + 0.25 * lnf);
-        const double vf0 = 0.75 * (0.75 * cfn + 0.25 * lfn) + 0.25 * (0.75 * cff + 0.25 * lff);
-        const double vn1 = 0.75 * (0.75 * cnn + 0.25 * unn) + 0.25 * (0.75 * cnf + 0.25 * unf);
-        const double vf1 = 0.75 * (0.75 * cfn + 0.25 * ufn) + 0.25 * (0.75 * cff + 0.25 * uff);
-        v[r][0] = v[r][0] + (0.75 * vn0 + 0.25 * vf0);
-        v[r][1] = v[r][1] + (0.75 * vn1 + 0.25 * vf1);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double vn = 0.75 * xi[0][tJ][e] + 0.25 * xi[0][tf][e];
+          const double vf = 0.75 * xi[1][tJ][e] + 0.25 * xi[1][tf][e];
+          v[r][e] = v[r][e] + (0.75 * vn + 0.25 * vf);
+        }
       }
     };
     auto prolong = [&](double (&v)[kRW][2], const double (&cv)[2][6]) {
