@@ -22,21 +22,35 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X spec (MI355X_MICROARCH.md "Chip-level parameters")
-PASS_A_BYTES = 24            # pass A: read r, p_old; write p_new
-PASS_B_EVEN_BYTES = 24       # pass B without x update: read p (stencil), r; write r (x deferred)
-# the x update every D-th iteration (PB_CG_DEFER_X = D, default 4): pass B reads p_i (stencil),
-# r, x and p_{i-1} .. p_{i-D+1}, writes r and x
-PASS_B_X_BYTES = {0: 40, 2: 48, 4: 64}
 PASS_B_X_NAME = {0: "cg_pass_b", 2: "cg_pass_b_odd", 4: "cg_pass_b_x4"}
-
-
-def cg_iter_bytes(defer):
-    """Algorithmic bytes per DoF of one CG iteration, averaged over a deferral cycle
-    (58 at D = 4; SURVEY §8d's fused 2-pass lower bound without deferral is 80)."""
-    if defer == 0:
-        return PASS_A_BYTES + PASS_B_X_BYTES[0]
-    return PASS_A_BYTES + ((defer - 1) * PASS_B_EVEN_BYTES + PASS_B_X_BYTES[defer]) / defer
+# Algorithmic bytes per DoF of each CG pass, by where p is stored (PB_CG_PSTORE_B, library
+# default 1, pb_solver.cpp):
+#  pstore 0: pass A reads r, p_old, writes p (24); pass B reads p (stencil), r, writes r (24);
+#            the x update every D-th iteration (PB_CG_DEFER_X = D, default 4) adds x read/write
+#            and p_{i-1} .. p_{i-D+1}
+#  pstore 1: pass A reads r, p_old (16, p.Ap only); pass B re-forms p from r, p_old, writes p and
+#            r into the other residual buffer (32); the x update adds x read/write and
+#            p_{i-2} .. p_{i-D+1} (p_{i-1} = p_old is already in the z-queue)
+PASS_BYTES = {
+    0: {"a": 24, "b_even": 24, "b_x": {0: 40, 2: 48, 4: 64}},
+    1: {"a": 16, "b_even": 32, "b_x": {0: 48, 2: 48, 4: 64}},
+}
 MATVEC_BYTES = 16            # y = A x: read x, write y
+
+
+def pstore_mode():
+    """The library's p-store placement (PB_CG_PSTORE_B, default 1)."""
+    return 0 if os.environ.get("PB_CG_PSTORE_B", "1") == "0" else 1
+
+
+def cg_iter_bytes(defer, pstore=1):
+    """Algorithmic bytes per DoF of one CG iteration, averaged over a deferral cycle (56 at D = 4
+    with p stored by pass B, 58 with p stored by pass A; SURVEY §8d's fused 2-pass lower bound
+    without deferral is 80)."""
+    pb_ = PASS_BYTES[pstore]
+    if defer == 0:
+        return pb_["a"] + pb_["b_x"][0]
+    return pb_["a"] + ((defer - 1) * pb_["b_even"] + pb_["b_x"][defer]) / defer
 SEED = 20231015
 
 
@@ -261,8 +275,12 @@ def main():
     if dist:
         dist.barrier()
     # timed region: HIP events around the roofline kernel only, on every 4th launch (events
-    # around every launch add ~2 % of gaps to the measured step; around every pass A ~0.7 %)
-    os.environ["PB_TIMING_ONLY"] = "cg_pass_a"
+    # around every launch add ~2 % of gaps to the measured step; around every pass A ~0.7 %).
+    # The roofline kernel is the one with the largest share of the step: pass A when it stores p
+    # (PB_CG_PSTORE_B=0), otherwise pass B without the x update (3 of 4 iterations at D = 4)
+    pstore = pstore_mode()
+    roof = "cg_pass_b_even" if (pstore and defer == 4) else "cg_pass_a"
+    os.environ["PB_TIMING_ONLY"] = roof
     os.environ["PB_TIMING_EVERY"] = "4"
     ctx.set_timing(True)
     ctx.reset_timing()
@@ -274,7 +292,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = t1 - t0
-    ms_a, cnt_a = ctx.timing("cg_pass_a")
+    ms_roof, cnt_roof = ctx.timing(roof)
     ctx.set_timing(False)
     os.environ.pop("PB_TIMING_ONLY", None)
     os.environ.pop("PB_TIMING_EVERY", None)
@@ -289,6 +307,7 @@ def main():
             defer = d_
             ms_b, cnt_b = ctx.timing(nm)
     ms_be, cnt_be = ctx.timing("cg_pass_b_even")
+    ms_a, cnt_a = ctx.timing("cg_pass_a")
     # per-rank communication in the diagnostic iterations: the halo exchange on the comm stream
     # (overlapped with pass A's interior planes), the two scalar allreduces per iteration, and
     # pass A including its wait for the halo
@@ -326,6 +345,13 @@ def main():
     t_b = ms_b / max(cnt_b, 1) / 1e3
     t_be = ms_be / max(cnt_be, 1) / 1e3
     t_a = ms_a / max(cnt_a, 1) / 1e3
+    t_roof = ms_roof / max(cnt_roof, 1) / 1e3  # inside the timed region
+    if roof == "cg_pass_a":
+        t_a = t_roof
+    else:
+        t_be = t_roof
+    PB = PASS_BYTES[pstore]
+    roof_bytes = PB["a"] if roof == "cg_pass_a" else PB["b_even"]
     t_mv = ms_mv / max(cnt_mv, 1) / 1e3
     gbs = lambda bytes_per_dof, t: bytes_per_dof * nloc / t / 1e9 if t > 0 else 0.0
 
@@ -351,25 +377,30 @@ def main():
                            if world > 1 else ""),
                        "ksp": "-ksp_type cg -pc_type jacobi, constant null space, rtol=0 (fixed iterations)"},
             "iter_per_s": args.steps / elapsed,
-            "achieved_GBps_cg": cg_iter_bytes(defer) * N / (elapsed / args.steps) / 1e9,
-            # the dominant kernel: pass A runs every iteration and takes the largest share of
-            # the step (44 % at D = 4); it is timed with HIP events inside the timed region
+            "achieved_GBps_cg": cg_iter_bytes(defer, pstore) * N / (elapsed / args.steps) / 1e9,
+            "cg_bytes_per_dof": cg_iter_bytes(defer, pstore),
+            "cg_pstore_b": pstore,
+            # the dominant kernel (largest share of the step), timed with HIP events inside the
+            # timed region
             "roofline": {"bound": "hbm",
-                         "kernel": "cg_pass_a (p = z + beta p fused into the 7-point stencil of p, "
-                                   "store p, p.Ap sums)",
-                         "achieved": gbs(PASS_A_BYTES, t_a), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs(PASS_A_BYTES, t_a) / HBM_PEAK_GBS,
-                         "traffic": None, "bytes_per_dof": PASS_A_BYTES,
-                         "avg_launch_ms": t_a * 1e3},
+                         "kernel": ("cg_pass_b_even (p = z + beta p_old re-formed on load, 7-point "
+                                    "stencil of p, r -= alpha A p, store p and r, residual sums)"
+                                    if roof == "cg_pass_b_even" else
+                                    "cg_pass_a (p = z + beta p_old fused into the 7-point stencil "
+                                    "of p, p.Ap sums" + (", store p)" if not pstore else ")")),
+                         "achieved": gbs(roof_bytes, t_roof), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs(roof_bytes, t_roof) / HBM_PEAK_GBS,
+                         "traffic": None, "bytes_per_dof": roof_bytes,
+                         "avg_launch_ms": t_roof * 1e3},
             "kernels": {
-                "cg_pass_a": {"avg_ms": t_a * 1e3, "GBps": gbs(PASS_A_BYTES, t_a),
-                              "frac": gbs(PASS_A_BYTES, t_a) / HBM_PEAK_GBS, "bytes_per_dof": PASS_A_BYTES},
-                "cg_pass_b_even": {"avg_ms": t_be * 1e3, "GBps": gbs(PASS_B_EVEN_BYTES, t_be),
-                                   "frac": gbs(PASS_B_EVEN_BYTES, t_be) / HBM_PEAK_GBS,
-                                   "bytes_per_dof": PASS_B_EVEN_BYTES},
-                PASS_B_X_NAME[defer]: {"avg_ms": t_b * 1e3, "GBps": gbs(PASS_B_X_BYTES[defer], t_b),
-                                       "frac": gbs(PASS_B_X_BYTES[defer], t_b) / HBM_PEAK_GBS,
-                                       "bytes_per_dof": PASS_B_X_BYTES[defer]},
+                "cg_pass_a": {"avg_ms": t_a * 1e3, "GBps": gbs(PB["a"], t_a),
+                              "frac": gbs(PB["a"], t_a) / HBM_PEAK_GBS, "bytes_per_dof": PB["a"]},
+                "cg_pass_b_even": {"avg_ms": t_be * 1e3, "GBps": gbs(PB["b_even"], t_be),
+                                   "frac": gbs(PB["b_even"], t_be) / HBM_PEAK_GBS,
+                                   "bytes_per_dof": PB["b_even"]},
+                PASS_B_X_NAME[defer]: {"avg_ms": t_b * 1e3, "GBps": gbs(PB["b_x"][defer], t_b),
+                                       "frac": gbs(PB["b_x"][defer], t_b) / HBM_PEAK_GBS,
+                                       "bytes_per_dof": PB["b_x"][defer]},
                 "matvec_star7": {"avg_ms": t_mv * 1e3, "GBps": gbs(MATVEC_BYTES, t_mv),
                                  "frac": gbs(MATVEC_BYTES, t_mv) / HBM_PEAK_GBS,
                                  "dofs_per_s": nloc / t_mv if t_mv > 0 else 0.0,
@@ -384,10 +415,11 @@ def main():
         if os.path.exists(traffic_file):
             try:
                 tr = json.load(open(traffic_file))
-                key = f"{n[0]}x{n[1]}x{n[2]}"
-                if key in tr and "cg_pass_a" in tr[key]:
-                    out["roofline"]["traffic"] = tr[key]["cg_pass_a"]["bytes_per_launch"]
-                    out["roofline"]["traffic_source"] = tr[key]["cg_pass_a"].get("source")
+                # PMC traffic is keyed by grid and p-store mode (the kernels differ)
+                key = f"{n[0]}x{n[1]}x{n[2]}" + ("" if not pstore else "/pstore_b")
+                if key in tr and roof in tr[key]:
+                    out["roofline"]["traffic"] = tr[key][roof]["bytes_per_launch"]
+                    out["roofline"]["traffic_source"] = tr[key][roof].get("source")
                 for role, kv in out["kernels"].items():
                     if role in tr.get(key, {}):
                         kv["traffic"] = tr[key][role]["bytes_per_launch"]

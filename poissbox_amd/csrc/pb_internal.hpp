@@ -262,18 +262,27 @@ struct CgState {
   int64_t nlog;  // history entries logged (PETSc KSPLogResidualHistory): its + 1, or its after a
                  // breakdown exit (beta = 0, indefinite PC / matrix) that skips the last norm
   int reason, done, pc, nullspace, defer_x;
+  double bbp;  // beta / betaold of the current pass A (stage 1), for pass B re-forming p
 };
 int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p, CgState* st,
                    double dinv, double* hist, int* h_done);
 int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st);
+// store = false: pass A only takes p.Ap; pass B forms and stores p (PB_CG_PSTORE_B, PStore)
 int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
                      double* p_new, const StencilPlanes& gp, CgState* st, int mode, int part_off,
-                     int* nblocks);
+                     int* nblocks, bool store = true);
+// pass B re-forming p (PB_CG_PSTORE_B): zsrc = the array pass A combined (r), r_out = the
+// residual's other buffer; r_out == nullptr: p is read as stored by pass A, r updated in place
+struct PStore {
+  const double* zsrc = nullptr;
+  double* r_out = nullptr;
+};
 int cg_finalize_pass_a(pb_ctx* ctx, int nparts, CgState* st);
 // p_prev[m] = p of iteration host_iter - 1 - m (m < 3; only the first defer-1 are read)
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
                      double* x, double* r, const StencilPlanes& gp, CgState* st, double* hist,
-                     int* h_done, int64_t host_iter, int defer, bool finalize = true);
+                     int* h_done, int64_t host_iter, int defer, bool finalize = true,
+                     const PStore& ps = PStore{});
 int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
 // Folded single-rank Jacobi iteration (finalize in the passes' prologues, pb_stencil.hip): state
 // in two slots st2[0..1]; pass A of iteration host_iter >= 1 runs stage 2 of host_iter - 1
@@ -281,11 +290,12 @@ int launch_cg_flush(pb_grid* g, double* x, const double* p, double alpha);
 // cg_fold_tail completes the last iteration of a batch and leaves the state in st2[0].
 int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const double* p_old,
                             double* p_new, const StencilPlanes& gp, CgState* st2, int nparts_b,
-                            double* hist, int* h_done, int64_t host_iter, int* nblocks);
+                            double* hist, int* h_done, int64_t host_iter, int* nblocks,
+                            bool store = true);
 int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
                             const double* const* p_prev, double* x, double* r,
                             const StencilPlanes& gp, CgState* st2, int nparts_a, int64_t host_iter,
-                            int defer, int* nparts_b);
+                            int defer, int* nparts_b, const PStore& ps = PStore{});
 int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_done,
                  int64_t host_iter);
 

@@ -28,6 +28,11 @@ struct pb_ksp {
   pb_op* P = nullptr;
   pb_ksp_opts opts;
   double* r = nullptr;
+  // PB_CG_PSTORE_B (Jacobi, fused operator): pass B forms and stores p and writes the residual to
+  // the other buffer -- iteration i reads rbuf(i), writes rbuf(i + 1)
+  double* r2 = nullptr;
+  bool pst = false;
+  double* rbuf(int64_t i) const { return (pst && (i & 1)) ? r2 : r; }
   // iteration i: p_old = pb[i % ns], p_new = pb[(i + 1) % ns]; ns = 2, or 4 with the depth-4
   // deferred x update (pb[2], pb[3] allocated on first use)
   double* pb[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -360,6 +365,15 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   k->defer_x = dx == 0 ? 0 : (dx == 2 ? 2 : 4);
   if (!fused_kind(k->A->kind)) k->defer_x = 0;  // generic path: x every iteration
   st.defer_x = k->defer_x;
+  // p stored by pass B (default): pass A read-only, 56 instead of 58 B/DoF per iteration and
+  // the passes closer to their patterns' rates -- 1.29 vs 1.36 ms/iteration at 512^3 on one box
+  // (profiles/r02/ab_pst_defer_512.jsonl); PB_CG_PSTORE_B=0 stores p in pass A
+  k->pst = env_int("PB_CG_PSTORE_B", 1) != 0 && fused_kind(k->A->kind) && !k->stored_z();
+  if (k->pst && !k->r2) {
+    const size_t vb = (size_t)g->nlocal * sizeof(double);
+    if (field_alloc(&k->r2, vb) != hipSuccess)
+      return set_error(PB_ERR_ALLOC, "CG residual buffer: out of device memory");
+  }
   if (k->defer_x == 4 && !k->pb[2]) {
     const size_t vb = (size_t)g->nlocal * sizeof(double);
     if (field_alloc(&k->pb[2], vb) != hipSuccess || field_alloc(&k->pb[3], vb) != hipSuccess)
@@ -436,7 +450,15 @@ static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
   // p of iterations i-1, i-2, i-3 (depth-4 deferral reads all three at i % 4 == 3)
   const double* p_prev[3] = {p_old, k->pb[(i + ns - 1) % ns], k->pb[(i + ns - 2) % ns]};
   // Jacobi: pass A builds z = dinv*r - mu on the fly; SOR / MG: z is stored (dinv = 1)
-  const double* zsrc = k->stored_z() ? k->z : k->r;
+  double* r = k->rbuf(i);
+  const double* zsrc = k->stored_z() ? k->z : r;
+  // PB_CG_PSTORE_B: pass A read-only, pass B stores p and the residual into the other buffer
+  PStore ps;
+  if (k->pst) {
+    ps.zsrc = zsrc;
+    ps.r_out = k->rbuf(i + 1);
+  }
+  const bool store_a = !k->pst;
   StencilPlanes gp;
   int nparts = 0;
   if (fold) {
@@ -444,24 +466,27 @@ static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
     gp.wrap = true;
     if (fold_a)
       PB_TRY(launch_cg_pass_a_folded(g, s, zsrc, p_old, p_new, gp, k->d_st, k->fold_nparts_b,
-                                     k->d_hist, k->h_done_dev, i, &nparts));
+                                     k->d_hist, k->h_done_dev, i, &nparts, store_a));
     else
-      PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
-    return launch_cg_pass_b_folded(g, s, p_new, p_prev, k->x->d, k->r, gp, k->d_st, nparts, i,
-                                   k->defer_x, &k->fold_nparts_b);
+      PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts,
+                              store_a));
+    return launch_cg_pass_b_folded(g, s, p_new, p_prev, k->x->d, r, gp, k->d_st, nparts, i,
+                                   k->defer_x, &k->fold_nparts_b, ps);
   }
   if (!ctx->split) {
     // periodic wrap read in place: pass A combines r, p_old of the wrap planes itself and pass B
     // reads p_new's wrap planes (no boundary-plane kernel on one rank)
     gp.ghost_lo = gp.ghost_hi = nullptr;
     gp.wrap = true;
-    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
+    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts,
+                            store_a));
   } else if (g->nzl < 3) {
     PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st));
     PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
-    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts));
+    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts,
+                            store_a));
   } else {
     // the p-plane halo exchange (RCCL, comm stream) overlaps pass A's interior planes
     PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st));
@@ -470,18 +495,20 @@ static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
     int nb1 = 0, nb2 = 0;
     ScopedTimer tm(ctx, "cg_pass_a");  // the whole pass A (both launches and the wait)
     PB_TRY(halo_begin(g, g->bnd_lo, g->bnd_hi));
-    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1));
+    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1,
+                            store_a));
     PB_TRY(halo_end(g));
-    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1, &nb2));
+    PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1, &nb2,
+                            store_a));
     nparts = nb1 + nb2;
   }
   PB_TRY(cg_finalize_pass_a(ctx, nparts, k->d_st));
-  PB_TRY(launch_cg_pass_b(g, s, p_new, p_prev, k->x->d, k->r, gp, k->d_st, k->d_hist,
-                          k->h_done_dev, i, k->defer_x, !k->stored_z()));
+  PB_TRY(launch_cg_pass_b(g, s, p_new, p_prev, k->x->d, r, gp, k->d_st, k->d_hist,
+                          k->h_done_dev, i, k->defer_x, !k->stored_z(), ps));
   if (k->stored_z()) {  // z = M^-1 r, then the residual sums over z
     int np = 0;
-    PB_TRY(pc_apply_dev(k, k->r, k->z, &k->d_st->done, &np));
-    if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
+    PB_TRY(pc_apply_dev(k, r, k->z, &k->d_st->done, &np));
+    if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, r, k->d_st, &np));
     PB_TRY(cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, i));
   }
   return PB_OK;
@@ -598,6 +625,7 @@ int pb_ksp_destroy(pb_ksp* k) {
   if (!k) return PB_OK;
   (void)wait_stream(k->A->grid->ctx, k->A->grid->ctx->stream, "pb_ksp_destroy");
   field_free(k->r);
+  field_free(k->r2);
   for (double* p : k->pb) field_free(p);
   field_free(k->w);
   field_free(k->z);

@@ -61,12 +61,15 @@ struct CombineLoad {
   const double* __restrict__ p;
   const CgState* st;
   double dinv, shift, bb;
+  // 1: the state is past stage 1 (betaold already overwritten): take pass A's beta/betaold from
+  // bbp, which stage 1 computed with the same operands (pass B re-forming p, PB_CG_PSTORE_B)
+  int after1 = 0;
   __device__ __forceinline__ void prepare() { prepare_from(*st); }
   template <class S>
   __device__ __forceinline__ void prepare_from(const S& s) {
     dinv = s.dinv;
     shift = -s.mu;
-    bb = s.it == 0 ? 0.0 : s.beta / s.betaold;
+    bb = after1 ? s.bbp : (s.it == 0 ? 0.0 : s.beta / s.betaold);
   }
   __device__ __forceinline__ const double* src(int a) const { return a == 0 ? r : p; }
   __device__ __forceinline__ double f(double rv, double pv) const {
@@ -98,11 +101,16 @@ struct StoreY {
   }
 };
 
-// CG pass A: store p_new, accumulate p.w (VecXDot(P, W))
-struct PassA {
+// CG pass A: store p_new, accumulate p.w (VecXDot(P, W)). STORE = false: the
+// p store moves to pass B, which re-forms p from r and p_old on load (PB_CG_PSTORE_B): pass A
+// becomes read-only (16 B/DoF) and pass B reads 2 / writes 2 arrays (32 B/DoF), same 48 B/DoF.
+// Read-only (STORE = false): 4-row tiles, one workgroup per CU (z-chunks of half the slab at
+// 512^3), measured 0.378 vs 0.391 ms for 8-row tiles (profiles/r02/ab_pst_defer_512.jsonl).
+template <bool STORE>
+struct PassAT {
   static constexpr int NS = 1, NE = 0;
-  static constexpr bool RAW = false, TALL = true;  // put() takes the Laplacian; 8-row tiles
-  static constexpr int WGCU = 3;                   // (4-row tiles; 1 with 8 rows)
+  static constexpr bool RAW = false, TALL = STORE;  // put() takes the Laplacian; 8-row tiles
+  static constexpr int WGCU = STORE ? 3 : 1;        // (4-row tiles; 1 with 8 rows)
   static constexpr bool PREFETCH = true;
   double* __restrict__ p_new;
   int nt_p;  // non-temporal p stores (PB_PASSA_NT, default on; cached stores, which pass B could
@@ -112,11 +120,12 @@ struct PassA {
   template <int V>
   __device__ __forceinline__ void put(RowIx idx, const double (&c)[V], const double (&w)[V],
                                       double (&)[1][V], double* acc, int nt) const {
-    store_row<V>(p_new, idx, c, nt && nt_p);
+    if constexpr (STORE) store_row<V>(p_new, idx, c, nt && nt_p);
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[0] += w[e] * c[e];
   }
 };
+using PassA = PassAT<true>;
 
 // CG pass B: r += (-a) w with w = A p recomputed; then the PC/null-space sums of the new
 // residual: s = dinv*r, t = s - mu_old:  sum t, sum t^2, sum t*r, sum r.
@@ -128,12 +137,22 @@ struct PassA {
 //   XU = 2 (no deferral):      x += alpha_i p_i every iteration.
 // Operands are prefetched one plane ahead (XU = 1: 3 operand rows, 238 VGPRs -- one workgroup
 // per CU is all the grid uses; measured 2 % faster than loading them in the plane's own step).
-template <int XU>
+#ifndef PB_PSTB_WGCU
+#define PB_PSTB_WGCU 1
+#endif
+#ifndef PB_PSTB_TALL
+#define PB_PSTB_TALL 0
+#endif
+// PST (PB_CG_PSTORE_B): the field is p re-formed from (r, p_old) by CombineLoad, stored to p_out;
+// r is read from op[0] (= r) and written to r_out (another buffer: neighbouring waves still read
+// r through the z-queue, an in-place update would race with them).
+template <int XU, bool PST = false>
 struct PassB {
   static constexpr int NS = 4, NE = XU == 1 ? 3 : (XU == 2 ? 2 : (XU == 3 ? 5 : 1));
   static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
   // one workgroup per CU (z-chunks of half the slab at 512^3): 8-10 % faster than 3 per CU
-  static constexpr int WGCU = 1;
+  static constexpr int WGCU = PST ? PB_PSTB_WGCU : 1;
+  static constexpr bool TALL = PST && XU == 0 && PB_PSTB_TALL;  // (A/B builds)
   static constexpr bool PREFETCH = true;
   double* __restrict__ x;
   double* __restrict__ r;
@@ -142,6 +161,11 @@ struct PassB {
   const double* __restrict__ p_m3;
   const CgState* st;
   double alpha, alpha_prev, dinv, mu, a2, a3;
+  double* __restrict__ r_out = nullptr;  // PST only
+  double* __restrict__ p_out = nullptr;
+  // PST: operands r (op 0) and p_{i-1} = p_old (op 2) are the centre plane's raw z-queue values
+  // (CombineLoad arrays 0 and 1) -- taken from the queue instead of loaded again
+  static constexpr int qop(int a) { return !PST ? -1 : (a == 0 ? 0 : (a == 2 ? 1 : -1)); }
   __device__ __forceinline__ void prepare() { prepare_from(*st); }
   template <class S>
   __device__ __forceinline__ void prepare_from(const S& s) {
@@ -172,7 +196,12 @@ struct PassB {
       acc[2] += t * rv[e];
       acc[3] += rv[e];
     }
-    store_row<V>(r, idx, rv, nt);
+    if constexpr (PST) {
+      store_row<V>(r_out, idx, rv, nt);
+      store_row<V>(p_out, idx, c, nt);
+    } else {
+      store_row<V>(r, idx, rv, nt);
+    }
     if constexpr (XU == 1) {
       double xv[V];
 #pragma unroll
@@ -218,6 +247,21 @@ struct Fold {
   int64_t host_iter = 0;          // stage 2: the iteration whose stage 2 this is
 };
 __device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st);
+
+// Epi::qop(a) (optional): operand a is raw z-queue array qop(a) of the centre plane (-1: loaded)
+template <class E, class = void>
+struct HasQop {
+  static constexpr bool v = false;
+};
+template <class E>
+struct HasQop<E, std::void_t<decltype(E::qop(0))>> {
+  static constexpr bool v = true;
+};
+template <class E>
+__device__ __forceinline__ constexpr int qop_of(int a) {
+  if constexpr (HasQop<E>::v) return E::qop(a);
+  else return -1;
+}
 
 // Load / Epi structs that read CG scalars have prepare_from(state): fed the register copy
 template <class T>
@@ -354,7 +398,20 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         for (int t = 0; t < TY; ++t)
 #pragma unroll
           for (int a = 0; a < Epi::NE; ++a)
-            load_row_nt<V>(ep.src(a), rix(base + (int64_t)(j0 + t) * nx), opn[t][a]);
+            if (qop_of<Epi>(a) < 0)
+              load_row_nt<V>(ep.src(a), rix(base + (int64_t)(j0 + t) * nx), opn[t][a]);
+      }
+    };
+    // operands that are raw queue values of a plane (Epi::qop): copied, not loaded
+    auto take_queue_ops = [&](const double (&raw)[NR][TY][V]) {
+      if constexpr (Epi::NE > 0 && Epi::PREFETCH && HasQop<Epi>::v) {
+#pragma unroll
+        for (int t = 0; t < TY; ++t)
+#pragma unroll
+          for (int a = 0; a < Epi::NE; ++a)
+            if (qop_of<Epi>(a) >= 0)
+#pragma unroll
+              for (int e = 0; e < V; ++e) opn[t][a][e] = raw[qop_of<Epi>(a)][t][e];
       }
     };
     auto issue_ops_now = [&](int kk) {  // operands without prefetch: plane kk straight to opc
@@ -410,6 +467,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
       }
       take_rows(r0, g0, q0);
       take_rows(r1, g1, q1);
+      take_queue_ops(r1);  // plane kf (owned, never a ghost)
       if constexpr (NR != 1) {
         issue_plane_ops(kf);
         issue_zrow(kf + dir);
@@ -419,6 +477,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
       const int k = kf + m * dir;
       take_zrow(q2);                    // plane k+dir (in flight since the previous step)
       take_plane_ops();                 // halo/edges/operands of plane k
+      take_queue_ops(zr);               // queue-sourced operands of plane k+dir
       issue_ops_now(k);
       issue_zrow(m + 2 <= nk ? k + 2 * dir : k + dir);  // (last step: a valid plane, unused)
       issue_plane_ops(m + 1 < nk ? k + dir : k);
@@ -879,6 +938,7 @@ __device__ __forceinline__ void cg_stage1(CgState& st, double dpi) {
   } else {
     st.dpiold = st.dpi;
     st.dpi = dpi;
+    st.bbp = i == 0 ? 0.0 : st.beta / st.betaold;  // CombineLoad's bb of this pass A
     st.betaold = st.beta;
     st.alpha_prev = st.alpha;
     st.alpha = st.beta / dpi;
@@ -1005,8 +1065,9 @@ __device__ __forceinline__ void cg_copy(CgState& d, const CgState& s) {
   d.pend_count = s.pend_count, d.nlog = s.nlog;
   d.reason = s.reason, d.done = s.done, d.pc = s.pc, d.nullspace = s.nullspace;
   d.defer_x = s.defer_x;
+  d.bbp = s.bbp;
 }
-static_assert(sizeof(CgState) == 224, "cg_copy lists every CgState field");
+static_assert(sizeof(CgState) == 232, "cg_copy lists every CgState field");
 
 __device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st) {
   double S[4];
@@ -1068,12 +1129,14 @@ int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState
 
 int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
                      double* p_new, const StencilPlanes& gp, CgState* st, int mode, int part_off,
-                     int* nblocks) {
+                     int* nblocks, bool store) {
   ScopedTimer tm(g->ctx,
                  timer_name(mode, "cg_pass_a", "cg_pass_a_interior", "cg_pass_a_boundary"));
   const int nt_p = env_int("PB_PASSA_NT", 1);  // read per launch (A/B tuning)
-  return launch_any(g, s, CombineLoad{r, p_old, st, 0.0, 0.0, 0.0}, gp, PassA{p_new, nt_p},
-                    &st->done, mode, part_off, nblocks);
+  const CombineLoad ld{r, p_old, st, 0.0, 0.0, 0.0};
+  if (!store)
+    return launch_any(g, s, ld, gp, PassAT<false>{p_new, nt_p}, &st->done, mode, part_off, nblocks);
+  return launch_any(g, s, ld, gp, PassA{p_new, nt_p}, &st->done, mode, part_off, nblocks);
 }
 
 // Folded iteration (one rank, Jacobi): partial sums of pass A at block 0, of pass B at
@@ -1082,7 +1145,8 @@ static int64_t fold_parts_b_off(const pb_ctx* ctx) { return ctx->partials_cap / 
 
 int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const double* p_old,
                             double* p_new, const StencilPlanes& gp, CgState* st2, int nparts_b,
-                            double* hist, int* h_done, int64_t host_iter, int* nblocks) {
+                            double* hist, int* h_done, int64_t host_iter, int* nblocks,
+                            bool store) {
   ScopedTimer tm(g->ctx, "cg_pass_a");
   pb_ctx* ctx = g->ctx;
   Fold f;
@@ -1096,8 +1160,11 @@ int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const do
   f.h_done = h_done;
   f.host_iter = host_iter - 1;  // stage 2 of the previous iteration
   const int nt_p = env_int("PB_PASSA_NT", 1);
-  return launch_any(g, s, CombineLoad{r, p_old, nullptr, 0.0, 0.0, 0.0}, gp, PassA{p_new, nt_p},
-                    nullptr, PLANES_ALL, 0, nblocks, 0, 0, f);
+  const CombineLoad ld{r, p_old, nullptr, 0.0, 0.0, 0.0};
+  if (!store)
+    return launch_any(g, s, ld, gp, PassAT<false>{p_new, nt_p}, nullptr, PLANES_ALL, 0, nblocks, 0,
+                      0, f);
+  return launch_any(g, s, ld, gp, PassA{p_new, nt_p}, nullptr, PLANES_ALL, 0, nblocks, 0, 0, f);
 }
 
 int cg_finalize_init(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done) {
@@ -1114,42 +1181,62 @@ int cg_finalize_stage2(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* 
 }
 
 // pass B variants by the x-update position; fold.stage = 1: stage 1 in the prologue (partials
-// of pass A at block 0, state st2[0] -> st2[1]) and the partials written at fold_parts_b_off()
-static int pass_b_launch(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
-                         double* x, double* r, const StencilPlanes& gp, CgState* st,
-                         int64_t host_iter, int defer, const Fold& f, int* nparts) {
-  const double* pp = p_prev[0];
+// of pass A at block 0, state st2[0] -> st2[1]) and the partials written at fold_parts_b_off().
+// ps.r_out != nullptr (PB_CG_PSTORE_B): pass B re-forms p = CombineLoad(ps.zsrc, p_old) on load,
+// stores it to p, reads r and writes the new residual to ps.r_out.
+template <int XU, bool PST>
+static int pass_b_one(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
+                      double* x, double* r, const StencilPlanes& gp, CgState* st, const Fold& f,
+                      const PStore& ps, int* nparts) {
   const int* skip = f.stage ? nullptr : &st->done;
   const int off = f.stage ? (int)fold_parts_b_off(g->ctx) : 0;
+  PassB<XU, PST> ep{x, r, p_prev[0], XU == 3 ? p_prev[1] : nullptr, XU == 3 ? p_prev[2] : nullptr,
+                    st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if constexpr (PST) {
+    ep.r_out = ps.r_out;
+    ep.p_out = const_cast<double*>(p);
+    CombineLoad ld{ps.zsrc, p_prev[0], st, 0.0, 0.0, 0.0};
+    ld.after1 = 1;
+    return launch_any(g, s, ld, gp, ep, skip, PLANES_ALL, off, nparts, 1, 0, f);
+  } else {
+    return launch_any(g, s, PlainLoad{p}, gp, ep, skip, PLANES_ALL, off, nparts, 1, 0, f);
+  }
+}
+
+template <bool PST>
+static int pass_b_pick(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
+                       double* x, double* r, const StencilPlanes& gp, CgState* st,
+                       int64_t host_iter, int defer, const Fold& f, const PStore& ps, int* nparts) {
   if (defer == 0) {
     ScopedTimer tm(g->ctx, "cg_pass_b");
-    return launch_any(g, s, PlainLoad{p}, gp,
-                      PassB<2>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-                      skip, PLANES_ALL, off, nparts, 1, 0, f);
+    return pass_b_one<2, PST>(g, s, p, p_prev, x, r, gp, st, f, ps, nparts);
   }
   if (host_iter % defer != defer - 1) {
     ScopedTimer tm(g->ctx, "cg_pass_b_even");
-    return launch_any(g, s, PlainLoad{p}, gp,
-                      PassB<0>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-                      skip, PLANES_ALL, off, nparts, 1, 0, f);
+    return pass_b_one<0, PST>(g, s, p, p_prev, x, r, gp, st, f, ps, nparts);
   }
   if (defer == 2) {
     ScopedTimer tm(g->ctx, "cg_pass_b_odd");
-    return launch_any(g, s, PlainLoad{p}, gp,
-                      PassB<1>{x, r, pp, nullptr, nullptr, st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-                      skip, PLANES_ALL, off, nparts, 1, 0, f);
+    return pass_b_one<1, PST>(g, s, p, p_prev, x, r, gp, st, f, ps, nparts);
   }
   ScopedTimer tm(g->ctx, "cg_pass_b_x4");
-  return launch_any(g, s, PlainLoad{p}, gp,
-                    PassB<3>{x, r, pp, p_prev[1], p_prev[2], st, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0},
-                    skip, PLANES_ALL, off, nparts, 1, 0, f);
+  return pass_b_one<3, PST>(g, s, p, p_prev, x, r, gp, st, f, ps, nparts);
+}
+
+static int pass_b_launch(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
+                         double* x, double* r, const StencilPlanes& gp, CgState* st,
+                         int64_t host_iter, int defer, const Fold& f, const PStore& ps,
+                         int* nparts) {
+  if (ps.r_out)
+    return pass_b_pick<true>(g, s, p, p_prev, x, r, gp, st, host_iter, defer, f, ps, nparts);
+  return pass_b_pick<false>(g, s, p, p_prev, x, r, gp, st, host_iter, defer, f, ps, nparts);
 }
 
 int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* const* p_prev,
                      double* x, double* r, const StencilPlanes& gp, CgState* st, double* hist,
-                     int* h_done, int64_t host_iter, int defer, bool finalize) {
+                     int* h_done, int64_t host_iter, int defer, bool finalize, const PStore& ps) {
   int nparts = 0;
-  PB_TRY(pass_b_launch(g, s, p, p_prev, x, r, gp, st, host_iter, defer, Fold{}, &nparts));
+  PB_TRY(pass_b_launch(g, s, p, p_prev, x, r, gp, st, host_iter, defer, Fold{}, ps, &nparts));
   if (!finalize) return PB_OK;  // preconditioned path: the sums come from z = M^-1 r later
   return cg_reduce_update(g->ctx, 2, nparts, 4, st, hist, h_done, host_iter);
 }
@@ -1157,7 +1244,7 @@ int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* c
 int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
                             const double* const* p_prev, double* x, double* r,
                             const StencilPlanes& gp, CgState* st2, int nparts_a, int64_t host_iter,
-                            int defer, int* nparts_b) {
+                            int defer, int* nparts_b, const PStore& ps) {
   Fold f;
   f.stage = 1;
   f.nparts = nparts_a;
@@ -1165,7 +1252,7 @@ int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
   f.parts = g->ctx->d_partials;
   f.in = st2;
   f.out = st2 + 1;
-  return pass_b_launch(g, s, p, p_prev, x, r, gp, nullptr, host_iter, defer, f, nparts_b);
+  return pass_b_launch(g, s, p, p_prev, x, r, gp, nullptr, host_iter, defer, f, ps, nparts_b);
 }
 
 // after the last folded iteration of a pb_ksp_iterate call: its stage 2 (in place on st2[1]),

@@ -15,13 +15,23 @@ import re
 import sys
 from collections import defaultdict
 
-# bench.py kernel roles -> kernel-name pattern (template arguments of pb::star7_kernel)
+# bench.py kernel roles -> kernel-name pattern (template arguments of pb::star7_kernel), by where
+# CG stores p: pass A (PB_CG_PSTORE_B=0, key <grid>) or pass B (default, key <grid>/pstore_b)
 ROLES = {
-    "matvec_star7": r"star7_kernel<.*PlainLoad, pb::StoreY>",
-    "cg_pass_a": r"star7_kernel<.*CombineLoad, pb::PassA",
-    "cg_pass_b_even": r"star7_kernel<.*PassB<0>",
-    "cg_pass_b_odd": r"star7_kernel<.*PassB<1>",
-    "cg_pass_b_x4": r"star7_kernel<.*PassB<3>",
+    "": {
+        "matvec_star7": r"star7_kernel<.*PlainLoad, pb::StoreY>",
+        "cg_pass_a": r"star7_kernel<.*CombineLoad, pb::PassAT<true>",
+        "cg_pass_b_even": r"star7_kernel<.*PassB<0, false>",
+        "cg_pass_b_odd": r"star7_kernel<.*PassB<1, false>",
+        "cg_pass_b_x4": r"star7_kernel<.*PassB<3, false>",
+    },
+    "/pstore_b": {
+        "matvec_star7": r"star7_kernel<.*PlainLoad, pb::StoreY>",
+        "cg_pass_a": r"star7_kernel<.*CombineLoad, pb::PassAT<false>",
+        "cg_pass_b_even": r"star7_kernel<.*PassB<0, true>",
+        "cg_pass_b_odd": r"star7_kernel<.*PassB<1, true>",
+        "cg_pass_b_x4": r"star7_kernel<.*PassB<3, true>",
+    },
 }
 
 
@@ -47,21 +57,23 @@ def main():
                 summ[f"{k} | {c}"] = {"launches": len(vals), "mean": sum(vals) / len(vals)}
                 means[k][c] = sum(vals) / len(vals)
         json.dump(summ, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1)
-    traffic = {}
-    for role, pat in ROLES.items():
-        for k, ctr in means.items():
-            if re.search(pat, k) and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
-                rd = 2 * ctr["FETCH_SIZE"] * 1024
-                wr = ctr["WRITE_SIZE"] * 1024
-                traffic[role] = {"bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
-                                 "kernel": k,
-                                 "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
-                                           "2x FETCH_SIZE (gfx950 half-count), KiB->B"}
     out = os.path.join(os.path.dirname(dst.rstrip("/")), "pmc_traffic.json")
     allt = json.load(open(out)) if os.path.exists(out) else {}
-    allt[key] = traffic
+    for suffix, roles in ROLES.items():
+        traffic = {}
+        for role, pat in roles.items():
+            for k, ctr in means.items():
+                if re.search(pat, k) and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
+                    rd = 2 * ctr["FETCH_SIZE"] * 1024
+                    wr = ctr["WRITE_SIZE"] * 1024
+                    traffic[role] = {"bytes_per_launch": rd + wr, "read_bytes": rd,
+                                     "write_bytes": wr, "kernel": k,
+                                     "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate "
+                                               "passes), 2x FETCH_SIZE (gfx950 half-count), KiB->B"}
+        if any(r.startswith("cg_") for r in traffic):  # this run's CG mode
+            allt[key + suffix] = traffic
+            print(key + suffix, json.dumps(traffic, indent=1))
     json.dump(allt, open(out, "w"), indent=1)
-    print(json.dumps(traffic, indent=1))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,135 @@
+// rw_mix_probe.hip -- streaming rates of the CG passes' access patterns at 512^3 fp64, in the
+// stencil engine's order (waves marching in z over 128-wide x-segments of TY rows, 4 waves per
+// block, z-chunks, one plane prefetched) and flat: two arrays read and NW = 0 / 1 / 2 written.
+// Question it answers: would moving pass A's p store into pass B (pass A read-only 16 B/DoF,
+// pass B read-2/write-2 32 B/DoF; same 48 B/DoF per iteration) be faster than the current
+// read-2/write-1 + read-2/write-1 split?
+// Build: hipcc -O3 --offload-arch=gfx950 -o rw_mix_probe rw_mix_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+constexpr int NX = 512, NY = 512, NZ = 512;
+constexpr long PLANE = (long)NX * NY;
+
+template <int TY, int NW>
+__global__ __launch_bounds__(256) void zm_rw(const double* __restrict__ a, const double* __restrict__ b,
+                                             double* __restrict__ y0, double* __restrict__ y1,
+                                             double* __restrict__ sink, int nchunk) {
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bb = blockIdx.x;
+  const int nb = gridDim.x, q = nb / 8, r = nb % 8, xcd = bb % 8, slot = bb / 8;
+  bb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  const int nseg = NX / 128, ntile = NY / (4 * TY);
+  const int seg = bb % nseg;
+  bb /= nseg;
+  const int tile = bb % ntile, chunk = bb / ntile;
+  const int kc = (NZ + nchunk - 1) / nchunk;
+  const int kb = chunk * kc, ke = min(kb + kc, NZ);
+  const int j0 = (tile * 4 + wid) * TY;
+  const int i0 = seg * 128 + 2 * lane;
+  dv2 va[TY], vb[TY];
+  dv2 acc = {0.0, 0.0};
+  auto ld = [&](int k) {
+    const long base = k * PLANE;
+#pragma unroll
+    for (int t = 0; t < TY; ++t) {
+      va[t] = *(const dv2*)(a + base + (long)(j0 + t) * NX + i0);
+      vb[t] = *(const dv2*)(b + base + (long)(j0 + t) * NX + i0);
+    }
+  };
+  ld(kb);
+  for (int k = kb; k < ke; ++k) {
+    dv2 ca[TY], cb[TY];
+#pragma unroll
+    for (int t = 0; t < TY; ++t) ca[t] = va[t], cb[t] = vb[t];
+    ld(k + 1 < ke ? k + 1 : k);
+    const long base = k * PLANE;
+#pragma unroll
+    for (int t = 0; t < TY; ++t) {
+      const dv2 p = ca[t] + 0.5 * cb[t];
+      if constexpr (NW == 0) acc += p * cb[t];
+      if constexpr (NW >= 1) __builtin_nontemporal_store(p, (dv2*)(y0 + base + (long)(j0 + t) * NX + i0));
+      if constexpr (NW >= 2)
+        __builtin_nontemporal_store(ca[t] - 0.25 * cb[t], (dv2*)(y1 + base + (long)(j0 + t) * NX + i0));
+    }
+  }
+  if constexpr (NW == 0) sink[blockIdx.x * 256 + threadIdx.x] = acc.x + acc.y;
+}
+
+template <int NW>
+__global__ __launch_bounds__(256) void flat_rw(const dv2* __restrict__ a, const dv2* __restrict__ b,
+                                               dv2* __restrict__ y0, dv2* __restrict__ y1,
+                                               double* __restrict__ sink, long n) {
+  dv2 acc = {0.0, 0.0};
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const dv2 av = a[i], bv = b[i];
+    const dv2 p = av + 0.5 * bv;
+    if constexpr (NW == 0) acc += p * bv;
+    if constexpr (NW >= 1) __builtin_nontemporal_store(p, y0 + i);
+    if constexpr (NW >= 2) __builtin_nontemporal_store(av - 0.25 * bv, y1 + i);
+  }
+  if constexpr (NW == 0) sink[blockIdx.x * 256 + threadIdx.x] = acc.x + acc.y;
+}
+
+int main() {
+  const long N = PLANE * NZ;
+  double *a, *b, *y0, *y1, *sink;
+  CK(hipMalloc(&a, N * 8));
+  CK(hipMalloc(&b, N * 8));
+  CK(hipMalloc(&y0, N * 8));
+  CK(hipMalloc(&y1, N * 8));
+  CK(hipMalloc(&sink, 4096L * 256 * 8));
+  CK(hipMemset(a, 0, N * 8));
+  CK(hipMemset(b, 0, N * 8));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto run = [&](const char* name, int nw, int p1, int p2, auto launch) {
+    for (int w = 0; w < 3; ++w) launch();
+    CK(hipDeviceSynchronize());
+    float best = 1e30f, tot = 0;
+    const int reps = 20;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0));
+      launch();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+      tot += ms;
+    }
+    const double bytes = (16.0 + 8.0 * nw) * N;
+    printf("{\"kernel\":\"%s\",\"nw\":%d,\"p1\":%d,\"p2\":%d,\"best_ms\":%.4f,\"avg_ms\":%.4f,"
+           "\"GBps_avg\":%.1f}\n",
+           name, nw, p1, p2, best, tot / reps, bytes / (tot / reps) / 1e6);
+    fflush(stdout);
+  };
+  for (int g : {1024, 2048, 4096}) {
+    run("flat", 0, g, 0, [&] { flat_rw<0><<<g, 256>>>((const dv2*)a, (const dv2*)b, (dv2*)y0, (dv2*)y1, sink, N / 2); });
+    run("flat", 1, g, 0, [&] { flat_rw<1><<<g, 256>>>((const dv2*)a, (const dv2*)b, (dv2*)y0, (dv2*)y1, sink, N / 2); });
+    run("flat", 2, g, 0, [&] { flat_rw<2><<<g, 256>>>((const dv2*)a, (const dv2*)b, (dv2*)y0, (dv2*)y1, sink, N / 2); });
+  }
+  for (int nc : {2, 4, 8, 16}) {
+    const int nb4 = (NX / 128) * (NY / 16) * nc, nb8 = (NX / 128) * (NY / 32) * nc;
+    run("seg_ty4", 0, 4, nc, [&] { zm_rw<4, 0><<<nb4, 256>>>(a, b, y0, y1, sink, nc); });
+    run("seg_ty4", 1, 4, nc, [&] { zm_rw<4, 1><<<nb4, 256>>>(a, b, y0, y1, sink, nc); });
+    run("seg_ty4", 2, 4, nc, [&] { zm_rw<4, 2><<<nb4, 256>>>(a, b, y0, y1, sink, nc); });
+    run("seg_ty8", 0, 8, nc, [&] { zm_rw<8, 0><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
+    run("seg_ty8", 1, 8, nc, [&] { zm_rw<8, 1><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
+    run("seg_ty8", 2, 8, nc, [&] { zm_rw<8, 2><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
+  }
+  return 0;
+}

@@ -11,8 +11,20 @@ def test_global_grid_weak_scaling():
 
 
 def test_cg_iter_bytes():
-    assert bench.cg_iter_bytes(4) == 58
+    # p stored by pass B (library default): 16 + (3 * 32 + 64) / 4
+    assert bench.cg_iter_bytes(4) == 56
+    assert bench.cg_iter_bytes(2) == 56
     assert bench.cg_iter_bytes(0) == 64
+    # p stored by pass A (PB_CG_PSTORE_B=0): 24 + (3 * 24 + 64) / 4
+    assert bench.cg_iter_bytes(4, 0) == 58
+    assert bench.cg_iter_bytes(0, 0) == 64
+
+
+def test_pstore_mode_env(monkeypatch):
+    monkeypatch.delenv("PB_CG_PSTORE_B", raising=False)
+    assert bench.pstore_mode() == 1
+    monkeypatch.setenv("PB_CG_PSTORE_B", "0")
+    assert bench.pstore_mode() == 0
 
 
 def test_host_info_fields():

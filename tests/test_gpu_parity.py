@@ -276,6 +276,48 @@ def test_cg_folded_finalize_bit_identical(ctx, monkeypatch, case):
     check_history(h1, ho)
 
 
+@pytest.mark.parametrize("n3", [(64, 32, 16), (512, 512, 8)])
+@pytest.mark.parametrize("fold", ["1", "0"])
+@pytest.mark.parametrize("defer", ["4", "2", "0"])
+def test_cg_pass_b_pstore_bit_identical(ctx, monkeypatch, n3, fold, defer):
+    """PB_CG_PSTORE_B=1: pass A only takes p.Ap, pass B re-forms p from (r, p_old), stores it and
+    writes the residual into a second buffer. Same arithmetic per value, so reason, iteration count,
+    history and x are bit-identical to the default split (p stored by pass A), with and without
+    the folded finalize and at every x-update deferral depth. On planes of >= 512^2 points the
+    storing pass A runs 8-row tiles and the read-only one 4-row tiles with one workgroup per CU:
+    other blocks, so p.Ap is summed in another order -- there the two runs agree to rounding
+    (history 1e-12) instead of bit for bit. Checked against the oracle as well."""
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(N, SEED), n3, h)
+    opts = ["-ksp_rtol", "1e-9", "-ksp_max_it", "60"]
+    monkeypatch.setenv("PB_CG_FOLD", fold)
+    monkeypatch.setenv("PB_CG_DEFER_X", defer)
+    out = {}
+    for pst in ("1", "0"):
+        monkeypatch.setenv("PB_CG_PSTORE_B", pst)
+        da = pb.DA(ctx, n3)
+        P, A, x, bv = pb.initialise_linear_system(da, h)
+        bv.set_values(b)
+        k = pb.KSP(A, P, pb.ksp_options(opts))
+        k.begin(bv, x)
+        k.iterate(5)   # odd split: the residual buffers swap parity across calls
+        k.iterate(1000)
+        reason, its, hist = k.end()
+        k.destroy()
+        out[pst] = (reason, its, np.asarray(hist), x.get_values())
+    (r1, i1, h1, x1), (r0, i0, h0, x0) = out["1"], out["0"]
+    assert (r1, i1) == (r0, i0)
+    if n3[0] * n3[1] < 512 * 512:
+        assert np.array_equal(h1, h0) and np.array_equal(x1, x0)
+    else:
+        assert np.max(np.abs(h1 - h0) / h0) < 1e-12
+        check_x(x1, x0, bar=1e-12)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-9, max_it=60)
+    assert (r1, i1) == (ro, itso)
+    check_history(h1, ho)
+
+
 def test_cg_zero_rhs_converges_immediately(ctx):
     n3 = (8, 8, 8)
     da = pb.DA(ctx, n3)
