@@ -23,7 +23,9 @@ typedef double dv2 __attribute__((ext_vector_type(2)));
 constexpr int NX = 512, NY = 512, NZ = 512;
 constexpr long PLANE = (long)NX * NY;
 
-template <int TY, int NW>
+// ROWS = 1: the 4 waves of a block take the 4 x-segments of the same TY rows (a block reads whole
+// 4 KiB rows) instead of 4 consecutive y-tiles of one segment
+template <int TY, int NW, int ROWS = 0>
 __global__ __launch_bounds__(256) void zm_rw(const double* __restrict__ a, const double* __restrict__ b,
                                              double* __restrict__ y0, double* __restrict__ y1,
                                              double* __restrict__ sink, int nchunk) {
@@ -32,12 +34,22 @@ __global__ __launch_bounds__(256) void zm_rw(const double* __restrict__ a, const
   const int nb = gridDim.x, q = nb / 8, r = nb % 8, xcd = bb % 8, slot = bb / 8;
   bb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   const int nseg = NX / 128, ntile = NY / (4 * TY);
-  const int seg = bb % nseg;
-  bb /= nseg;
-  const int tile = bb % ntile, chunk = bb / ntile;
+  int seg, tile, chunk, j0;
+  if (ROWS) {  // block = TY rows x all 4 segments (NX = 512)
+    const int nrow = NY / TY;
+    seg = wid;
+    tile = bb % nrow;
+    chunk = bb / nrow;
+    j0 = tile * TY;
+  } else {
+    seg = bb % nseg;
+    bb /= nseg;
+    tile = bb % ntile;
+    chunk = bb / ntile;
+    j0 = (tile * 4 + wid) * TY;
+  }
   const int kc = (NZ + nchunk - 1) / nchunk;
   const int kb = chunk * kc, ke = min(kb + kc, NZ);
-  const int j0 = (tile * 4 + wid) * TY;
   const int i0 = seg * 128 + 2 * lane;
   dv2 va[TY], vb[TY];
   dv2 acc = {0.0, 0.0};
@@ -130,6 +142,15 @@ int main() {
     run("seg_ty8", 0, 8, nc, [&] { zm_rw<8, 0><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
     run("seg_ty8", 1, 8, nc, [&] { zm_rw<8, 1><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
     run("seg_ty8", 2, 8, nc, [&] { zm_rw<8, 2><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
+  }
+  for (int nc : {2, 4, 8}) {
+    const int nb4 = (NY / 4) * nc, nb8 = (NY / 8) * nc;
+    run("rows_ty4", 0, 4, nc, [&] { zm_rw<4, 0, 1><<<nb4, 256>>>(a, b, y0, y1, sink, nc); });
+    run("rows_ty4", 1, 4, nc, [&] { zm_rw<4, 1, 1><<<nb4, 256>>>(a, b, y0, y1, sink, nc); });
+    run("rows_ty4", 2, 4, nc, [&] { zm_rw<4, 2, 1><<<nb4, 256>>>(a, b, y0, y1, sink, nc); });
+    run("rows_ty8", 0, 8, nc, [&] { zm_rw<8, 0, 1><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
+    run("rows_ty8", 1, 8, nc, [&] { zm_rw<8, 1, 1><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
+    run("rows_ty8", 2, 8, nc, [&] { zm_rw<8, 2, 1><<<nb8, 256>>>(a, b, y0, y1, sink, nc); });
   }
   return 0;
 }
