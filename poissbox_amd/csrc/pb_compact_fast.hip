@@ -57,6 +57,7 @@ struct FastPass {
   const double* in[2];
   double* out[2];
   int nout;
+  const int* skip;  // pb_ctx::op_skip (exit at entry once set)
 };
 
 static Pcr make_pcr(int64_t n, double alpha) {
@@ -108,6 +109,7 @@ __device__ __forceinline__ int fidx(const FastPass& p, int l, int e) {
 
 __global__ __launch_bounds__(kFT) void compact_fast_kernel(FastPass p) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  if (p.skip && *p.skip) return;  // (uniform: the whole block leaves before any barrier)
   const int tile = blockIdx.x;
   const int outer = tile / p.ntiles_inner;
   const int inner0 = (tile % p.ntiles_inner) * p.TL;
@@ -213,6 +215,7 @@ __global__ __launch_bounds__(kFT) void compact_fast_kernel(FastPass p) {
 }
 
 static int launch_pass(pb_ctx* ctx, FastPass& p) {
+  p.skip = ctx->op_skip;
   p.TL = kTile / p.n;
   if (p.TL < 1) return set_error(PB_ERR_UNSUPPORTED, "compact fast path: line length > %d", kTile);
   if (p.TL > p.ninner) p.TL = p.ninner;

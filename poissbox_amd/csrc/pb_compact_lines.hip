@@ -47,6 +47,7 @@ struct LinePass {
   int ninner, ntiles_inner, nouter, TL, P;
   int ablate;  // tuning only (PB_LINES_ABLATE=1): copy lines through, no solves
   LineOp J, L;
+  const int* skip;  // pb_ctx::op_skip (exit at entry once set)
 };
 
 static LineOp make_line_op(int kind, int C, double h) {
@@ -289,6 +290,7 @@ struct LineCfg {
 
 template <int C, int LAYOUT, int PASS, class K, int V>
 __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
+  if (p.skip && *p.skip) return;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int TL = K::TL, LPW = K::LPW, NT = K::NT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -418,6 +420,7 @@ __device__ __forceinline__ void wave_sync() {
 
 template <int C>
 __global__ __launch_bounds__(256) void compact_lines_x_direct(LinePass p, int64_t nlines) {
+  if (p.skip && *p.skip) return;
   constexpr int LP = Lds<C>::LP, CP = Lds<C>::CP;
   __shared__ double strip[4][2 * LP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -484,6 +487,7 @@ static int launch_x_direct(pb_ctx* ctx, LinePass& p, int64_t nlines) {
 // redistributed through a wave-private LDS strip like the X pass
 template <int C>
 __global__ __launch_bounds__(256) void lines_solve_direct(LinePass p, int64_t nlines) {
+  if (p.skip && *p.skip) return;
   constexpr int LP = Lds<C>::LP, CP = Lds<C>::CP;
   __shared__ double strip[4][LP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -664,6 +668,7 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
   static const char* names[3] = {"compact_lines_x", "compact_lines_y", "compact_lines_z"};
   ScopedTimer tm(ctx, names[axis]);
   LinePass p{};
+  p.skip = ctx->op_skip;
   static const int ablate = env_int("PB_LINES_ABLATE", 0);
   p.ablate = ablate;
   p.in0 = in0;
@@ -715,6 +720,7 @@ int lines_solve_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_str
     return PB_ERR_UNSUPPORTED;
   const int C = (int)(n / 64);
   LinePass p{};
+  p.skip = ctx->op_skip;
   p.in0 = d;
   p.out0 = d;
   p.J = make_solve_op(alpha, C);

@@ -58,6 +58,10 @@ struct TimerSlot {
 }  // namespace pb
 
 struct pb_ctx {
+  // device "done" flag of the KSP whose iteration is being enqueued (OpApplySkip): operator
+  // kernels launched meanwhile exit at entry once it is set -- the host enqueues iterations
+  // ahead of its lagged convergence poll, and an operator apply is the costly part of them
+  const int* op_skip = nullptr;
   int device = 0;
   int rank = 0;
   int nranks = 1;

@@ -112,6 +112,14 @@ static int star7_apply(pb_op* op, const double* x, double* y) {
   return launch_star7_apply(g, s, x, y, gp, PLANES_BOUNDARY);
 }
 
+// KSP iterations enqueued ahead of the convergence poll: the operator kernels launched inside
+// the guard's scope exit at entry once the KSP's device flag is set (pb_ctx::op_skip)
+struct OpApplySkip {
+  pb_ctx* ctx;
+  OpApplySkip(pb_ctx* c, const int* flag) : ctx(c) { ctx->op_skip = flag; }
+  ~OpApplySkip() { ctx->op_skip = nullptr; }
+};
+
 static int op_apply_raw(pb_op* op, const double* x, double* y) {
   pb_grid* g = op->grid;
   if (op->kind == PB_OP_COMPACT) return compact_lapl_fast(g, op->deltas, x, y, op->work);
@@ -411,7 +419,10 @@ static int enqueue_generic_iteration(pb_ksp* k) {
   double* p = k->pb[0];
   int np = 0;
   PB_TRY(launch_cg_generic_p(g, k->r, p, k->d_st));
-  PB_TRY(op_apply_raw(k->A, p, k->w));
+  {
+    OpApplySkip guard(ctx, &k->d_st->done);
+    PB_TRY(op_apply_raw(k->A, p, k->w));
+  }
   PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
   PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
   PB_TRY(launch_cg_generic_xr(g, p, k->w, k->x->d, k->r, k->d_st, &np));
@@ -426,7 +437,10 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   double* p = k->pb[0];
   int np = 0;
   PB_TRY(launch_cg_generic_p(g, k->z, p, k->d_st));  // dinv = 1: z - mu
-  PB_TRY(op_apply_raw(k->A, p, k->w));
+  {
+    OpApplySkip guard(ctx, &k->d_st->done);
+    PB_TRY(op_apply_raw(k->A, p, k->w));
+  }
   PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
   PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
   PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, k->r, k->d_st));

@@ -676,7 +676,7 @@ int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
   // plane per chunk, direction-free, and does not flip it)
   const int rev = g->ctx->zflip;
   if (mode != PLANES_BOUNDARY) g->ctx->zflip ^= 1;
-  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, nullptr, mode, 0, nullptr, rev);
+  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, g->ctx->op_skip, mode, 0, nullptr, rev);
 }
 
 // ---------------------------------------------------------------------------------------------
