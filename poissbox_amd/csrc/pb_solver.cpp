@@ -550,7 +550,12 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
   for (; n < iters && !k->stopped; ++n) {
     PB_TRY(enqueue_iteration(k, fold, fold && n > 0));
     const int64_t hi = k->host_iter++;
-    PB_HIP(hipEventRecord(k->ring[hi % R], ctx->stream));
+    // only the iterations the poll below waits for get an event (j = 0 mod C; folded j + 1): an
+    // event record between two kernels costs the stream ~6 us of idle time (measured 5.9 us per
+    // iteration with one record per iteration; profiles/r02/cg_gaps_*.txt)
+    static const bool every = env_int("PB_KSP_EVENT_ALL", 0) != 0;  // (A/B: one per iteration)
+    if (every || hi % C == (fold ? 1 : 0) % C)
+      PB_HIP(hipEventRecord(k->ring[hi % R], ctx->stream));
     // lagged, rank-consistent poll: decide on the flag of iteration hi + 1 - C only (folded:
     // that flag is written by the next iteration's pass A, so wait for that iteration's event)
     if ((hi + 1) % C == 0 && hi + 1 >= C) {

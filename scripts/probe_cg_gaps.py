@@ -1,6 +1,6 @@
-"""Kernel trace of plain CG iterations (no HIP-event timing at all) at 512^3: run under
-rocprofv3 --kernel-trace, then `python scripts/probe_cg_gaps.py --gaps <kernel_trace.csv>` prints
-the per-iteration kernel time and the idle gaps between consecutive launches."""
+"""Kernel trace of plain CG iterations (no HIP-event timing at all) at n^3 (argv[1], default 512):
+run under rocprofv3 --kernel-trace, then `python scripts/probe_cg_gaps.py --gaps <kernel_trace.csv>`
+prints the per-iteration kernel time and the idle gaps between consecutive launches."""
 import csv
 import os
 import sys
@@ -9,7 +9,7 @@ if len(sys.argv) > 2 and sys.argv[1] == "--gaps":
     rows = sorted(csv.DictReader(open(sys.argv[2])), key=lambda r: int(r["Start_Timestamp"]))
     seq = [(r["Kernel_Name"].split("(")[0], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
            for r in rows]
-    ia = [i for i, s in enumerate(seq) if "PassA" in s[0]]
+    ia = [i for i, s in enumerate(seq) if "PassAT" in s[0]]
     a, b = ia[len(ia) // 4], ia[len(ia) // 4 + 40]  # 40 iterations from the steady state
     busy = sum(e - s for _, s, e in seq[a:b]) / 1e3
     span = (seq[b][1] - seq[a][1]) / 1e3
@@ -27,7 +27,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import poissbox_amd as pb  # noqa: E402
 
 ctx = pb.Context(0)
-da = pb.initialise_grid(ctx, (512, 512, 512))
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+da = pb.initialise_grid(ctx, (n, n, n))
 P, A, x, b = pb.initialise_linear_system(da, da.spacing)
 xt = pb.Vec(da)
 xt.set_random(1)
