@@ -286,17 +286,21 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
                                                          const int* __restrict__ skip, Fold fold) {
   Load ld = ld0;
   Epi ep = ep0;
-  if (fold.stage) {
-    CgState sst;  // register copy
-    fold_prologue(fold, sst);
-    if (sst.done) return;  // uniform: every wave computed the same state
-    prepare_state(ld, sst, 0);
-    prepare_state(ep, sst, 0);
-  } else {
+  if (!fold.stage) {
     if (skip && *skip) return;  // device-side convergence flag (uniform)
     ld.prepare();
     ep.prepare();
   }
+  // folded finalize: run after the first planes' loads are issued (they need no CG scalar), so
+  // the partial-sum loads and the plane loads are in flight together
+  auto do_fold = [&]() -> bool {
+    CgState sst;  // register copy
+    fold_prologue(fold, sst);
+    if (sst.done) return false;  // uniform: every wave computed the same state
+    prepare_state(ld, sst, 0);
+    prepare_state(ep, sst, 0);
+    return true;
+  };
   constexpr int NS = Epi::NS, NR = Load::NR;
   constexpr int NE = Epi::NE > 0 ? Epi::NE : 1;
   double acc[NS > 0 ? NS : 1];
@@ -336,6 +340,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   const int64_t row_dn = (int64_t)(j0 == 0 ? g.ny - 1 : j0 - 1) * nx;
   const int64_t row_up = (int64_t)((j0 + TY >= g.ny) ? 0 : j0 + TY) * nx;
   auto rix = [&](int64_t row) { return RowIx{row, boff}; };
+  if (fold.stage && !wave_on && !do_fold()) return;
 
   if (wave_on) {
     // combined z-queue (planes k-1, k, k+1) and raw prefetch of plane k+2
@@ -465,6 +470,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
         issue_plane_ops(kf);
         issue_zrow(kf + dir);
       }
+      if (fold.stage && !do_fold()) return;
       take_rows(r0, g0, q0);
       take_rows(r1, g1, q1);
       take_queue_ops(r1);  // plane kf (owned, never a ghost)
