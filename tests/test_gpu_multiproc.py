@@ -77,6 +77,59 @@ def test_multiprocess_compact_lapl(world):
         assert np.max(np.abs(y - ref[k0:k0 + nk].reshape(-1))) <= 1e-12 * np.max(np.abs(ref))
 
 
+N_CFG4 = (1024, 1024, 1024)
+CFG4_ITS = 8
+
+
+def _gpu_rank_cfg4(rank, world, tr):
+    """One rank of BASELINE config 4's decomposition: a 1024x1024x128 slab of the 1024^3 grid."""
+    import hashlib
+    import poissbox_amd as pb
+    ctx = pb.Context(0, rank, world)
+    ctx.set_host_transport(tr.sendrecv, tr.allreduce, tr.alltoallv)
+    da = pb.DA(ctx, N_CFG4)
+    (_, _, k0), (_, _, nk) = da.get_corners()
+    h = da.spacing
+    P, A, x, b = pb.initialise_linear_system(da, h)
+    xt = pb.Vec(da)
+    xt.set_random(SEED)
+    A.mult(xt, b)
+    digest = hashlib.blake2b(b.get_values().tobytes()).hexdigest()
+    opts = ["-ksp_type", "cg", "-pc_type", "jacobi", "-ksp_rtol", "0", "-ksp_atol", "0",
+            "-ksp_max_it", str(CFG4_ITS), "-ksp_divtol", "1e300"]
+    reason, its, hist = pb.solve(P, A, x, b, opts)
+    out = (k0, nk, digest, reason, its, np.asarray(hist))
+    ctx.destroy()
+    return out
+
+
+def test_config4_geometry_eight_ranks():
+    """BASELINE config 4's decomposition (1024^3 over 8 ranks, 1024x1024x128 slabs, halo planes of
+    8 MiB, two allreduces per iteration) as 8 processes on the one GPU through the host transport:
+    every rank's b = A x_true slab bit-exact against the oracle's, and a fixed-iteration CG + Jacobi
+    history against the oracle's whole-grid solve (src/poissbox.f90:269-298)."""
+    import hashlib
+    from oracle import oracle as O
+    world = 8
+    res = _run(world, _gpu_rank_cfg4)
+    assert [(r[0], r[1]) for r in res] == [(128 * q, 128) for q in range(world)]
+    n = N_CFG4
+    h = tuple(1.0 / m for m in n)
+    threads = min(16, os.cpu_count() or 1)
+    xs = O.fill_random(int(np.prod(n)), SEED)
+    bo = O.stencil(xs, n, h, nthreads=threads)
+    del xs
+    plane = n[0] * n[1]
+    for k0, nk, digest, *_ in res:
+        assert digest == hashlib.blake2b(bo[k0 * plane:(k0 + nk) * plane].tobytes()).hexdigest()
+    _, ro, itso, ho = O.cg_solve(bo, n, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=CFG4_ITS,
+                                 nthreads=threads)
+    del bo
+    for *_, reason, its, hist in res:
+        assert (reason, its) == (ro, itso) == (reason, CFG4_ITS)
+        check_history(hist, ho)
+
+
 def test_bench_two_ranks_host_transport():
     """bench.py's multi-rank orchestration (torch.distributed.run, barrier, max-over-ranks,
     weak-scaling grid) on one GPU through the host transport, at a small per-GPU size."""
