@@ -27,8 +27,10 @@ __device__ __forceinline__ void block_sums(double* acc, double* parts) {
         ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
+// first (the solve's first iteration, KSPSolve_CG's VecCopy(Z, P)): p = z, p_old is not read
+// (it is not initialised: the stored-z setup skips the p = 0 pass)
 __global__ __launch_bounds__(256) void cg_gen_p_kernel(const double* __restrict__ r, double* p,
-                                                       int64_t n, const CgState* st) {
+                                                       int64_t n, const CgState* st, int first) {
   if (st->done) return;
   const double dinv = st->dinv, shift = -st->mu;
   const double bb = st->it == 0 ? 0.0 : st->beta / st->betaold;
@@ -36,7 +38,7 @@ __global__ __launch_bounds__(256) void cg_gen_p_kernel(const double* __restrict_
        i += (int64_t)gridDim.x * blockDim.x) {
     double z = dinv * r[i];
     z = z + shift;
-    p[i] = z + bb * p[i];
+    p[i] = first ? z : z + bb * p[i];
   }
 }
 
@@ -72,16 +74,24 @@ __global__ __launch_bounds__(256) void cg_gen_xr_kernel(const double* __restrict
   block_sums<4>(acc, parts);
 }
 
-// preconditioned path (z = M^-1 r from SOR / MG): x += a p ; r += (-a) w, no sums
+// preconditioned path (z = M^-1 r from SOR / MG / FFT): x += a p ; r = r_in + (-a) w, no sums.
+// first: x0 = 0 is implicit (x = a p, x not read) and r_in = b (r0 = b - A x0 = b, not copied);
+// a breakdown before the update leaves x = x0 = 0
 __global__ __launch_bounds__(256) void cg_pc_xr_kernel(const double* __restrict__ p,
                                                        const double* __restrict__ w, double* x,
-                                                       double* r, int64_t n, const CgState* st) {
-  if (st->done) return;
+                                                       const double* r_in, double* r, int64_t n,
+                                                       const CgState* st, int first) {
+  const bool done = st->done;
+  if (done && !first) return;
   const double a = st->alpha;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    x[i] = x[i] + a * p[i];
-    r[i] = r[i] + (-a) * w[i];
+    if (done) {
+      x[i] = 0.0;
+      continue;
+    }
+    x[i] = first ? a * p[i] : x[i] + a * p[i];
+    r[i] = r_in[i] + (-a) * w[i];
   }
 }
 
@@ -112,10 +122,10 @@ static int gen_blocks(pb_ctx* ctx, int64_t n) {
   return (int)(b > cap ? cap : (b < 1 ? 1 : b));
 }
 
-int launch_cg_generic_p(pb_grid* g, const double* r, double* p, CgState* st) {
+int launch_cg_generic_p(pb_grid* g, const double* r, double* p, CgState* st, int first) {
   const int nb = gen_blocks(g->ctx, g->nlocal);
   hipLaunchKernelGGL(cg_gen_p_kernel, dim3(nb), dim3(256), 0, g->ctx->stream, r, p, g->nlocal,
-                     (const CgState*)st);
+                     (const CgState*)st, first);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
@@ -139,11 +149,11 @@ int launch_cg_generic_xr(pb_grid* g, const double* p, const double* w, double* x
   return PB_OK;
 }
 
-int launch_cg_pc_xr(pb_grid* g, const double* p, const double* w, double* x, double* r,
-                    CgState* st) {
+int launch_cg_pc_xr(pb_grid* g, const double* p, const double* w, double* x, const double* r_in,
+                    double* r, CgState* st, int first) {
   const int nb = gen_blocks(g->ctx, g->nlocal);
-  hipLaunchKernelGGL(cg_pc_xr_kernel, dim3(nb), dim3(256), 0, g->ctx->stream, p, w, x, r,
-                     g->nlocal, (const CgState*)st);
+  hipLaunchKernelGGL(cg_pc_xr_kernel, dim3(nb), dim3(256), 0, g->ctx->stream, p, w, x, r_in, r,
+                     g->nlocal, (const CgState*)st, first);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }

@@ -22,6 +22,7 @@
 #include <cmath>
 
 #include "pb_internal.hpp"
+#include "pb_device.hpp"
 
 #pragma clang fp contract(fast)
 
@@ -46,6 +47,8 @@ struct LinePass {
   int64_t li, lo, es;  // address of (outer, inner line, element e) = outer*lo + inner*li + e*es
   int ninner, ntiles_inner, nouter, TL, P;
   int ablate;  // tuning only (PB_LINES_ABLATE=1): copy lines through, no solves
+  int remap;   // XCD-aware tile order (PB_LINES_REMAP, default off: Z pass 0.74-0.78 vs 0.715-0.72 ms
+               // at 512^3, profiles/r02/ab_remap_compact.jsonl)
   LineOp J, L;
   const int* skip;  // pb_ctx::op_skip (exit at entry once set)
 };
@@ -301,7 +304,7 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
     nl = min(TL, p.ninner - inner0);
     base = (int64_t)outer * p.lo + (int64_t)inner0 * p.li;
   };
-  int t = blockIdx.x;
+  int t = xcd_block(p.remap);
   if (t >= ntiles) return;
   double keep[LPW][C];
   // one tile: its input registers `pre` go to LDS, then (PF) tile tn's input is fetched into them
@@ -669,6 +672,7 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
   ScopedTimer tm(ctx, names[axis]);
   LinePass p{};
   p.skip = ctx->op_skip;
+  p.remap = env_int("PB_LINES_REMAP", 0);
   static const int ablate = env_int("PB_LINES_ABLATE", 0);
   p.ablate = ablate;
   p.in0 = in0;
@@ -721,6 +725,7 @@ int lines_solve_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_str
   const int C = (int)(n / 64);
   LinePass p{};
   p.skip = ctx->op_skip;
+  p.remap = env_int("PB_LINES_REMAP", 0);
   p.in0 = d;
   p.out0 = d;
   p.J = make_solve_op(alpha, C);

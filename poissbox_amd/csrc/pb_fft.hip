@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "pb_internal.hpp"
+#include "pb_device.hpp"
 
 namespace pb {
 
@@ -43,6 +44,8 @@ struct DhtPass {
   const double* tab;  // [Lx | Jx | Ly | Jy | Lz | Jz] (SCALE only)
   int nx, ny, j0;     // global x / y sizes, global y of the box's row 0 (SCALE only)
   double scale, thr;  // 1 / (nx ny nz) and the null-mode threshold (SCALE only)
+  int remap;          // XCD-aware tile order (PB_FFT_REMAP, default on): consecutive tiles share an
+                      // XCD; Z pass 1.35-1.36 vs 1.375-1.378 ms at 512^3 (ab_remap_fft.jsonl)
 };
 
 struct cplx {
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
   constexpr int n = T::n, NT = T::NT, LP = T::LP;
   if (skip && *skip) return;  // CG's device convergence flag (uniform)
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int tile = blockIdx.x;
+  const int tile = xcd_block(p.remap);
   const int64_t outer = tile / p.ntiles_inner;
   const int inner0 = (tile % p.ntiles_inner) * TL;
   const int64_t base = outer * p.lo + (int64_t)inner0 * p.li;
@@ -464,7 +467,10 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
 // one DHT along an axis of the box b (b[2] = planes), in place or from `in`
 static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, const double* in,
                     double* out, const int* skip, int j0 = 0) {
+  static const char* names[3] = {"pc_fft_x", "pc_fft_y", "pc_fft_z"};
+  ScopedTimer tm(ctx, names[axis]);
   DhtPass p{};
+  p.remap = env_int("PB_FFT_REMAP", 1);
   p.in = in;
   p.out = out;
   p.w = f->tw[axis];

@@ -357,7 +357,7 @@ int yslab_from(pb_grid* g, const YSlabPlan& p, const double* fy, double* f);
 // all-to-all with per-peer counts; blocks are contiguous in rank order on both sides
 int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,
                      const int64_t* rcount);
-int launch_cg_generic_p(pb_grid* g, const double* r, double* p, CgState* st);
+int launch_cg_generic_p(pb_grid* g, const double* r, double* p, CgState* st, int first = 0);
 int launch_cg_generic_dot(pb_grid* g, const double* p, const double* w, CgState* st, int* nparts);
 int launch_cg_generic_xr(pb_grid* g, const double* p, const double* w, double* x, double* r,
                          CgState* st, int* nparts);
@@ -377,8 +377,8 @@ int grid_create_part(pb_ctx* ctx, const int64_t n[3], const double L[3], int64_t
                      pb_grid** out);
 
 // ---- preconditioned CG pieces (pb_cg_generic.hip) ----
-int launch_cg_pc_xr(pb_grid* g, const double* p, const double* w, double* x, double* r,
-                    CgState* st);
+int launch_cg_pc_xr(pb_grid* g, const double* p, const double* w, double* x, const double* r_in,
+                    double* r, CgState* st, int first);
 int launch_cg_pc_sums(pb_grid* g, const double* z, const double* r, CgState* st, int* nparts);
 int cg_finalize_init(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done);
 

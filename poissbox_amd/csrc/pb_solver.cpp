@@ -42,6 +42,7 @@ struct pb_ksp {
   pb::FftPc* fft = nullptr;  // spectral preconditioner (PB_PC_FFT)
   int fold_nparts_b = 0;     // partial-sum blocks of the last folded pass B
   bool stored_z() const { return mg || fft; }  // PCs whose z = M^-1 r is stored (not Jacobi)
+  bool lazy0 = false;  // r0 = b, x0 = 0, p0 = 0 left implicit by pb_ksp_begin
   CgState* d_st = nullptr;
   double* d_hist = nullptr;
   int64_t nhist = 0;
@@ -388,15 +389,22 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
       return set_error(PB_ERR_ALLOC, "CG direction buffers: out of device memory");
   }
   PB_HIP(hipMemcpyAsync(k->d_st, &st, sizeof(st), hipMemcpyHostToDevice, ctx->stream));
+  // stored z with an operator without a stencil engine (compact A): r0 = b, x0 = 0 and p0 = 0 are
+  // implicit -- the setup reads b in place of r, and the first iteration writes p = z, x = alpha p
+  // and r = b - alpha w without reading them (three vector passes fewer)
+  k->lazy0 = k->stored_z() && !fused_kind(k->A->kind) && env_int("PB_KSP_LAZY0", 1) != 0;
   if (k->stored_z()) {
     // r = b, x = 0, p = 0; z = M^-1 r; sums of z (KSPSolve_CG setup, PC_LEFT)
     const size_t vb = (size_t)g->nlocal * sizeof(double);
-    PB_HIP(hipMemcpyAsync(k->r, b->d, vb, hipMemcpyDeviceToDevice, ctx->stream));
-    PB_HIP(hipMemsetAsync(x->d, 0, vb, ctx->stream));
-    PB_HIP(hipMemsetAsync(k->pb[0], 0, vb, ctx->stream));
+    const double* r0 = k->lazy0 ? b->d : k->r;
+    if (!k->lazy0) {
+      PB_HIP(hipMemcpyAsync(k->r, b->d, vb, hipMemcpyDeviceToDevice, ctx->stream));
+      PB_HIP(hipMemsetAsync(x->d, 0, vb, ctx->stream));
+      PB_HIP(hipMemsetAsync(k->pb[0], 0, vb, ctx->stream));
+    }
     int np = 0;
-    PB_TRY(pc_apply_dev(k, k->r, k->z, nullptr, &np));
-    if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
+    PB_TRY(pc_apply_dev(k, r0, k->z, nullptr, &np));
+    if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, r0, k->d_st, &np));
     PB_TRY(cg_finalize_init(ctx, np, k->d_st, k->d_hist, k->h_done_dev));
   } else {
     PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->pb[0], k->d_st, st.dinv, k->d_hist,
@@ -436,14 +444,15 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   pb_ctx* ctx = g->ctx;
   double* p = k->pb[0];
   int np = 0;
-  PB_TRY(launch_cg_generic_p(g, k->z, p, k->d_st));  // dinv = 1: z - mu
+  const int first = k->lazy0 && k->host_iter == 0;  // r0 = b, x0 = 0, p0 = 0 implicit
+  PB_TRY(launch_cg_generic_p(g, k->z, p, k->d_st, first));  // dinv = 1: z - mu
   {
     OpApplySkip guard(ctx, &k->d_st->done);
     PB_TRY(op_apply_raw(k->A, p, k->w));
   }
   PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
   PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
-  PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, k->r, k->d_st));
+  PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, first ? k->b->d : k->r, k->r, k->d_st, first));
   PB_TRY(pc_apply_dev(k, k->r, k->z, &k->d_st->done, &np));
   if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
@@ -589,6 +598,9 @@ int pb_ksp_end(pb_ksp* k, pb_ksp_result* res, double* history, int64_t cap) {
   if (!k->begun) return set_error(PB_ERR_STATE, "pb_ksp_end before pb_ksp_begin");
   pb_ctx* ctx = k->A->grid->ctx;
   PB_SYNC(ctx, "pb_ksp_end");
+  if (k->lazy0 && k->host_iter == 0) {  // stopped at the setup: x = x0 = 0 was never written
+    PB_HIP(hipMemsetAsync(k->x->d, 0, (size_t)k->A->grid->nlocal * sizeof(double), ctx->stream));
+  }
   CgState st;
   PB_HIP(hipMemcpyAsync(&st, k->d_st, sizeof(st), hipMemcpyDeviceToHost, ctx->stream));
   PB_SYNC(ctx, "pb_ksp_end");

@@ -31,9 +31,21 @@ def main():
             k.pc_apply(r, z)
         ctx.sync()
         ms = (time.perf_counter() - t0) * 1e3 / reps
-        cfg = {kk: v for kk, v in os.environ.items() if kk.startswith("PB_FFT")}
+        # per-pass averages (HIP events around each line pass, a separate set of applies)
+        ctx.set_timing(True)
+        ctx.reset_timing()
+        for _ in range(reps):
+            k.pc_apply(r, z)
+        ctx.sync()
+        passes = {}
+        for nm in ("pc_fft_x", "pc_fft_y", "pc_fft_z"):
+            t, c = ctx.timing(nm)
+            if c:
+                passes[nm] = round(t / c, 4)
+        ctx.set_timing(False)
+        cfg = {kk: v for kk, v in os.environ.items() if kk.startswith(("PB_FFT", "PB_LINES"))}
         print(json.dumps({"n": n, "pc_apply_ms": ms, "GBps_80B": 80 * n ** 3 / ms / 1e6,
-                          "cfg": cfg}), flush=True)
+                          "passes_ms": passes, "cfg": cfg}), flush=True)
         for o in (k, r, z, P):
             o.destroy()
         da.destroy()

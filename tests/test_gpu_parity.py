@@ -822,6 +822,42 @@ def test_cg_compact_operator_mg_pc(ctx):
     check_x(x.get_values(), xo)
 
 
+@pytest.mark.parametrize("pc", ["fft", "mg"])
+def test_cg_compact_lazy_initial_state(ctx, monkeypatch, pc):
+    """Stored-z CG on the compact operator leaves r0 = b, x0 = 0 and p0 = 0 implicit
+    (PB_KSP_LAZY0, default on): the setup reads b in place of r and the first iteration writes
+    p = z, x = alpha p, r = b - alpha w without reading them. Same reason, iterations, history and
+    x as the explicit setup passes, whatever x held before (KSPSolve_CG's zero initial guess); a
+    right-hand side that converges at the setup returns x = 0."""
+    m = 64 if pc == "fft" else 32  # the spectral PC takes extents 64..1024
+    n3 = (m, m, m)
+    h = (2 * np.pi / m,) * 3
+    N = m ** 3
+    b = O.lapl(O.fill_random(N, SEED), n3, h)
+    da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+    P = pb.Mat(da, pb.ASSEMBLED27, h)
+    A = pb.Mat(da, pb.COMPACT, h)
+    Pm = A if pc == "fft" else P  # the spectral PC inverts the compact symbol (config 5)
+    opts = ["-pc_type", pc, "-ksp_rtol", "1e-8"]
+    x, bv = pb.Vec(da), pb.Vec(da)
+    res = {}
+    for lazy in ("1", "0"):
+        monkeypatch.setenv("PB_KSP_LAZY0", lazy)
+        x.set_random(99)  # stale content
+        bv.set_values(b)
+        reason, its, hist = pb.solve(Pm, A, x, bv, opts)
+        res[lazy] = (reason, its, np.asarray(hist), x.get_values())
+    (r1, i1, h1, x1), (r0, i0, h0, x0) = res["1"], res["0"]
+    assert (r1, i1) == (r0, i0) and r1 == 2 and i1 >= 1
+    assert np.array_equal(h1, h0) and np.array_equal(x1, x0)
+    monkeypatch.setenv("PB_KSP_LAZY0", "1")
+    x.set_random(99)
+    bv.set_values(np.zeros(N))
+    reason, its, hist = pb.solve(Pm, A, x, bv, opts)
+    assert reason > 0 and its == 0
+    assert np.all(x.get_values() == 0.0)
+
+
 @pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("pc,omega,n3", [("sor", 2.5, (16, 12, 8)), ("mg", 2.2, (16, 16, 16)),
                                          ("mg", 2.2, (32, 32, 32))])
