@@ -31,6 +31,7 @@
 #include "pb_internal.hpp"
 #include "pb_device.hpp"
 
+
 namespace pb {
 
 namespace {
@@ -46,6 +47,12 @@ struct DhtPass {
   double scale, thr;  // 1 / (nx ny nz) and the null-mode threshold (SCALE only)
   int remap;          // XCD-aware tile order (PB_FFT_REMAP, default on): consecutive tiles share an
                       // XCD; Z pass 1.35-1.36 vs 1.375-1.378 ms at 512^3 (ab_remap_fft.jsonl)
+  // CG's residual sums taken by the last pass (X inverse) as it writes z: t = z - mu, over the
+  // tile, against r = sr -> parts[block * 4 + (t, t^2, t r, r)] (cg_pc_sums_kernel's sums)
+  const double* sr;
+  double* parts;
+  const CgState* st;
+  int nparts_out;     // (host) partial blocks written
 };
 
 struct cplx {
@@ -104,19 +111,40 @@ __device__ __forceinline__ double mirror_lane(double v, int lane) {
 }
 
 // lane-dependent twiddles of fft_wave, loaded once per wave before the tile arrives
-template <int C>
+template <int C, bool LAZY = false>
 struct WaveTw {
-  cplx t2[C];   // exp(-2 pi i lane k2 / n), k2 >= 1
-  cplx st[6];   // stage h = 32 >> s: exp(-2 pi i (lane & (h-1)) n / (2h) / n)
+  cplx t2_[C];   // exp(-2 pi i lane k2 / n), k2 >= 1
+  cplx st_[6];   // stage h = 32 >> s: exp(-2 pi i (lane & (h-1)) n / (2h) / n)
   __device__ __forceinline__ void load(const double* w, int lane) {
     constexpr int n = 64 * C;
 #pragma unroll
-    for (int k2 = 1; k2 < C; ++k2) t2[k2] = tw(w, (lane * k2) & (n - 1));
+    for (int k2 = 1; k2 < C; ++k2) t2_[k2] = tw(w, (lane * k2) & (n - 1));
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
       const int h = 32 >> s;
-      st[s] = tw(w, (lane & (h - 1)) * (n / (2 * h)));
+      st_[s] = tw(w, (lane & (h - 1)) * (n / (2 * h)));
     }
+  }
+  __device__ __forceinline__ cplx t2(int k2) const { return t2_[k2]; }
+  __device__ __forceinline__ cplx st(int s) const { return st_[s]; }
+};
+// LAZY: the twiddles are read from the (L1/L2-resident) table where they are used instead of
+// being held in 52 VGPRs for the whole kernel. Taken by the Z pass (two transforms and the symbol
+// scaling) on lines of >= 512 points: 182 -> 144 VGPRs, 2 -> 3 waves per SIMD, 512^3 Z pass
+// 1.356 -> 1.28 ms; on 256-point lines (124 VGPRs, 4 waves either way) it is slower
+// (0.137 vs 0.132 ms, profiles/r02/ab_fft_twlazy.jsonl)
+template <int C>
+struct WaveTw<C, true> {
+  const double* w_;
+  int lane_;
+  __device__ __forceinline__ void load(const double* w, int lane) {
+    w_ = w;
+    lane_ = lane;
+  }
+  __device__ __forceinline__ cplx t2(int k2) const { return tw(w_, (lane_ * k2) & (64 * C - 1)); }
+  __device__ __forceinline__ cplx st(int s) const {
+    const int h = 32 >> s;
+    return tw(w_, (lane_ & (h - 1)) * (64 * C / (2 * h)));
   }
 };
 
@@ -135,8 +163,8 @@ __device__ __forceinline__ void dif_stage(cplx (&z)[C], const cplx wh, int lane)
 
 // z (lane owns elements lane + 64 m, m < C) -> spectrum: lane L holds Z[k2 + C bitrev6(L)] in
 // z[k2]. n = 64 C, w = exp(-2 pi i k / n).
-template <int C>
-__device__ __forceinline__ void fft_wave(cplx (&z)[C], const double* w, const WaveTw<C>& T,
+template <int C, class TW>
+__device__ __forceinline__ void fft_wave(cplx (&z)[C], const double* w, const TW& T,
                                          int lane) {
   constexpr int n = 64 * C, LB = ilog2(C);
   // (1) C-point DFT over m in registers (radix-2 DIT, bit-reversed input order)
@@ -155,14 +183,14 @@ __device__ __forceinline__ void fft_wave(cplx (&z)[C], const double* w, const Wa
       }
   // (2) twiddles exp(-2 pi i lane k2 / n)
 #pragma unroll
-  for (int k2 = 0; k2 < C; ++k2) z[k2] = k2 ? cmul(t[k2], T.t2[k2]) : t[k2];
+  for (int k2 = 0; k2 < C; ++k2) z[k2] = k2 ? cmul(t[k2], T.t2(k2)) : t[k2];
   // (3) 64-point DFT across lanes: radix-2 DIF, partner lane ^ h
-  dif_stage<32>(z, T.st[0], lane);
-  dif_stage<16>(z, T.st[1], lane);
-  dif_stage<8>(z, T.st[2], lane);
-  dif_stage<4>(z, T.st[3], lane);
-  dif_stage<2>(z, T.st[4], lane);
-  dif_stage<1>(z, T.st[5], lane);
+  dif_stage<32>(z, T.st(0), lane);
+  dif_stage<16>(z, T.st(1), lane);
+  dif_stage<8>(z, T.st(2), lane);
+  dif_stage<4>(z, T.st(3), lane);
+  dif_stage<2>(z, T.st(4), lane);
+  dif_stage<1>(z, T.st(5), lane);
 }
 
 // Hartley spectra of the two real lines packed in z (spectrum layout of fft_wave): hx, hy at
@@ -200,8 +228,8 @@ struct DhtTile {
 
 // one DHT of the wave's two lines (pair p) in LDS, in place; SCALE: multiply by s(k) before the
 // write-back (callers run the inverse transform again afterwards)
-template <int C, bool SCALE>
-__device__ __forceinline__ void dht_pair(double* lds, int l0, const DhtPass& p, const WaveTw<C>& T,
+template <int C, bool SCALE, class TW>
+__device__ __forceinline__ void dht_pair(double* lds, int l0, const DhtPass& p, const TW& T,
                                          int lane, int64_t outer, int inner0) {
   constexpr int LP = 64 * C + 1;
   constexpr int n = 64 * C;
@@ -250,7 +278,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 // LAYOUT 1: lines contiguous (es = 1). MODE 0: one DHT; MODE 1: DHT, 1/(N lambda), DHT.
 // One tile per block (a persistent form that prefetched the next tile into registers during the
 // transforms measured 10-30 % slower: twice the VGPRs, half the resident waves).
-template <int C, int TL, int LAYOUT, int MODE>
+template <int C, int TL, int LAYOUT, int MODE, bool SUMS = false>
 __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int* skip) {
   using T = DhtTile<C, TL>;
   constexpr int n = T::n, NT = T::NT, LP = T::LP;
@@ -261,7 +289,7 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
   const int inner0 = (tile % p.ntiles_inner) * TL;
   const int64_t base = outer * p.lo + (int64_t)inner0 * p.li;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  WaveTw<C> twv;
+  WaveTw<C, MODE == 1 && C >= 8> twv;
   twv.load(p.w, lane);  // in flight while the tile loads
   typedef double dv2 __attribute__((ext_vector_type(2)));
   // tile -> LDS (16-byte pairs along the contiguous direction)
@@ -295,6 +323,8 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
     }
   }
   __syncthreads();
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const double mu = SUMS ? p.st->mu : 0.0;
 #pragma unroll 4
   for (int f = threadIdx.x; f < NP; f += NT) {
     int l, e;
@@ -313,7 +343,36 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
       v.x = lds[l * LP + e];
       v.y = lds[l * LP + e + 1];
     }
-    __builtin_nontemporal_store(v, (dv2*)(p.out + base + l * p.li + e * p.es));
+    const int64_t a = base + l * p.li + e * p.es;
+    __builtin_nontemporal_store(v, (dv2*)(p.out + a));
+    if constexpr (SUMS) {
+      const dv2 rv = __builtin_nontemporal_load((const dv2*)(p.sr + a));
+      const double t0 = v.x - mu, t1 = v.y - mu;
+      acc[0] += t0;
+      acc[1] += t0 * t0;
+      acc[2] += t0 * rv.x;
+      acc[3] += rv.x;
+      acc[0] += t1;
+      acc[1] += t1 * t1;
+      acc[2] += t1 * rv.y;
+      acc[3] += rv.y;
+    }
+  }
+  if constexpr (SUMS) {  // fixed-order block reduction: wave butterflies, then waves in order
+    __syncthreads();     // the tile's LDS reads are done
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double v = acc[q];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0) lds[wave * 4 + q] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      double v = lds[threadIdx.x];
+      for (int w = 1; w < NT / 64; ++w) v += lds[w * 4 + threadIdx.x];
+      p.parts[(int64_t)blockIdx.x * 4 + threadIdx.x] = v;
+    }
   }
 }
 
@@ -323,24 +382,37 @@ int launch_dht_tl(pb_ctx* ctx, DhtPass& p, const int* skip) {
   p.ntiles_inner = p.ninner / TL;
   const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
   auto kern = dht_lines_kernel<C, TL, LAYOUT, MODE>;
+  auto kern_s = dht_lines_kernel<C, TL, LAYOUT, MODE, LAYOUT == 1 && MODE == 0>;
   static bool attr = false;
   if (!attr) {
     PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)T::LDS));
+    PB_HIP(hipFuncSetAttribute((const void*)kern_s, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)T::LDS));
     attr = true;
+  }
+  if (p.parts) {
+    if (LAYOUT != 1 || MODE != 0)
+      return set_error(PB_ERR_STATE, "fft pc: residual sums on the X pass only");
+    if (ntiles * 4 > ctx->partials_cap)
+      return set_error(PB_ERR_UNSUPPORTED, "fft pc: %lld tiles exceed the partials capacity",
+                       (long long)ntiles);
+    p.nparts_out = (int)ntiles;
+    kern = kern_s;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(T::NT), T::LDS, ctx->stream, p, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
 
-// lines per tile by pass (PB_FFT_TL_X / _Y / _Z; default 16, 8 for the Z pass -- measured at
-// 512^3: X/Y 16 vs 8 vs 32 lines 0.52 / 0.57 / 0.66 ms, Z 8 lines 1.43 ms vs 1.64 with 16 --
-// and 8 for 1024-long lines): a power of two dividing ninner (>= 64)
+// lines per tile by pass (PB_FFT_TL_X / _Y / _Z; default 16, 8 for the Z pass on lines of >= 512
+// points -- measured at 512^3: X/Y 16 vs 8 vs 32 lines 0.52 / 0.57 / 0.66 ms, Z 8 lines 1.28 ms
+// vs 1.65 with 16; at 256^3 the Z pass is faster with 16, 0.121 vs 0.132 ms -- and 8 for
+// 1024-long lines): a power of two dividing ninner (>= 64)
 template <int C, int LAYOUT, int MODE>
 int launch_dht_c(pb_ctx* ctx, DhtPass& p, const int* skip) {
   const char* knob = LAYOUT == 1 ? "PB_FFT_TL_X" : (MODE == 1 ? "PB_FFT_TL_Z" : "PB_FFT_TL_Y");
-  int tl = env_int(knob, (LAYOUT == 0 && MODE == 1) ? 8 : 16);
+  int tl = env_int(knob, (LAYOUT == 0 && MODE == 1 && C >= 8) ? 8 : 16);
   if (C >= 16 && tl > 8) tl = 8;
   while (tl > 4 && p.ninner % tl) tl /= 2;
   if (p.ninner % tl)
@@ -466,7 +538,8 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
 
 // one DHT along an axis of the box b (b[2] = planes), in place or from `in`
 static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, const double* in,
-                    double* out, const int* skip, int j0 = 0) {
+                    double* out, const int* skip, int j0 = 0, const double* sr = nullptr,
+                    const CgState* st = nullptr, int* np = nullptr) {
   static const char* names[3] = {"pc_fft_x", "pc_fft_y", "pc_fft_z"};
   ScopedTimer tm(ctx, names[axis]);
   DhtPass p{};
@@ -481,7 +554,14 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
     p.es = 1;
     p.ninner = (int)ny;
     p.nouter = (int)nz;
-    return launch_dht<1, 0>(ctx, nx, p, skip);
+    if (np) {  // CG's residual sums ride on this (last) pass
+      p.sr = sr;
+      p.st = st;
+      p.parts = ctx->d_partials;
+    }
+    PB_TRY((launch_dht<1, 0>(ctx, nx, p, skip)));
+    if (np) *np = p.nparts_out;
+    return PB_OK;
   }
   if (axis == 1) {  // inner = i, outer = k, elements along j
     p.li = 1;
@@ -506,7 +586,9 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   return launch_dht<0, 1>(ctx, nz, p, skip);
 }
 
-int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip) {
+int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgState* sums_st,
+                int* nparts) {
+  if (nparts) *nparts = 0;
   pb_grid* g = f->g;
   pb_ctx* ctx = g->ctx;
   ScopedTimer tm(ctx, "pc_fft");
@@ -525,6 +607,9 @@ int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip) {
     PB_TRY(yslab_from(g, yp, fy, z));
   }
   PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
+  // with sums_st: the residual sums of CG (PB_FFT_SUMS, default on) are taken by the last pass
+  static const int fused = env_int("PB_FFT_SUMS", 1);
+  if (sums_st && nparts && fused) return dht_axis(ctx, f, b, 0, z, z, skip, 0, r, sums_st, nparts);
   return dht_axis(ctx, f, b, 0, z, z, skip);
 }
 
