@@ -402,7 +402,10 @@ int mg_plan_levels(const int64_t n[3], int nranks, int levels_req);
 struct FftPc;
 // compact: invert the compact operator's symbol (else the 7-point star's); power-of-two extents
 int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out);
-int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip = nullptr);
+// sums_st / nparts: the last pass also takes CG's residual sums of z against r (mu from sums_st)
+// into ctx->d_partials, *nparts blocks (0: the caller takes them)
+int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip = nullptr,
+                const CgState* sums_st = nullptr, int* nparts = nullptr);
 void fftpc_destroy(FftPc* f);
 
 // ---- context scratch: at least n doubles, valid until the next call on this context ----

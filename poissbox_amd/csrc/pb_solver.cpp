@@ -336,7 +336,7 @@ static int ensure_done_cap(pb_ksp* k, int64_t need) {
 // PC itself (MG's last sweep), 0 if the caller must take the sums
 static int pc_apply_dev(pb_ksp* k, const double* r, double* z, const int* skip, int* np) {
   *np = 0;
-  if (k->fft) return fftpc_apply(k->fft, r, z, skip);
+  if (k->fft) return fftpc_apply(k->fft, r, z, skip, k->d_st, np);
   return mg_apply(k->mg, r, z, skip, k->d_st, np);
 }
 
