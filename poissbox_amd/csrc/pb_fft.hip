@@ -32,6 +32,13 @@
 #include "pb_device.hpp"
 
 
+#ifndef PB_FFT_TW_LAZY
+#define PB_FFT_TW_LAZY 0
+#endif
+#ifndef PB_FFT_SCALE_LDS
+#define PB_FFT_SCALE_LDS 1
+#endif
+
 namespace pb {
 
 namespace {
@@ -128,11 +135,12 @@ struct WaveTw {
   __device__ __forceinline__ cplx t2(int k2) const { return t2_[k2]; }
   __device__ __forceinline__ cplx st(int s) const { return st_[s]; }
 };
-// LAZY: the twiddles are read from the (L1/L2-resident) table where they are used instead of
-// being held in 52 VGPRs for the whole kernel. Taken by the Z pass (two transforms and the symbol
-// scaling) on lines of >= 512 points: 182 -> 144 VGPRs, 2 -> 3 waves per SIMD, 512^3 Z pass
-// 1.356 -> 1.28 ms; on 256-point lines (124 VGPRs, 4 waves either way) it is slower
-// (0.137 vs 0.132 ms, profiles/r02/ab_fft_twlazy.jsonl)
+// LAZY (PB_FFT_TW_LAZY builds, Z pass): the twiddles are read from the (L1/L2-resident) table
+// where they are used instead of being held in 52 VGPRs for the whole kernel. With the symbol
+// scaling in the transform's epilogue the Z pass took 182 VGPRs and LAZY gained (144 VGPRs, 512^3
+// 1.356 -> 1.28 ms, profiles/r02/ab_fft_twlazy.jsonl); with the scaling as its own LDS step
+// (scale_pair) the pass takes 128 VGPRs either way and the register twiddles are faster
+// (1.09 vs 1.19 ms, ab_fft_scale.jsonl)
 template <int C>
 struct WaveTw<C, true> {
   const double* w_;
@@ -274,6 +282,37 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The Z pass's 1/(N lambda) scaling as its own step over the wave's two spectra in LDS (element k
+// of both lines per lane, k = lane + 64 m: coalesced symbol-table reads), between two unscaled
+// transforms -- the same arithmetic as the SCALE epilogue of dht_pair, without its symbol values
+// and spectra live in registers beside the transform's (PB_FFT_SCALE_LDS): 512^3 Z pass 182 -> 128
+// VGPRs, 2 -> 4 waves per SIMD, 1.356 -> 1.09 ms; 256^3 124 -> 88 VGPRs (ab_fft_scale.jsonl)
+template <int C>
+__device__ __forceinline__ void scale_pair(double* lds, int l0, const DhtPass& p, int lane,
+                                           int64_t outer, int inner0) {
+  constexpr int LP = 64 * C + 1;
+  constexpr int n = 64 * C;
+  const int nx = p.nx, ny = p.ny;
+  const int i0 = inner0 + l0, j = p.j0 + (int)outer;
+  const double* Lx = p.tab;
+  const double* Jx = Lx + nx;
+  const double* Ly = Jx + nx;
+  const double* Jy = Ly + ny;
+  const double* Lz = Jy + ny;
+  const double* Jz = Lz + n;
+  const double ly = Ly[j], jy = Jy[j];
+  const double a0 = Lx[i0] * jy + Jx[i0] * ly, c0 = Jx[i0] * jy;
+  const double a1 = Lx[i0 + 1] * jy + Jx[i0 + 1] * ly, c1 = Jx[i0 + 1] * jy;
+#pragma unroll
+  for (int m = 0; m < C; ++m) {
+    const int k = lane + 64 * m;
+    const double lam0 = a0 * Jz[k] + c0 * Lz[k], lam1 = a1 * Jz[k] + c1 * Lz[k];
+    const double hx = lds[l0 * LP + k], hy = lds[(l0 + 1) * LP + k];
+    lds[l0 * LP + k] = fabs(lam0) > p.thr ? hx * (p.scale / lam0) : 0.0;
+    lds[(l0 + 1) * LP + k] = fabs(lam1) > p.thr ? hy * (p.scale / lam1) : 0.0;
+  }
+}
+
 // LAYOUT 0: the tile's lines are adjacent (li = 1), elements strided (rows of TL doubles);
 // LAYOUT 1: lines contiguous (es = 1). MODE 0: one DHT; MODE 1: DHT, 1/(N lambda), DHT.
 // One tile per block (a persistent form that prefetched the next tile into registers during the
@@ -289,7 +328,7 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
   const int inner0 = (tile % p.ntiles_inner) * TL;
   const int64_t base = outer * p.lo + (int64_t)inner0 * p.li;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  WaveTw<C, MODE == 1 && C >= 8> twv;
+  WaveTw<C, MODE == 1 && PB_FFT_TW_LAZY> twv;
   twv.load(p.w, lane);  // in flight while the tile loads
   typedef double dv2 __attribute__((ext_vector_type(2)));
   // tile -> LDS (16-byte pairs along the contiguous direction)
@@ -316,9 +355,13 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
   __syncthreads();
   const int l0 = 2 * wave;
   if (l0 < p.ninner - inner0) {
-    dht_pair<C, MODE == 1>(lds, l0, p, twv, lane, outer, inner0);
+    dht_pair<C, MODE == 1 && !PB_FFT_SCALE_LDS>(lds, l0, p, twv, lane, outer, inner0);
     if (MODE == 1) {
       wave_sync_lds();
+      if (PB_FFT_SCALE_LDS) {
+        scale_pair<C>(lds, l0, p, lane, outer, inner0);
+        wave_sync_lds();
+      }
       dht_pair<C, false>(lds, l0, p, twv, lane, outer, inner0);
     }
   }
