@@ -35,6 +35,15 @@
 #ifndef PB_FFT_TW_LAZY
 #define PB_FFT_TW_LAZY 0
 #endif
+// loads / stores of a tile in flight per thread (#pragma unroll count of the tile copy loops)
+#ifndef PB_FFT_TILE_UNROLL
+#define PB_FFT_TILE_UNROLL 4
+#endif
+#define PB_FFT_STR(x) #x
+#define PB_FFT_UNROLL(n) _Pragma(PB_FFT_STR(unroll n))
+#ifndef PB_FFT_X_WAVE
+#define PB_FFT_X_WAVE 1
+#endif
 #ifndef PB_FFT_SCALE_LDS
 #define PB_FFT_SCALE_LDS 1
 #endif
@@ -331,12 +340,23 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
   WaveTw<C, MODE == 1 && PB_FFT_TW_LAZY> twv;
   twv.load(p.w, lane);  // in flight while the tile loads
   typedef double dv2 __attribute__((ext_vector_type(2)));
-  // tile -> LDS (16-byte pairs along the contiguous direction)
-  constexpr int NP = TL * n / 2;
-#pragma unroll 4
-  for (int f = threadIdx.x; f < NP; f += NT) {
+  // tile -> LDS (16-byte pairs along the contiguous direction). WAVE (X pass, contiguous lines of
+  // <= 256 points): each wave loads and stores only its own two lines, so the block needs no
+  // barrier around the transforms and its waves run independently (PB_FFT_X_WAVE): 256^3 X pass
+  // 0.078 -> 0.062 ms; on 512-point lines it takes 136 VGPRs (3 waves per SIMD) and is slower,
+  // 0.56 vs 0.49 ms (profiles/r02/ab_fft_xwave.jsonl)
+  constexpr bool WAVE = LAYOUT == 1 && PB_FFT_X_WAVE && C <= 4;
+  constexpr int NP = WAVE ? n : TL * n / 2;  // pairs moved by the block (WAVE: by the wave)
+  constexpr int NS = WAVE ? 64 : NT;
+  const int fid = WAVE ? lane : (int)threadIdx.x;
+  const int l0 = 2 * wave;
+  PB_FFT_UNROLL(PB_FFT_TILE_UNROLL)
+  for (int f = fid; f < NP; f += NS) {
     int l, e;
-    if (LAYOUT == 0) {
+    if (WAVE) {
+      l = l0 + f / (n / 2);
+      e = (f % (n / 2)) * 2;
+    } else if (LAYOUT == 0) {
       l = (f % (TL / 2)) * 2;
       e = f / (TL / 2);
     } else {
@@ -352,8 +372,10 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
       lds[l * LP + e + 1] = v.y;
     }
   }
-  __syncthreads();
-  const int l0 = 2 * wave;
+  if (WAVE)
+    wave_sync_lds();
+  else
+    __syncthreads();
   if (l0 < p.ninner - inner0) {
     dht_pair<C, MODE == 1 && !PB_FFT_SCALE_LDS>(lds, l0, p, twv, lane, outer, inner0);
     if (MODE == 1) {
@@ -365,13 +387,19 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
       dht_pair<C, false>(lds, l0, p, twv, lane, outer, inner0);
     }
   }
-  __syncthreads();
+  if (WAVE)
+    wave_sync_lds();
+  else
+    __syncthreads();
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const double mu = SUMS ? p.st->mu : 0.0;
-#pragma unroll 4
-  for (int f = threadIdx.x; f < NP; f += NT) {
+  PB_FFT_UNROLL(PB_FFT_TILE_UNROLL)
+  for (int f = fid; f < NP; f += NS) {
     int l, e;
-    if (LAYOUT == 0) {
+    if (WAVE) {
+      l = l0 + f / (n / 2);
+      e = (f % (n / 2)) * 2;
+    } else if (LAYOUT == 0) {
       l = (f % (TL / 2)) * 2;
       e = f / (TL / 2);
     } else {
