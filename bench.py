@@ -6,8 +6,11 @@ Weak scaling: every GPU owns a 512^3 z-slab worth of DoF; the global grid double
 (N=1: 512^3, N=2: 512x512x1024, N=4: 512x1024x1024, N=8: 1024^3 = SURVEY config 4).
 Strong scaling (--scaling strong [--base 512|1024]): the base^3 grid split over all GPUs.
 N > 1 lines carry per-rank halo / allreduce times (per_rank_comm).
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
-(one rank per GPU; RCCL unique id broadcast over the gloo process group).
+Launch: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either under
+torch.distributed.run (one rank per GPU), or plain: with no WORLD_SIZE in the environment
+bench.py starts the N rank processes itself (self_launch: child processes, no exec, before any
+GPU call) and relays rank 0's line. RCCL unique id broadcast over the gloo process group; the line
+records the transport and the size of the RCCL communicator as RCCL reports it (rccl_nranks).
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -201,6 +204,91 @@ def cpu_baseline(mode="full"):
             "host": info, "rows": rows, "skipped_rows": skipped, "variants": cpu_variants(T)}
 
 
+def self_launch(nranks, argv, timeout_s=None, cmd=None):
+    """`bench.py --gpus N` with no launcher in the environment (no WORLD_SIZE): start the N rank
+    processes here, one per GPU, as torch.distributed.run would (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / a free MASTER_PORT). They are plain child processes started before
+    this process has touched the GPU -- it never does: no HIP call, no torch import, no exec.
+    Rank 0's stdout (the one JSON line) is relayed; every other child output goes to stderr.
+    If a rank fails, the others get PB_BENCH_GRACE_S (30) to finish before their process groups
+    are killed; the whole run is bounded by PB_BENCH_TIMEOUT_S (1800). Returns the exit status:
+    0 only if every rank exited 0 and rank 0 printed its line."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+
+    timeout_s = timeout_s or float(os.environ.get("PB_BENCH_TIMEOUT_S", "1800"))
+    grace_s = float(os.environ.get("PB_BENCH_GRACE_S", "30"))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), PB_BENCH_LAUNCHER="self")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+        procs.append(subprocess.Popen((cmd or [sys.executable, os.path.abspath(__file__)]) + list(argv),
+                                      env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr,
+                                      start_new_session=True))
+    lines = []
+    reader = threading.Thread(target=lambda: lines.extend(
+        l.decode(errors="replace") for l in procs[0].stdout), daemon=True)
+    reader.start()
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+
+    t0 = time.monotonic()
+    failed_at, first_fail = None, 0
+    while any(p.poll() is None for p in procs):
+        now = time.monotonic()
+        bad = [p.poll() for p in procs if p.poll() not in (None, 0)]
+        if failed_at is None and bad:
+            failed_at, first_fail = now, bad[0]
+        if now - t0 > timeout_s or (failed_at is not None and now - failed_at > grace_s):
+            print(f"bench self-launch: {'timeout' if now - t0 > timeout_s else 'a rank failed'};"
+                  f" killing the remaining ranks", file=sys.stderr, flush=True)
+            kill_all()
+            break
+        time.sleep(0.2)
+    codes = [p.wait() for p in procs]
+    reader.join(timeout=10)
+    json_lines = [l for l in lines if l.lstrip().startswith("{")]
+    for l in json_lines[-1:]:
+        sys.stdout.write(l if l.endswith("\n") else l + "\n")
+        sys.stdout.flush()
+    if any(codes):
+        print(f"bench self-launch: rank exit codes {codes}", file=sys.stderr, flush=True)
+        first = first_fail or next(c for c in codes if c)  # the rank that failed first
+        return first if first > 0 else 128 - first  # killed by signal s: 128 + s, as a shell
+    return 0 if json_lines else 1
+
+
+def dry_run(args):
+    """--dry-run: the launch and the control plane only (no GPU call, no library load): every
+    rank joins the gloo group and rank 0 prints one JSON line with the grid it would run and the
+    ranks that joined. Lets the CPU tier check the self-launch path end to end."""
+    from poissbox_amd.dist import init_from_env
+    rank, world, local_rank, dist = init_from_env("gloo")
+    seen = [rank]
+    if dist:
+        seen = [None] * world
+        dist.all_gather_object(seen, (rank, local_rank, os.getpid()))
+    n = global_grid(world, args.base) if args.scaling == "weak" else (args.base,) * 3
+    out = {"dry_run": True, "n_gpus": world, "grid": list(n), "ranks": seen,
+           "launcher": os.environ.get("PB_BENCH_LAUNCHER", "env" if dist else "none")}
+    if dist:
+        dist.destroy_process_group()
+    return out if rank == 0 else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -219,7 +307,16 @@ def main():
     ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                     help="multi-rank transport: RCCL (default) or the gloo host transport "
                          "(lets several ranks share one GPU for testing)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and join the ranks, print the plan; no GPU work")
     args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks here (child processes; this process never touches the GPU)
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+    if world != args.gpus:
+        sys.exit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
 
     # stdout carries exactly one JSON line (rank 0): everything else any library prints on fd 1 --
     # gloo's connection messages, RCCL's version banner -- is sent to stderr
@@ -227,12 +324,11 @@ def main():
     json_fd = os.dup(1)
     os.dup2(2, 1)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            sys.exit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} ranks")
+    if args.dry_run:
+        out = dry_run(args)
+        if out:
+            os.write(json_fd, (json.dumps(out) + "\n").encode())
+        return
 
     import poissbox_amd as pb
     from poissbox_amd.dist import GlooTransport, broadcast_uid, init_from_env
@@ -258,6 +354,8 @@ def main():
     if dist and args.transport == "host":
         tr = GlooTransport(dist)
         ctx.set_host_transport(tr.sendrecv, tr.allreduce)
+    # what the transport itself reports (RCCL: ncclCommCount / ncclCommUserRank)
+    comm_transport, comm_nranks, comm_rank = ctx.comm_info()
     da = pb.initialise_grid(ctx, n)
     h = da.spacing
     P, A, x, b = pb.initialise_linear_system(da, h)
@@ -311,7 +409,8 @@ def main():
     # per-rank communication in the diagnostic iterations: the halo exchange on the comm stream
     # (overlapped with pass A's interior planes), the two scalar allreduces per iteration, and
     # pass A including its wait for the halo
-    comm = {"rank": rank, "iterations": diag_steps}
+    comm = {"rank": rank, "iterations": diag_steps, "device": device,
+            "transport": comm_transport, "comm_nranks": comm_nranks, "comm_rank": comm_rank}
     for nm in ("halo_comm", "allreduce", "cg_pass_a", "halo"):
         ms_, cnt_ = ctx.timing(nm)
         comm[f"{nm}_ms_per_iter"] = ms_ / diag_steps
@@ -407,6 +506,10 @@ def main():
                                  "bytes_per_dof": MATVEC_BYTES},
             },
             "cg_x_update_every": defer,
+            "launcher": os.environ.get("PB_BENCH_LAUNCHER",
+                                       "torch.distributed.run" if dist else "none"),
+            "transport": comm_transport,
+            "rccl_nranks": comm_nranks if comm_transport == "rccl" else None,
             "per_rank_comm": per_rank if world > 1 else None,
             "ksp_state": {"reason": pb.REASONS.get(reason, reason), "its": its,
                           "rnorm0": float(hist[0]), "rnorm_last": float(hist[-1])},

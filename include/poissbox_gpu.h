@@ -55,7 +55,9 @@ int pb_lapl_star_coeffs(double dx, double dy, double dz, double c[27]);
 /* ---- context / communicator (replaces MPI_Init + PetscInitialize, src/example.f90:43-47) ---- */
 /* 128-byte RCCL unique id; rank 0 creates it and the caller broadcasts it (any channel). */
 int pb_comm_unique_id(unsigned char uid[128]);
-/* nranks == 1: uid may be NULL. nranks > 1: uid from rank 0's pb_comm_unique_id. */
+/* nranks == 1: uid may be NULL. nranks > 1: uid from rank 0's pb_comm_unique_id. The RCCL
+ * communicator init is bounded by PB_COMM_TIMEOUT_MS: if not every rank joins in time (a peer
+ * died during start-up, or holds another id) the call returns PB_ERR_COMM instead of blocking. */
 int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb_ctx** ctx);
 /* Test transport: route halo exchange and allreduce through host callbacks instead of RCCL
  * (lets several ranks share one GPU in tests). Must be called before any grid is created.
@@ -80,8 +82,10 @@ int pb_ctx_get_rank(const pb_ctx* ctx, int* rank, int* nranks);
  * or PMI_RANK/PMI_SIZE; one process = rank 0 of 1 on `device` (-1: LOCAL_RANK). Several ranks
  * take GPU LOCAL_RANK mod visible GPUs (PB_DEVICE overrides) and connect over
  *   PB_TRANSPORT=rccl (default when every rank has its own GPU): rank 0's unique id is passed in
- *     a file PB_RENDEZVOUS_DIR/pb_uid_<job> (default /tmp; job = PB_JOB_ID, else MASTER_PORT),
- *     removed once the communicator is up;
+ *     a file PB_RENDEZVOUS_DIR/pb_uid_<job> (default /tmp; job = PB_JOB_ID, else MASTER_PORT,
+ *     plus torchrun's TORCHELASTIC_RESTART_COUNT), removed once the communicator is up; a file
+ *     last written more than PB_RENDEZVOUS_SLACK_S (120) before the reading process started is
+ *     a crashed run's leftover and is ignored (likewise the shm segment below);
  *   PB_TRANSPORT=shm (default when ranks outnumber GPUs): a built-in POSIX shared-memory host
  *     transport (halo planes and scalar sums; ranks may share one GPU; no all-to-all, so the
  *     compact operators need RCCL or a host alltoallv callback on a split grid). */
@@ -97,6 +101,12 @@ int pb_ctx_barrier(pb_ctx* ctx); /* synchronize + all ranks rendezvous */
  * (ncclCommAbort) and returns PB_ERR_COMM, and every later communicating call on the context
  * returns PB_ERR_COMM at once. *failed = 1 after such a failure. */
 int pb_ctx_comm_status(const pb_ctx* ctx, int* failed);
+/* What the context communicates over (≙ MPI_Comm_size of PETSC_COMM_WORLD as the transport
+ * itself sees it): PB_TRANSPORT_RCCL with the communicator's own ncclCommCount /
+ * ncclCommUserRank, PB_TRANSPORT_HOST (host callbacks or the shm transport) with the context's
+ * rank layout, or PB_TRANSPORT_NONE (one rank, wrap planes in place) with 1 / 0. */
+enum pb_transport { PB_TRANSPORT_NONE = 0, PB_TRANSPORT_RCCL = 1, PB_TRANSPORT_HOST = 2 };
+int pb_ctx_comm_info(const pb_ctx* ctx, int* transport, int* comm_nranks, int* comm_rank);
 int pb_ctx_destroy(pb_ctx* ctx);
 /* Per-kernel timing with HIP events on the context's stream (off by default). */
 int pb_ctx_set_timing(pb_ctx* ctx, int enable);

@@ -54,6 +54,7 @@ _SIGS = {
     "pb_ctx_sync": [c_p],
     "pb_ctx_barrier": [c_p],
     "pb_ctx_comm_status": [c_p, C.POINTER(C.c_int)],
+    "pb_ctx_comm_info": [c_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "pb_ctx_create_from_env": [C.c_int, C.POINTER(c_p)],
     "pb_ctx_allreduce_host": [c_p, P_d, C.c_int],
     "pb_ctx_destroy": [c_p],

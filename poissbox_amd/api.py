@@ -153,6 +153,16 @@ class Context:
         L.call("pb_ctx_comm_status", self.h, C.byref(v))
         return bool(v.value)
 
+    TRANSPORTS = {0: "none", 1: "rccl", 2: "host"}
+
+    def comm_info(self):
+        """(transport, communicator size, rank in it) as the transport itself reports them:
+        RCCL's ncclCommCount / ncclCommUserRank, the host transport's rank layout, or
+        ("none", 1, 0) on one rank (pb_ctx_comm_info)."""
+        t, n, r = C.c_int(), C.c_int(), C.c_int()
+        L.call("pb_ctx_comm_info", self.h, C.byref(t), C.byref(n), C.byref(r))
+        return self.TRANSPORTS.get(t.value, t.value), n.value, r.value
+
     def set_timing(self, on=True):
         L.call("pb_ctx_set_timing", self.h, int(bool(on)))
 

@@ -58,12 +58,8 @@ int64_t yslab_len(const pb_grid* g) {
   return d.ny_slab;
 }
 
-// staging (max of the two slab sizes) and the small rank tables (j -> rank, j0, nyl) as
-// doubles-sized slots
-int64_t yslab_aux_len(const pb_grid* g) {
-  const int64_t tables = (g->n[1] + 2 * g->ctx->nranks + 1) / 2 + 1;
-  return std::max<int64_t>(yslab_len(g), g->nlocal) + tables;
-}
+// staging: the larger of the two slab sizes (the rank tables live with the grid)
+int64_t yslab_aux_len(const pb_grid* g) { return std::max<int64_t>(yslab_len(g), g->nlocal); }
 
 int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p) {
   pb_ctx* ctx = g->ctx;
@@ -72,17 +68,26 @@ int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p) {
   make_plan(g, p);
   const int64_t nx = g->n[0], ny = g->n[1];
   p->stage = aux;
-  p->tab = (int*)(aux + std::max<int64_t>(p->ny_slab, g->nlocal));
-  // rank tables (tiny, uploaded per call on the stream)
-  std::vector<int> htab(ny + 2 * P);
-  for (int r = 0; r < P; ++r) {
-    for (int64_t j = p->j0[r]; j < p->j0[r] + p->nyl[r]; ++j) htab[j] = r;
-    htab[ny + r] = (int)p->j0[r];
-    htab[ny + P + r] = (int)p->nyl[r];
+  if (!g->yslab_tab) {
+    // rank tables: built and uploaded once per grid (they depend on the partition only)
+    std::vector<int> htab(ny + 2 * P);
+    for (int r = 0; r < P; ++r) {
+      for (int64_t j = p->j0[r]; j < p->j0[r] + p->nyl[r]; ++j) htab[j] = r;
+      htab[ny + r] = (int)p->j0[r];
+      htab[ny + P + r] = (int)p->nyl[r];
+    }
+    int* tab = nullptr;
+    if (hipMalloc(&tab, htab.size() * sizeof(int)) != hipSuccess)
+      return set_error(PB_ERR_ALLOC, "y-slab rank tables: out of device memory");
+    const hipError_t e =
+        hipMemcpy(tab, htab.data(), htab.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(tab);
+      return set_error(PB_ERR_HIP, "y-slab rank tables: %s", hipGetErrorString(e));
+    }
+    g->yslab_tab = tab;
   }
-  PB_HIP(hipMemcpyAsync(p->tab, htab.data(), htab.size() * sizeof(int), hipMemcpyHostToDevice,
-                        ctx->stream));
-  PB_SYNC(ctx, "compact transpose");  // htab stays valid until the copy is done
+  p->tab = g->yslab_tab;
   p->zc.resize(P);  // z-slab block for rank q; y-slab block from rank q
   p->yc.resize(P);
   for (int q = 0; q < P; ++q) {

@@ -128,6 +128,9 @@ struct pb_grid {
   // ghost2 = [planes -2, -1 | nzl, nzl+1], h_stage2 = host staging (8 planes)
   double* ghost2 = nullptr;
   double* h_stage2 = nullptr;
+  // z-slab <-> y-slab rank tables (j -> rank, j0, nyl; pb_compact_dist.hip), uploaded once on
+  // first use, so the transposes inside CG iterations never wait on the host
+  int* yslab_tab = nullptr;
   // the whole domain on this rank even on a multi-rank context (host-array compact entry points:
   // the reference's module procedures work on process-local arrays)
   bool whole = false;

@@ -7,7 +7,11 @@
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
+#include <string>
+#include <thread>
 #include <unordered_map>
 
 #include "pb_internal.hpp"
@@ -165,8 +169,10 @@ static int bounded_wait(pb_ctx* ctx, Query query, const char* what) {
       if (ms > limit_ms) {
         if (ctx->comm_failed)
           return set_error(PB_ERR_COMM, "%s: still pending after a communication failure", what);
-        return comm_fail(ctx, "%s: no progress for %lld ms (PB_COMM_TIMEOUT_MS); a peer rank "
-                         "is dead or stalled", what, (long long)ms);
+        // the bound covers everything queued ahead of the wait, local kernels included
+        return comm_fail(ctx, "%s: not done after %lld ms (PB_COMM_TIMEOUT_MS bounds every wait "
+                         "on a multi-rank context, queued local work included); a peer rank is "
+                         "dead or stalled", what, (long long)ms);
       }
     }
     if (spin > 4096) {  // past the first few hundred microseconds: back off
@@ -472,6 +478,59 @@ int pb_comm_unique_id(unsigned char uid[128]) {
   return PB_OK;
 }
 
+namespace {
+// ncclCommInitRank bounded by PB_COMM_TIMEOUT_MS. RCCL's bootstrap waits for every rank without
+// a limit, so a peer that dies during start-up (or a rank that was handed a stale unique id)
+// would block the caller forever. The init runs on a helper thread; this thread waits for it with
+// the context's timeout and, on expiry, returns PB_ERR_COMM. There is no communicator handle to
+// abort before ncclCommInitRank returns, so a timed-out helper is detached: should the init ever
+// complete late, the helper destroys the communicator it made. The communicator itself is an
+// ordinary blocking one, so the halo / allreduce calls of the hot path are unchanged.
+struct CommInit {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false, abandoned = false;
+  ncclResult_t rc = ncclSuccess;
+  ncclComm_t comm = nullptr;
+};
+
+int comm_init_bounded(pb_ctx* ctx, int nranks, const ncclUniqueId& id, int rank) {
+  auto st = std::make_shared<CommInit>();
+  const int device = ctx->device;
+  std::thread th([st, device, nranks, id, rank] {
+    (void)hipSetDevice(device);
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
+    std::lock_guard<std::mutex> lk(st->mu);
+    st->rc = r;
+    st->comm = c;
+    st->done = true;
+    if (st->abandoned && r == ncclSuccess && c) (void)ncclCommDestroy(c);
+    st->cv.notify_all();
+  });
+  std::unique_lock<std::mutex> lk(st->mu);
+  const bool ok = st->cv.wait_for(lk, std::chrono::milliseconds(ctx->comm_timeout_ms),
+                                  [&] { return st->done; });
+  if (!ok) {
+    st->abandoned = true;
+    lk.unlock();
+    th.detach();
+    fprintf(stderr, "[poissbox rank %d] RCCL communicator init: not every rank joined within "
+            "%lld ms\n", rank, (long long)ctx->comm_timeout_ms);
+    return set_error(PB_ERR_COMM, "RCCL communicator init (rank %d of %d): not every rank joined "
+                     "within %lld ms (PB_COMM_TIMEOUT_MS); a peer died during start-up or holds "
+                     "another unique id", rank, nranks, (long long)ctx->comm_timeout_ms);
+  }
+  lk.unlock();
+  th.join();
+  if (st->rc != ncclSuccess)
+    return set_error(PB_ERR_COMM, "ncclCommInitRank (rank %d of %d): %s", rank, nranks,
+                     ncclGetErrorString(st->rc));
+  ctx->comm = st->comm;
+  return PB_OK;
+}
+}  // namespace
+
 int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb_ctx** out) {
   PB_CHECK_ARG(out, "ctx out is NULL");
   PB_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank/nranks");
@@ -498,19 +557,45 @@ int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb
   PB_HIP(hipMalloc(&ctx->d_scalars, 64 * sizeof(double)));
   PB_HIP(hipMemsetAsync(ctx->d_scalars, 0, 64 * sizeof(double), ctx->stream));
   PB_HIP(hipHostMalloc(&ctx->h_scalars, 64 * sizeof(double), hipHostMallocDefault));
+  int rc = PB_OK;
   if (nranks > 1 && uid) {
     ncclUniqueId id;
     memcpy(&id, uid, 128);
-    PB_NCCL(ncclCommInitRank(&ctx->comm, nranks, id, rank));
+    rc = comm_init_bounded(ctx, nranks, id, rank);
   }
   ctx->split = nranks > 1;
-  if (nranks == 1 && env_int("PB_FORCE_COMM", 0)) {
+  if (rc == PB_OK && nranks == 1 && env_int("PB_FORCE_COMM", 0)) {
     ncclUniqueId id;
-    PB_NCCL(ncclGetUniqueId(&id));
-    PB_NCCL(ncclCommInitRank(&ctx->comm, 1, id, 0));
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    rc = r == ncclSuccess ? comm_init_bounded(ctx, 1, id, 0)
+                          : set_error(PB_ERR_COMM, "ncclGetUniqueId: %s", ncclGetErrorString(r));
     ctx->split = true;
   }
+  if (rc != PB_OK) {
+    std::string msg = g_err;
+    ctx->split = false;  // nothing communicating is queued: plain teardown
+    pb_ctx_destroy(ctx);
+    return set_error(rc, "%s", msg.c_str());
+  }
   *out = ctx;
+  return PB_OK;
+}
+
+int pb_ctx_comm_info(const pb_ctx* ctx, int* transport, int* comm_nranks, int* comm_rank) {
+  PB_CHECK_ARG(ctx, "ctx is NULL");
+  int t = PB_TRANSPORT_NONE, n = 1, r = 0;
+  if (ctx->comm) {
+    t = PB_TRANSPORT_RCCL;
+    PB_NCCL(ncclCommCount(ctx->comm, &n));
+    PB_NCCL(ncclCommUserRank(ctx->comm, &r));
+  } else if (ctx->h_sendrecv) {
+    t = PB_TRANSPORT_HOST;
+    n = ctx->nranks;
+    r = ctx->rank;
+  }
+  if (transport) *transport = t;
+  if (comm_nranks) *comm_nranks = n;
+  if (comm_rank) *comm_rank = r;
   return PB_OK;
 }
 
@@ -675,6 +760,7 @@ int pb_grid_destroy(pb_grid* g) {
   (void)wait_stream(g->ctx, g->ctx->stream, "pb_grid_destroy");
   (void)hipFree(g->ghost_lo);
   if (g->ghost2) (void)hipFree(g->ghost2);
+  if (g->yslab_tab) (void)hipFree(g->yslab_tab);
   if (g->h_stage) (void)hipHostFree(g->h_stage);
   if (g->h_stage2) (void)hipHostFree(g->h_stage2);
   delete g;

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "pb_internal.hpp"
@@ -261,6 +262,13 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   pb_ksp* k = new pb_ksp();
   k->A = A;
   k->P = P;
+  // every failure below releases what was built so far (pb_ksp_destroy takes a partial KSP:
+  // each field, the PC objects and the state are freed only if they exist)
+  auto fail = [k](int rc) {
+    const std::string msg = pb_last_error();
+    pb_ksp_destroy(k);
+    return set_error(rc, "%s", msg.c_str());
+  };
   if (opts) k->opts = *opts;
   else pb_ksp_opts_default(&k->opts);
   if (k->opts.check_every < 1) k->opts.check_every = 8;
@@ -270,47 +278,33 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
     k->opts.check_every = 2;
   const int pc = k->opts.pc_type;
   if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG &&
-      pc != PB_PC_FFT) {
-    delete k;
-    return set_error(PB_ERR_UNSUPPORTED, "unknown pc_type %d", pc);
-  }
+      pc != PB_PC_FFT)
+    return fail(set_error(PB_ERR_UNSUPPORTED, "unknown pc_type %d", pc));
   pb_grid* g = A->grid;
   const size_t vb = (size_t)g->nlocal * sizeof(double);
   if (pc == PB_PC_SOR || pc == PB_PC_MG) {
     // the smoother / coarse operators are the 7-point P (src/coefficients.f90 star)
-    if (P->kind == PB_OP_COMPACT) {
-      delete k;
-      return set_error(PB_ERR_UNSUPPORTED, "SOR / MG preconditioning needs a 7-point P");
-    }
+    if (P->kind == PB_OP_COMPACT)
+      return fail(set_error(PB_ERR_UNSUPPORTED, "SOR / MG preconditioning needs a 7-point P"));
     const int rc = mg_create(g, P->deltas, pc, k->opts.mg_levels, k->opts.mg_coarse_its,
                              k->opts.sor_omega, &k->mg);
-    if (rc != PB_OK) {
-      delete k;
-      return rc;
-    }
+    if (rc != PB_OK) return fail(rc);
   }
   if (pc == PB_PC_FFT) {
     // the symbol of P: the compact operator (config 5: A = P = compact) or the 7-point star
     const int rc = fftpc_create(g, P->deltas, P->kind == PB_OP_COMPACT, &k->fft);
-    if (rc != PB_OK) {
-      delete k;
-      return rc;
-    }
+    if (rc != PB_OK) return fail(rc);
   }
   if (field_alloc(&k->r, vb) != hipSuccess || field_alloc(&k->pb[0], vb) != hipSuccess ||
-      field_alloc(&k->pb[1], vb) != hipSuccess) {
-    delete k;
-    return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
-  }
+      field_alloc(&k->pb[1], vb) != hipSuccess)
+    return fail(set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory"));
   if (!fused_kind(A->kind) || k->stored_z()) {
-    if (field_alloc(&k->w, vb) != hipSuccess || field_alloc(&k->z, vb) != hipSuccess) {
-      if (k->mg) mg_destroy(k->mg);
-      fftpc_destroy(k->fft);
-      delete k;
-      return set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory");
-    }
+    if (field_alloc(&k->w, vb) != hipSuccess || field_alloc(&k->z, vb) != hipSuccess)
+      return fail(set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory"));
   }
-  PB_HIP(hipMalloc(&k->d_st, 2 * sizeof(CgState)));  // [1]: the folded iteration's second slot
+  // [1]: the folded iteration's second slot
+  if (hipMalloc(&k->d_st, 2 * sizeof(CgState)) != hipSuccess)
+    return fail(set_error(PB_ERR_ALLOC, "KSP state: out of device memory"));
   *out = k;
   return PB_OK;
 }
@@ -662,7 +656,7 @@ int pb_ksp_destroy(pb_ksp* k) {
   field_free(k->z);
   if (k->mg) mg_destroy(k->mg);
   fftpc_destroy(k->fft);
-  (void)hipFree(k->d_st);
+  if (k->d_st) (void)hipFree(k->d_st);
   if (k->d_hist) (void)hipFree(k->d_hist);
   if (k->h_done) (void)hipHostFree(k->h_done);
   for (hipEvent_t e : k->ring) (void)hipEventDestroy(e);

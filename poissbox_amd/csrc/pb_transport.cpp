@@ -40,19 +40,68 @@ int env_first(const char* const* names, int dflt) {
   return dflt;
 }
 
+std::string sanitized(const char* v) {
+  std::string s(v);
+  for (char& c : s)
+    if (!isalnum((unsigned char)c)) c = '_';
+  return s;
+}
+
+// The rendezvous name of this launch: the job (PB_JOB_ID, else the launcher's port / job id) plus
+// torchrun's restart count, so an elastic restart on the same MASTER_PORT never meets the files
+// of the attempt before it.
 std::string job_key() {
   const char* names[] = {"PB_JOB_ID", "MASTER_PORT", "OMPI_MCA_ess_base_jobid", "PMI_JOBID",
                          nullptr};
+  std::string key = "default";
   for (const char* const* n = names; *n; ++n) {
     const char* v = getenv(*n);
     if (v && *v) {
-      std::string s(v);
-      for (char& c : s)
-        if (!isalnum((unsigned char)c)) c = '_';
-      return s;
+      key = sanitized(v);
+      break;
     }
   }
-  return "default";
+  const char* rc = getenv("TORCHELASTIC_RESTART_COUNT");
+  if (rc && *rc) key += "_r" + sanitized(rc);
+  return key;
+}
+
+// Wall-clock start of this process (seconds since the epoch): /proc/self/stat's start time in
+// clock ticks after boot plus /proc/stat's btime. 0 if unavailable.
+double process_start_epoch_s() {
+  double boot = 0.0;
+  if (FILE* f = fopen("/proc/stat", "r")) {
+    char line[256];
+    while (fgets(line, sizeof line, f))
+      if (!strncmp(line, "btime ", 6)) boot = atof(line + 6);
+    fclose(f);
+  }
+  unsigned long long ticks = 0;
+  if (FILE* f = fopen("/proc/self/stat", "r")) {
+    char buf[1024];
+    const size_t n = fread(buf, 1, sizeof buf - 1, f);
+    fclose(f);
+    buf[n] = '\0';
+    const char* p = strrchr(buf, ')');  // the command name may contain spaces
+    for (int field = 2; p && *p && field < 22; ++p)
+      if (*p == ' ') ++field;
+    if (p) ticks = strtoull(p, nullptr, 10);
+  }
+  const long hz = sysconf(_SC_CLK_TCK);
+  if (boot <= 0.0 || !ticks || hz <= 0) return 0.0;
+  return boot + (double)ticks / (double)hz;
+}
+
+// A rendezvous object (uid file, shm segment) last written before this launch began belongs to
+// an earlier run that died before cleaning up: ignore it. "Before this launch" = more than
+// PB_RENDEZVOUS_SLACK_S (default 120) before this process started (the ranks of one launch start
+// within that of each other).
+bool fresh_enough(const struct stat& st) {
+  static const double start = process_start_epoch_s();
+  if (start <= 0.0) return true;
+  const double slack = std::max(0, env_int("PB_RENDEZVOUS_SLACK_S", 120));
+  const double mtime = (double)st.st_mtim.tv_sec + 1e-9 * (double)st.st_mtim.tv_nsec;
+  return mtime >= start - slack;
 }
 
 int64_t now_ms() {
@@ -162,7 +211,8 @@ int shm_attach(pb_ctx* ctx, const std::string& key, Shm** out) {
     for (;;) {  // rank 0 creates the segment and sizes it; wait for both
       fd = shm_open(name.c_str(), O_RDWR, 0600);
       struct stat st;
-      if (fd >= 0 && fstat(fd, &st) == 0 && (size_t)st.st_size == bytes) break;
+      if (fd >= 0 && fstat(fd, &st) == 0 && (size_t)st.st_size == bytes && fresh_enough(st))
+        break;
       if (fd >= 0) close(fd);
       fd = -1;
       if (now_ms() - t0 > ctx->comm_timeout_ms) {
@@ -233,7 +283,9 @@ int uid_rendezvous(int rank, const std::string& key, unsigned char uid[128], int
   for (;;) {
     FILE* f = fopen(path.c_str(), "rb");
     if (f) {
-      const size_t got = fread(uid, 1, 128, f);
+      struct stat st;
+      const bool fresh = fstat(fileno(f), &st) == 0 && fresh_enough(st);
+      const size_t got = fresh ? fread(uid, 1, 128, f) : 0;
       fclose(f);
       if (got == 128) return PB_OK;
     }

@@ -105,6 +105,12 @@ module poissbox_gpu
        type(c_ptr), value :: ctx
        integer(c_int) :: rank, nranks
      end function
+     integer(c_int) function c_pb_ctx_comm_info(ctx, transport, comm_nranks, comm_rank) &
+          bind(C, name="pb_ctx_comm_info")
+       import :: c_int, c_ptr
+       type(c_ptr), value :: ctx
+       integer(c_int) :: transport, comm_nranks, comm_rank
+     end function
      integer(c_int) function c_pb_ctx_allreduce_host(ctx, vals, count) &
           bind(C, name="pb_ctx_allreduce_host")
        import :: c_int, c_ptr, c_double

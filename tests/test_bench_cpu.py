@@ -41,3 +41,51 @@ def test_cpu_rows_and_variants_small():
     v = bench.cpu_variants(2, iters=4)
     assert [r["op"] for r in v] == ["7-point", "faithful 27-term", "faithful 27-term"]
     assert all(r["value"] > 0 for r in v)
+
+
+def test_self_launch_dry_run_two_and_four_ranks():
+    """`bench.py --gpus N` with no launcher in the environment starts the N ranks itself (child
+    processes, no GPU call in the parent) and relays rank 0's single JSON line."""
+    import json
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    for n in (2, 4):
+        p = subprocess.run([sys.executable, bench.__file__, "--gpus", str(n), "--dry-run"],
+                           capture_output=True, text=True, env=env, timeout=120)
+        assert p.returncode == 0, p.stderr[-2000:]
+        lines = [l for l in p.stdout.splitlines() if l.strip()]
+        assert len(lines) == 1, p.stdout
+        out = json.loads(lines[0])
+        assert out["n_gpus"] == n and out["launcher"] == "self"
+        assert [r[0] for r in out["ranks"]] == list(range(n))
+        assert [r[1] for r in out["ranks"]] == list(range(n))  # LOCAL_RANK = device per rank
+        assert len({r[2] for r in out["ranks"]}) == n          # n separate processes
+        assert tuple(out["grid"]) == bench.global_grid(n)
+
+
+def test_self_launch_failing_rank_is_an_error():
+    """A rank that exits non-zero makes the launcher exit non-zero; a rank that hangs is killed
+    after the grace period instead of hanging the run."""
+    import sys
+    fail = ["-c", "import os, sys; sys.exit(3 if os.environ['RANK'] == '1' else 0)"]
+    assert bench.self_launch(2, [], cmd=[sys.executable] + fail) == 3
+    hang = ["-c", "import os, sys, time; print('{}'); sys.stdout.flush(); "
+                  "os.environ['RANK'] == '1' and sys.exit(5); time.sleep(600)"]
+    os_env = __import__("os").environ
+    old = os_env.get("PB_BENCH_GRACE_S")
+    os_env["PB_BENCH_GRACE_S"] = "1"
+    try:
+        import time
+        t0 = time.monotonic()
+        assert bench.self_launch(2, [], cmd=[sys.executable] + hang) == 5
+        assert time.monotonic() - t0 < 60
+    finally:
+        if old is None:
+            os_env.pop("PB_BENCH_GRACE_S")
+        else:
+            os_env["PB_BENCH_GRACE_S"] = old
+    ok = ["-c", "import os; os.environ['RANK'] == '0' and print('{\"metric\": 1}')"]
+    assert bench.self_launch(2, [], cmd=[sys.executable] + ok) == 0
