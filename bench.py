@@ -204,6 +204,19 @@ def cpu_baseline(mode="full"):
             "host": info, "rows": rows, "skipped_rows": skipped, "variants": cpu_variants(T)}
 
 
+def sustained_row(samples, nloc, gbs):
+    """The sustained matvec row from per-launch durations (ms): average, median, and the first /
+    last ten launches' averages (drift under sustained load)."""
+    if not len(samples):
+        return None
+    s = np.asarray(samples, dtype=np.float64)
+    avg = float(s.mean())
+    return {"launches": int(len(s)), "avg_ms": avg, "median_ms": float(np.median(s)),
+            "first10_ms": float(s[:10].mean()), "last10_ms": float(s[-10:].mean()),
+            "GBps": gbs(MATVEC_BYTES, avg / 1e3), "frac": gbs(MATVEC_BYTES, avg / 1e3) / HBM_PEAK_GBS,
+            "bytes_per_dof": MATVEC_BYTES}
+
+
 def self_launch(nranks, argv, timeout_s=None, cmd=None):
     """`bench.py --gpus N` with no launcher in the environment (no WORLD_SIZE): start the N rank
     processes here, one per GPU, as torch.distributed.run would (RANK / LOCAL_RANK / WORLD_SIZE /
@@ -296,6 +309,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--base", type=int, default=512, help="per-GPU cube edge (default 512)")
     ap.add_argument("--matvecs", type=int, default=20)
+    ap.add_argument("--sustained", type=int, default=100,
+                    help="back-to-back matvecs of the sustained-rate row (SURVEY §8(d) (i))")
     ap.add_argument("--grid", default=None,
                     help="nx,ny,nz global grid override (diagnostics; default: weak scaling)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
@@ -437,6 +452,13 @@ def main():
         A.mult(x, y)
     ctx.sync()
     ms_mv, cnt_mv = ctx.timing("stencil")
+    # sustained: SURVEY §8(d) (i)'s 100 back-to-back matvecs, HIP events around each launch; the
+    # first and last ten show whether the rate drifts under sustained load (clocks, heat)
+    ctx.reset_timing()
+    for _ in range(args.sustained):
+        A.mult(x, y)
+    ctx.sync()
+    mv_s = ctx.timing_samples("stencil")
     ctx.set_timing(False)
 
     nloc = da.nlocal
@@ -505,6 +527,7 @@ def main():
                                  "dofs_per_s": nloc / t_mv if t_mv > 0 else 0.0,
                                  "bytes_per_dof": MATVEC_BYTES},
             },
+            "matvec_star7_sustained": sustained_row(mv_s, nloc, gbs),
             "cg_x_update_every": defer,
             "launcher": os.environ.get("PB_BENCH_LAUNCHER",
                                        "torch.distributed.run" if dist else "none"),

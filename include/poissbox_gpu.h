@@ -112,6 +112,11 @@ int pb_ctx_destroy(pb_ctx* ctx);
 int pb_ctx_set_timing(pb_ctx* ctx, int enable);
 /* name: "stencil", "cg_pass_a", "cg_pass_b", ...; returns total ms and launch count since reset */
 int pb_ctx_get_timing(pb_ctx* ctx, const char* name, double* total_ms, int64_t* count);
+/* The per-launch durations behind pb_ctx_get_timing (the first 65536 since the last reset):
+ * copies min(cap, *count) of them into ms; *count = how many there are. Lets a caller tell the
+ * launches that ran from those that exited at entry (a converged solve's enqueued-ahead work). */
+int pb_ctx_get_timing_samples(pb_ctx* ctx, const char* name, float* ms, int64_t cap,
+                              int64_t* count);
 int pb_ctx_reset_timing(pb_ctx* ctx);
 
 /* ---- slab partition (replaces DMDACreate3d's PETSC_DECIDE split, src/poissbox.f90:191-202) ---- */

@@ -171,6 +171,16 @@ class Context:
         L.call("pb_ctx_get_timing", self.h, name.encode(), C.byref(ms), C.byref(cnt))
         return ms.value, cnt.value
 
+    def timing_samples(self, name):
+        """Per-launch durations (ms) of a timed phase since the last reset (numpy float32)."""
+        cnt = C.c_int64()
+        L.call("pb_ctx_get_timing_samples", self.h, name.encode(), None, 0, C.byref(cnt))
+        out = np.zeros(cnt.value, dtype=np.float32)
+        if cnt.value:
+            L.call("pb_ctx_get_timing_samples", self.h, name.encode(),
+                   out.ctypes.data_as(C.POINTER(C.c_float)), cnt.value, C.byref(cnt))
+        return out
+
     def reset_timing(self):
         L.call("pb_ctx_reset_timing", self.h)
 

@@ -53,7 +53,9 @@ int set_error(int code, const char* fmt, ...);
 struct TimerSlot {
   double total_ms = 0.0;
   int64_t count = 0;
+  std::vector<float> samples;  // per-launch ms, the first kMaxTimerSamples since the last reset
 };
+constexpr size_t kMaxTimerSamples = 1 << 16;
 
 }  // namespace pb
 

@@ -120,6 +120,7 @@ void timers_collect(pb_ctx* ctx) {
     TimerSlot& t = ctx->timers[p.first];
     t.total_ms += ms;
     t.count += 1;
+    if (t.samples.size() < kMaxTimerSamples) t.samples.push_back(ms);
     ctx->event_pool.push_back(p.second.first);
     ctx->event_pool.push_back(p.second.second);
   }
@@ -695,6 +696,17 @@ int pb_ctx_get_timing(pb_ctx* ctx, const char* name, double* total_ms, int64_t* 
   auto it = ctx->timers.find(name);
   if (total_ms) *total_ms = it == ctx->timers.end() ? 0.0 : it->second.total_ms;
   if (count) *count = it == ctx->timers.end() ? 0 : it->second.count;
+  return PB_OK;
+}
+
+int pb_ctx_get_timing_samples(pb_ctx* ctx, const char* name, float* ms, int64_t cap,
+                               int64_t* count) {
+  PB_CHECK_ARG(ctx && name && count && (ms || cap == 0) && cap >= 0, "bad args");
+  timers_collect(ctx);
+  auto it = ctx->timers.find(name);
+  const int64_t n = it == ctx->timers.end() ? 0 : (int64_t)it->second.samples.size();
+  for (int64_t i = 0; i < std::min(n, cap); ++i) ms[i] = it->second.samples[(size_t)i];
+  *count = n;
   return PB_OK;
 }
 

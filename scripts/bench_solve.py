@@ -51,14 +51,26 @@ def main():
             reason, its, hist = k.solve(b, x)
             ctx.sync()
             dt = time.perf_counter() - t0
-            mg_ms, mg_cnt = ctx.timing("pc_fft" if pc == "fft" else "mg_apply")
+            # per-launch averages over the launches that ran: the host enqueues iterations ahead
+            # of its lagged convergence poll, and the launches after convergence exit at entry
+            # (pb_ctx::op_skip, a few us) -- they are told apart by their duration and left out;
+            # each part is divided by its own count of launches that ran
+            def ran(nm):
+                s = ctx.timing_samples(nm)
+                if not len(s):
+                    return None
+                keep = s[s > 0.1 * float(s.max())]
+                return {"avg_ms": float(keep.mean()), "launches": int(len(keep)),
+                        "skipped": int(len(s) - len(keep))}
+            pc_t = ran("pc_fft" if pc == "fft" else "mg_apply")
             parts = {}
             for nm in ("mg_fine_smooth_first", "mg_fine_resid_restrict", "mg_fine_prolong_post",
                        "mg_coarse_levels", "cg_pass_a", "cg_pass_b", "cg_pass_b_even",
-                       "cg_pass_b_odd", "cg_pass_b_x4", "compact_lapl_fast"):
-                ms_, c_ = ctx.timing(nm)
-                if c_ and mg_cnt:
-                    parts[nm] = ms_ / mg_cnt
+                       "cg_pass_b_odd", "cg_pass_b_x4", "compact_lapl_fast", "cg_gen_p",
+                       "cg_gen_dot", "cg_pc_xr", "pc_fft_x", "pc_fft_y", "pc_fft_z"):
+                t_ = ran(nm)
+                if t_:
+                    parts[nm] = t_
             ctx.set_timing(False)
             r = pb.Vec(da)
             A.mult(x, r)
@@ -66,8 +78,8 @@ def main():
             out = {"n": n, "op": op, "pc": pc, "reason": int(reason), "its": int(its), "solve_ms": dt * 1e3,
                    "ms_per_it": dt * 1e3 / max(its, 1), "levels": k.pc_levels,
                    "rel_residual": r.norm() / b.norm(),
-                   "pc_apply_ms": (mg_ms / mg_cnt) if mg_cnt else None,
-                   "per_apply_ms": parts}
+                   "pc_apply_ms": pc_t["avg_ms"] if pc_t else None,
+                   "pc_applies": pc_t, "per_launch": parts}
             print(json.dumps(out), flush=True)
             r.destroy()
             k.destroy()

@@ -89,3 +89,12 @@ def test_self_launch_failing_rank_is_an_error():
             os_env["PB_BENCH_GRACE_S"] = old
     ok = ["-c", "import os; os.environ['RANK'] == '0' and print('{\"metric\": 1}')"]
     assert bench.self_launch(2, [], cmd=[sys.executable] + ok) == 0
+
+
+def test_sustained_row():
+    import numpy as np
+    gbs = lambda b, t: b * 1000 / t / 1e9
+    r = bench.sustained_row(np.r_[np.full(10, 1.0), np.full(80, 1.5), np.full(10, 2.0)], 1000, gbs)
+    assert r["launches"] == 100 and r["first10_ms"] == 1.0 and r["last10_ms"] == 2.0
+    assert abs(r["avg_ms"] - 1.5) < 1e-12 and r["median_ms"] == 1.5
+    assert bench.sustained_row([], 1, gbs) is None
