@@ -18,12 +18,18 @@
 // Z forward * 1/(N lambda) * Z inverse (one kernel), Y inverse, X inverse. On a split grid the Z
 // pass runs on y-slabs with complete z-lines (the compact operators' z-slab <-> y-slab transposes).
 //
-// Line kernel: a block loads a tile of TL lines into LDS (coalesced rows), each wave takes two
-// real lines x, y and runs ONE complex FFT of z = x + i y of length n = 64*C: C-point DFTs in
-// registers (lane owns elements lane + 64 m), twiddles, then a 64-point DFT across the lanes by six
-// radix-2 decimation-in-frequency stages over wave shuffles (output in bit-reversed lane order);
-// the two Hartley spectra follow from Z(k) and Z(-k) (one more shuffle), and go back to LDS in
-// natural order for the coalesced store. Twiddles come from a per-axis table exp(-2 pi i k / n).
+// Line kernel (r03): a block stages a tile of TL lines in LDS (coalesced rows: TL x-adjacent lines
+// give TL*8-byte row pieces on the strided passes, 128 B at TL = 16 -- 64-B pieces cap that pattern
+// at ~2.6 TB/s, scripts/zpass_probe.hip), each wave takes two real lines x, y and runs ONE complex
+// FFT of z = x + i y in place in LDS as a self-sorting Stockham transform: passes of radix 8
+// (then 4, 2, 3, 5) -- every lane reads R elements n/R apart, twiddles them, runs the R-point DFT in
+// registers and writes them back at (j / Ns) Ns R + j % Ns + r Ns. The two Hartley spectra follow
+// from Z(k) and Z(n - k), read from LDS. Line lengths n = 2^a 3^b 5^c (a >= 1) in 32..1024. The
+// element index is padded by one double every 16 in LDS, so the scattered writes of the first
+// pass hit distinct banks. Twiddles exp(-2 pi i k / n) come from a per-axis table, copied into LDS
+// per block for n <= 512. (r02's engine ran the 64-point cross-lane part of the transform as six
+// radix-2 stages of DPP / permlane exchanges: 2.5x the VALU work, and its Z pass, which runs two
+// transforms, was compute-bound at 1.0-1.1 ms at 512^3 whatever the tile width.)
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -31,22 +37,7 @@
 #include "pb_internal.hpp"
 #include "pb_device.hpp"
 
-
-#ifndef PB_FFT_TW_LAZY
-#define PB_FFT_TW_LAZY 0
-#endif
-// loads / stores of a tile in flight per thread (#pragma unroll count of the tile copy loops)
-#ifndef PB_FFT_TILE_UNROLL
-#define PB_FFT_TILE_UNROLL 4
-#endif
-#define PB_FFT_STR(x) #x
-#define PB_FFT_UNROLL(n) _Pragma(PB_FFT_STR(unroll n))
-#ifndef PB_FFT_X_WAVE
-#define PB_FFT_X_WAVE 1
-#endif
-#ifndef PB_FFT_SCALE_LDS
-#define PB_FFT_SCALE_LDS 1
-#endif
+#pragma clang fp contract(fast)
 
 namespace pb {
 
@@ -77,211 +68,95 @@ struct cplx {
 __device__ __forceinline__ cplx cmul(cplx a, cplx b) {
   return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
-__device__ __forceinline__ cplx tw(const double* w, int k) { return {w[2 * k], w[2 * k + 1]}; }
+__device__ __forceinline__ cplx cadd(cplx a, cplx b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cplx csub(cplx a, cplx b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cplx cmi(cplx a) { return {a.im, -a.re}; }  // -i a
+__device__ __forceinline__ cplx cpi(cplx a) { return {-a.im, a.re}; }  // +i a
+__device__ __forceinline__ cplx cscale(cplx a, double s) { return {a.re * s, a.im * s}; }
 
-__host__ __device__ constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v >> 1); }
-__host__ __device__ constexpr int bitrev(int v, int bits) {
-  int r = 0;
-  for (int b = 0; b < bits; ++b) r |= ((v >> b) & 1) << (bits - 1 - b);
-  return r;
+// ---- Stockham plans: n = 2^a 3^b 5^c; radix 8 while 8 divides what is left, then 4, 2, 3, 5 ----
+__host__ __device__ constexpr int plan_radix_at(int n, int p) {
+  int rest = n;
+  for (int q = 0; q <= p; ++q) {
+    if (rest <= 1) return 0;
+    const int r = rest % 8 == 0 ? 8
+                  : rest % 4 == 0 ? 4
+                  : rest % 2 == 0 ? 2
+                  : rest % 3 == 0 ? 3
+                  : rest % 5 == 0 ? 5 : 0;
+    if (r == 0) return 0;
+    if (q == p) return r;
+    rest /= r;
+  }
+  return 0;
+}
+__host__ __device__ constexpr bool plan_complete(int n) {
+  int rest = n;
+  for (int p = 0; rest > 1; ++p) {
+    const int r = plan_radix_at(n, p);
+    if (r == 0) return false;
+    rest /= r;
+  }
+  return true;
 }
 
-// ---- lane exchanges without LDS: value of lane ^ H (H = 1..32) and of lane ^ 63 ----
-// H = 1, 2: DPP quad_perm; 4, 8: DPP row shifts up / down and a select; 16, 32: the gfx950
-// permlane swaps. All VALU: no LDS round trip per FFT stage (the r02 first cut used
-// __shfl_xor = ds_bpermute, twice per double).
-template <int CTRL>
-__device__ __forceinline__ int dpp32(int v) {
-  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true);  // bound_ctrl: no old operand
-}
-template <int H>
-__device__ __forceinline__ int xor_lane32(int v, int lane) {
-  if constexpr (H == 1) return dpp32<0xB1>(v);  // quad_perm [1, 0, 3, 2]
-  else if constexpr (H == 2) return dpp32<0x4E>(v);  // quad_perm [2, 3, 0, 1]
-  else if constexpr (H == 4 || H == 8) {
-    const int up = dpp32<0x100 + H>(v);  // row_shl:H -> lane + H
-    const int dn = dpp32<0x110 + H>(v);  // row_shr:H -> lane - H
-    return (lane & H) ? dn : up;
-  } else if constexpr (H == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (lane & 16) ? (int)r[0] : (int)r[1];
+// LDS index of element e in a line: one pad double every 16 (bank spread of the pass writes)
+__host__ __device__ constexpr int lpad(int e) { return e + (e >> 4); }
+
+// ---- R-point DFTs in registers, forward (exp(-2 pi i j k / R)) ----
+template <int R>
+__device__ __forceinline__ void dft(cplx (&v)[R]) {
+  if constexpr (R == 2) {
+    const cplx a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  } else if constexpr (R == 3) {
+    constexpr double c1 = -0.5, s1 = -0.86602540378443864676;  // cos, sin(-2 pi / 3)
+    const cplx t = cadd(v[1], v[2]), d = csub(v[1], v[2]);
+    const cplx m = {v[0].re + c1 * t.re, v[0].im + c1 * t.im};
+    v[0] = cadd(v[0], t);
+    const cplx sd = cscale(cpi(d), s1);  // i s1 d
+    v[1] = cadd(m, sd);
+    v[2] = csub(m, sd);
+  } else if constexpr (R == 4) {
+    const cplx t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    const cplx t2 = cadd(v[1], v[3]), t3 = csub(v[1], v[3]);
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, cmi(t3));
+    v[3] = csub(t1, cmi(t3));
+  } else if constexpr (R == 5) {
+    constexpr double c1 = 0.30901699437494742410, c2 = -0.80901699437494742410;  // cos 2pi/5, 4pi/5
+    constexpr double s1 = -0.95105651629515357212, s2 = -0.58778525229247312917;  // -sin 2pi/5, 4pi/5
+    const cplx b1 = cadd(v[1], v[4]), b2 = cadd(v[2], v[3]);
+    const cplx d1 = csub(v[1], v[4]), d2 = csub(v[2], v[3]);
+    const cplx a0 = v[0];
+    const cplx m1 = {a0.re + c1 * b1.re + c2 * b2.re, a0.im + c1 * b1.im + c2 * b2.im};
+    const cplx m2 = {a0.re + c2 * b1.re + c1 * b2.re, a0.im + c2 * b1.im + c1 * b2.im};
+    const cplx e1 = cpi({s1 * d1.re + s2 * d2.re, s1 * d1.im + s2 * d2.im});
+    const cplx e2 = cpi({s2 * d1.re - s1 * d2.re, s2 * d1.im - s1 * d2.im});
+    v[0] = cadd(a0, cadd(b1, b2));
+    v[1] = cadd(m1, e1);
+    v[4] = csub(m1, e1);
+    v[2] = cadd(m2, e2);
+    v[3] = csub(m2, e2);
   } else {
-    static_assert(H == 32, "xor_lane32: H in {1, 2, 4, 8, 16, 32}");
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return (lane & 32) ? (int)r[0] : (int)r[1];
-  }
-}
-template <int H>
-__device__ __forceinline__ double xor_lane(double v, int lane) {
-  const long long b = __builtin_bit_cast(long long, v);
-  const int lo = xor_lane32<H>((int)b, lane), hi = xor_lane32<H>((int)(b >> 32), lane);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-// lane ^ 63 = row_mirror (lane ^ 15), then ^ 16, ^ 32
-__device__ __forceinline__ double mirror_lane(double v, int lane) {
-  const long long b = __builtin_bit_cast(long long, v);
-  int lo = dpp32<0x140>((int)b), hi = dpp32<0x140>((int)(b >> 32));
-  lo = xor_lane32<32>(xor_lane32<16>(lo, lane), lane);
-  hi = xor_lane32<32>(xor_lane32<16>(hi, lane), lane);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-
-// lane-dependent twiddles of fft_wave, loaded once per wave before the tile arrives
-template <int C, bool LAZY = false>
-struct WaveTw {
-  cplx t2_[C];   // exp(-2 pi i lane k2 / n), k2 >= 1
-  cplx st_[6];   // stage h = 32 >> s: exp(-2 pi i (lane & (h-1)) n / (2h) / n)
-  __device__ __forceinline__ void load(const double* w, int lane) {
-    constexpr int n = 64 * C;
-#pragma unroll
-    for (int k2 = 1; k2 < C; ++k2) t2_[k2] = tw(w, (lane * k2) & (n - 1));
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int h = 32 >> s;
-      st_[s] = tw(w, (lane & (h - 1)) * (n / (2 * h)));
-    }
-  }
-  __device__ __forceinline__ cplx t2(int k2) const { return t2_[k2]; }
-  __device__ __forceinline__ cplx st(int s) const { return st_[s]; }
-};
-// LAZY (PB_FFT_TW_LAZY builds, Z pass): the twiddles are read from the (L1/L2-resident) table
-// where they are used instead of being held in 52 VGPRs for the whole kernel. With the symbol
-// scaling in the transform's epilogue the Z pass took 182 VGPRs and LAZY gained (144 VGPRs, 512^3
-// 1.356 -> 1.28 ms, profiles/r02/ab_fft_twlazy.jsonl); with the scaling as its own LDS step
-// (scale_pair) the pass takes 128 VGPRs either way and the register twiddles are faster
-// (1.09 vs 1.19 ms, ab_fft_scale.jsonl)
-template <int C>
-struct WaveTw<C, true> {
-  const double* w_;
-  int lane_;
-  __device__ __forceinline__ void load(const double* w, int lane) {
-    w_ = w;
-    lane_ = lane;
-  }
-  __device__ __forceinline__ cplx t2(int k2) const { return tw(w_, (lane_ * k2) & (64 * C - 1)); }
-  __device__ __forceinline__ cplx st(int s) const {
-    const int h = 32 >> s;
-    return tw(w_, (lane_ & (h - 1)) * (64 * C / (2 * h)));
-  }
-};
-
-template <int H, int C>
-__device__ __forceinline__ void dif_stage(cplx (&z)[C], const cplx wh, int lane) {
-  const bool upper = lane & H;
-#pragma unroll
-  for (int k2 = 0; k2 < C; ++k2) {
-    const cplx p = {xor_lane<H>(z[k2].re, lane), xor_lane<H>(z[k2].im, lane)};
-    if (upper)
-      z[k2] = cmul({p.re - z[k2].re, p.im - z[k2].im}, wh);
-    else
-      z[k2] = {z[k2].re + p.re, z[k2].im + p.im};
-  }
-}
-
-// z (lane owns elements lane + 64 m, m < C) -> spectrum: lane L holds Z[k2 + C bitrev6(L)] in
-// z[k2]. n = 64 C, w = exp(-2 pi i k / n).
-template <int C, class TW>
-__device__ __forceinline__ void fft_wave(cplx (&z)[C], const double* w, const TW& T,
-                                         int lane) {
-  constexpr int n = 64 * C, LB = ilog2(C);
-  // (1) C-point DFT over m in registers (radix-2 DIT, bit-reversed input order)
-  cplx t[C];
-#pragma unroll
-  for (int i = 0; i < C; ++i) t[i] = z[bitrev(i, LB)];
-#pragma unroll
-  for (int len = 2; len <= C; len <<= 1)
-#pragma unroll
-    for (int i = 0; i < C; i += len)
-#pragma unroll
-      for (int j = 0; j < len / 2; ++j) {
-        const cplx u = t[i + j], v = cmul(t[i + j + len / 2], tw(w, j * (n / len)));
-        t[i + j] = {u.re + v.re, u.im + v.im};
-        t[i + j + len / 2] = {u.re - v.re, u.im - v.im};
-      }
-  // (2) twiddles exp(-2 pi i lane k2 / n)
-#pragma unroll
-  for (int k2 = 0; k2 < C; ++k2) z[k2] = k2 ? cmul(t[k2], T.t2(k2)) : t[k2];
-  // (3) 64-point DFT across lanes: radix-2 DIF, partner lane ^ h
-  dif_stage<32>(z, T.st(0), lane);
-  dif_stage<16>(z, T.st(1), lane);
-  dif_stage<8>(z, T.st(2), lane);
-  dif_stage<4>(z, T.st(3), lane);
-  dif_stage<2>(z, T.st(4), lane);
-  dif_stage<1>(z, T.st(5), lane);
-}
-
-// Hartley spectra of the two real lines packed in z (spectrum layout of fft_wave): hx, hy at
-// k = k2 + C bitrev6(lane)
-template <int C>
-__device__ __forceinline__ void hartley_split(const cplx (&z)[C], double (&hx)[C], double (&hy)[C],
-                                              int lane) {
-  const int k1 = bitrev(lane, 6);
-#pragma unroll
-  for (int k2 = 0; k2 < C; ++k2) {
-    // partner -k mod n: k2 = 0 -> (0, -k1 mod 64), lane bitrev6((64 - k1) & 63) (a bpermute);
-    // else (C - k2, 63 - k1), lane bitrev6(63 - k1) = lane ^ 63
-    const int k2p = k2 == 0 ? 0 : C - k2;
-    cplx m;
-    if (k2 == 0) {
-      const int src = bitrev((64 - k1) & 63, 6);
-      m = {__shfl(z[0].re, src, 64), __shfl(z[0].im, src, 64)};
-    } else {
-      m = {mirror_lane(z[k2p].re, lane), mirror_lane(z[k2p].im, lane)};
-    }
-    hx[k2] = 0.5 * ((z[k2].re + m.re) - (z[k2].im - m.im));
-    hy[k2] = 0.5 * ((z[k2].im + m.im) + (z[k2].re - m.re));
-  }
-}
-
-template <int C, int TL_>
-struct DhtTile {
-  static constexpr int n = 64 * C;
-  static constexpr int TL = TL_;       // lines per tile (LDS: TL * (n + 1) doubles)
-  static constexpr int NW = TL / 2;    // waves: two lines each
-  static constexpr int NT = 64 * NW;
-  static constexpr int LP = n + 1;     // odd line pitch: column writes spread over banks
-  static constexpr size_t LDS = (size_t)TL * LP * sizeof(double);
-};
-
-// one DHT of the wave's two lines (pair p) in LDS, in place; SCALE: multiply by s(k) before the
-// write-back (callers run the inverse transform again afterwards)
-template <int C, bool SCALE, class TW>
-__device__ __forceinline__ void dht_pair(double* lds, int l0, const DhtPass& p, const TW& T,
-                                         int lane, int64_t outer, int inner0) {
-  constexpr int LP = 64 * C + 1;
-  constexpr int n = 64 * C;
-  cplx z[C];
-#pragma unroll
-  for (int m = 0; m < C; ++m) z[m] = {lds[l0 * LP + lane + 64 * m], lds[(l0 + 1) * LP + lane + 64 * m]};
-  fft_wave<C>(z, p.w, T, lane);
-  double hx[C], hy[C];
-  hartley_split<C>(z, hx, hy, lane);
-  const int k1 = bitrev(lane, 6);
-  if constexpr (SCALE) {  // Z pass: line (i, j) -> kx = i, ky = j; element -> kz
-    const int nx = p.nx, ny = p.ny;
-    const int i0 = inner0 + l0, j = p.j0 + (int)outer;
-    const double* Lx = p.tab;
-    const double* Jx = Lx + nx;
-    const double* Ly = Jx + nx;
-    const double* Jy = Ly + ny;
-    const double* Lz = Jy + ny;
-    const double* Jz = Lz + n;
-    const double ly = Ly[j], jy = Jy[j];
-    const double a0 = Lx[i0] * jy + Jx[i0] * ly, c0 = Jx[i0] * jy;
-    const double a1 = Lx[i0 + 1] * jy + Jx[i0 + 1] * ly, c1 = Jx[i0 + 1] * jy;
-#pragma unroll
-    for (int k2 = 0; k2 < C; ++k2) {
-      const int k = k2 + C * k1;
-      const double lam0 = a0 * Jz[k] + c0 * Lz[k], lam1 = a1 * Jz[k] + c1 * Lz[k];
-      hx[k2] = fabs(lam0) > p.thr ? hx[k2] * (p.scale / lam0) : 0.0;
-      hy[k2] = fabs(lam1) > p.thr ? hy[k2] * (p.scale / lam1) : 0.0;
-    }
-  }
-#pragma unroll
-  for (int k2 = 0; k2 < C; ++k2) {
-    const int k = k2 + C * k1;
-    lds[l0 * LP + k] = hx[k2];
-    lds[(l0 + 1) * LP + k] = hy[k2];
+    static_assert(R == 8, "radix 2, 3, 4, 5 or 8");
+    constexpr double h = 0.70710678118654752440;
+    cplx e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+    dft<4>(e);
+    dft<4>(o);
+    const cplx w1 = {h * (o[1].re + o[1].im), h * (o[1].im - o[1].re)};   // (1 - i)/sqrt2 o1
+    const cplx w2 = cmi(o[2]);                                               // -i o2
+    const cplx w3 = {h * (o[3].im - o[3].re), -h * (o[3].re + o[3].im)};  // (-1 - i)/sqrt2 o3
+    v[0] = cadd(e[0], o[0]);
+    v[4] = csub(e[0], o[0]);
+    v[1] = cadd(e[1], w1);
+    v[5] = csub(e[1], w1);
+    v[2] = cadd(e[2], w2);
+    v[6] = csub(e[2], w2);
+    v[3] = cadd(e[3], w3);
+    v[7] = csub(e[3], w3);
   }
 }
 
@@ -291,142 +166,296 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// The Z pass's 1/(N lambda) scaling as its own step over the wave's two spectra in LDS (element k
-// of both lines per lane, k = lane + 64 m: coalesced symbol-table reads), between two unscaled
-// transforms -- the same arithmetic as the SCALE epilogue of dht_pair, without its symbol values
-// and spectra live in registers beside the transform's (PB_FFT_SCALE_LDS): 512^3 Z pass 182 -> 128
-// VGPRs, 2 -> 4 waves per SIMD, 1.356 -> 1.09 ms; 256^3 124 -> 88 VGPRs (ab_fft_scale.jsonl)
-template <int C>
-__device__ __forceinline__ void scale_pair(double* lds, int l0, const DhtPass& p, int lane,
-                                           int64_t outer, int inner0) {
-  constexpr int LP = 64 * C + 1;
-  constexpr int n = 64 * C;
-  const int nx = p.nx, ny = p.ny;
-  const int i0 = inner0 + l0, j = p.j0 + (int)outer;
+// One Stockham pass of radix R over the wave's two lines (A = re, B = im rows in LDS), after
+// NS points of every sub-transform are done. tw: (re, im) of exp(-2 pi i k / N) (LDS or global).
+template <int N, int R, int NS>
+__device__ __forceinline__ void stockham_pass(double* A, double* B, const double* tw, int lane) {
+  constexpr int NB = N / R, T = (NB + 63) / 64;
+  cplx v[T][R];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int j = lane + 64 * t;
+    if (NB % 64 == 0 || j < NB) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = lpad(j + r * NB);
+        v[t][r] = {A[e], B[e]};
+      }
+      if constexpr (NS > 1) {
+        const int k = j % NS;
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          const int wi = r * k * (N / (NS * R));
+          v[t][r] = cmul(v[t][r], {tw[2 * wi], tw[2 * wi + 1]});
+        }
+      }
+      dft<R>(v[t]);
+    }
+  }
+  wave_sync_lds();
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int j = lane + 64 * t;
+    if (NB % 64 == 0 || j < NB) {
+      const int d = (j / NS) * NS * R + j % NS;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = lpad(d + r * NS);
+        A[e] = v[t][r].re;
+        B[e] = v[t][r].im;
+      }
+    }
+  }
+  wave_sync_lds();
+}
+
+template <int N, int P, int NS>
+__device__ __forceinline__ void fft_passes(double* A, double* B, const double* tw, int lane) {
+  constexpr int R = plan_radix_at(N, P);
+  if constexpr (R != 0) {
+    stockham_pass<N, R, NS>(A, B, tw, lane);
+    fft_passes<N, P + 1, NS * R>(A, B, tw, lane);
+  }
+}
+
+// DHT of the two real lines in rows A, B (in place, natural order): FFT of z = x + i y, then
+// H_x(k) = Re X - Im X, H_y(k) = Re Y - Im Y with X, Y from Z(k) and Z(-k)
+template <int N>
+__device__ __forceinline__ void dht2(double* A, double* B, const double* tw, int lane) {
+  fft_passes<N, 0, 1>(A, B, tw, lane);
+  constexpr int T = (N + 63) / 64;
+  double hx[T], hy[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int k = lane + 64 * t;
+    if (N % 64 == 0 || k < N) {
+      const int m = k == 0 ? 0 : N - k;
+      const double zr = A[lpad(k)], zi = B[lpad(k)], mr = A[lpad(m)], mi = B[lpad(m)];
+      hx[t] = 0.5 * ((zr + mr) - (zi - mi));
+      hy[t] = 0.5 * ((zi + mi) + (zr - mr));
+    }
+  }
+  wave_sync_lds();
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int k = lane + 64 * t;
+    if (N % 64 == 0 || k < N) {
+      A[lpad(k)] = hx[t];
+      B[lpad(k)] = hy[t];
+    }
+  }
+  wave_sync_lds();
+}
+
+// The Z pass's 1/(N lambda) on the wave's two spectra (lines i0, i0 + 1 at row j): element k of
+// both lines per lane, coalesced symbol-table reads; 1/lambda := 0 on the null modes
+template <int N>
+__device__ __forceinline__ void scale2(double* A, double* B, const DhtPass& p, int lane,
+                                       int64_t outer, int i0) {
+  const int nx = p.nx, ny = p.ny, j = p.j0 + (int)outer;
   const double* Lx = p.tab;
   const double* Jx = Lx + nx;
   const double* Ly = Jx + nx;
   const double* Jy = Ly + ny;
   const double* Lz = Jy + ny;
-  const double* Jz = Lz + n;
+  const double* Jz = Lz + N;
   const double ly = Ly[j], jy = Jy[j];
   const double a0 = Lx[i0] * jy + Jx[i0] * ly, c0 = Jx[i0] * jy;
   const double a1 = Lx[i0 + 1] * jy + Jx[i0 + 1] * ly, c1 = Jx[i0 + 1] * jy;
-#pragma unroll
-  for (int m = 0; m < C; ++m) {
-    const int k = lane + 64 * m;
-    const double lam0 = a0 * Jz[k] + c0 * Lz[k], lam1 = a1 * Jz[k] + c1 * Lz[k];
-    const double hx = lds[l0 * LP + k], hy = lds[(l0 + 1) * LP + k];
-    lds[l0 * LP + k] = fabs(lam0) > p.thr ? hx * (p.scale / lam0) : 0.0;
-    lds[(l0 + 1) * LP + k] = fabs(lam1) > p.thr ? hy * (p.scale / lam1) : 0.0;
+  constexpr int T = (N + 63) / 64;
+#pragma unroll 2
+  for (int t = 0; t < T; ++t) {
+    const int k = lane + 64 * t;
+    if (N % 64 == 0 || k < N) {
+      const double lam0 = a0 * Jz[k] + c0 * Lz[k], lam1 = a1 * Jz[k] + c1 * Lz[k];
+      const int e = lpad(k);
+      A[e] = fabs(lam0) > p.thr ? A[e] * (p.scale / lam0) : 0.0;
+      B[e] = fabs(lam1) > p.thr ? B[e] * (p.scale / lam1) : 0.0;
+    }
   }
+  wave_sync_lds();
 }
 
+template <int N, int TL_>
+struct DhtTile {
+  static constexpr int TL = TL_;              // lines per tile
+  static constexpr int NW = TL / 2;           // waves: two lines each
+  static constexpr int NT = 64 * NW;
+  static constexpr int LP = (lpad(N - 1) + 1) | 1;  // line pitch (doubles), odd
+  static constexpr bool TWL = N <= 512;       // twiddle table in LDS (else read from L1/L2)
+  static constexpr int TWO = TL * LP;         // twiddle table offset (even: TL is)
+  static constexpr size_t LDS = (size_t)(TWO + (TWL ? 2 * N : 0)) * sizeof(double);
+};
+
+// tile lines per block: 16 (8 waves), 8 for 1024-point lines (LDS)
+template <int N>
+constexpr int tile_lines() { return N > 512 ? 8 : 16; }
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
 // LAYOUT 0: the tile's lines are adjacent (li = 1), elements strided (rows of TL doubles);
-// LAYOUT 1: lines contiguous (es = 1). MODE 0: one DHT; MODE 1: DHT, 1/(N lambda), DHT.
-// One tile per block (a persistent form that prefetched the next tile into registers during the
-// transforms measured 10-30 % slower: twice the VGPRs, half the resident waves).
-template <int C, int TL, int LAYOUT, int MODE, bool SUMS = false>
-__global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int* skip) {
-  using T = DhtTile<C, TL>;
-  constexpr int n = T::n, NT = T::NT, LP = T::LP;
+// LAYOUT 1: lines contiguous (es = 1), each wave loads / stores its own two lines (no block
+// barrier around the transforms). MODE 0: one DHT; MODE 1: DHT, 1/(N lambda), DHT.
+// Persistent blocks (as many as are resident) walk the tiles; the next tile's input is fetched
+// into registers while the current one is transformed and stored, so HBM reads overlap the
+// transforms (+32 VGPRs at n = 512; occupancy stays LDS-bound at two blocks per CU).
+template <int N, int LAYOUT, int MODE, bool SUMS>
+__global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_lines_kernel(
+    DhtPass p, const int* skip) {
+  using T = DhtTile<N, tile_lines<N>()>;
+  constexpr int TL = T::TL, NT = T::NT, LP = T::LP;
   if (skip && *skip) return;  // CG's device convergence flag (uniform)
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int tile = xcd_block(p.remap);
-  const int64_t outer = tile / p.ntiles_inner;
-  const int inner0 = (tile % p.ntiles_inner) * TL;
-  const int64_t base = outer * p.lo + (int64_t)inner0 * p.li;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  WaveTw<C, MODE == 1 && PB_FFT_TW_LAZY> twv;
-  twv.load(p.w, lane);  // in flight while the tile loads
-  typedef double dv2 __attribute__((ext_vector_type(2)));
-  // tile -> LDS (16-byte pairs along the contiguous direction). WAVE (X pass, contiguous lines of
-  // <= 256 points): each wave loads and stores only its own two lines, so the block needs no
-  // barrier around the transforms and its waves run independently (PB_FFT_X_WAVE): 256^3 X pass
-  // 0.078 -> 0.062 ms; on 512-point lines it takes 136 VGPRs (3 waves per SIMD) and is slower,
-  // 0.56 vs 0.49 ms (profiles/r02/ab_fft_xwave.jsonl)
-  constexpr bool WAVE = LAYOUT == 1 && PB_FFT_X_WAVE && C <= 4;
-  constexpr int NP = WAVE ? n : TL * n / 2;  // pairs moved by the block (WAVE: by the wave)
-  constexpr int NS = WAVE ? 64 : NT;
-  const int fid = WAVE ? lane : (int)threadIdx.x;
   const int l0 = 2 * wave;
-  PB_FFT_UNROLL(PB_FFT_TILE_UNROLL)
-  for (int f = fid; f < NP; f += NS) {
-    int l, e;
-    if (WAVE) {
-      l = l0 + f / (n / 2);
-      e = (f % (n / 2)) * 2;
-    } else if (LAYOUT == 0) {
+  const double* tw = p.w;
+  if constexpr (T::TWL) {
+    double* twl = lds + T::TWO;
+    for (int i = threadIdx.x; i < N; i += NT) {
+      const dv2 v = *(const dv2*)(p.w + 2 * i);
+      twl[2 * i] = v.x;
+      twl[2 * i + 1] = v.y;
+    }
+    tw = twl;
+  }
+  // tile t: lines [inner0, inner0 + nl) of row `outer`
+  const int ntiles = p.ntiles_inner * p.nouter;
+  auto tile_of = [&](int t, int64_t& outer, int& inner0, int& nl, int64_t& base) {
+    outer = t / p.ntiles_inner;
+    inner0 = (t % p.ntiles_inner) * TL;
+    nl = min(TL, p.ninner - inner0);  // even: every extent is
+    base = outer * p.lo + (int64_t)inner0 * p.li;
+  };
+  // 16-byte pairs along the contiguous direction; WAVE (LAYOUT 1): a wave moves its own lines
+  constexpr bool WAVE = LAYOUT == 1;
+  constexpr int NP = WAVE ? N : TL * N / 2;  // pairs moved by the block (WAVE: by the wave)
+  constexpr int NS = WAVE ? 64 : NT;
+  constexpr int NR = (NP + NS - 1) / NS;    // pairs per thread (the last round may be partial)
+  const int fid = WAVE ? lane : (int)threadIdx.x;
+  // (l, e) of the thread's q-th pair; l = TL (no line) past the tile's pairs
+  // (the thread index goes through an empty asm per use: recomputing (l, e) costs a few VALU
+  // ops, while letting the compiler hoist every pair's coordinates and addresses out of the tile
+  // loop held ~50 more VGPRs and halved the resident waves)
+  auto coord = [&](int q, int& l, int& e) {
+    int fv = fid;
+    asm volatile("" : "+v"(fv));
+    const int f = fv + q * NS;
+    if (NP % NS != 0 && f >= NP) {
+      l = TL;
+      e = 0;
+    } else if (WAVE) {
+      l = l0 + f / (N / 2);
+      e = (f % (N / 2)) * 2;
+    } else {
       l = (f % (TL / 2)) * 2;
       e = f / (TL / 2);
-    } else {
-      l = f / (n / 2);
-      e = (f % (n / 2)) * 2;
     }
-    const dv2 v = __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es));
-    if (LAYOUT == 0) {
-      lds[l * LP + e] = v.x;
-      lds[(l + 1) * LP + e] = v.y;
-    } else {
-      lds[l * LP + e] = v.x;
-      lds[l * LP + e + 1] = v.y;
-    }
-  }
-  if (WAVE)
-    wave_sync_lds();
-  else
-    __syncthreads();
-  if (l0 < p.ninner - inner0) {
-    dht_pair<C, MODE == 1 && !PB_FFT_SCALE_LDS>(lds, l0, p, twv, lane, outer, inner0);
-    if (MODE == 1) {
-      wave_sync_lds();
-      if (PB_FFT_SCALE_LDS) {
-        scale_pair<C>(lds, l0, p, lane, outer, inner0);
-        wave_sync_lds();
+  };
+  constexpr bool PF = N <= 512;
+  dv2 pre[PF ? NR : 1];
+  auto fetch = [&](int t) {
+    int64_t outer, base;
+    int inner0, nl;
+    tile_of(t, outer, inner0, nl, base);
+    if constexpr (PF) {
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        int l, e;
+        coord(q, l, e);
+        if (l < nl)
+          pre[q] = __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es));
       }
-      dht_pair<C, false>(lds, l0, p, twv, lane, outer, inner0);
     }
-  }
-  if (WAVE)
-    wave_sync_lds();
-  else
-    __syncthreads();
+  };
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const double mu = SUMS ? p.st->mu : 0.0;
-  PB_FFT_UNROLL(PB_FFT_TILE_UNROLL)
-  for (int f = fid; f < NP; f += NS) {
-    int l, e;
-    if (WAVE) {
-      l = l0 + f / (n / 2);
-      e = (f % (n / 2)) * 2;
-    } else if (LAYOUT == 0) {
-      l = (f % (TL / 2)) * 2;
-      e = f / (TL / 2);
-    } else {
-      l = f / (n / 2);
-      e = (f % (n / 2)) * 2;
+  // PF: prefetch the next tile into registers (lines of <= 512 points; longer lines have no
+  // registers to spare: their tile is loaded where it is needed)
+  const int G = gridDim.x;
+  int t = blockIdx.x;
+  if (PF && t < ntiles) fetch(t);
+  for (; t < ntiles; t += G) {
+    int64_t outer, base;
+    int inner0, nl;
+    tile_of(t, outer, inner0, nl, base);
+
+    if (WAVE)
+      wave_sync_lds();
+    else
+      __syncthreads();  // the previous tile's LDS reads are done (and the twiddle table is in)
+    auto put = [&](int l, int e, dv2 v) {
+      if (LAYOUT == 0) {
+        lds[l * LP + lpad(e)] = v.x;
+        lds[(l + 1) * LP + lpad(e)] = v.y;
+      } else {
+        lds[l * LP + lpad(e)] = v.x;
+        lds[l * LP + lpad(e + 1)] = v.y;
+      }
+    };
+    if constexpr (PF) {
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        int l, e;
+        coord(q, l, e);
+        if (l < nl) put(l, e, pre[q]);
+      }
+    } else {  // a few loads in flight at a time (registers)
+#pragma unroll 4
+      for (int q = 0; q < NR; ++q) {
+        int l, e;
+        coord(q, l, e);
+        if (l < nl)
+          put(l, e, __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es)));
+      }
     }
-    dv2 v;
-    if (LAYOUT == 0) {
-      v.x = lds[l * LP + e];
-      v.y = lds[(l + 1) * LP + e];
-    } else {
-      v.x = lds[l * LP + e];
-      v.y = lds[l * LP + e + 1];
+    if (WAVE && t == (int)blockIdx.x)
+      __syncthreads();  // first tile: the twiddle table (written by the whole block) is in
+    else if (WAVE)
+      wave_sync_lds();
+    else
+      __syncthreads();
+    if (PF && t + G < ntiles) fetch(t + G);  // in flight during the transforms and the stores
+    if (l0 < nl) {
+      double* A = lds + l0 * LP;
+      double* B = A + LP;
+      dht2<N>(A, B, tw, lane);
+      if constexpr (MODE == 1) {
+        scale2<N>(A, B, p, lane, outer, inner0 + l0);
+        dht2<N>(A, B, tw, lane);
+      }
     }
-    const int64_t a = base + l * p.li + e * p.es;
-    __builtin_nontemporal_store(v, (dv2*)(p.out + a));
-    if constexpr (SUMS) {
-      const dv2 rv = __builtin_nontemporal_load((const dv2*)(p.sr + a));
-      const double t0 = v.x - mu, t1 = v.y - mu;
-      acc[0] += t0;
-      acc[1] += t0 * t0;
-      acc[2] += t0 * rv.x;
-      acc[3] += rv.x;
-      acc[0] += t1;
-      acc[1] += t1 * t1;
-      acc[2] += t1 * rv.y;
-      acc[3] += rv.y;
+    if (WAVE)
+      wave_sync_lds();
+    else
+      __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      int l, e;
+      coord(q, l, e);
+      if (l < nl) {
+        dv2 v;
+        if (LAYOUT == 0) {
+          v.x = lds[l * LP + lpad(e)];
+          v.y = lds[(l + 1) * LP + lpad(e)];
+        } else {
+          v.x = lds[l * LP + lpad(e)];
+          v.y = lds[l * LP + lpad(e + 1)];
+        }
+        const int64_t a = base + l * p.li + e * p.es;
+        __builtin_nontemporal_store(v, (dv2*)(p.out + a));
+        if constexpr (SUMS) {
+          const dv2 rv = __builtin_nontemporal_load((const dv2*)(p.sr + a));
+          const double t0 = v.x - mu, t1 = v.y - mu;
+          acc[0] += t0;
+          acc[1] += t0 * t0;
+          acc[2] += t0 * rv.x;
+          acc[3] += rv.x;
+          acc[0] += t1;
+          acc[1] += t1 * t1;
+          acc[2] += t1 * rv.y;
+          acc[3] += rv.y;
+        }
+      }
     }
   }
   if constexpr (SUMS) {  // fixed-order block reduction: wave butterflies, then waves in order
@@ -447,72 +476,71 @@ __global__ __launch_bounds__(32 * TL) void dht_lines_kernel(DhtPass p, const int
   }
 }
 
-template <int C, int TL, int LAYOUT, int MODE>
-int launch_dht_tl(pb_ctx* ctx, DhtPass& p, const int* skip) {
-  using T = DhtTile<C, TL>;
-  p.ntiles_inner = p.ninner / TL;
+template <int N, int LAYOUT, int MODE>
+int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
+  using T = DhtTile<N, tile_lines<N>()>;
+  if (p.ninner % 2)
+    return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines (even counts only)", p.ninner);
+  p.ntiles_inner = (p.ninner + T::TL - 1) / T::TL;
   const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
-  auto kern = dht_lines_kernel<C, TL, LAYOUT, MODE>;
-  auto kern_s = dht_lines_kernel<C, TL, LAYOUT, MODE, LAYOUT == 1 && MODE == 0>;
-  static bool attr = false;
-  if (!attr) {
+  auto kern = dht_lines_kernel<N, LAYOUT, MODE, false>;
+  auto kern_s = dht_lines_kernel<N, LAYOUT, MODE, LAYOUT == 1 && MODE == 0>;
+  static int occ = 0;
+  if (!occ) {
     PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)T::LDS));
     PB_HIP(hipFuncSetAttribute((const void*)kern_s, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)T::LDS));
-    attr = true;
+    PB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern_s, T::NT, T::LDS));
+    if (occ < 1) occ = 1;
   }
+  // persistent: one resident round of blocks (PB_FFT_BLOCKS_PER_CU overrides, tuning)
+  static const int bpc = env_int("PB_FFT_BLOCKS_PER_CU", 0);
+  int64_t nblocks = (int64_t)(bpc > 0 ? bpc : occ) * ctx->num_cus;
+  if (nblocks > ntiles) nblocks = ntiles;
   if (p.parts) {
     if (LAYOUT != 1 || MODE != 0)
       return set_error(PB_ERR_STATE, "fft pc: residual sums on the X pass only");
-    if (ntiles * 4 > ctx->partials_cap)
-      return set_error(PB_ERR_UNSUPPORTED, "fft pc: %lld tiles exceed the partials capacity",
-                       (long long)ntiles);
-    p.nparts_out = (int)ntiles;
+    if (nblocks * 4 > ctx->partials_cap)
+      return set_error(PB_ERR_UNSUPPORTED, "fft pc: %lld blocks exceed the partials capacity",
+                       (long long)nblocks);
+    p.nparts_out = (int)nblocks;
     kern = kern_s;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(T::NT), T::LDS, ctx->stream, p, skip);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(T::NT), T::LDS, ctx->stream, p, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
 
-// lines per tile by pass (PB_FFT_TL_X / _Y / _Z; default 16, 8 for the Z pass on lines of >= 512
-// points -- measured at 512^3: X/Y 16 vs 8 vs 32 lines 0.52 / 0.57 / 0.66 ms, Z 8 lines 1.28 ms
-// vs 1.65 with 16; at 256^3 the Z pass is faster with 16, 0.121 vs 0.132 ms -- and 8 for
-// 1024-long lines): a power of two dividing ninner (>= 64)
-template <int C, int LAYOUT, int MODE>
-int launch_dht_c(pb_ctx* ctx, DhtPass& p, const int* skip) {
-  const char* knob = LAYOUT == 1 ? "PB_FFT_TL_X" : (MODE == 1 ? "PB_FFT_TL_Z" : "PB_FFT_TL_Y");
-  int tl = env_int(knob, (LAYOUT == 0 && MODE == 1 && C >= 8) ? 8 : 16);
-  if (C >= 16 && tl > 8) tl = 8;
-  while (tl > 4 && p.ninner % tl) tl /= 2;
-  if (p.ninner % tl)
-    return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines do not tile", p.ninner);
-  switch (tl) {
-    case 32:
-      if constexpr (C < 16) return launch_dht_tl<C, 32, LAYOUT, MODE>(ctx, p, skip);
-      break;
-    case 16: return launch_dht_tl<C, 16, LAYOUT, MODE>(ctx, p, skip);
-    case 8: return launch_dht_tl<C, 8, LAYOUT, MODE>(ctx, p, skip);
-    default: return launch_dht_tl<C, 4, LAYOUT, MODE>(ctx, p, skip);
-  }
-  return launch_dht_tl<C, 8, LAYOUT, MODE>(ctx, p, skip);
-}
+// the line lengths with a compiled transform: 2^a (32..1024), 3 * 2^a (48..768), 5 * 2^a (40..640)
+#define PB_FFT_LENGTHS(X) \
+  X(32) X(64) X(128) X(256) X(512) X(1024) X(48) X(96) X(192) X(384) X(768) X(40) X(80) \
+  X(160) X(320) X(640)
 
 template <int LAYOUT, int MODE>
 int launch_dht(pb_ctx* ctx, int64_t n, DhtPass& p, const int* skip) {
   switch (n) {
-    case 64: return launch_dht_c<1, LAYOUT, MODE>(ctx, p, skip);
-    case 128: return launch_dht_c<2, LAYOUT, MODE>(ctx, p, skip);
-    case 256: return launch_dht_c<4, LAYOUT, MODE>(ctx, p, skip);
-    case 512: return launch_dht_c<8, LAYOUT, MODE>(ctx, p, skip);
-    case 1024: return launch_dht_c<16, LAYOUT, MODE>(ctx, p, skip);
+#define PB_FFT_CASE(L)                                                 \
+  case L:                                                              \
+    static_assert(plan_complete(L), "length without a Stockham plan"); \
+    return launch_dht_n<L, LAYOUT, MODE>(ctx, p, skip);
+    PB_FFT_LENGTHS(PB_FFT_CASE)
+#undef PB_FFT_CASE
   }
-  return set_error(PB_ERR_UNSUPPORTED, "fft pc: line length %lld (64..1024, power of two)",
+  return set_error(PB_ERR_UNSUPPORTED,
+                   "fft pc: line length %lld (2^a 32..1024, 3*2^a 48..768, 5*2^a 40..640)",
                    (long long)n);
 }
 
-bool dht_length_ok(int64_t n) { return n >= 64 && n <= 1024 && (n & (n - 1)) == 0; }
+bool dht_length_ok(int64_t n) {
+  switch (n) {
+#define PB_FFT_OK(L) case L:
+    PB_FFT_LENGTHS(PB_FFT_OK)
+#undef PB_FFT_OK
+    return true;
+  }
+  return false;
+}
 
 }  // namespace
 
@@ -549,8 +577,8 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
   for (int d = 0; d < 3; ++d)
     if (!dht_length_ok(g->n[d]))
       return set_error(PB_ERR_UNSUPPORTED,
-                       "-pc_type fft: every grid extent must be a power of two in 64..1024 "
-                       "(got %lld x %lld x %lld)",
+                       "-pc_type fft: every grid extent must be 2^a (32..1024), 3*2^a (48..768) "
+                       "or 5*2^a (40..640) (got %lld x %lld x %lld)",
                        (long long)g->n[0], (long long)g->n[1], (long long)g->n[2]);
   if (grid_split(g) && g->n[1] < g->ctx->nranks)
     return set_error(PB_ERR_UNSUPPORTED, "-pc_type fft: ny < ranks");

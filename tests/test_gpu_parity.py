@@ -944,7 +944,10 @@ def _fft_case(n3, compact):
 
 @pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 256), (256, 128, 64), (1024, 64, 64),
-                                (64, 1024, 64), (64, 64, 512)])
+                                (64, 1024, 64), (64, 64, 512), (32, 32, 32),
+                                # mixed radix (r03): 3 * 2^a and 5 * 2^a line lengths
+                                (96, 96, 96), (48, 80, 40), (192, 160, 128), (64, 768, 48),
+                                (640, 40, 32), (384, 32, 320)])
 def test_fft_pc_apply_vs_oracle(ctx, n3, compact):
     N = int(np.prod(n3))
     h, kind = _fft_case(n3, compact)
@@ -988,7 +991,8 @@ def test_cg_fft_pc_matches_oracle(ctx, n3, compact):
 
 
 @pytest.mark.parametrize("compact", [False, True])
-@pytest.mark.parametrize("nranks,n3", [(2, (64, 64, 64)), (4, (128, 64, 64)), (3, (64, 64, 64))])
+@pytest.mark.parametrize("nranks,n3", [(2, (64, 64, 64)), (4, (128, 64, 64)), (3, (64, 64, 64)),
+                                       (2, (96, 80, 48)), (3, (40, 96, 96))])
 def test_multirank_fft_pc(nranks, n3, compact):
     """Split grid: the Z pass runs on y-slabs (z-slab <-> y-slab transposes); per-rank result
     equals the single-grid oracle."""
@@ -1040,8 +1044,31 @@ def test_multirank_cg_compact_fft(nranks):
         check_x(xs, xo.reshape(n3[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
 
 
+@pytest.mark.parametrize("n3", [(96, 96, 96), (192, 160, 128)])
+def test_cg_compact_fft_mixed_radix(ctx, n3):
+    """Config 5 beyond powers of two: compact A = P on 3 * 2^a and 5 * 2^a extents, spectral PC
+    (mixed-radix Stockham transforms), CG to rtol 1e-10 -- the oracle's reason / its / x."""
+    N = int(np.prod(n3))
+    h = tuple(2 * np.pi / m for m in n3)
+    b = O.lapl(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-10, pc="fft", op="compact", nthreads=8)
+    assert ro == 2 and itso <= 3
+    da = pb.DA(ctx, n3, tuple(2 * np.pi for _ in n3))
+    A = pb.Mat(da, pb.COMPACT, h)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(A, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "1e-10"])
+    assert (reason, its) == (ro, itso)
+    assert abs(hist[0] - ho[0]) / ho[0] < 1e-12
+    check_x(x.get_values(), xo)
+    r = pb.Vec(da)
+    A.mult(x, r)
+    r.axpy(-1.0, bv)
+    assert r.norm() <= 1e-9 * bv.norm()
+
+
 def test_fft_pc_rejects_bad_extents(ctx):
-    for n3 in [(48, 64, 64), (64, 32, 64), (64, 64, 2048)]:
+    for n3 in [(70, 64, 64), (64, 24, 64), (64, 64, 2048), (64, 64, 75), (64, 1280, 64)]:
         da = pb.DA(ctx, n3)
         P = pb.Mat(da, pb.STAR7, tuple(1.0 / m for m in n3))
         with pytest.raises(pb.PbError):

@@ -293,7 +293,7 @@ def _fft_symbols_np(n, h, compact):
 
 
 @pytest.mark.parametrize("compact", [False, True])
-@pytest.mark.parametrize("n3", [(16, 8, 12), (32, 32, 32), (64, 32, 16)])
+@pytest.mark.parametrize("n3", [(16, 8, 12), (32, 32, 32), (64, 32, 16), (24, 20, 30)])
 def test_fft_pc_inverts_reference_operator(n3, compact):
     """P (P^+ (P x)) = P x: the symbol the PC inverts is the operator's, checked through the
     oracle's stencil / compact lapl (pinned to the reference's known answers and flang build);
