@@ -65,6 +65,7 @@ struct DhtPass {
 struct cplx {
   double re, im;
 };
+typedef double dv2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ cplx cmul(cplx a, cplx b) {
   return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
@@ -167,7 +168,11 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 // One Stockham pass of radix R over the wave's two lines (A = re, B = im rows in LDS), after
-// NS points of every sub-transform are done. tw: (re, im) of exp(-2 pi i k / N) (LDS or global).
+// NS points of every sub-transform are done. tw: the per-pass twiddle table (fft_twiddles): the
+// pass's entries start at complex NS - 1, butterfly k's R - 1 factors exp(-2 pi i r k / (NS R))
+// are consecutive (one 16-byte read each; lanes of distinct k hit distinct banks, lanes of the
+// same k broadcast -- a plain exp(-2 pi i m / N) table read at m = r k N / (NS R) was 4- to 8-way
+// bank-conflicted: 42 % of the Z pass's LDS cycles were conflict cycles).
 template <int N, int R, int NS>
 __device__ __forceinline__ void stockham_pass(double* A, double* B, const double* tw, int lane) {
   constexpr int NB = N / R, T = (NB + 63) / 64;
@@ -182,11 +187,11 @@ __device__ __forceinline__ void stockham_pass(double* A, double* B, const double
         v[t][r] = {A[e], B[e]};
       }
       if constexpr (NS > 1) {
-        const int k = j % NS;
+        const double* w = tw + 2 * (NS - 1 + (j % NS) * (R - 1));
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          const int wi = r * k * (N / (NS * R));
-          v[t][r] = cmul(v[t][r], {tw[2 * wi], tw[2 * wi + 1]});
+          const dv2 c = *(const dv2*)(w + 2 * (r - 1));
+          v[t][r] = cmul(v[t][r], {c.x, c.y});
         }
       }
       dft<R>(v[t]);
@@ -247,11 +252,16 @@ __device__ __forceinline__ void dht2(double* A, double* B, const double* tw, int
   wave_sync_lds();
 }
 
-// The Z pass's 1/(N lambda) on the wave's two spectra (lines i0, i0 + 1 at row j): element k of
-// both lines per lane, coalesced symbol-table reads; 1/lambda := 0 on the null modes
+// The Z pass as F* diag(s) F per line (for a real symbol even in k, H diag(s) H = F* diag(s) F):
+// from Z = F(x + i y), W(k) = s_x(k) X(k) + i s_y(k) Y(k) = ((s_x + s_y)/2) Z(k)
+// + ((s_x - s_y)/2) conj Z(-k) with s = 1/(N lambda) of line x (i0) and line y (i0 + 1)
+// (1/lambda := 0 on the null modes); conj(W) goes back to A, B, so that a second forward FFT and
+// a conjugation on the store give F* W = x' + i y'. One FFT + this step replaces the second
+// Hartley split and the separate scaling step of DHT, scale, DHT (80 of 362 LDS operations per
+// wave and tile at 512 points).
 template <int N>
-__device__ __forceinline__ void scale2(double* A, double* B, const DhtPass& p, int lane,
-                                       int64_t outer, int i0) {
+__device__ __forceinline__ void scale_combine2(double* A, double* B, const DhtPass& p, int lane,
+                                               int64_t outer, int i0) {
   const int nx = p.nx, ny = p.ny, j = p.j0 + (int)outer;
   const double* Lx = p.tab;
   const double* Jx = Lx + nx;
@@ -263,14 +273,28 @@ __device__ __forceinline__ void scale2(double* A, double* B, const DhtPass& p, i
   const double a0 = Lx[i0] * jy + Jx[i0] * ly, c0 = Jx[i0] * jy;
   const double a1 = Lx[i0 + 1] * jy + Jx[i0 + 1] * ly, c1 = Jx[i0 + 1] * jy;
   constexpr int T = (N + 63) / 64;
-#pragma unroll 2
+  double wr[T], wi[T];
+#pragma unroll
   for (int t = 0; t < T; ++t) {
     const int k = lane + 64 * t;
     if (N % 64 == 0 || k < N) {
+      const int m = k == 0 ? 0 : N - k;
       const double lam0 = a0 * Jz[k] + c0 * Lz[k], lam1 = a1 * Jz[k] + c1 * Lz[k];
-      const int e = lpad(k);
-      A[e] = fabs(lam0) > p.thr ? A[e] * (p.scale / lam0) : 0.0;
-      B[e] = fabs(lam1) > p.thr ? B[e] * (p.scale / lam1) : 0.0;
+      const double sx = fabs(lam0) > p.thr ? p.scale / lam0 : 0.0;
+      const double sy = fabs(lam1) > p.thr ? p.scale / lam1 : 0.0;
+      const double hp = 0.5 * (sx + sy), hm = 0.5 * (sx - sy);
+      const double zr = A[lpad(k)], zi = B[lpad(k)], mr = A[lpad(m)], mi = B[lpad(m)];
+      wr[t] = hp * zr + hm * mr;
+      wi[t] = hp * zi - hm * mi;
+    }
+  }
+  wave_sync_lds();
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int k = lane + 64 * t;
+    if (N % 64 == 0 || k < N) {
+      A[lpad(k)] = wr[t];
+      B[lpad(k)] = -wi[t];  // conj(W)
     }
   }
   wave_sync_lds();
@@ -290,8 +314,6 @@ struct DhtTile {
 // tile lines per block: 16 (8 waves), 8 for 1024-point lines (LDS)
 template <int N>
 constexpr int tile_lines() { return N > 512 ? 8 : 16; }
-
-typedef double dv2 __attribute__((ext_vector_type(2)));
 
 // LAYOUT 0: the tile's lines are adjacent (li = 1), elements strided (rows of TL doubles);
 // LAYOUT 1: lines contiguous (es = 1), each wave loads / stores its own two lines (no block
@@ -351,7 +373,10 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
       e = f / (TL / 2);
     }
   };
-  constexpr bool PF = N <= 512;
+  // PF (persistent blocks, next tile prefetched into registers): the contiguous X pass at <= 512
+  // points (512^3: 0.448 -> 0.398 ms). The strided passes run one tile per block and rely on the
+  // second resident block for overlap (prefetching there measured slower: Z 0.707 -> 0.808 ms)
+  constexpr bool PF = LAYOUT == 1 && N <= 512;
   dv2 pre[PF ? NR : 1];
   auto fetch = [&](int t) {
     int64_t outer, base;
@@ -371,8 +396,8 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
   const double mu = SUMS ? p.st->mu : 0.0;
   // PF: prefetch the next tile into registers (lines of <= 512 points; longer lines have no
   // registers to spare: their tile is loaded where it is needed)
-  const int G = gridDim.x;
-  int t = blockIdx.x;
+  const int G = PF ? (int)gridDim.x : ntiles;
+  int t = PF ? (int)blockIdx.x : xcd_block(p.remap);
   if (PF && t < ntiles) fetch(t);
   for (; t < ntiles; t += G) {
     int64_t outer, base;
@@ -408,7 +433,7 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
           put(l, e, __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es)));
       }
     }
-    if (WAVE && t == (int)blockIdx.x)
+    if (WAVE && t < G)
       __syncthreads();  // first tile: the twiddle table (written by the whole block) is in
     else if (WAVE)
       wave_sync_lds();
@@ -418,9 +443,11 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
     if (l0 < nl) {
       double* A = lds + l0 * LP;
       double* B = A + LP;
-      dht2<N>(A, B, tw, lane);
-      if constexpr (MODE == 1) {
-        scale2<N>(A, B, p, lane, outer, inner0 + l0);
+      if constexpr (MODE == 1) {  // F* diag(s) F: FFT, scale-combine, FFT, conjugate (store)
+        fft_passes<N, 0, 1>(A, B, tw, lane);
+        scale_combine2<N>(A, B, p, lane, outer, inner0 + l0);
+        fft_passes<N, 0, 1>(A, B, tw, lane);
+      } else {
         dht2<N>(A, B, tw, lane);
       }
     }
@@ -437,6 +464,7 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
         if (LAYOUT == 0) {
           v.x = lds[l * LP + lpad(e)];
           v.y = lds[(l + 1) * LP + lpad(e)];
+          if (MODE == 1) v.y = -v.y;  // the conjugation of F* W = conj(F conj W)
         } else {
           v.x = lds[l * LP + lpad(e)];
           v.y = lds[l * LP + lpad(e + 1)];
@@ -494,10 +522,11 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
     PB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern_s, T::NT, T::LDS));
     if (occ < 1) occ = 1;
   }
-  // persistent: one resident round of blocks (PB_FFT_BLOCKS_PER_CU overrides, tuning)
+  // persistent (X pass): one resident round of blocks (PB_FFT_BLOCKS_PER_CU overrides, tuning);
+  // strided passes: one tile per block
   static const int bpc = env_int("PB_FFT_BLOCKS_PER_CU", 0);
   int64_t nblocks = (int64_t)(bpc > 0 ? bpc : occ) * ctx->num_cus;
-  if (nblocks > ntiles) nblocks = ntiles;
+  if (LAYOUT == 0 || N > 512 || nblocks > ntiles) nblocks = ntiles;
   if (p.parts) {
     if (LAYOUT != 1 || MODE != 0)
       return set_error(PB_ERR_STATE, "fft pc: residual sums on the X pass only");
@@ -592,10 +621,20 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
   int64_t off = 0;
   for (int d = 0; d < 3; ++d) {
     const int64_t n = g->n[d];
-    for (int64_t k = 0; k < n; ++k) {
-      const long double t = -2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
-      ht[2 * (off + k)] = (double)cosl(t);
-      ht[2 * (off + k) + 1] = (double)sinl(t);
+    // per-pass twiddles of the Stockham plan (stockham_pass): pass p (after NS points) holds
+    // exp(-2 pi i r k / (NS R)) at complex NS - 1 + k (R - 1) + r - 1; N - 1 entries in all
+    int64_t ns = 1;
+    for (int pass = 0; ns < n; ++pass) {
+      const int R = plan_radix_at((int)n, pass);
+      for (int64_t k = 0; k < ns; ++k)
+        for (int r = 1; r < R; ++r) {
+          const long double t = -2.0L * 3.14159265358979323846264338327950288L * (long double)(r * k) /
+                                (long double)(ns * R);
+          const int64_t idx = ns - 1 + k * (R - 1) + (r - 1);
+          ht[2 * (off + idx)] = (double)cosl(t);
+          ht[2 * (off + idx) + 1] = (double)sinl(t);
+        }
+      ns *= R;
     }
     double* L = hs + 2 * off;
     double* J = L + n;
