@@ -60,6 +60,11 @@ struct DhtPass {
   double* parts;
   const CgState* st;
   int nparts_out;     // (host) partial blocks written
+  int stagger, ncu;   // PB_FFT_STAGGER=s: the second resident round of blocks (blockIdx in
+                      // [ncu, 2 ncu)) sleeps s x 8128 cycles first, so co-resident blocks run out of
+                      // phase (one loads while the other transforms) -- A/B knob
+  int ablate;         // timing experiments only (PB_FFT_ABLATE): 1 = no transforms (tile copy
+                      // through LDS), 2 = no global loads / stores (transforms on stale LDS)
 };
 
 struct cplx {
@@ -101,8 +106,12 @@ __host__ __device__ constexpr bool plan_complete(int n) {
   return true;
 }
 
-// LDS index of element e in a line: one pad double every 16 (bank spread of the pass writes)
-__host__ __device__ constexpr int lpad(int e) { return e + (e >> 4); }
+// LDS index of element e in a line: one pad double every 2^PB_FFT_PAD_SHIFT (bank spread of the
+// strided pass writes)
+#ifndef PB_FFT_PAD_SHIFT
+#define PB_FFT_PAD_SHIFT 4
+#endif
+__host__ __device__ constexpr int lpad(int e) { return e + (e >> PB_FFT_PAD_SHIFT); }
 
 // ---- R-point DFTs in registers, forward (exp(-2 pi i j k / R)) ----
 template <int R>
@@ -224,29 +233,31 @@ __device__ __forceinline__ void fft_passes(double* A, double* B, const double* t
 }
 
 // DHT of the two real lines in rows A, B (in place, natural order): FFT of z = x + i y, then
-// H_x(k) = Re X - Im X, H_y(k) = Re Y - Im Y with X, Y from Z(k) and Z(-k)
+// H_x(k) = Re X - Im X, H_y(k) = Re Y - Im Y with X, Y from Z(k) and Z(-k). A lane owns the
+// pair (k, N - k) (k = 0 owns the two self-paired points 0 and N/2): it reads both and writes
+// both, so no wave barrier and no registers are held between the reads and the writes.
 template <int N>
 __device__ __forceinline__ void dht2(double* A, double* B, const double* tw, int lane) {
   fft_passes<N, 0, 1>(A, B, tw, lane);
-  constexpr int T = (N + 63) / 64;
-  double hx[T], hy[T];
+  constexpr int H = N / 2, T = (H + 63) / 64;
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     const int k = lane + 64 * t;
-    if (N % 64 == 0 || k < N) {
-      const int m = k == 0 ? 0 : N - k;
-      const double zr = A[lpad(k)], zi = B[lpad(k)], mr = A[lpad(m)], mi = B[lpad(m)];
-      hx[t] = 0.5 * ((zr + mr) - (zi - mi));
-      hy[t] = 0.5 * ((zi + mi) + (zr - mr));
-    }
-  }
-  wave_sync_lds();
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int k = lane + 64 * t;
-    if (N % 64 == 0 || k < N) {
-      A[lpad(k)] = hx[t];
-      B[lpad(k)] = hy[t];
+    if (H % 64 == 0 || k < H) {
+      const int m = k == 0 ? H : N - k;  // k = 0: points 0 and N/2, each its own partner
+      const int ek = lpad(k), em = lpad(m);
+      const double zr = A[ek], zi = B[ek], mr = A[em], mi = B[em];
+      if (k == 0) {
+        A[ek] = 0.5 * ((zr + zr) - (zi - zi));
+        B[ek] = 0.5 * ((zi + zi) + (zr - zr));
+        A[em] = 0.5 * ((mr + mr) - (mi - mi));
+        B[em] = 0.5 * ((mi + mi) + (mr - mr));
+      } else {
+        A[ek] = 0.5 * ((zr + mr) - (zi - mi));
+        B[ek] = 0.5 * ((zi + mi) + (zr - mr));
+        A[em] = 0.5 * ((mr + zr) - (mi - zi));
+        B[em] = 0.5 * ((mi + zi) + (mr - zr));
+      }
     }
   }
   wave_sync_lds();
@@ -272,29 +283,37 @@ __device__ __forceinline__ void scale_combine2(double* A, double* B, const DhtPa
   const double ly = Ly[j], jy = Jy[j];
   const double a0 = Lx[i0] * jy + Jx[i0] * ly, c0 = Jx[i0] * jy;
   const double a1 = Lx[i0 + 1] * jy + Jx[i0 + 1] * ly, c1 = Jx[i0 + 1] * jy;
-  constexpr int T = (N + 63) / 64;
-  double wr[T], wi[T];
-#pragma unroll
+  // the symbol is even in k (the host tables are mirrored exactly): one (hp, hm) per pair
+  auto factors = [&](int k, double& hp, double& hm) {
+    const double lam0 = a0 * Jz[k] + c0 * Lz[k], lam1 = a1 * Jz[k] + c1 * Lz[k];
+    const double sx = fabs(lam0) > p.thr ? p.scale / lam0 : 0.0;
+    const double sy = fabs(lam1) > p.thr ? p.scale / lam1 : 0.0;
+    hp = 0.5 * (sx + sy);
+    hm = 0.5 * (sx - sy);
+  };
+  constexpr int H = N / 2, T = (H + 63) / 64;
+#pragma unroll 2
   for (int t = 0; t < T; ++t) {
     const int k = lane + 64 * t;
-    if (N % 64 == 0 || k < N) {
-      const int m = k == 0 ? 0 : N - k;
-      const double lam0 = a0 * Jz[k] + c0 * Lz[k], lam1 = a1 * Jz[k] + c1 * Lz[k];
-      const double sx = fabs(lam0) > p.thr ? p.scale / lam0 : 0.0;
-      const double sy = fabs(lam1) > p.thr ? p.scale / lam1 : 0.0;
-      const double hp = 0.5 * (sx + sy), hm = 0.5 * (sx - sy);
-      const double zr = A[lpad(k)], zi = B[lpad(k)], mr = A[lpad(m)], mi = B[lpad(m)];
-      wr[t] = hp * zr + hm * mr;
-      wi[t] = hp * zi - hm * mi;
-    }
-  }
-  wave_sync_lds();
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int k = lane + 64 * t;
-    if (N % 64 == 0 || k < N) {
-      A[lpad(k)] = wr[t];
-      B[lpad(k)] = -wi[t];  // conj(W)
+    if (H % 64 == 0 || k < H) {
+      const int m = k == 0 ? H : N - k;  // k = 0: points 0 and N/2, each its own partner
+      const int ek = lpad(k), em = lpad(m);
+      const double zr = A[ek], zi = B[ek], mr = A[em], mi = B[em];
+      double hp, hm;
+      factors(k, hp, hm);
+      if (k == 0) {
+        double hp2, hm2;
+        factors(m, hp2, hm2);
+        A[ek] = hp * zr + hm * zr;
+        B[ek] = -(hp * zi - hm * zi);
+        A[em] = hp2 * mr + hm2 * mr;
+        B[em] = -(hp2 * mi - hm2 * mi);
+      } else {  // conj(W) with W(k) = hp Z(k) + hm conj Z(N - k), and the same for N - k
+        A[ek] = hp * zr + hm * mr;
+        B[ek] = -(hp * zi - hm * mi);
+        A[em] = hp * mr + hm * zr;
+        B[em] = -(hp * mi - hm * zi);
+      }
     }
   }
   wave_sync_lds();
@@ -321,12 +340,14 @@ constexpr int tile_lines() { return N > 512 ? 8 : 16; }
 // Persistent blocks (as many as are resident) walk the tiles; the next tile's input is fetched
 // into registers while the current one is transformed and stored, so HBM reads overlap the
 // transforms (+32 VGPRs at n = 512; occupancy stays LDS-bound at two blocks per CU).
-template <int N, int LAYOUT, int MODE, bool SUMS>
+template <int N, int LAYOUT, int MODE, bool SUMS, bool PFS = false>
 __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_lines_kernel(
     DhtPass p, const int* skip) {
   using T = DhtTile<N, tile_lines<N>()>;
   constexpr int TL = T::TL, NT = T::NT, LP = T::LP;
   if (skip && *skip) return;  // CG's device convergence flag (uniform)
+  if (p.stagger && (int)blockIdx.x >= p.ncu && (int)blockIdx.x < 2 * p.ncu)
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l0 = 2 * wave;
@@ -376,7 +397,7 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
   // PF (persistent blocks, next tile prefetched into registers): the contiguous X pass at <= 512
   // points (512^3: 0.448 -> 0.398 ms). The strided passes run one tile per block and rely on the
   // second resident block for overlap (prefetching there measured slower: Z 0.707 -> 0.808 ms)
-  constexpr bool PF = LAYOUT == 1 && N <= 512;
+  constexpr bool PF = (LAYOUT == 1 || PFS) && N <= 512;
   dv2 pre[PF ? NR : 1];
   auto fetch = [&](int t) {
     int64_t outer, base;
@@ -387,7 +408,7 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
       for (int q = 0; q < NR; ++q) {
         int l, e;
         coord(q, l, e);
-        if (l < nl)
+        if (l < nl && p.ablate != 2)
           pre[q] = __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es));
       }
     }
@@ -422,14 +443,14 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
       for (int q = 0; q < NR; ++q) {
         int l, e;
         coord(q, l, e);
-        if (l < nl) put(l, e, pre[q]);
+        if (l < nl && p.ablate != 2) put(l, e, pre[q]);
       }
     } else {  // a few loads in flight at a time (registers)
 #pragma unroll 4
       for (int q = 0; q < NR; ++q) {
         int l, e;
         coord(q, l, e);
-        if (l < nl)
+        if (l < nl && p.ablate != 2)
           put(l, e, __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es)));
       }
     }
@@ -440,7 +461,7 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
     else
       __syncthreads();
     if (PF && t + G < ntiles) fetch(t + G);  // in flight during the transforms and the stores
-    if (l0 < nl) {
+    if (l0 < nl && p.ablate != 1) {
       double* A = lds + l0 * LP;
       double* B = A + LP;
       if constexpr (MODE == 1) {  // F* diag(s) F: FFT, scale-combine, FFT, conjugate (store)
@@ -470,6 +491,10 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
           v.y = lds[l * LP + lpad(e + 1)];
         }
         const int64_t a = base + l * p.li + e * p.es;
+        if (p.ablate == 2) {
+          if (v.x == 12345.678) p.out[a] = v.y;  // keeps the LDS reads (never true on real data)
+          continue;
+        }
         __builtin_nontemporal_store(v, (dv2*)(p.out + a));
         if constexpr (SUMS) {
           const dv2 rv = __builtin_nontemporal_load((const dv2*)(p.sr + a));
@@ -513,11 +538,16 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
   auto kern = dht_lines_kernel<N, LAYOUT, MODE, false>;
   auto kern_s = dht_lines_kernel<N, LAYOUT, MODE, LAYOUT == 1 && MODE == 0>;
+  // PB_FFT_PF_STRIDED=1: persistent + prefetch on the strided passes too (A/B)
+  static const int pfs = env_int("PB_FFT_PF_STRIDED", 0);
+  auto kern_p = dht_lines_kernel<N, LAYOUT, MODE, false, LAYOUT == 0>;
   static int occ = 0;
   if (!occ) {
     PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)T::LDS));
     PB_HIP(hipFuncSetAttribute((const void*)kern_s, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)T::LDS));
+    PB_HIP(hipFuncSetAttribute((const void*)kern_p, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)T::LDS));
     PB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern_s, T::NT, T::LDS));
     if (occ < 1) occ = 1;
@@ -526,7 +556,9 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   // strided passes: one tile per block
   static const int bpc = env_int("PB_FFT_BLOCKS_PER_CU", 0);
   int64_t nblocks = (int64_t)(bpc > 0 ? bpc : occ) * ctx->num_cus;
-  if (LAYOUT == 0 || N > 512 || nblocks > ntiles) nblocks = ntiles;
+  const bool persist = N <= 512 && (LAYOUT == 1 || pfs);
+  if (!persist || nblocks > ntiles) nblocks = ntiles;
+  if (LAYOUT == 0 && persist) kern = kern_p;
   if (p.parts) {
     if (LAYOUT != 1 || MODE != 0)
       return set_error(PB_ERR_STATE, "fft pc: residual sums on the X pass only");
@@ -586,7 +618,9 @@ struct FftPc {
 static void axis_symbols(int compact, int64_t n, double h, double* L, double* J) {
   const double a_d = 63.0 / 62.0 / h, b_d = 17.0 / 62.0 / (3.0 * h), al_d = 9.0 / 62.0;
   const double a_i = 0.75, b_i = 1.0 / 20.0, al_i = 3.0 / 10.0;
-  for (int64_t k = 0; k < n; ++k) {
+  // k <= n/2 evaluated, the rest mirrored: the tables are exactly even (L[n-k] = L[k]), which the
+  // Z pass's pairwise scale step relies on
+  for (int64_t k = 0; k <= n / 2; ++k) {
     const long double t = 2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
     if (!compact) {
       L[k] = (double)((2.0L * cosl(t) - 2.0L) / ((long double)h * (long double)h));
@@ -599,6 +633,10 @@ static void axis_symbols(int compact, int64_t n, double h, double* L, double* J)
     const long double ti = 1.0L + 2.0L * al_i * cosl(t);
     L[k] = (double)(-4.0L * sd * sd / (td * td));
     J[k] = (double)(4.0L * si * si / (ti * ti));
+  }
+  for (int64_t k = n / 2 + 1; k < n; ++k) {
+    L[k] = L[n - k];
+    J[k] = J[n - k];
   }
 }
 
@@ -682,6 +720,9 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   ScopedTimer tm(ctx, names[axis]);
   DhtPass p{};
   p.remap = env_int("PB_FFT_REMAP", 1);
+  p.ablate = env_int("PB_FFT_ABLATE", 0);
+  p.stagger = env_int("PB_FFT_STAGGER", 0);
+  p.ncu = ctx->num_cus;
   p.in = in;
   p.out = out;
   p.w = f->tw[axis];
