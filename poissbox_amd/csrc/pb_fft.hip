@@ -340,10 +340,10 @@ constexpr int tile_lines() { return N > 512 ? 8 : 16; }
 // Persistent blocks (as many as are resident) walk the tiles; the next tile's input is fetched
 // into registers while the current one is transformed and stored, so HBM reads overlap the
 // transforms (+32 VGPRs at n = 512; occupancy stays LDS-bound at two blocks per CU).
-template <int N, int LAYOUT, int MODE, bool SUMS, bool PFS = false>
-__global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_lines_kernel(
-    DhtPass p, const int* skip) {
-  using T = DhtTile<N, tile_lines<N>()>;
+template <int N, int TL_, int LAYOUT, int MODE, bool SUMS, bool PFS>
+__global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(DhtPass p,
+                                                                             const int* skip) {
+  using T = DhtTile<N, TL_>;
   constexpr int TL = T::TL, NT = T::NT, LP = T::LP;
   if (skip && *skip) return;  // CG's device convergence flag (uniform)
   if (p.stagger && (int)blockIdx.x >= p.ncu && (int)blockIdx.x < 2 * p.ncu)
@@ -529,39 +529,32 @@ __global__ __launch_bounds__(32 * tile_lines<N>(), N <= 512 ? 4 : 1) void dht_li
   }
 }
 
-template <int N, int LAYOUT, int MODE>
-int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
-  using T = DhtTile<N, tile_lines<N>()>;
-  if (p.ninner % 2)
-    return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines (even counts only)", p.ninner);
+// TL lines per tile, PFS: persistent blocks + register prefetch on a strided pass
+template <int N, int TL, int LAYOUT, int MODE, bool PFS>
+int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
+  using T = DhtTile<N, TL>;
   p.ntiles_inner = (p.ninner + T::TL - 1) / T::TL;
   const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
-  auto kern = dht_lines_kernel<N, LAYOUT, MODE, false>;
-  auto kern_s = dht_lines_kernel<N, LAYOUT, MODE, LAYOUT == 1 && MODE == 0>;
-  // PB_FFT_PF_STRIDED=1: persistent + prefetch on the strided passes too (A/B)
-  static const int pfs = env_int("PB_FFT_PF_STRIDED", 0);
-  auto kern_p = dht_lines_kernel<N, LAYOUT, MODE, false, LAYOUT == 0>;
+  constexpr bool SUMS = LAYOUT == 1 && MODE == 0;
+  auto kern = dht_lines_kernel<N, TL, LAYOUT, MODE, false, PFS>;
+  auto kern_s = dht_lines_kernel<N, TL, LAYOUT, MODE, SUMS, PFS>;
   static int occ = 0;
   if (!occ) {
     PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)T::LDS));
     PB_HIP(hipFuncSetAttribute((const void*)kern_s, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)T::LDS));
-    PB_HIP(hipFuncSetAttribute((const void*)kern_p, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)T::LDS));
     PB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern_s, T::NT, T::LDS));
     if (occ < 1) occ = 1;
   }
-  // persistent (X pass): one resident round of blocks (PB_FFT_BLOCKS_PER_CU overrides, tuning);
-  // strided passes: one tile per block
+  // persistent passes: one resident round of blocks (PB_FFT_BLOCKS_PER_CU overrides, tuning);
+  // the others one tile per block
   static const int bpc = env_int("PB_FFT_BLOCKS_PER_CU", 0);
   int64_t nblocks = (int64_t)(bpc > 0 ? bpc : occ) * ctx->num_cus;
-  const bool persist = N <= 512 && (LAYOUT == 1 || pfs);
+  const bool persist = N <= 512 && (LAYOUT == 1 || PFS);
   if (!persist || nblocks > ntiles) nblocks = ntiles;
-  if (LAYOUT == 0 && persist) kern = kern_p;
   if (p.parts) {
-    if (LAYOUT != 1 || MODE != 0)
-      return set_error(PB_ERR_STATE, "fft pc: residual sums on the X pass only");
+    if (!SUMS) return set_error(PB_ERR_STATE, "fft pc: residual sums on the X pass only");
     if (nblocks * 4 > ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fft pc: %lld blocks exceed the partials capacity",
                        (long long)nblocks);
@@ -571,6 +564,31 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(T::NT), T::LDS, ctx->stream, p, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
+}
+
+// Launch shapes (512^3, profiles/r03/fft_ab*.jsonl): the strided passes stage 16-line tiles
+// (128-B row pieces), persistent with register prefetch on 512-point lines (Y 0.50 -> 0.46 ms;
+// at 256 points one tile per block is faster). PB_FFT_PF_STRIDED = 0 / 1 forces either;
+// PB_FFT_TL_Z = 32 (512-point lines): 32-line Z tiles, 256-B pieces, one block per CU.
+template <int N, int LAYOUT, int MODE>
+int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
+  if (p.ninner % 2)
+    return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines (even counts only)", p.ninner);
+  constexpr int TL = tile_lines<N>();
+  if constexpr (LAYOUT == 1) {
+    return launch_dht_k<N, TL, 1, MODE, false>(ctx, p, skip);
+  } else {
+    static const int pfs = env_int("PB_FFT_PF_STRIDED", N == 512 ? 1 : 0);
+    if constexpr (N == 512 && MODE == 1) {
+      static const int tlz = env_int("PB_FFT_TL_Z", 16);
+      if (tlz == 32)
+        return pfs ? launch_dht_k<N, 32, 0, 1, true>(ctx, p, skip)
+                   : launch_dht_k<N, 32, 0, 1, false>(ctx, p, skip);
+    }
+    if constexpr (N <= 512)
+      if (pfs) return launch_dht_k<N, TL, 0, MODE, true>(ctx, p, skip);
+    return launch_dht_k<N, TL, 0, MODE, false>(ctx, p, skip);
+  }
 }
 
 // the line lengths with a compiled transform: 2^a (32..1024), 3 * 2^a (48..768), 5 * 2^a (40..640)
