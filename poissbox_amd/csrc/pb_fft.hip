@@ -25,8 +25,8 @@
 // (then 4, 2, 3, 5) -- every lane reads R elements n/R apart, twiddles them, runs the R-point DFT in
 // registers and writes them back at (j / Ns) Ns R + j % Ns + r Ns. The two Hartley spectra follow
 // from Z(k) and Z(n - k), read from LDS. Line lengths n = 2^a 3^b 5^c (a >= 1) in 32..1024. The
-// element index is padded by one double every 16 in LDS, so the scattered writes of the first
-// pass hit distinct banks. Twiddles exp(-2 pi i k / n) come from a per-axis table, copied into LDS
+// element index is XOR-swizzled in LDS (lpad), so the scattered writes of the first pass hit
+// distinct banks. Twiddles exp(-2 pi i k / n) come from a per-axis table, copied into LDS
 // per block for n <= 512. (r02's engine ran the 64-point cross-lane part of the transform as six
 // radix-2 stages of DPP / permlane exchanges: 2.5x the VALU work, and its Z pass, which runs two
 // transforms, was compute-bound at 1.0-1.1 ms at 512^3 whatever the tile width.)
@@ -106,12 +106,17 @@ __host__ __device__ constexpr bool plan_complete(int n) {
   return true;
 }
 
-// LDS index of element e in a line: one pad double every 2^PB_FFT_PAD_SHIFT (bank spread of the
-// strided pass writes)
-#ifndef PB_FFT_PAD_SHIFT
-#define PB_FFT_PAD_SHIFT 4
-#endif
-__host__ __device__ constexpr int lpad(int e) { return e + (e >> PB_FFT_PAD_SHIFT); }
+// LDS index of element e in a line: the low four bits XOR-ed with bits 4..7 -- a permutation
+// inside each aligned block of 16 elements, so 32 contiguous lanes still hit 64 distinct banks,
+// while the stride-R writes of the first Stockham pass spread over all banks (an LDS bank model
+// of the 512-point passes: 72 read cycles against 128 for one pad double every 16 elements, the
+// same write cycles, and no padding)
+__host__ __device__ constexpr int lpad(int e) { return e ^ ((e >> 4) & 15); }
+__host__ __device__ constexpr int lpad_max(int n) {
+  int m = 0;
+  for (int e = 0; e < n; ++e) m = lpad(e) > m ? lpad(e) : m;
+  return m;
+}
 
 // ---- R-point DFTs in registers, forward (exp(-2 pi i j k / R)) ----
 template <int R>
@@ -324,7 +329,7 @@ struct DhtTile {
   static constexpr int TL = TL_;              // lines per tile
   static constexpr int NW = TL / 2;           // waves: two lines each
   static constexpr int NT = 64 * NW;
-  static constexpr int LP = (lpad(N - 1) + 1) | 1;  // line pitch (doubles), odd
+  static constexpr int LP = (lpad_max(N) + 1) | 1;  // line pitch (doubles), odd
   static constexpr bool TWL = N <= 512;       // twiddle table in LDS (else read from L1/L2)
   static constexpr int TWO = TL * LP;         // twiddle table offset (even: TL is)
   static constexpr size_t LDS = (size_t)(TWO + (TWL ? 2 * N : 0)) * sizeof(double);
