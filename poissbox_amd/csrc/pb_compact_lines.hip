@@ -46,7 +46,8 @@ struct LinePass {
   double* out1;
   int64_t li, lo, es;  // address of (outer, inner line, element e) = outer*lo + inner*li + e*es
   int ninner, ntiles_inner, nouter, TL, P;
-  int ablate;  // tuning only (PB_LINES_ABLATE=1): copy lines through, no solves
+  int ablate;  // tuning only (PB_LINES_ABLATE): 1 = copy lines through, no solves; 2 = no global
+               // loads / stores in the tiled passes (solves on stale LDS)
   int remap;   // XCD-aware tile order (PB_LINES_REMAP, default off: Z pass 0.74-0.78 vs 0.715-0.72 ms
                // at 512^3, profiles/r02/ab_remap_compact.jsonl)
   LineOp J, L;
@@ -215,7 +216,7 @@ __device__ __forceinline__ void tile_fetch(const LinePass& p, const double* __re
     const int f = threadIdx.x + NT * r;
     tile_coord<C, LAYOUT, TL, V>(f, l, e);
     const double* a = src + base + l * p.li + e * p.es;
-    if ((T::NF % NT == 0 || f < T::NF) && l < nl) {
+    if ((T::NF % NT == 0 || f < T::NF) && l < nl && p.ablate != 2) {
       if (V == 2) {
         const dv2 w = __builtin_nontemporal_load((const dv2*)a);
         t.v[r][0] = w.x;
@@ -260,6 +261,10 @@ __device__ __forceinline__ void tile_store(const LinePass& p, double* __restrict
         dv2 w;
         w.x = lds[Lds<C>::word(l, e)];
         w.y = lds[Lds<C>::word(l + dl, e + de)];
+        if (p.ablate == 2) {
+          if (w.x == 12345.678) *a = w.y;  // keeps the LDS reads (never true on real data)
+          continue;
+        }
         __builtin_nontemporal_store(w, (dv2*)a);
       } else {
         __builtin_nontemporal_store(lds[Lds<C>::word(l, e)], a);

@@ -16,4 +16,10 @@ rc=$?; echo "star7 rc=$rc"; cat gpurun_out/solve/solve_star7.jsonl; [ $rc -eq 0 
 cd /tmp && export TMPDIR=/tmp
 OP=compact PCS=fft NO_CPU=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/solve/kt_cfg5 -o cfg5 --output-format csv \
   -- python3 $R/scripts/bench_solve.py 512 > $R/gpurun_out/solve/kt_cfg5.jsonl 2> $R/gpurun_out/solve/kt_cfg5.err
-rc=$?; echo "kt rc=$rc"; exit $rc
+rc=$?; echo "kt rc=$rc"; [ $rc -eq 0 ] || exit $rc
+cd $R
+for cfg in "TAG=default" "PB_LINES_ABLATE=1" "PB_LINES_ABLATE=2" "PB_LINES_CFG=6" "PB_LINES_CFG=7"; do
+  env $cfg timeout -k 10 120 python scripts/bench_compact.py 512 256 >> gpurun_out/solve/compact_ab.jsonl 2>> gpurun_out/solve/compact_ab.err
+  rc=$?; echo "compact $cfg rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+cat gpurun_out/solve/compact_ab.jsonl
