@@ -176,7 +176,10 @@ __device__ __forceinline__ void line_op(const double (&x)[C], double (&r)[C], co
 template <int C>
 struct Lds {
   static constexpr int CP = (C % 2 == 0) ? C + 1 : C;
-  static constexpr int LP = 64 * CP + 4;  // line pitch (doubles)
+  // line pitch (doubles): 64 CP + 1 = 1 mod 16, so the tile copies' 16-lane groups (8 lines x 2
+  // elements) hit 16 distinct banks; the r01/r02 pitch 64 CP + 4 put lines 0, 4, 8, 12 on one bank
+  // (4-way conflicts on every tile write: 4x the LDS write cycles of the copy, by a bank model)
+  static constexpr int LP = 64 * CP + 1;
   __device__ static __forceinline__ int word(int l, int e) { return l * LP + (e / C) * CP + (e % C); }
 };
 
