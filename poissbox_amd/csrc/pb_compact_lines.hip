@@ -46,8 +46,8 @@ struct LinePass {
   double* out1;
   int64_t li, lo, es;  // address of (outer, inner line, element e) = outer*lo + inner*li + e*es
   int ninner, ntiles_inner, nouter, TL, P;
-  int ablate;  // tuning only (PB_LINES_ABLATE): 1 = copy lines through, no solves; 2 = no global
-               // loads / stores in the tiled passes (solves on stale LDS)
+  int ablate;  // tuning only (PB_LINES_ABLATE=1): copy lines through, no solves (the build flag
+               // -DPB_LINES_ABLATE_TRAFFIC=1 drops the tiled passes' global loads / stores instead)
   int remap;   // XCD-aware tile order (PB_LINES_REMAP, default off: Z pass 0.74-0.78 vs 0.715-0.72 ms
                // at 512^3, profiles/r02/ab_remap_compact.jsonl)
   LineOp J, L;
@@ -208,25 +208,34 @@ struct TileRegs {
   double v[R][V];
 };
 
-// issue every global load of the tile (no wait: the registers are consumed by tile_put later)
+// issue every global load of the tile (no wait: the registers are consumed by tile_put later).
+// Every load is unconditional, from a valid address (pairs past the tile re-load line 0 / the
+// tile's first element; tile_put ignores them): a load under a runtime `if` made the compiler
+// wait for each load before issuing the next (s_waitcnt vmcnt(0) ahead of every
+// global_load_dwordx4 in the r02 ISA of the persistent Z / Y passes), i.e. one HBM round trip per
+// pair instead of the whole tile in flight.
+#ifndef PB_LINES_ABLATE_TRAFFIC
+#define PB_LINES_ABLATE_TRAFFIC 0  // timing builds only: no global loads / stores in tiled passes
+#endif
 template <int C, int LAYOUT, int TL, int V, int NT>
 __device__ __forceinline__ void tile_fetch(const LinePass& p, const double* __restrict__ src,
                                            int64_t base, int nl, TileRegs<C, LAYOUT, TL, V, NT>& t) {
   using T = TileRegs<C, LAYOUT, TL, V, NT>;
+  if (PB_LINES_ABLATE_TRAFFIC) return;
 #pragma unroll
   for (int r = 0; r < T::R; ++r) {
     int l, e;
     const int f = threadIdx.x + NT * r;
     tile_coord<C, LAYOUT, TL, V>(f, l, e);
-    const double* a = src + base + l * p.li + e * p.es;
-    if ((T::NF % NT == 0 || f < T::NF) && l < nl && p.ablate != 2) {
-      if (V == 2) {
-        const dv2 w = __builtin_nontemporal_load((const dv2*)a);
-        t.v[r][0] = w.x;
-        t.v[r][V - 1] = w.y;
-      } else {
-        t.v[r][0] = __builtin_nontemporal_load(a);
-      }
+    const bool ok = (T::NF % NT == 0 || f < T::NF) && l < nl;
+    const int lc = ok ? l : 0, ec = ok ? e : 0;  // selects, not a branch around the load
+    const double* a = src + base + lc * p.li + ec * p.es;
+    if (V == 2) {
+      const dv2 w = __builtin_nontemporal_load((const dv2*)a);
+      t.v[r][0] = w.x;
+      t.v[r][V - 1] = w.y;
+    } else {
+      t.v[r][0] = __builtin_nontemporal_load(a);
     }
   }
 }
@@ -264,7 +273,7 @@ __device__ __forceinline__ void tile_store(const LinePass& p, double* __restrict
         dv2 w;
         w.x = lds[Lds<C>::word(l, e)];
         w.y = lds[Lds<C>::word(l + dl, e + de)];
-        if (p.ablate == 2) {
+        if (PB_LINES_ABLATE_TRAFFIC) {
           if (w.x == 12345.678) *a = w.y;  // keeps the LDS reads (never true on real data)
           continue;
         }

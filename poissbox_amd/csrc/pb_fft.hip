@@ -63,9 +63,13 @@ struct DhtPass {
   int stagger, ncu;   // PB_FFT_STAGGER=s: the second resident round of blocks (blockIdx in
                       // [ncu, 2 ncu)) sleeps s x 8128 cycles first, so co-resident blocks run out of
                       // phase (one loads while the other transforms) -- A/B knob
-  int ablate;         // timing experiments only (PB_FFT_ABLATE): 1 = no transforms (tile copy
-                      // through LDS), 2 = no global loads / stores (transforms on stale LDS)
+  int ablate;         // timing experiments only (PB_FFT_ABLATE=1): no transforms (tile copy
+                      // through LDS); builds with -DPB_FFT_ABLATE_TRAFFIC=1 drop the global loads
+                      // and stores instead (transforms on stale LDS)
 };
+#ifndef PB_FFT_ABLATE_TRAFFIC
+#define PB_FFT_ABLATE_TRAFFIC 0
+#endif
 
 struct cplx {
   double re, im;
@@ -404,18 +408,25 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
   // second resident block for overlap (prefetching there measured slower: Z 0.707 -> 0.808 ms)
   constexpr bool PF = (LAYOUT == 1 || PFS) && N <= 512;
   dv2 pre[PF ? NR : 1];
+  // Every tile load is unconditional, from a valid address (pairs past the tile re-read the
+  // tile's first pair; put ignores them): a load under a runtime `if` made the compiler wait for
+  // each load before issuing the next (s_waitcnt vmcnt(0) after every global_load_dwordx4 in the
+  // ISA), one HBM round trip per pair instead of all of them in flight.
+  auto load_pair = [&](int64_t base, int nl, int q) -> dv2 {
+    int l, e;
+    coord(q, l, e);
+    const bool ok = l < nl;
+    const int lc = ok ? l : 0, ec = ok ? e : 0;  // selects, not a branch around the load
+    if (PB_FFT_ABLATE_TRAFFIC) return dv2{0.0, 0.0};
+    return __builtin_nontemporal_load((const dv2*)(p.in + base + lc * p.li + ec * p.es));
+  };
   auto fetch = [&](int t) {
     int64_t outer, base;
     int inner0, nl;
     tile_of(t, outer, inner0, nl, base);
     if constexpr (PF) {
 #pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        int l, e;
-        coord(q, l, e);
-        if (l < nl && p.ablate != 2)
-          pre[q] = __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es));
-      }
+      for (int q = 0; q < NR; ++q) pre[q] = load_pair(base, nl, q);
     }
   };
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -448,15 +459,22 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
       for (int q = 0; q < NR; ++q) {
         int l, e;
         coord(q, l, e);
-        if (l < nl && p.ablate != 2) put(l, e, pre[q]);
+        if (l < nl) put(l, e, pre[q]);
       }
-    } else {  // a few loads in flight at a time (registers)
-#pragma unroll 4
-      for (int q = 0; q < NR; ++q) {
-        int l, e;
-        coord(q, l, e);
-        if (l < nl && p.ablate != 2)
-          put(l, e, __builtin_nontemporal_load((const dv2*)(p.in + base + l * p.li + e * p.es)));
+    } else {  // QB loads in flight at a time (registers), then their LDS writes
+      constexpr int QB = N <= 512 ? (NR < 8 ? NR : 8) : 4;
+#pragma unroll
+      for (int q0 = 0; q0 < NR; q0 += QB) {
+        dv2 v[QB];
+#pragma unroll
+        for (int q = 0; q < QB; ++q)
+          if (q0 + q < NR) v[q] = load_pair(base, nl, q0 + q);
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+          int l, e;
+          coord(q0 + q, l, e);
+          if (q0 + q < NR && l < nl) put(l, e, v[q]);
+        }
       }
     }
     if (WAVE && t < G)
@@ -496,7 +514,7 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
           v.y = lds[l * LP + lpad(e + 1)];
         }
         const int64_t a = base + l * p.li + e * p.es;
-        if (p.ablate == 2) {
+        if (PB_FFT_ABLATE_TRAFFIC) {
           if (v.x == 12345.678) p.out[a] = v.y;  // keeps the LDS reads (never true on real data)
           continue;
         }
