@@ -589,10 +589,11 @@ int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
   return PB_OK;
 }
 
-// Launch shapes (512^3, profiles/r03/fft_ab*.jsonl): the strided passes stage 16-line tiles
-// (128-B row pieces), persistent with register prefetch on 512-point lines (Y 0.50 -> 0.46 ms;
-// at 256 points one tile per block is faster). PB_FFT_PF_STRIDED = 0 / 1 forces either;
-// PB_FFT_TL_Z = 32 (512-point lines): 32-line Z tiles, 256-B pieces, one block per CU.
+// Launch shapes (512^3, profiles/r03/fft_ab*.jsonl, lines_ab.jsonl): the strided passes stage
+// 16-line tiles (128-B row pieces), one tile per block -- with unconditional tile loads that
+// beats persistent blocks with register prefetch (Y 0.389 vs 0.452 ms, Z 0.646 vs 0.651;
+// PB_FFT_PF_STRIDED=1 selects those); PB_FFT_TL_Z = 32 (512-point lines): 32-line Z tiles, 256-B
+// pieces, one block per CU (measured no faster).
 template <int N, int LAYOUT, int MODE>
 int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   if (p.ninner % 2)
@@ -601,7 +602,7 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   if constexpr (LAYOUT == 1) {
     return launch_dht_k<N, TL, 1, MODE, false>(ctx, p, skip);
   } else {
-    static const int pfs = env_int("PB_FFT_PF_STRIDED", N == 512 ? 1 : 0);
+    static const int pfs = env_int("PB_FFT_PF_STRIDED", 0);
     if constexpr (N == 512 && MODE == 1) {
       static const int tlz = env_int("PB_FFT_TL_Z", 16);
       if (tlz == 32)
