@@ -19,6 +19,7 @@
 // TL consecutive i at fixed k), X pass (along i, tile = TL consecutive contiguous lines).
 // The results match the reference to rounding (operation order differs from Thomas + Sherman-
 // Morrison in src/tridsol.f90:34-74); the bit-exact reference-order path stays in pb_compact.hip.
+#include <algorithm>
 #include <cmath>
 
 #include "pb_internal.hpp"
@@ -52,6 +53,13 @@ struct LinePass {
                // at 512^3, profiles/r02/ab_remap_compact.jsonl)
   LineOp J, L;
   const int* skip;  // pb_ctx::op_skip (exit at entry once set)
+  // CG fusions (CgFuse): Z pass forming p from in0 = z and in1 = p_old (CGP kernels), X pass
+  // taking p . w partial sums (DOT kernels)
+  double* p_out;
+  const CgState* st;
+  int first;
+  const double* dot_p;
+  double* parts;
 };
 
 static LineOp make_line_op(int kind, int C, double h) {
@@ -285,6 +293,36 @@ __device__ __forceinline__ void tile_store(const LinePass& p, double* __restrict
   }
 }
 
+// CGP: p = (dinv z - mu) + (beta / beta_old) p_old on the tile's pairs (z in `pre`, p_old in
+// `pold`), written back into `pre` and stored to p_out at the pairs' own addresses. The products
+// and sums round separately, as cg_gen_p_kernel's (built without contraction): bit-identical.
+template <int C, int LAYOUT, int TL, int V, int NT>
+__device__ __forceinline__ void cg_form_p(const LinePass& p, int64_t base, int nl,
+                                          TileRegs<C, LAYOUT, TL, V, NT>& pre,
+                                          const TileRegs<C, LAYOUT, TL, V, NT>& pold) {
+  using T = TileRegs<C, LAYOUT, TL, V, NT>;
+  const CgState* st = p.st;
+  const double dinv = st->dinv, shift = -st->mu;
+  const double bb = st->it == 0 ? 0.0 : st->beta / st->betaold;
+#pragma unroll
+  for (int r = 0; r < T::R; ++r) {
+    int l, e;
+    const int f = threadIdx.x + NT * r;
+    tile_coord<C, LAYOUT, TL, V>(f, l, e);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      const double z = __dadd_rn(__dmul_rn(dinv, pre.v[r][q]), shift);
+      pre.v[r][q] = p.first ? z : __dadd_rn(z, __dmul_rn(bb, pold.v[r][q]));
+    }
+    if ((T::NF % NT == 0 || f < T::NF) && l < nl && !PB_LINES_ABLATE_TRAFFIC) {
+      dv2 w;
+      w.x = pre.v[r][0];
+      w.y = pre.v[r][V - 1];
+      __builtin_nontemporal_store(w, (dv2*)(p.p_out + base + l * p.li + e * p.es));
+    }
+  }
+}
+
 template <int C>
 __device__ __forceinline__ void chunk_read(const double* lds, int l, int lane, double (&x)[C]) {
   const int w0 = l * Lds<C>::LP + lane * Lds<C>::CP;
@@ -308,8 +346,12 @@ struct LineCfg {
   static constexpr int TL = TL_, NW = NW_, PF = PF_, NT = 64 * NW_, LPW = TL_ / NW_;
 };
 
-template <int C, int LAYOUT, int PASS, class K, int V>
+// CGP (PASS 0, V = 2): in0 = z, in1 = p_old; the tile's input is p = (dinv z - mu) + beta/
+// beta_old p_old (cg_gen_p_kernel's operations, unfused roundings: bit-identical), also stored to
+// p_out as it goes into LDS
+template <int C, int LAYOUT, int PASS, class K, int V, bool CGP = false>
 __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
+  static_assert(!CGP || (PASS == 0 && V == 2 && K::PF == 1), "CGP: Z pass, pairs, prefetch");
   if (p.skip && *p.skip) return;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   constexpr int TL = K::TL, LPW = K::LPW, NT = K::NT;
@@ -324,6 +366,7 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
   int t = xcd_block(p.remap);
   if (t >= ntiles) return;
   double keep[LPW][C];
+  TileRegs<C, LAYOUT, TL, V, NT> pold;  // CGP: p_old of the prefetched tile (dead otherwise)
   // one tile: its input registers `pre` go to LDS, then (PF) tile tn's input is fetched into them
   // while this tile is solved and stored
   auto step = [&](int t, TileRegs<C, LAYOUT, TL, V, NT>& pre, int tn) {
@@ -333,11 +376,15 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
     if (K::PF && tn < ntiles) tile_of(tn, base_n, nl_n);
     __syncthreads();  // previous tile's LDS reads are done
     if (!K::PF) tile_fetch(p, p.in0, base, nl, pre);
+    if constexpr (CGP) cg_form_p<C, LAYOUT, TL, V, NT>(p, base, nl, pre, pold);
     tile_put(lds, nl, pre);
     __syncthreads();
     if (K::PF) {
       if (PASS == 0 || PASS == 3) {
-        if (tn < ntiles) tile_fetch(p, p.in0, base_n, nl_n, pre);
+        if (tn < ntiles) {
+          tile_fetch(p, p.in0, base_n, nl_n, pre);
+          if constexpr (CGP) tile_fetch(p, p.in1, base_n, nl_n, pold);
+        }
       } else {
         tile_fetch(p, p.in1, base, nl, pre);
       }
@@ -424,6 +471,7 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
       int n0;
       tile_of(t, b0, n0);
       tile_fetch(p, p.in0, b0, n0, pre);
+      if constexpr (CGP) tile_fetch(p, p.in1, b0, n0, pold);
     }
     for (; t < ntiles; t += gridDim.x) step(t, pre, t + gridDim.x);
   }
@@ -438,15 +486,10 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int C>
-__global__ __launch_bounds__(256) void compact_lines_x_direct(LinePass p, int64_t nlines) {
-  if (p.skip && *p.skip) return;
+template <int C, bool DOT>
+__device__ __forceinline__ void x_direct_line(const LinePass& p, int64_t line, double* sl,
+                                              int lane, double& acc) {
   constexpr int LP = Lds<C>::LP, CP = Lds<C>::CP;
-  __shared__ double strip[4][2 * LP];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t line = (int64_t)blockIdx.x * 4 + wave;
-  if (line >= nlines) return;
-  double* sl = strip[wave];
   const int64_t off = line * (64 * C);
   constexpr int NP = 32 * C;  // 16-byte pieces per line
   constexpr int R = (NP + 63) / 64;
@@ -483,6 +526,14 @@ __global__ __launch_bounds__(256) void compact_lines_x_direct(LinePass p, int64_
 #pragma unroll
   for (int m = 0; m < C; ++m) sl[lane * CP + m] = r1[m] + r2[m];
   wave_sync();
+  dv2 pp[R];
+  if constexpr (DOT) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int q = lane + 64 * r;
+      pp[r] = __builtin_nontemporal_load((const dv2*)(p.dot_p + off) + (NP % 64 == 0 || q < NP ? q : 0));
+    }
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int q = lane + 64 * r;
@@ -491,12 +542,55 @@ __global__ __launch_bounds__(256) void compact_lines_x_direct(LinePass p, int64_
       o.x = sl[w(2 * q)];
       o.y = sl[w(2 * q + 1)];
       __builtin_nontemporal_store(o, (dv2*)(p.out0 + off) + q);
+      if constexpr (DOT) {
+        acc += o.x * pp[r].x;
+        acc += o.y * pp[r].y;
+      }
     }
+  }
+  wave_sync();  // the strip is reused by the wave's next line
+}
+
+// DOT: CG's p . w partial sums as w is written (p = p.dot_p): the waves walk lines
+// grid-stride (line = 4 block + wave + 4 grid k), each lane sums its w p products in order, then a
+// fixed-order block reduction (lane butterflies, waves in order) -> p.parts[block]
+template <int C, bool DOT = false>
+__global__ __launch_bounds__(256) void compact_lines_x_direct(LinePass p, int64_t nlines) {
+  if (p.skip && *p.skip) return;
+  constexpr int LP = Lds<C>::LP, CP = Lds<C>::CP;
+  __shared__ double strip[4][2 * LP];
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double acc = 0.0;
+  for (int64_t line = (int64_t)blockIdx.x * 4 + wave; line < nlines;
+       line += DOT ? (int64_t)gridDim.x * 4 : nlines) {
+    x_direct_line<C, DOT>(p, line, strip[wave], lane, acc);
+  }
+  if constexpr (DOT) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) red[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) p.parts[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
   }
 }
 
+
 template <int C>
 static int launch_x_direct(pb_ctx* ctx, LinePass& p, int64_t nlines) {
+  CgFuse* cf = ctx->cg_fuse;
+  if (cf && cf->dot_p) {  // p . w partial sums: a fixed grid of at most 16 blocks per CU
+    const int64_t nb = std::min<int64_t>((nlines + 3) / 4, (int64_t)ctx->num_cus * 16);
+    if (nb > ctx->partials_cap) return set_error(PB_ERR_UNSUPPORTED, "x pass: partials");
+    p.dot_p = cf->dot_p;
+    p.parts = ctx->d_partials;
+    hipLaunchKernelGGL((compact_lines_x_direct<C, true>), dim3((unsigned)nb), dim3(256), 0,
+                       ctx->stream, p, nlines);
+    PB_HIP(hipGetLastError());
+    cf->nparts = (int)nb;
+    cf->fused_dot = true;
+    return PB_OK;
+  }
   hipLaunchKernelGGL(compact_lines_x_direct<C>, dim3((unsigned)((nlines + 3) / 4)), dim3(256), 0,
                      ctx->stream, p, nlines);
   PB_HIP(hipGetLastError());
@@ -583,13 +677,23 @@ static LineOp make_solve_op(double alpha, int C) {
   return o;
 }
 
+// the CgFuse passes apply: one rank (no z-slab <-> y-slab transposes), register line solves in
+// every direction, the Z pass with prefetch (lines of <= 512 points) on an even x extent, default
+// launch shapes
+bool compact_cg_fusable(const pb_grid* g) {
+  return !grid_split(g) && compact_lines_supported(g->n[0]) && compact_lines_supported(g->n[1]) &&
+         compact_lines_supported(g->n[2]) && g->n[2] <= 512 && g->n[0] % 2 == 0 &&
+         !env_int("PB_LINES_CFG", 0) && env_int("PB_LINES_XDIRECT", 1) &&
+         env_int("PB_CG_FUSE", 1);
+}
+
 bool compact_lines_supported(int64_t n) {
   if (n % 64) return false;
   const int64_t C = n / 64;
   return C == 1 || C == 2 || C == 3 || C == 4 || C == 6 || C == 8 || C == 12 || C == 16;
 }
 
-template <int C, int LAYOUT, int PASS, class K, int V>
+template <int C, int LAYOUT, int PASS, class K, int V, bool CGP = false>
 static int launch_lines_v(pb_ctx* ctx, LinePass& p, int64_t nouter) {
   p.TL = K::TL;
   p.P = Lds<C>::LP;
@@ -597,7 +701,7 @@ static int launch_lines_v(pb_ctx* ctx, LinePass& p, int64_t nouter) {
   p.nouter = (int)nouter;
   const int64_t ntiles = (int64_t)p.ntiles_inner * nouter;
   const size_t lds = (size_t)K::TL * Lds<C>::LP * sizeof(double);
-  auto kern = compact_lines_kernel<C, LAYOUT, PASS, K, V>;
+  auto kern = compact_lines_kernel<C, LAYOUT, PASS, K, V, CGP>;
   static int occ = 0;
   if (!occ) {
     PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -703,6 +807,27 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
     p.lo = nx;
     p.es = nx * ny;
     p.ninner = (int)nx;
+    CgFuse* cf = ctx->cg_fuse;
+    if (cf && cf->z && C <= 8 && nx % 2 == 0 && ((uintptr_t)cf->z & 15) == 0 &&
+        ((uintptr_t)out0 & 15) == 0 && !env_int("PB_LINES_CFG", 0)) {
+      // CG's p formed by the Z pass from z and p_old (CgFuse); in0 is not read
+      p.in0 = cf->z;
+      p.in1 = cf->p_old;
+      p.p_out = cf->p_out;
+      p.st = cf->st;
+      p.first = cf->first;
+      int rc = PB_ERR_UNSUPPORTED;
+      switch (C) {
+        case 1: rc = launch_lines_v<1, 0, 0, LineCfg<16, 16, 1>, 2, true>(ctx, p, ny); break;
+        case 2: rc = launch_lines_v<2, 0, 0, LineCfg<16, 16, 1>, 2, true>(ctx, p, ny); break;
+        case 3: rc = launch_lines_v<3, 0, 0, LineCfg<16, 16, 1>, 2, true>(ctx, p, ny); break;
+        case 4: rc = launch_lines_v<4, 0, 0, LineCfg<16, 16, 1>, 2, true>(ctx, p, ny); break;
+        case 6: rc = launch_lines_v<6, 0, 0, LineCfg<16, 16, 1>, 2, true>(ctx, p, ny); break;
+        case 8: rc = launch_lines_v<8, 0, 0, LineCfg<16, 16, 1>, 2, true>(ctx, p, ny); break;
+      }
+      if (rc == PB_OK) cf->fused_z = true;
+      return rc;
+    }
     return launch_lines<0, 0>(ctx, p, n, ny);
   }
   if (axis == 1) {

@@ -57,6 +57,7 @@ struct TimerSlot {
 };
 constexpr size_t kMaxTimerSamples = 1 << 16;
 
+struct CgFuse;
 }  // namespace pb
 
 struct pb_ctx {
@@ -64,6 +65,9 @@ struct pb_ctx {
   // kernels launched meanwhile exit at entry once it is set -- the host enqueues iterations
   // ahead of its lagged convergence poll, and an operator apply is the costly part of them
   const int* op_skip = nullptr;
+  // CG fusions for the compact operator inside a stored-z CG iteration (CgFuse), set around one
+  // operator apply like op_skip
+  pb::CgFuse* cg_fuse = nullptr;
   int device = 0;
   int rank = 0;
   int nranks = 1;
@@ -331,6 +335,7 @@ inline hipError_t field_alloc(T** p, size_t bytes) {
 
 // ---- register-resident line solves (pb_compact_lines.hip) ----
 bool compact_lines_supported(int64_t n);
+bool compact_cg_fusable(const pb_grid* g);  // CgFuse applies to the compact operator on g
 int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, const double* in0,
                        const double* in1, double* out0, double* out1);
 // batched periodic (alpha,1,alpha) solve in registers (n = 64*C); PB_ERR_UNSUPPORTED otherwise
@@ -362,6 +367,22 @@ int yslab_from(pb_grid* g, const YSlabPlan& p, const double* fy, double* f);
 // all-to-all with per-peer counts; blocks are contiguous in rank order on both sides
 int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,
                      const int64_t* rcount);
+// Config-5 iteration fusions (compact A with a stored-z preconditioner, one rank, register line
+// solves): the compact operator's Z pass forms p = (dinv z - mu) + beta/beta_old p_old from its
+// tile loads and stores p (cg_gen_p_kernel's arithmetic, bit-identical), and its X pass takes the
+// per-block partial sums of p . w as it writes w (cg_gen_dot_kernel's job). The caller sets
+// ctx->cg_fuse around the apply; the passes report what they fused, the caller runs the
+// separate kernels for anything they did not.
+struct CgFuse {
+  const double* z = nullptr;      // Z pass: stored z, the source of p
+  const double* p_old = nullptr;  // previous direction (not used when first)
+  double* p_out = nullptr;        // p as formed
+  const CgState* st = nullptr;
+  int first = 0;                  // KSPSolve_CG's i = 0 (p = z - mu)
+  const double* dot_p = nullptr;  // X pass: p, for the p . w partial sums into ctx->d_partials
+  int nparts = 0;                 // out: partial-sum blocks written by the X pass
+  bool fused_z = false, fused_dot = false;  // out
+};
 int launch_cg_generic_p(pb_grid* g, const double* r, double* p, CgState* st, int first = 0);
 int launch_cg_generic_dot(pb_grid* g, const double* p, const double* w, CgState* st, int* nparts);
 int launch_cg_generic_xr(pb_grid* g, const double* p, const double* w, double* x, double* r,

@@ -858,6 +858,50 @@ def test_cg_compact_lazy_initial_state(ctx, monkeypatch, pc):
     assert np.all(x.get_values() == 0.0)
 
 
+@pytest.mark.parametrize("pc,m", [("fft", 64), ("fft", 128), ("mg", 64), ("sor", 64)])
+def test_cg_compact_fused_passes(ctx, monkeypatch, pc, m):
+    """Stored-z CG on the compact operator with the CgFuse passes (default): the compact Z pass
+    forms p = (z - mu) + beta/beta_old p_old (cg_gen_p_kernel's arithmetic) and the X pass takes
+    the p . w partial sums. Against PB_CG_FUSE=0 (separate p and dot passes): same reason and
+    iterations, p . w summed in another order so the history and x agree to rounding; and the
+    oracle's reason / its / history at the CG bars (fixed 6 iterations for the slow MG / SOR)."""
+    n3 = (m, m, m)
+    h = (2 * np.pi / m,) * 3
+    N = m ** 3
+    b = O.lapl(O.fill_random(N, SEED), n3, h)
+    da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+    P = pb.Mat(da, pb.ASSEMBLED27, h)
+    A = pb.Mat(da, pb.COMPACT, h)
+    Pm = A if pc == "fft" else P
+    if pc == "fft":
+        opts = ["-pc_type", pc, "-ksp_rtol", "1e-10"]
+        kw = dict(rtol=1e-10)
+    else:
+        opts = ["-pc_type", pc, "-ksp_rtol", "0", "-ksp_atol", "0", "-ksp_max_it", "6",
+                "-ksp_divtol", "1e300"]
+        kw = dict(rtol=0.0, atol=0.0, dtol=1e300, max_it=6)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("PB_CG_FUSE", fuse)
+        bv.set_values(b)
+        reason, its, hist = pb.solve(Pm, A, x, bv, opts)
+        res[fuse] = (reason, its, np.asarray(hist), x.get_values())
+    monkeypatch.setenv("PB_CG_FUSE", "1")
+    (r1, i1, h1, x1), (r0, i0, h0, x0) = res["1"], res["0"]
+    assert (r1, i1) == (r0, i0)
+    assert np.max(np.abs(h1 - h0) / h0) < 1e-12
+    assert np.max(np.abs(x1 - x0)) <= 1e-12 * np.max(np.abs(x0))
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, pc=pc, op="compact",
+                                  pc_compact=(pc == "fft"), nthreads=8, **kw)
+    assert (r1, i1) == (ro, itso)
+    if pc == "fft":
+        assert abs(h1[0] - ho[0]) / ho[0] < 1e-12
+    else:
+        check_history(h1, ho, bar=HIST_RTOL_PC)
+    check_x(x1, xo, scale=np.max(np.abs(xo)))
+
+
 @pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("pc,omega,n3", [("sor", 2.5, (16, 12, 8)), ("mg", 2.2, (16, 16, 16)),
                                          ("mg", 2.2, (32, 32, 32))])
