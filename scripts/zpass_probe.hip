@@ -81,6 +81,27 @@ __global__ __launch_bounds__(32 * TL) void tile_lds(const double* __restrict__ i
   }
 }
 
+// wave-direct: a block of NW waves owns 2 NW x-adjacent lines of one row j; wave w moves lines
+// (2w, 2w+1) itself, lane l the elements e = l + 64 r (r < NZ / 64), one 16-B pair per element --
+// the access of a Z-pass whose first and last Stockham passes run from registers (every wave
+// instruction touches 64 rows; the NW waves of the block together cover each 2NW*8-byte piece)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void wave_direct(const double* __restrict__ in,
+                                                      double* __restrict__ out) {
+  constexpr int TL = 2 * NW, NR = NZ / 64;
+  const int ntx = NX / TL;
+  const int tx = blockIdx.x % ntx, j = blockIdx.x / ntx;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long base = (long)j * NX + tx * TL + 2 * w;
+  dv2 v[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    v[r] = __builtin_nontemporal_load((const dv2*)(in + base + (long)(lane + 64 * r) * PLANE));
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    __builtin_nontemporal_store(v[r], (dv2*)(out + base + (long)(lane + 64 * r) * PLANE));
+}
+
 __global__ __launch_bounds__(256) void flat_copy(const dv2* __restrict__ in, dv2* __restrict__ out,
                                                  long n) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
@@ -134,6 +155,14 @@ static void run_lds() {
   });
 }
 
+template <int NW>
+static void run_direct() {
+  run("wave_direct", 2 * NW, 0, [=] {
+    hipLaunchKernelGGL(wave_direct<NW>, dim3((NX / (2 * NW)) * NY), dim3(64 * NW), 0, 0, g_in,
+                       g_out);
+  });
+}
+
 int main() {
   const size_t n = (size_t)NX * NY * NZ;
   CK(hipMalloc(&g_in, n * 8));
@@ -143,21 +172,12 @@ int main() {
     hipLaunchKernelGGL(flat_copy, dim3(256 * 32), dim3(256), 0, 0, (const dv2*)g_in, (dv2*)g_out,
                        (long)(n / 2));
   });
-  run_lds<8>();
   run_lds<16>();
-  regs<8, 4, 512>();
-  regs<8, 8, 512>();
+  run_direct<4>();
+  run_direct<8>();
+  run_direct<16>();
+  run_lds<16>();
   regs<16, 4, 512>();
-  regs<16, 16, 512>();
-  regs<32, 4, 512>();
-  regs<32, 16, 512>();
-  regs<64, 4, 512>();
-  regs<64, 16, 512>();
-  regs<128, 4, 512>();
-  regs<128, 16, 512>();
-  regs<16, 2, 64>();
   regs<64, 8, 64>();
-  regs<256, 8, 64>();
-  regs<512, 8, 64>();
   return 0;
 }

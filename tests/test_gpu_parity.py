@@ -890,7 +890,10 @@ def test_cg_compact_fused_passes(ctx, monkeypatch, pc, m):
     monkeypatch.setenv("PB_CG_FUSE", "1")
     (r1, i1, h1, x1), (r0, i0, h0, x0) = res["1"], res["0"]
     assert (r1, i1) == (r0, i0)
-    assert np.max(np.abs(h1 - h0) / h0) < 1e-12
+    # with the spectral PC the converged norm is rounding noise (~1e-14 of the first): measured
+    # against ||z_0|| there; every norm against itself for the slowly converging MG / SOR runs
+    scale = h0[0] if pc == "fft" else h0
+    assert np.max(np.abs(h1 - h0) / scale) < 1e-12
     assert np.max(np.abs(x1 - x0)) <= 1e-12 * np.max(np.abs(x0))
     xo, ro, itso, ho = O.cg_solve(b, n3, h, pc=pc, op="compact",
                                   pc_compact=(pc == "fft"), nthreads=8, **kw)
