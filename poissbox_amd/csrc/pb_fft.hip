@@ -27,7 +27,8 @@
 // from Z(k) and Z(n - k), read from LDS. Line lengths n = 2^a 3^b 5^c (a >= 1) in 32..1024. The
 // element index is XOR-swizzled in LDS (lpad), so the scattered writes of the first pass hit
 // distinct banks. Twiddles exp(-2 pi i k / n) come from a per-axis table, copied into LDS
-// per block for n <= 512. (r02's engine ran the 64-point cross-lane part of the transform as six
+// per block for n <= 512. X passes at 512 / 1024 points run register edges instead
+// (dht_reg_x_kernel): no tile staging, the first and last Stockham passes on registers. (r02's engine ran the 64-point cross-lane part of the transform as six
 // radix-2 stages of DPP / permlane exchanges: 2.5x the VALU work, and its Z pass, which runs two
 // transforms, was compute-bound at 1.0-1.1 ms at 512^3 whatever the tile width.)
 #include <algorithm>
@@ -85,7 +86,7 @@ __device__ __forceinline__ cplx cpi(cplx a) { return {-a.im, a.re}; }  // +i a
 __device__ __forceinline__ cplx cscale(cplx a, double s) { return {a.re * s, a.im * s}; }
 
 // ---- Stockham plans: n = 2^a 3^b 5^c; radix 8 while 8 divides what is left, then 4, 2, 3, 5 ----
-__host__ __device__ constexpr int plan_radix_at(int n, int p) {
+__host__ __device__ constexpr int natural_radix_at(int n, int p) {
   int rest = n;
   for (int q = 0; q <= p; ++q) {
     if (rest <= 1) return 0;
@@ -100,6 +101,27 @@ __host__ __device__ constexpr int plan_radix_at(int n, int p) {
   }
   return 0;
 }
+__host__ __device__ constexpr int natural_len(int n) {
+  int rest = n, p = 0;
+  for (; rest > 1; ++p) {
+    const int r = natural_radix_at(n, p);
+    if (r == 0) return 0;
+    rest /= r;
+  }
+  return p;
+}
+// The plan used everywhere (kernels and the host twiddle tables): the natural order, except that a
+// last radix that differs from the first moves to second place when that makes the first and last
+// passes equal (1024: 8 8 8 2 -> 8 2 8 8), so the register-edge kernel (dht_reg_kernel) can run
+// the first and last passes from registers
+__host__ __device__ constexpr int plan_radix_at(int n, int p) {
+  const int L = natural_len(n);
+  const bool rot = L >= 3 && natural_radix_at(n, L - 1) != natural_radix_at(n, 0) &&
+                   natural_radix_at(n, L - 2) == natural_radix_at(n, 0);
+  if (!rot || p == 0 || p >= L) return natural_radix_at(n, p);
+  return p == 1 ? natural_radix_at(n, L - 1) : natural_radix_at(n, p - 1);
+}
+__host__ __device__ constexpr int plan_len(int n) { return natural_len(n); }
 __host__ __device__ constexpr bool plan_complete(int n) {
   int rest = n;
   for (int p = 0; rest > 1; ++p) {
@@ -328,6 +350,82 @@ __device__ __forceinline__ void scale_combine2(double* A, double* B, const DhtPa
   wave_sync_lds();
 }
 
+// ---- register edges (r03): lane l of a wave owns butterflies jb = l + 64 t of the first and of
+// the last Stockham pass (plans whose first and last radix agree and N / R is a multiple of 64:
+// 512, 1024), whose elements jb + (N / R) r are exactly the ones it would load and store: the first
+// pass can run on registers and the last one can leave the natural-order spectrum in registers.
+// Each saves one LDS sweep (ds_write_b64 moves 85 B/clk per CU against 256 for ds_read_b64,
+// MI355X_MICROARCH.md §LDS). ----
+template <int N>
+struct RegPlan {
+  static constexpr int R = plan_radix_at(N, 0);
+  static constexpr int NB = N / R;  // butterflies of the first and of the last pass
+  static constexpr int T = NB / 64;
+  static constexpr int NP = plan_len(N);
+  static constexpr bool OK = NB % 64 == 0 && NP >= 2 && plan_radix_at(N, NP - 1) == R;
+};
+
+// first pass (NS = 1) on v, outputs to the wave's LDS rows
+template <int N, int R, int T>
+__device__ __forceinline__ void first_pass_regs(cplx (&v)[T][R], double* A, double* B, int lane) {
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    dft<R>(v[t]);
+    const int jb = lane + 64 * t;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int e = lpad(jb * R + r);
+      A[e] = v[t][r].re;
+      B[e] = v[t][r].im;
+    }
+  }
+  wave_sync_lds();
+}
+
+// middle passes P in [1, PL)
+template <int N, int P, int PL, int NS>
+__device__ __forceinline__ void mid_passes(double* A, double* B, const double* tw, int lane) {
+  if constexpr (P < PL) {
+    constexpr int R = plan_radix_at(N, P);
+    stockham_pass<N, R, NS>(A, B, tw, lane);
+    mid_passes<N, P + 1, PL, NS * R>(A, B, tw, lane);
+  }
+}
+
+// last pass (NS = N / R) from the wave's LDS rows into v: v[t][r] = Z(jb + NB r)
+template <int N, int R, int T>
+__device__ __forceinline__ void last_pass_regs(cplx (&v)[T][R], const double* A, const double* B,
+                                               const double* tw, int lane) {
+  constexpr int NB = N / R;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int jb = lane + 64 * t;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int e = lpad(jb + r * NB);
+      v[t][r] = {A[e], B[e]};
+    }
+    const double* w = tw + 2 * (NB - 1 + jb * (R - 1));
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      const dv2 c = *(const dv2*)(w + 2 * (r - 1));
+      v[t][r] = cmul(v[t][r], {c.x, c.y});
+    }
+    dft<R>(v[t]);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void fft_regs(cplx (&v)[RegPlan<N>::T][RegPlan<N>::R], double* A,
+                                         double* B, const double* tw, int lane) {
+  using RP = RegPlan<N>;
+  first_pass_regs<N, RP::R, RP::T>(v, A, B, lane);
+  mid_passes<N, 1, RP::NP - 1, RP::R>(A, B, tw, lane);
+  last_pass_regs<N, RP::R, RP::T>(v, A, B, tw, lane);
+  wave_sync_lds();  // the last pass's reads are done before the rows are written again
+}
+
+
 template <int N, int TL_>
 struct DhtTile {
   static constexpr int TL = TL_;              // lines per tile
@@ -552,6 +650,139 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
   }
 }
 
+// X passes (contiguous lines) on register edges: wave w of a 512-thread block owns lines
+// (2w, 2w+1) of a 16-line tile and loads its elements jb + NB r straight from HBM (two coalesced
+// 8-byte rows per element); the first pass runs on them, the last leaves Z(k) in registers, one
+// partner exchange gives Z(N - k) for the Hartley split, and the spectra go straight back to HBM.
+// No tile staging in LDS and no block barrier after the twiddle table (the waves run
+// independently): 512^3 X pass 0.42 -> 0.365 ms (profiles/r03/fft_reg_ab.jsonl). On the strided
+// passes the same per-lane rows (one 16-byte piece of each row per wave instruction) stream at
+// 0.58 TB/s (scripts/zpass_probe.hip, wave_direct), so those keep the LDS tile.
+template <int N, bool SUMS>
+__global__ __launch_bounds__(512, N <= 512 ? 4 : 2) void dht_reg_x_kernel(DhtPass p,
+                                                                          const int* skip) {
+  using RP = RegPlan<N>;
+  static_assert(RP::OK, "register-edge plan");
+  constexpr int R = RP::R, NB = RP::NB, T = RP::T;
+  constexpr int TL = 16, LP = (lpad_max(N) + 1) | 1;
+  constexpr bool TWL = N <= 512;
+  if (skip && *skip) return;  // CG's device convergence flag (uniform)
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double* tw = p.w;
+  if constexpr (TWL) {
+    double* twl = lds + TL * LP;
+    for (int i = threadIdx.x; i < N; i += 512) {
+      const dv2 c = *(const dv2*)(p.w + 2 * i);
+      twl[2 * i] = c.x;
+      twl[2 * i + 1] = c.y;
+    }
+    tw = twl;
+    __syncthreads();
+  }
+  const int tile = xcd_block(p.remap);
+  const int64_t outer = tile / p.ntiles_inner;
+  const int inner0 = (tile % p.ntiles_inner) * TL;
+  const int nl = min(TL, p.ninner - inner0);
+  const int l0 = 2 * wave;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (l0 < nl) {
+    const int64_t base = outer * p.lo + (int64_t)(inner0 + l0) * p.li;  // es == 1
+    cplx v[T][R];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = lane + 64 * t + NB * r;
+        v[t][r] = {__builtin_nontemporal_load(p.in + base + e),
+                   __builtin_nontemporal_load(p.in + base + p.li + e)};
+      }
+    double* A = lds + l0 * LP;
+    double* B = A + LP;
+    fft_regs<N>(v, A, B, tw, lane);
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = lpad(lane + 64 * t + NB * r);
+        A[e] = v[t][r].re;
+        B[e] = v[t][r].im;
+      }
+    wave_sync_lds();
+    const double mu = SUMS ? p.st->mu : 0.0;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int k = lane + 64 * t + NB * r;
+        const int em = lpad(k == 0 ? 0 : N - k);
+        const double zr = v[t][r].re, zi = v[t][r].im, mr = A[em], mi = B[em];
+        const double hx = 0.5 * ((zr + mr) - (zi - mi));  // dht2's split
+        const double hy = 0.5 * ((zi + mi) + (zr - mr));
+        __builtin_nontemporal_store(hx, p.out + base + k);
+        __builtin_nontemporal_store(hy, p.out + base + p.li + k);
+        if (SUMS) {  // CG's residual sums (t, t^2, t r, r), t = z - mu
+          const double rx = __builtin_nontemporal_load(p.sr + base + k);
+          const double ry = __builtin_nontemporal_load(p.sr + base + p.li + k);
+          const double t0 = hx - mu, t1 = hy - mu;
+          acc[0] += t0;
+          acc[1] += t0 * t0;
+          acc[2] += t0 * rx;
+          acc[3] += rx;
+          acc[0] += t1;
+          acc[1] += t1 * t1;
+          acc[2] += t1 * ry;
+          acc[3] += ry;
+        }
+      }
+  }
+  if constexpr (SUMS) {  // fixed-order block reduction: wave butterflies, then waves in order
+    __syncthreads();     // every wave's LDS rows are done
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double sv = acc[q];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) sv += __shfl_xor(sv, off, 64);
+      if (lane == 0) lds[wave * 4 + q] = sv;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      double sv = lds[threadIdx.x];
+      for (int w = 1; w < 8; ++w) sv += lds[w * 4 + threadIdx.x];
+      p.parts[(int64_t)blockIdx.x * 4 + threadIdx.x] = sv;
+    }
+  }
+}
+
+template <int N>
+int launch_dht_reg_x(pb_ctx* ctx, DhtPass& p, const int* skip) {
+  constexpr int TL = 16, LP = (lpad_max(N) + 1) | 1;
+  constexpr size_t LDS = (size_t)(TL * LP + (N <= 512 ? 2 * N : 0)) * sizeof(double);
+  p.ntiles_inner = (p.ninner + TL - 1) / TL;
+  const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
+  auto kern = dht_reg_x_kernel<N, false>;
+  auto kern_s = dht_reg_x_kernel<N, true>;
+  static bool attr = false;
+  if (!attr) {
+    PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)LDS));
+    PB_HIP(hipFuncSetAttribute((const void*)kern_s, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)LDS));
+    attr = true;
+  }
+  if (ntiles > INT32_MAX) return set_error(PB_ERR_UNSUPPORTED, "fft pc: too many tiles");
+  if (p.parts) {
+    if (ntiles * 4 > ctx->partials_cap)
+      return set_error(PB_ERR_UNSUPPORTED, "fft pc: %lld blocks exceed the partials capacity",
+                       (long long)ntiles);
+    p.nparts_out = (int)ntiles;
+    kern = kern_s;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(512), LDS, ctx->stream, p, skip);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
 // TL lines per tile, PFS: persistent blocks + register prefetch on a strided pass
 template <int N, int TL, int LAYOUT, int MODE, bool PFS>
 int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
@@ -598,6 +829,11 @@ template <int N, int LAYOUT, int MODE>
 int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   if (p.ninner % 2)
     return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines (even counts only)", p.ninner);
+  if constexpr (RegPlan<N>::OK && LAYOUT == 1) {
+    // PB_FFT_REG=0: the X passes on the LDS-tile kernel
+    static const int reg = env_int("PB_FFT_REG", 1);
+    if (reg) return launch_dht_reg_x<N>(ctx, p, skip);
+  }
   constexpr int TL = tile_lines<N>();
   if constexpr (LAYOUT == 1) {
     return launch_dht_k<N, TL, 1, MODE, false>(ctx, p, skip);
