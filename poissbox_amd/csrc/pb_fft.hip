@@ -64,6 +64,15 @@ struct DhtPass {
   int stagger, ncu;   // PB_FFT_STAGGER=s: the second resident round of blocks (blockIdx in
                       // [ncu, 2 ncu)) sleeps s x 8128 cycles first, so co-resident blocks run out of
                       // phase (one loads while the other transforms) -- A/B knob
+  // CG's x / r update on the first X pass (register-edge kernel): the line input is
+  // r = ru_in + (-alpha) ru_w, also stored to ru_out; ru_x = ru_x + alpha ru_p (ru_first: alpha p)
+  const double* ru_in;
+  const double* ru_w;
+  double* ru_out;
+  const double* ru_p;
+  double* ru_x;
+  int ru_first;
+  const CgState* ru_st;
   int ablate;         // timing experiments only (PB_FFT_ABLATE=1): no transforms (tile copy
                       // through LDS); builds with -DPB_FFT_ABLATE_TRAFFIC=1 drop the global loads
                       // and stores instead (transforms on stale LDS)
@@ -658,15 +667,26 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
 // independently): 512^3 X pass 0.42 -> 0.365 ms (profiles/r03/fft_reg_ab.jsonl). On the strided
 // passes the same per-lane rows (one 16-byte piece of each row per wave instruction) stream at
 // 0.58 TB/s (scripts/zpass_probe.hip, wave_direct), so those keep the LDS tile.
-template <int N, bool SUMS>
+template <int N, bool SUMS, bool RUPD>
 __global__ __launch_bounds__(512, N <= 512 ? 4 : 2) void dht_reg_x_kernel(DhtPass p,
                                                                           const int* skip) {
+  static_assert(!(SUMS && RUPD), "sums on the last pass, the r update on the first");
   using RP = RegPlan<N>;
   static_assert(RP::OK, "register-edge plan");
   constexpr int R = RP::R, NB = RP::NB, T = RP::T;
   constexpr int TL = 16, LP = (lpad_max(N) + 1) | 1;
   constexpr bool TWL = N <= 512;
-  if (skip && *skip) return;  // CG's device convergence flag (uniform)
+  if (skip && *skip) {  // CG's device convergence flag (uniform)
+    if (RUPD && p.ru_first) {  // a breakdown before the first update leaves x = x0 = 0
+      const int tile = blockIdx.x;
+      const int64_t outer = tile / p.ntiles_inner;
+      const int inner0 = (tile % p.ntiles_inner) * TL;
+      const int nl = min(TL, p.ninner - inner0);
+      for (int i = threadIdx.x; i < nl * N; i += 512)
+        p.ru_x[outer * p.lo + (int64_t)(inner0 + i / N) * p.li + i % N] = 0.0;
+    }
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const double* tw = p.w;
@@ -680,23 +700,50 @@ __global__ __launch_bounds__(512, N <= 512 ? 4 : 2) void dht_reg_x_kernel(DhtPas
     tw = twl;
     __syncthreads();
   }
-  const int tile = xcd_block(p.remap);
+  const int l0 = 2 * wave;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  // one tile per block; with the sums, a resident grid walks the tiles (fewer partial blocks for
+  // the finalize to reduce: 512 instead of 16384 at 512^3)
+  auto do_tile = [&](int tile) {
   const int64_t outer = tile / p.ntiles_inner;
   const int inner0 = (tile % p.ntiles_inner) * TL;
   const int nl = min(TL, p.ninner - inner0);
-  const int l0 = 2 * wave;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  wave_sync_lds();  // the wave's LDS reads of its previous tile are done
   if (l0 < nl) {
     const int64_t base = outer * p.lo + (int64_t)(inner0 + l0) * p.li;  // es == 1
     cplx v[T][R];
+    if constexpr (RUPD) {  // cg_pc_xr_kernel's arithmetic, rounded as there (no contraction)
+      const double a = p.ru_st->alpha, ma = -a;
+      const bool first = p.ru_first;
 #pragma unroll
-    for (int t = 0; t < T; ++t)
+      for (int t = 0; t < T; ++t)
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int e = lane + 64 * t + NB * r;
-        v[t][r] = {__builtin_nontemporal_load(p.in + base + e),
-                   __builtin_nontemporal_load(p.in + base + p.li + e)};
-      }
+        for (int r = 0; r < R; ++r) {
+          const int64_t e0 = base + lane + 64 * t + NB * r, e1 = e0 + p.li;
+          const double r0 = __dadd_rn(__builtin_nontemporal_load(p.ru_in + e0),
+                                      __dmul_rn(ma, __builtin_nontemporal_load(p.ru_w + e0)));
+          const double r1 = __dadd_rn(__builtin_nontemporal_load(p.ru_in + e1),
+                                      __dmul_rn(ma, __builtin_nontemporal_load(p.ru_w + e1)));
+          __builtin_nontemporal_store(r0, p.ru_out + e0);
+          __builtin_nontemporal_store(r1, p.ru_out + e1);
+          v[t][r] = {r0, r1};
+          const double ap0 = __dmul_rn(a, __builtin_nontemporal_load(p.ru_p + e0));
+          const double ap1 = __dmul_rn(a, __builtin_nontemporal_load(p.ru_p + e1));
+          const double x0 = first ? ap0 : __dadd_rn(__builtin_nontemporal_load(p.ru_x + e0), ap0);
+          const double x1 = first ? ap1 : __dadd_rn(__builtin_nontemporal_load(p.ru_x + e1), ap1);
+          __builtin_nontemporal_store(x0, p.ru_x + e0);
+          __builtin_nontemporal_store(x1, p.ru_x + e1);
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int e = lane + 64 * t + NB * r;
+          v[t][r] = {__builtin_nontemporal_load(p.in + base + e),
+                     __builtin_nontemporal_load(p.in + base + p.li + e)};
+        }
+    }
     double* A = lds + l0 * LP;
     double* B = A + LP;
     fft_regs<N>(v, A, B, tw, lane);
@@ -736,6 +783,13 @@ __global__ __launch_bounds__(512, N <= 512 ? 4 : 2) void dht_reg_x_kernel(DhtPas
         }
       }
   }
+  };
+  if constexpr (SUMS) {
+    const int ntiles = p.ntiles_inner * p.nouter;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) do_tile(tile);
+  } else {
+    do_tile(xcd_block(p.remap));
+  }
   if constexpr (SUMS) {  // fixed-order block reduction: wave butterflies, then waves in order
     __syncthreads();     // every wave's LDS rows are done
 #pragma unroll
@@ -760,25 +814,36 @@ int launch_dht_reg_x(pb_ctx* ctx, DhtPass& p, const int* skip) {
   constexpr size_t LDS = (size_t)(TL * LP + (N <= 512 ? 2 * N : 0)) * sizeof(double);
   p.ntiles_inner = (p.ninner + TL - 1) / TL;
   const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
-  auto kern = dht_reg_x_kernel<N, false>;
-  auto kern_s = dht_reg_x_kernel<N, true>;
+  auto kern = dht_reg_x_kernel<N, false, false>;
+  auto kern_s = dht_reg_x_kernel<N, true, false>;
+  auto kern_r = dht_reg_x_kernel<N, false, true>;
   static bool attr = false;
   if (!attr) {
-    PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)LDS));
-    PB_HIP(hipFuncSetAttribute((const void*)kern_s, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)LDS));
+    for (auto k : {kern, kern_s, kern_r})
+      PB_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)LDS));
     attr = true;
   }
+  if (p.ru_st) {
+    if (p.parts) return set_error(PB_ERR_STATE, "fft pc: r update and sums on one pass");
+    kern = kern_r;
+  }
   if (ntiles > INT32_MAX) return set_error(PB_ERR_UNSUPPORTED, "fft pc: too many tiles");
+  int64_t nblocks = ntiles;
   if (p.parts) {
-    if (ntiles * 4 > ctx->partials_cap)
+    static int occ = 0;
+    if (!occ) {
+      PB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern_s, 512, LDS));
+      if (occ < 1) occ = 1;
+    }
+    nblocks = std::min<int64_t>(ntiles, (int64_t)occ * ctx->num_cus);
+    if (nblocks * 4 > ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fft pc: %lld blocks exceed the partials capacity",
-                       (long long)ntiles);
-    p.nparts_out = (int)ntiles;
+                       (long long)nblocks);
+    p.nparts_out = (int)nblocks;
     kern = kern_s;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)ntiles), dim3(512), LDS, ctx->stream, p, skip);
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(512), LDS, ctx->stream, p, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
@@ -825,15 +890,20 @@ int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
 // beats persistent blocks with register prefetch (Y 0.389 vs 0.452 ms, Z 0.646 vs 0.651;
 // PB_FFT_PF_STRIDED=1 selects those); PB_FFT_TL_Z = 32 (512-point lines): 32-line Z tiles, 256-B
 // pieces, one block per CU (measured no faster).
+static bool reg_x_on() {
+  static const int reg = env_int("PB_FFT_REG", 1);
+  return reg != 0;
+}
+
 template <int N, int LAYOUT, int MODE>
 int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   if (p.ninner % 2)
     return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines (even counts only)", p.ninner);
   if constexpr (RegPlan<N>::OK && LAYOUT == 1) {
     // PB_FFT_REG=0: the X passes on the LDS-tile kernel
-    static const int reg = env_int("PB_FFT_REG", 1);
-    if (reg) return launch_dht_reg_x<N>(ctx, p, skip);
+    if (reg_x_on()) return launch_dht_reg_x<N>(ctx, p, skip);
   }
+  if (p.ru_st) return set_error(PB_ERR_STATE, "fft pc: r update on the register-edge X pass only");
   constexpr int TL = tile_lines<N>();
   if constexpr (LAYOUT == 1) {
     return launch_dht_k<N, TL, 1, MODE, false>(ctx, p, skip);
@@ -993,7 +1063,8 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
 // one DHT along an axis of the box b (b[2] = planes), in place or from `in`
 static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, const double* in,
                     double* out, const int* skip, int j0 = 0, const double* sr = nullptr,
-                    const CgState* st = nullptr, int* np = nullptr) {
+                    const CgState* st = nullptr, int* np = nullptr,
+                    const RUpdate* ru = nullptr) {
   static const char* names[3] = {"pc_fft_x", "pc_fft_y", "pc_fft_z"};
   ScopedTimer tm(ctx, names[axis]);
   DhtPass p{};
@@ -1015,6 +1086,15 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
       p.sr = sr;
       p.st = st;
       p.parts = ctx->d_partials;
+    }
+    if (ru) {  // CG's x / r update rides on this (first) pass
+      p.ru_in = ru->r_in;
+      p.ru_w = ru->w;
+      p.ru_out = ru->r_out;
+      p.ru_p = ru->p;
+      p.ru_x = ru->x;
+      p.ru_first = ru->first;
+      p.ru_st = ru->st;
     }
     PB_TRY((launch_dht<1, 0>(ctx, nx, p, skip)));
     if (np) *np = p.nparts_out;
@@ -1043,14 +1123,20 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   return launch_dht<0, 1>(ctx, nz, p, skip);
 }
 
+bool fftpc_fuses_r_update(const FftPc* f) {
+  return reg_x_on() && (f->g->n[0] == 512 || f->g->n[0] == 1024) && f->g->n[1] % 2 == 0;
+}
+
 int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgState* sums_st,
-                int* nparts) {
+                int* nparts, const RUpdate* ru) {
   if (nparts) *nparts = 0;
   pb_grid* g = f->g;
   pb_ctx* ctx = g->ctx;
+  if (ru && !fftpc_fuses_r_update(f))
+    return set_error(PB_ERR_STATE, "fft pc: r update needs the register-edge X pass");
   ScopedTimer tm(ctx, "pc_fft");
   const int64_t b[3] = {g->n[0], g->n[1], g->nzl};
-  PB_TRY(dht_axis(ctx, f, b, 0, r, z, skip));
+  PB_TRY(dht_axis(ctx, f, b, 0, r, z, skip, 0, nullptr, nullptr, nullptr, ru));
   PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
   if (!grid_split(g)) {
     PB_TRY(dht_axis(ctx, f, b, 2, z, z, skip));

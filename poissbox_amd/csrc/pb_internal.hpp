@@ -430,8 +430,23 @@ struct FftPc;
 int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out);
 // sums_st / nparts: the last pass also takes CG's residual sums of z against r (mu from sums_st)
 // into ctx->d_partials, *nparts blocks (0: the caller takes them)
+// CG's x / r update on the PC's first pass (cg_pc_xr_kernel's arithmetic): r = r_in + (-alpha) w
+// is formed as the pass loads it, stored to r_out and transformed; x = x + alpha p (first: alpha p)
+// rides along. With CG's done flag set the pass exits, after writing x = 0 on a first iteration.
+struct RUpdate {
+  const double* r_in;
+  const double* w;
+  double* r_out;
+  const double* p;
+  double* x;
+  int first;
+  const CgState* st;
+};
 int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip = nullptr,
-                const CgState* sums_st = nullptr, int* nparts = nullptr);
+                const CgState* sums_st = nullptr, int* nparts = nullptr,
+                const RUpdate* ru = nullptr);
+// whether fftpc_apply takes an RUpdate on this grid (X passes on the register-edge kernel)
+bool fftpc_fuses_r_update(const FftPc* f);
 void fftpc_destroy(FftPc* f);
 
 // ---- context scratch: at least n doubles, valid until the next call on this context ----

@@ -272,10 +272,14 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   if (opts) k->opts = *opts;
   else pb_ksp_opts_default(&k->opts);
   if (k->opts.check_every < 1) k->opts.check_every = 8;
-  // SOR / MG / FFT iterations are expensive and few: poll the device flag more often
+  // SOR / MG / FFT iterations are expensive and few: poll the device flag more often -- every
+  // iteration with the spectral PC (1-3 iterations per solve: an iteration enqueued ahead of the
+  // poll costs its skipped launches, ~0.15 ms of a 512^3 config-5 solve, more than the idle
+  // stream time of waiting for each iteration)
   if ((k->opts.pc_type == PB_PC_SOR || k->opts.pc_type == PB_PC_MG ||
        k->opts.pc_type == PB_PC_FFT) && k->opts.check_every > 2)
     k->opts.check_every = 2;
+  if (k->opts.pc_type == PB_PC_FFT) k->opts.check_every = std::max(1, env_int("PB_FFT_POLL", 1));
   const int pc = k->opts.pc_type;
   if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG &&
       pc != PB_PC_FFT)
@@ -471,8 +475,18 @@ static int enqueue_pc_iteration(pb_ksp* k) {
     PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
   }
   PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
-  PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, first ? k->b->d : k->r, k->r, k->d_st, first));
-  PB_TRY(pc_apply_dev(k, k->r, k->z, &k->d_st->done, &np));
+  const double* r_in = first ? k->b->d : k->r;
+  const int rupd = env_int("PB_FFT_RUPD", 1);
+  if (k->fft && rupd && fftpc_fuses_r_update(k->fft)) {
+    // r = r_in - alpha w formed by the spectral PC's first pass as it loads r, x = x + alpha p
+    // beside it (8 B/DoF and one vector pass fewer)
+    const RUpdate ru{r_in, k->w, k->r, p, k->x->d, first, k->d_st};
+    np = 0;
+    PB_TRY(fftpc_apply(k->fft, k->r, k->z, &k->d_st->done, k->d_st, &np, &ru));
+  } else {
+    PB_TRY(launch_cg_pc_xr(g, p, k->w, k->x->d, r_in, k->r, k->d_st, first));
+    PB_TRY(pc_apply_dev(k, k->r, k->z, &k->d_st->done, &np));
+  }
   if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
 }

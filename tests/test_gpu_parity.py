@@ -1014,7 +1014,7 @@ def test_fft_pc_apply_vs_oracle(ctx, n3, compact):
 
 
 @pytest.mark.parametrize("compact", [False, True])
-@pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 128)])
+@pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 128), (512, 64, 64)])
 def test_cg_fft_pc_matches_oracle(ctx, n3, compact):
     """CG + the spectral PC: A = P (7-point star, or config 5's compact operator). One iteration
     reaches rounding level, so after ||z_0|| the logged norms are rounding noise: they are checked
@@ -1035,6 +1035,30 @@ def test_cg_fft_pc_matches_oracle(ctx, n3, compact):
     assert abs(hist[0] - ho[0]) / ho[0] < 1e-12
     assert np.max(np.abs(np.asarray(hist[1:]) - ho[1:])) / ho[0] < 1e-10
     check_x(x.get_values(), xo)
+
+
+@pytest.mark.parametrize("n3", [(512, 64, 64), (1024, 32, 64)])
+def test_cg_fft_r_update_fused(ctx, monkeypatch, n3):
+    """512- and 1024-point x lines: the spectral PC's first (register-edge) X pass forms CG's
+    residual r = r_in - alpha w as it loads it (PB_FFT_RUPD, default on) with cg_pc_xr_kernel's
+    rounding, and x is updated on its own: reason, iterations, history and x bit-identical to the
+    separate x / r pass (PB_FFT_RUPD=0)."""
+    N = int(np.prod(n3))
+    h, kind = _fft_case(n3, True)
+    b = O.lapl(O.fill_random(N, SEED), n3, h)
+    da = pb.DA(ctx, n3)
+    A = pb.Mat(da, kind, h)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    res = {}
+    for rupd in ("1", "0"):
+        monkeypatch.setenv("PB_FFT_RUPD", rupd)
+        x.set_random(5)
+        bv.set_values(b)
+        reason, its, hist = pb.solve(A, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "1e-12"])
+        res[rupd] = (reason, its, np.asarray(hist), x.get_values())
+    (r1, i1, h1, x1), (r0, i0, h0, x0) = res["1"], res["0"]
+    assert (r1, i1) == (r0, i0) and r1 > 0 and i1 >= 1
+    assert np.array_equal(h1, h0) and np.array_equal(x1, x0)
 
 
 @pytest.mark.parametrize("compact", [False, True])
