@@ -446,9 +446,11 @@ struct DhtTile {
   static constexpr size_t LDS = (size_t)(TWO + (TWL ? 2 * N : 0)) * sizeof(double);
 };
 
-// tile lines per block: 16 (8 waves), 8 for 1024-point lines (LDS)
+// tile lines per block: 16 (8 waves; 1024-point lines: one block per CU for LDS, which beats two
+// blocks of 8-line tiles with 64-B row pieces: 1024^3 Z pass 8.52 -> 6.74 ms, Y 4.42 -> 4.14 ms,
+// profiles/r03/fft1024_tl_ab.jsonl), 8 for 768-point lines
 template <int N>
-constexpr int tile_lines() { return N > 512 ? 8 : 16; }
+constexpr int tile_lines() { return N == 1024 ? 16 : (N > 512 ? 8 : 16); }
 
 // LAYOUT 0: the tile's lines are adjacent (li = 1), elements strided (rows of TL doubles);
 // LAYOUT 1: lines contiguous (es = 1), each wave loads / stores its own two lines (no block
@@ -917,6 +919,12 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
     }
     if constexpr (N <= 512)
       if (pfs) return launch_dht_k<N, TL, 0, MODE, true>(ctx, p, skip);
+    if constexpr (N > 512) {
+      // PB_FFT_TL_LONG=8 / 16: the tile width on 768 / 1024-point lines (A/B)
+      static const int tll = env_int("PB_FFT_TL_LONG", 0);
+      if (tll == 16 && TL != 16) return launch_dht_k<N, 16, 0, MODE, false>(ctx, p, skip);
+      if (tll == 8 && TL != 8) return launch_dht_k<N, 8, 0, MODE, false>(ctx, p, skip);
+    }
     return launch_dht_k<N, TL, 0, MODE, false>(ctx, p, skip);
   }
 }

@@ -512,7 +512,10 @@ __global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
 static constexpr int kTYR = 2;         // own fine rows per wave (one coarse row)
 static constexpr int kRR = kTYR + 6;   // b rows held: j0-3 .. j0+4 (red values on all of them)
 
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void
+#ifndef PB_PRR_WPE
+#define PB_PRR_WPE 2  // waves per SIMD the register allocation aims for (A/B builds)
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PB_PRR_WPE))) void
 presmooth_restrict_kernel(Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz,
                           double cc, double omega, const double* __restrict__ b,
                           double* __restrict__ xout, double* __restrict__ bc, const int* skip) {
@@ -703,8 +706,11 @@ struct PostGeo {
   int64_t cplane;
 };
 
+#ifndef PB_POST_WPE
+#define PB_POST_WPE 2  // waves per SIMD the register allocation aims for (A/B builds)
+#endif
 template <bool SUMS>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) void post_sweep_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PB_POST_WPE))) void post_sweep_kernel(
     Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
     const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
     double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {

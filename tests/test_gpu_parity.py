@@ -991,7 +991,7 @@ def _fft_case(n3, compact):
 
 @pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 256), (256, 128, 64), (1024, 64, 64),
-                                (64, 1024, 64), (64, 64, 512), (32, 32, 32),
+                                (64, 1024, 64), (64, 64, 512), (32, 32, 32), (32, 64, 1024),
                                 # mixed radix (r03): 3 * 2^a and 5 * 2^a line lengths
                                 (96, 96, 96), (48, 80, 40), (192, 160, 128), (64, 768, 48),
                                 (640, 40, 32), (384, 32, 320)])
@@ -1110,6 +1110,32 @@ def test_multirank_cg_compact_fft(nranks):
         return k0, nk, reason, its, hist, x.get_values()
 
     for k0, nk, reason, its, hist, xs in run_ranks(nranks, body):
+        assert (reason, its) == (ro, itso)
+        assert abs(hist[0] - ho[0]) / ho[0] < 1e-12
+        check_x(xs, xo.reshape(n3[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
+
+
+def test_multirank_cg_compact_fft_register_edges():
+    """Config 5 decomposed with 512-point x lines: the spectral PC's X passes on the register-edge
+    kernel, its first X pass carrying CG's x / r update and its last the residual sums, on two
+    z-slab ranks (Z pass on y-slabs) -- reason / its / x against the single-grid oracle."""
+    n3 = (512, 32, 64)
+    N = int(np.prod(n3))
+    h = tuple(2 * np.pi / m for m in n3)
+    b = O.lapl(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-10, pc="fft", op="compact", nthreads=8)
+    assert ro == 2
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        A = pb.Mat(da, pb.COMPACT, h)
+        x, bv = pb.Vec(da), pb.Vec(da)
+        bv.set_values(b.reshape(n3[2], -1)[k0:k0 + nk])
+        reason, its, hist = pb.solve(A, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "1e-10"])
+        return k0, nk, reason, its, hist, x.get_values()
+
+    for k0, nk, reason, its, hist, xs in run_ranks(2, body):
         assert (reason, its) == (ro, itso)
         assert abs(hist[0] - ho[0]) / ho[0] < 1e-12
         check_x(xs, xo.reshape(n3[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
