@@ -28,9 +28,11 @@
 // element index is XOR-swizzled in LDS (lpad), so the scattered writes of the first pass hit
 // distinct banks. Twiddles exp(-2 pi i k / n) come from a per-axis table, copied into LDS
 // per block for n <= 512. X passes at 512 / 1024 points run register edges instead
-// (dht_reg_x_kernel): no tile staging, the first and last Stockham passes on registers. (r02's engine ran the 64-point cross-lane part of the transform as six
-// radix-2 stages of DPP / permlane exchanges: 2.5x the VALU work, and its Z pass, which runs two
-// transforms, was compute-bound at 1.0-1.1 ms at 512^3 whatever the tile width.)
+// (dht_reg_x_kernel): no tile staging, the first and last Stockham passes on registers, and the
+// first / last X pass also carry CG's x / r update / residual sums. (r02's engine ran the
+// 64-point cross-lane part of the transform as six radix-2 stages of DPP / permlane exchanges:
+// 2.5x the VALU work, and its Z pass, which runs two transforms, was compute-bound at 1.0-1.1 ms
+// at 512^3 whatever the tile width.)
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -455,9 +457,9 @@ constexpr int tile_lines() { return N == 1024 ? 16 : (N > 512 ? 8 : 16); }
 // LAYOUT 0: the tile's lines are adjacent (li = 1), elements strided (rows of TL doubles);
 // LAYOUT 1: lines contiguous (es = 1), each wave loads / stores its own two lines (no block
 // barrier around the transforms). MODE 0: one DHT; MODE 1: DHT, 1/(N lambda), DHT.
-// Persistent blocks (as many as are resident) walk the tiles; the next tile's input is fetched
-// into registers while the current one is transformed and stored, so HBM reads overlap the
-// transforms (+32 VGPRs at n = 512; occupancy stays LDS-bound at two blocks per CU).
+// One tile per block, except with PF (the LDS-tile X pass on <= 512 points, or PFS): persistent
+// blocks walk the tiles and fetch the next tile's input into registers while the current one is
+// transformed and stored (+32 VGPRs at n = 512; occupancy stays LDS-bound at two blocks per CU).
 template <int N, int TL_, int LAYOUT, int MODE, bool SUMS, bool PFS>
 __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(DhtPass p,
                                                                              const int* skip) {
