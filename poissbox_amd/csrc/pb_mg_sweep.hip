@@ -690,6 +690,493 @@ presmooth_restrict_kernel(Sweep2Geo g, int ncx, int64_t cplane, double cx, doubl
 }
 
 // ---------------------------------------------------------------------------------------------
+// The same pre-smoothing + residual + restriction pass with rows shared between the waves of a
+// block (r03). presmooth_restrict_kernel's waves load eight b rows for their two own rows and form
+// red values on eight rows, black values on six and the residual on four. Here a block of NW
+// waves stacks NW x TY rows (TY / 2 coarse rows per wave) and each wave forms red, black and
+// residual values on its own rows only; the values one row out come from the neighbouring waves
+// through LDS (red values, the smoothed pairs, and the residual's x sums), one block barrier per
+// plane. Red values of plane k+3 and the smoothed pairs of plane k+1 are published one iteration
+// before their use; the residual's x sums of plane k too -- the restriction of plane k runs one
+// iteration late. Each step loses a row at the block's ends (red -> black -> residual -> y sum),
+// so a block stores its fine rows 4 .. NW TY - 5 and blocks advance by NW TY - 8 rows. Same
+// operations on the same operands as presmooth_restrict_kernel: bit-identical.
+// ---------------------------------------------------------------------------------------------
+template <int NW, int TY>
+__global__ __launch_bounds__(64 * NW) void presmooth_restrict_xch_kernel(
+    Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
+    double omega, const double* __restrict__ b, double* __restrict__ xout,
+    double* __restrict__ bc, const int* skip) {
+  static_assert(TY % 2 == 0 && TY >= 2, "whole coarse rows per wave");
+  constexpr int RB = NW * TY;  // block rows
+  constexpr int SB = RB - 8;   // stored rows per block
+  constexpr int NCR = TY / 2;  // coarse rows per wave
+  // per plane parity, per wave: red values of own rows 0 / TY-1 (plane k+3), smoothed pairs of
+  // rows 0 / TY-1 (plane k+1: e0, e1 each), residual x sums of rows 0 / TY-1 (plane k)
+  __shared__ double xch[2][8][NW][64];
+  if (skip && *skip) return;
+  const double icc = 1.0 / cc;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bid = xcd_block(g.remap);
+  const int seg = bid % g.nseg;
+  bid /= g.nseg;
+  const int tile = bid % g.ntile;
+  const int chunk = bid / g.ntile;
+  const int kb = chunk * g.kc;  // even (kc even)
+  const int ke = min(kb + g.kc, g.nzl);
+  const int nx = g.nx, ny = g.ny, nz = g.nzl;
+  if (kb >= nz) return;  // block-uniform
+  const int g0 = tile * SB - 4;  // fine row of block row 0 (even)
+  const int br0 = wid * TY;
+  const int j0 = g0 + br0;       // even: fine rows 2 J0 .. of coarse rows J0 ..
+  auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
+  int ip = seg * kSegOut + 2 * (lane - kSegLead);
+  if (ip < 0) ip += nx;
+  if (ip >= nx) ip -= nx;
+  const int o = seg * kSegOut + 2 * (lane - kSegLead);
+  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
+  int64_t ro[TY];
+  int par_row[TY];
+  unsigned row_ok = 0;  // own rows this wave stores (x; coarse row c when rows 2c, 2c+1 are)
+#pragma unroll
+  for (int r = 0; r < TY; ++r) {
+    const int j = wrap(j0 + r, ny);
+    ro[r] = (int64_t)j * nx;
+    par_row[r] = (ip + j) & 1;
+    const int brow = br0 + r;
+    if (brow >= 4 && brow < RB - 4 && g0 + brow < ny) row_ok |= 1u << r;
+  }
+  const unsigned boff = (unsigned)ip * 8u;
+  auto rix = [&](int64_t row) { return RowIx{row, boff}; };
+  auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+  auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
+  auto ldraw = [&](double (&dst)[TY][2], int kk) {
+    const int64_t base = (int64_t)wrapk(kk) * g.plane;
+#pragma unroll
+    for (int r = 0; r < TY; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
+  };
+  auto redv = [&](const double (&v)[TY][2], int kk, double (&red)[TY]) {
+    const int kp = kpar(kk);
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      const double bv = pick(((par_row[r] + kp) & 1) != 0, v[r]);  // red point is element 1
+      const double t = (bv - 0.0) * icc;
+      red[r] = (1.0 - omega) * 0.0 + omega * t;
+    }
+  };
+  // black half-sweep at plane kk on the own rows; rh: red values of rows -1 / TY of plane kk
+  auto black = [&](const double (&rm)[TY], const double (&rc)[TY], const double (&rp)[TY],
+                   const double (&rh)[2], const double (&bb)[TY][2], int kk,
+                   double (&out)[TY][2]) {
+    const int kp = kpar(kk);
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      const bool a1 = ((par_row[r] + kp) & 1) != 1;  // the black point is element 1
+      const double lo = dpp_from_lower(rc[r]);
+      const double hi = dpp_from_upper(rc[r]);
+      const double xl = a1 ? rc[r] : lo;
+      const double xr = a1 ? hi : rc[r];
+      double nb = cz * rm[r];
+      nb = nb + cy * (r == 0 ? rh[0] : rc[r == 0 ? 0 : r - 1]);
+      nb = nb + cx * xl;
+      nb = nb + cx * xr;
+      nb = nb + cy * (r == TY - 1 ? rh[1] : rc[r == TY - 1 ? r : r + 1]);
+      nb = nb + cz * rp[r];
+      const double t = (pick(a1, bb[r]) - nb) * icc;
+      const double v = (1.0 - omega) * 0.0 + omega * t;
+      out[r][0] = a1 ? rc[r] : v;
+      out[r][1] = a1 ? v : rc[r];
+    }
+  };
+  const int wm = wid > 0 ? wid - 1 : wid, wp = wid < NW - 1 ? wid + 1 : wid;
+  const int J0 = j0 >> 1;
+  const int I = o >> 1;
+  const double w[4] = {0.125, 0.375, 0.375, 0.125};
+  // queues at iteration k: red values of planes k, k+1, k+2 (and rows -1 / TY of plane k+1);
+  // smoothed pairs of planes k-1, k; b of planes k, k+1, k+2; the residual x sums of plane k-1
+  double rq0[TY], rq1[TY], rq2[TY], rh1[2];
+  double s1m[TY][2], s1c[TY][2];
+  double bq0[TY][2], bq1[TY][2], bq2[TY][2];
+  double sxp[TY];
+  double accA[NCR], accB[NCR];
+  {
+    double raw[TY][2];
+    ldraw(raw, kb - 3);
+    redv(raw, kb - 3, rq0);
+    ldraw(bq1, kb - 2);
+    redv(bq1, kb - 2, rq1);
+    ldraw(bq2, kb - 1);
+    redv(bq2, kb - 1, rq2);
+    // rows -1 / TY of plane kb-2 now; those of plane kb-1 as if iteration kb-4 had formed them
+    xch[(kb - 3) & 1][0][wid][lane] = rq1[0];
+    xch[(kb - 3) & 1][1][wid][lane] = rq1[TY - 1];
+    __syncthreads();
+    rh1[0] = xch[(kb - 3) & 1][1][wm][lane];
+    rh1[1] = xch[(kb - 3) & 1][0][wp][lane];
+    xch[(kb - 4) & 1][0][wid][lane] = rq2[0];
+    xch[(kb - 4) & 1][1][wid][lane] = rq2[TY - 1];
+  }
+#pragma unroll
+  for (int r = 0; r < TY; ++r) {
+    sxp[r] = 0.0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) s1m[r][e] = s1c[r][e] = bq0[r][e] = 0.0;
+  }
+#pragma unroll
+  for (int c = 0; c < NCR; ++c) accA[c] = accB[c] = 0.0;
+  // planes kb-3, kb-2: black warm-up; residual on kb-1 .. ke; restriction of plane k-1
+#pragma unroll 1
+  for (int k = kb - 3; k <= ke + 1; ++k) {
+    double raw[TY][2], s1p[TY][2], rh2[2], sh[2][2], sxh[2];
+    ldraw(raw, k + 3);  // in flight during this plane's work (consumed at the rotation)
+    __syncthreads();
+    {
+      const int rp = (k - 1) & 1;
+      rh2[0] = xch[rp][1][wm][lane];  // red, plane k+2
+      rh2[1] = xch[rp][0][wp][lane];
+      sh[0][0] = xch[rp][4][wm][lane];  // smoothed pairs, plane k: row -1
+      sh[0][1] = xch[rp][5][wm][lane];
+      sh[1][0] = xch[rp][2][wp][lane];  // row TY
+      sh[1][1] = xch[rp][3][wp][lane];
+      sxh[0] = xch[rp][7][wm][lane];  // residual x sums, plane k-1
+      sxh[1] = xch[rp][6][wp][lane];
+    }
+    const int cur = k & 1;
+    black(rq0, rq1, rq2, rh1, bq1, k + 1, s1p);  // smoothed pairs of plane k+1
+    xch[cur][2][wid][lane] = s1p[0][0];
+    xch[cur][3][wid][lane] = s1p[0][1];
+    xch[cur][4][wid][lane] = s1p[TY - 1][0];
+    xch[cur][5][wid][lane] = s1p[TY - 1][1];
+    double sxc[TY];
+    if (k >= kb - 1 && k <= ke) {
+      // x = S1 on the own rows; res = b - A S1 (z-, y-, x-, c, x+, y+, z+), then its x sums
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const double lo = dpp_from_lower(s1c[r][1]);
+        const double hi = dpp_from_upper(s1c[r][0]);
+        double rv[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double xl = e == 0 ? lo : s1c[r][0];
+          const double xr = e == 1 ? hi : s1c[r][1];
+          const double ym = r == 0 ? sh[0][e] : s1c[r == 0 ? 0 : r - 1][e];
+          const double yp = r == TY - 1 ? sh[1][e] : s1c[r == TY - 1 ? r : r + 1][e];
+          double a = cz * s1m[r][e];
+          a = a + cy * ym;
+          a = a + cx * xl;
+          a = a + cc * s1c[r][e];
+          a = a + cx * xr;
+          a = a + cy * yp;
+          a = a + cz * s1p[r][e];
+          rv[e] = bq0[r][e] - a;
+        }
+        const double rlo = dpp_from_lower(rv[1]);
+        const double rhi = dpp_from_upper(rv[0]);
+        double sx = w[0] * rlo;
+        sx = sx + w[1] * rv[0];
+        sx = sx + w[2] * rv[1];
+        sx = sx + w[3] * rhi;
+        sxc[r] = sx;
+      }
+      if (k >= kb && k < ke && out_ok) {
+        const int64_t base = (int64_t)k * g.plane;
+#pragma unroll
+        for (int r = 0; r < TY; ++r)
+          if (row_ok >> r & 1u) store_row<2>(xout, rix(base + ro[r]), s1c[r], g.nt);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < TY; ++r) sxc[r] = 0.0;
+    }
+    xch[cur][6][wid][lane] = sxc[0];
+    xch[cur][7][wid][lane] = sxc[TY - 1];
+    const int kr = k - 1;  // restriction of plane k-1: y sums of fine rows 2J-1 .. 2J+2
+    if (kr >= kb - 1) {
+#pragma unroll
+      for (int c = 0; c < NCR; ++c) {
+        double sy = 0.0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const int r = 2 * c - 1 + bb;
+          const double sxv = r < 0 ? sxh[0] : (r >= TY ? sxh[1] : sxp[r < 0 ? 0 : (r >= TY ? 0 : r)]);
+          sy = sy + w[bb] * sxv;
+        }
+        if (kr & 1) {  // kr = 2K-1: third term of K-1, first of K
+          accB[c] = accB[c] + 0.375 * sy;
+          accA[c] = 0.0;
+          accA[c] = accA[c] + 0.125 * sy;
+        } else {       // kr = 2K: last term of K-1 (complete), second of K
+          accB[c] = accB[c] + 0.125 * sy;
+          if (kr >= kb + 2 && out_ok && (row_ok >> (2 * c) & 1u))
+            bc[(int64_t)((kr >> 1) - 1) * cplane + (int64_t)wrap(J0 + c, ny >> 1) * ncx + I] =
+                accB[c];
+          accA[c] = accA[c] + 0.375 * sy;
+          accB[c] = accA[c];
+        }
+      }
+    }
+    // rotate: red (k+1, k+2, k+3), smoothed pairs (k, k+1), b (k+1, k+2, k+3), x sums (k)
+    double rn[TY];
+    redv(raw, k + 3, rn);
+    xch[cur][0][wid][lane] = rn[0];
+    xch[cur][1][wid][lane] = rn[TY - 1];
+    rh1[0] = rh2[0];
+    rh1[1] = rh2[1];
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      rq0[r] = rq1[r];
+      rq1[r] = rq2[r];
+      rq2[r] = rn[r];
+      sxp[r] = sxc[r];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        s1m[r][e] = s1c[r][e];
+        s1c[r][e] = s1p[r][e];
+        bq0[r][e] = bq1[r][e];
+        bq1[r][e] = bq2[r][e];
+        bq2[r][e] = raw[r][e];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// presmooth_restrict_xch_kernel with the plane loop unrolled by four (r03). Its queues (red values,
+// smoothed pairs, b rows, x sums, halo values) become rings of four or two register slots whose
+// roles rotate with the unrolled copy, so no value is copied from one iteration to the next, and
+// each copy knows its plane's parity: with one rank (k0 = 0) and even extents, pair origins and
+// row origins, the colour of every element is known at compile time, so the colour choices are
+// register choices instead of selects and each half-sweep needs one DPP shift per row, not two.
+// A chunk runs a whole number of four-plane steps (up to three planes more than it needs; they
+// store nothing). Same operations on the same operands: bit-identical.
+// ---------------------------------------------------------------------------------------------
+template <int NW, int TY>
+__global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
+    Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
+    double omega, const double* __restrict__ b, double* __restrict__ xout,
+    double* __restrict__ bc, const int* skip) {
+  static_assert(TY % 2 == 0 && TY >= 2, "whole coarse rows per wave");
+  constexpr int RB = NW * TY;
+  constexpr int SB = RB - 8;
+  constexpr int NCR = TY / 2;
+  __shared__ double xch[2][8][NW][64];  // as presmooth_restrict_xch_kernel's
+  if (skip && *skip) return;
+  const double icc = 1.0 / cc;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bid = xcd_block(g.remap);
+  const int seg = bid % g.nseg;
+  bid /= g.nseg;
+  const int tile = bid % g.ntile;
+  const int chunk = bid / g.ntile;
+  const int kb = chunk * g.kc;  // even (kc even)
+  const int ke = min(kb + g.kc, g.nzl);
+  const int nx = g.nx, ny = g.ny, nz = g.nzl;
+  if (kb >= nz) return;
+  const int g0 = tile * SB - 4;
+  const int br0 = wid * TY;
+  const int j0 = g0 + br0;  // even
+  auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
+  int ip = seg * kSegOut + 2 * (lane - kSegLead);  // even
+  if (ip < 0) ip += nx;
+  if (ip >= nx) ip -= nx;
+  const int o = seg * kSegOut + 2 * (lane - kSegLead);
+  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
+  int64_t ro[TY];
+  unsigned row_ok = 0;
+#pragma unroll
+  for (int r = 0; r < TY; ++r) {
+    ro[r] = (int64_t)wrap(j0 + r, ny) * nx;
+    const int brow = br0 + r;
+    if (brow >= 4 && brow < RB - 4 && g0 + brow < ny) row_ok |= 1u << r;
+  }
+  const unsigned boff = (unsigned)ip * 8u;
+  auto rix = [&](int64_t row) { return RowIx{row, boff}; };
+  auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+  auto ldraw = [&](double (&dst)[TY][2], int kk) {
+    const int64_t base = (int64_t)wrapk(kk) * g.plane;
+#pragma unroll
+    for (int r = 0; r < TY; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
+  };
+  // element holding the red point of own row r on a plane of parity P (pair origin i even, row
+  // origin j0 even, k0 = 0): presmooth_restrict_kernel's ((i + j) & 1) + kpar != 0
+  auto red_e = [](int r, int P) { return (r + P) & 1; };
+  auto redv = [&](auto Pc, const double (&v)[TY][2], double (&red)[TY]) {
+    constexpr int P = decltype(Pc)::value;
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      const double t = (v[r][red_e(r, P)] - 0.0) * icc;
+      red[r] = (1.0 - omega) * 0.0 + omega * t;
+    }
+  };
+  auto black = [&](auto Pc, const double (&rm)[TY], const double (&rc)[TY],
+                   const double (&rp)[TY], const double (&rh)[2], const double (&bb)[TY][2],
+                   double (&out)[TY][2]) {
+    constexpr int P = decltype(Pc)::value;
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      const int be = 1 - red_e(r, P);  // the black point's element
+      const double xl = be ? rc[r] : dpp_from_lower(rc[r]);
+      const double xr = be ? dpp_from_upper(rc[r]) : rc[r];
+      double nb = cz * rm[r];
+      nb = nb + cy * (r == 0 ? rh[0] : rc[r == 0 ? 0 : r - 1]);
+      nb = nb + cx * xl;
+      nb = nb + cx * xr;
+      nb = nb + cy * (r == TY - 1 ? rh[1] : rc[r == TY - 1 ? r : r + 1]);
+      nb = nb + cz * rp[r];
+      const double t = (bb[r][be] - nb) * icc;
+      const double v = (1.0 - omega) * 0.0 + omega * t;
+      out[r][1 - be] = rc[r];
+      out[r][be] = v;
+    }
+  };
+  const int wm = wid > 0 ? wid - 1 : wid, wp = wid < NW - 1 ? wid + 1 : wid;
+  const int J0 = j0 >> 1;
+  const int I = o >> 1;
+  const double w[4] = {0.125, 0.375, 0.375, 0.125};
+  double R[4][TY];     // red values: planes k, k+1, k+2 and (new) k+3 at slots Q .. Q+3
+  double S[4][TY][2];  // smoothed pairs: planes k-1, k, k+1 at slots Q .. Q+2
+  double B[4][TY][2];  // b rows: planes k .. k+3 at slots Q .. Q+3
+  double X[2][TY];     // residual x sums: planes k-1, k at slots Q, Q+1
+  double H[2][2];      // red values of rows -1 / TY: planes k+1, k+2 at slots Q, Q+1
+  double accA[NCR], accB[NCR];
+  ldraw(B[3], kb - 3);
+  redv(std::integral_constant<int, 1>{}, B[3], R[0]);  // planes kb-3 (odd), kb-2, kb-1
+  ldraw(B[1], kb - 2);
+  redv(std::integral_constant<int, 0>{}, B[1], R[1]);
+  ldraw(B[2], kb - 1);
+  redv(std::integral_constant<int, 1>{}, B[2], R[2]);
+  xch[1][0][wid][lane] = R[1][0];
+  xch[1][1][wid][lane] = R[1][TY - 1];
+  __syncthreads();
+  H[0][0] = xch[1][1][wm][lane];
+  H[0][1] = xch[1][0][wp][lane];
+  xch[0][0][wid][lane] = R[2][0];
+  xch[0][1][wid][lane] = R[2][TY - 1];
+#pragma unroll
+  for (int r = 0; r < TY; ++r) {
+    X[0][r] = 0.0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) S[0][r][e] = S[1][r][e] = B[0][r][e] = 0.0;
+  }
+#pragma unroll
+  for (int c = 0; c < NCR; ++c) accA[c] = accB[c] = 0.0;
+  // one plane: k = kb - 3 + Q (mod 4), parity KP = (Q + 1) & 1 (kb even)
+  auto body = [&](auto Qc, int k) {
+    constexpr int Q = decltype(Qc)::value;
+    constexpr int KP = (Q + 1) & 1;
+    double (&rq0)[TY] = R[Q];
+    double (&rq1)[TY] = R[(Q + 1) & 3];
+    double (&rq2)[TY] = R[(Q + 2) & 3];
+    double (&rn)[TY] = R[(Q + 3) & 3];
+    double (&s1m)[TY][2] = S[Q];
+    double (&s1c)[TY][2] = S[(Q + 1) & 3];
+    double (&s1p)[TY][2] = S[(Q + 2) & 3];
+    double (&bq0)[TY][2] = B[Q];
+    double (&bq1)[TY][2] = B[(Q + 1) & 3];
+    double (&raw)[TY][2] = B[(Q + 3) & 3];
+    double (&sxp)[TY] = X[Q & 1];
+    double (&sxc)[TY] = X[(Q + 1) & 1];
+    double (&rh1)[2] = H[Q & 1];
+    double (&rh2)[2] = H[(Q + 1) & 1];
+    ldraw(raw, k + 3);
+    __syncthreads();
+    double sh[2][2], sxh[2];
+    {
+      constexpr int rp = KP ^ 1;  // written by plane k-1
+      rh2[0] = xch[rp][1][wm][lane];
+      rh2[1] = xch[rp][0][wp][lane];
+      sh[0][0] = xch[rp][4][wm][lane];
+      sh[0][1] = xch[rp][5][wm][lane];
+      sh[1][0] = xch[rp][2][wp][lane];
+      sh[1][1] = xch[rp][3][wp][lane];
+      sxh[0] = xch[rp][7][wm][lane];
+      sxh[1] = xch[rp][6][wp][lane];
+    }
+    black(std::integral_constant<int, KP ^ 1>{}, rq0, rq1, rq2, rh1, bq1, s1p);  // plane k+1
+    xch[KP][2][wid][lane] = s1p[0][0];
+    xch[KP][3][wid][lane] = s1p[0][1];
+    xch[KP][4][wid][lane] = s1p[TY - 1][0];
+    xch[KP][5][wid][lane] = s1p[TY - 1][1];
+    if (k >= kb - 1 && k <= ke) {
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const double lo = dpp_from_lower(s1c[r][1]);
+        const double hi = dpp_from_upper(s1c[r][0]);
+        double rv[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double xl = e == 0 ? lo : s1c[r][0];
+          const double xr = e == 1 ? hi : s1c[r][1];
+          const double ym = r == 0 ? sh[0][e] : s1c[r == 0 ? 0 : r - 1][e];
+          const double yp = r == TY - 1 ? sh[1][e] : s1c[r == TY - 1 ? r : r + 1][e];
+          double a = cz * s1m[r][e];
+          a = a + cy * ym;
+          a = a + cx * xl;
+          a = a + cc * s1c[r][e];
+          a = a + cx * xr;
+          a = a + cy * yp;
+          a = a + cz * s1p[r][e];
+          rv[e] = bq0[r][e] - a;
+        }
+        const double rlo = dpp_from_lower(rv[1]);
+        const double rhi = dpp_from_upper(rv[0]);
+        double sx = w[0] * rlo;
+        sx = sx + w[1] * rv[0];
+        sx = sx + w[2] * rv[1];
+        sx = sx + w[3] * rhi;
+        sxc[r] = sx;
+      }
+      if (k >= kb && k < ke && out_ok) {
+        const int64_t base = (int64_t)k * g.plane;
+#pragma unroll
+        for (int r = 0; r < TY; ++r)
+          if (row_ok >> r & 1u) store_row<2>(xout, rix(base + ro[r]), s1c[r], g.nt);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < TY; ++r) sxc[r] = 0.0;
+    }
+    xch[KP][6][wid][lane] = sxc[0];
+    xch[KP][7][wid][lane] = sxc[TY - 1];
+    const int kr = k - 1;  // restriction of plane k-1 (parity KP ^ 1)
+    if (kr >= kb - 1) {
+#pragma unroll
+      for (int c = 0; c < NCR; ++c) {
+        double sy = 0.0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const int r = 2 * c - 1 + bb;
+          const double sxv = r < 0 ? sxh[0] : (r >= TY ? sxh[1] : sxp[r < 0 ? 0 : (r >= TY ? 0 : r)]);
+          sy = sy + w[bb] * sxv;
+        }
+        if constexpr ((KP ^ 1) == 1) {  // kr = 2K-1
+          accB[c] = accB[c] + 0.375 * sy;
+          accA[c] = 0.0;
+          accA[c] = accA[c] + 0.125 * sy;
+        } else {  // kr = 2K
+          accB[c] = accB[c] + 0.125 * sy;
+          if (kr >= kb + 2 && kr <= ke && out_ok && (row_ok >> (2 * c) & 1u))
+            bc[(int64_t)((kr >> 1) - 1) * cplane + (int64_t)wrap(J0 + c, ny >> 1) * ncx + I] =
+                accB[c];
+          accA[c] = accA[c] + 0.375 * sy;
+          accB[c] = accA[c];
+        }
+      }
+    }
+    redv(std::integral_constant<int, KP ^ 1>{}, raw, rn);  // plane k+3
+    xch[KP][0][wid][lane] = rn[0];
+    xch[KP][1][wid][lane] = rn[TY - 1];
+  };
+#pragma unroll 1
+  for (int k = kb - 3; k <= ke + 1; k += 4) {
+    body(std::integral_constant<int, 0>{}, k);
+    body(std::integral_constant<int, 1>{}, k + 1);
+    body(std::integral_constant<int, 2>{}, k + 2);
+    body(std::integral_constant<int, 3>{}, k + 3);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Post-smoothing with the prolongation folded in (one rank): the sweep's input
 // xin = x_s + P x_c is formed as the planes arrive -- x_s (the pre-smoothed iterate) and the
 // coarse correction x_c are read, the prolongated input is never stored. Then both half-sweeps
@@ -957,6 +1444,566 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PB_POS
   if constexpr (SUMS) block_partials<4>(acc, parts);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same post-smoothing with rows shared between the waves of a block (r03). post_sweep_kernel's
+// waves each load TY2 + 4 rows of x_s (and TY2 + 2 of b, 12 coarse rows) for their TY2 own rows --
+// 2.3x the rows they store -- because the two half-sweeps need input two rows out, and they
+// recompute the first half on the TY2 + 2 middle rows. Here a block of NW waves stacks NW x TY
+// rows and each wave loads and sweeps only its own rows: the input (prolongated) rows and the
+// first-half values one row out come from the neighbouring waves through LDS, with one block
+// barrier per plane (written one iteration ahead of their use, double-buffered by plane parity).
+// The block's two outer rows at each end are halo (their inputs end at the block), so blocks
+// advance by NW TY - 4 rows. Same operations on the same operands as post_sweep_kernel (the
+// prolongation's per-coarse-row x stage, the half-sweeps' operand order): bit-identical.
+// ---------------------------------------------------------------------------------------------
+template <bool SUMS, int NW, int TY, int PF>
+__global__ __launch_bounds__(64 * NW) void post_sweep_xch_kernel(
+    Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
+    const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
+    double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
+  static_assert(TY % 2 == 0 && TY >= 2, "own rows start on an even fine row (prolongation parity)");
+  constexpr int RB = NW * TY;     // block rows
+  constexpr int SB = RB - 4;      // stored rows per block
+  constexpr int NC = TY / 2 + 2;  // coarse rows under a wave's own rows (near and far)
+  // per plane parity: prolongated input, own row 0 (e0, e1) and row TY-1 (e0, e1); first-half
+  // (c1) values of own rows 0 and TY-1
+  __shared__ double xch[2][6][NW][64];
+  if (skip && *skip) return;
+  const double icc = 1.0 / cc;
+  constexpr int c1 = 1;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const double mu = SUMS ? st->mu : 0.0;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bid = xcd_block(g.remap);
+  const int seg = bid % g.nseg;
+  bid /= g.nseg;
+  const int tile = bid % g.ntile;
+  const int chunk = bid / g.ntile;
+  const int nx = g.nx, ny = g.ny, nz = g.nzl;
+  const int kb = chunk * g.kc;
+  const int ke = min(kb + g.kc, nz);
+  if (kb < nz) {  // block-uniform: every wave takes part in the barriers
+    const int g0 = tile * SB - 2;   // fine row of block row 0 (even)
+    const int br0 = wid * TY;       // block row of own row 0
+    const int j0 = g0 + br0;        // even, may lie outside [0, ny): rows wrap periodically
+    auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
+    int ip = seg * kSegOut + 2 * (lane - kSegLead);
+    if (ip < 0) ip += nx;
+    if (ip >= nx) ip -= nx;
+    const int o = seg * kSegOut + 2 * (lane - kSegLead);
+    const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
+    int64_t ro[TY];
+    int par_row[TY + 2];  // rows -1 .. TY
+    unsigned row_ok = 0;  // own rows this wave stores (wave-uniform bit mask)
+#pragma unroll
+    for (int r = -1; r <= TY; ++r) {
+      const int j = wrap(j0 + r, ny);
+      par_row[r + 1] = (ip + j) & 1;
+      if (r >= 0 && r < TY) {
+        ro[r] = (int64_t)j * nx;
+        const int brow = br0 + r;
+        if (brow >= 2 && brow < RB - 2 && g0 + brow < ny) row_ok |= 1u << r;
+      }
+    }
+    const unsigned boff = (unsigned)ip * 8u;
+    auto rix = [&](int64_t row) { return RowIx{row, boff}; };
+    auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+    auto pl = [&](int kk) -> int64_t { return (int64_t)wrapk(kk) * g.plane; };
+    auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
+    int64_t crow[NC];  // coarse rows J0-1 .. J0+TY/2 (J0 = j0 / 2)
+#pragma unroll
+    for (int t = 0; t < NC; ++t) crow[t] = (int64_t)wrap((j0 >> 1) - 1 + t, cgeo.ncy) * cgeo.ncx;
+    const unsigned cboff = (unsigned)(ip >> 1) * 8u;
+    auto ldx = [&](double (&dst)[TY][2], double (&cv)[2][NC], int kk) {
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 0; r < TY; ++r) load_row<2>(xs, rix(base + ro[r]), dst[r]);
+      const int kw = wrapk(kk);
+      const int K = kw >> 1;
+      int fK = (kw & 1) ? K + 1 : K - 1;
+      if (fK < 0) fK += cgeo.ncz;
+      if (fK >= cgeo.ncz) fK -= cgeo.ncz;
+      const double* cn = xc + (int64_t)K * cgeo.cplane;
+      const double* cf = xc + (int64_t)fK * cgeo.cplane;
+#pragma unroll
+      for (int t = 0; t < NC; ++t) {
+        cv[0][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cn + crow[t]) + cboff);
+        cv[1][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cf + crow[t]) + cboff);
+      }
+    };
+    // x_s + P x_c on the own rows (post_sweep_kernel's prolong_p with an even first row)
+    auto prolong = [&](double (&v)[TY][2], const double (&cv)[2][NC]) {
+      double xi[2][NC][2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int t = 0; t < NC; ++t) {
+          const double c = cv[q][t];
+          xi[q][t][0] = 0.75 * c + 0.25 * dpp_from_lower(c);
+          xi[q][t][1] = 0.75 * c + 0.25 * dpp_from_upper(c);
+        }
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const int tJ = 1 + (r >> 1);
+        const int tf = (r & 1) ? tJ + 1 : tJ - 1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double vn = 0.75 * xi[0][tJ][e] + 0.25 * xi[0][tf][e];
+          const double vf = 0.75 * xi[1][tJ][e] + 0.25 * xi[1][tf][e];
+          v[r][e] = v[r][e] + (0.75 * vn + 0.25 * vf);
+        }
+      }
+    };
+    auto ldb = [&](double (&dst)[TY][2], int kk) {
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 0; r < TY; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
+    };
+    auto ec1 = [&](int kk, int r) -> bool { return ((par_row[r + 1] + kpar(kk)) & 1) != c1; };
+    // first half-sweep at plane kk on the own rows; xcn holds rows -1 .. TY of plane kk
+    auto half1 = [&](const double (&zmv)[TY], const double (&xcn)[TY + 2][2],
+                     const double (&xp)[TY][2], const double (&bb)[TY][2], int kk,
+                     double (&out)[TY]) {
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const bool a1 = ec1(kk, r);
+        const double lo = dpp_from_lower(xcn[r + 1][1]);
+        const double hi = dpp_from_upper(xcn[r + 1][0]);
+        const double xl = a1 ? xcn[r + 1][0] : lo;
+        const double xr = a1 ? hi : xcn[r + 1][1];
+        const double zm = zmv[r];
+        const double ym = pick(a1, xcn[r]);
+        const double yp = pick(a1, xcn[r + 2]);
+        const double zp = pick(a1, xp[r]);
+        const double bv = pick(a1, bb[r]);
+        const double xo = pick(a1, xcn[r + 1]);
+        double nb = cz * zm;
+        nb = nb + cy * ym;
+        nb = nb + cx * xl;
+        nb = nb + cx * xr;
+        nb = nb + cy * yp;
+        nb = nb + cz * zp;
+        const double t = (bv - nb) * icc;
+        out[r] = (1.0 - omega) * xo + omega * t;
+      }
+    };
+    auto c2of = [&](const double (&v)[TY][2], int kk, double (&out)[TY]) {
+#pragma unroll
+      for (int r = 0; r < TY; ++r) out[r] = pick(!ec1(kk, r), v[r]);
+    };
+    auto c1of = [&](const double (&v)[TY][2], int kk, double (&out)[TY]) {
+#pragma unroll
+      for (int r = 0; r < TY; ++r) out[r] = pick(ec1(kk, r), v[r]);
+    };
+    // second half-sweep at plane kk on the own rows; sh: c1 values of rows -1 and TY
+    auto half2 = [&](int kk, const double (&sm)[TY], const double (&sc)[TY],
+                     const double (&sp)[TY], const double (&sh)[2], const double (&xo)[TY],
+                     const double (&bo)[TY], const double (&bc1)[SUMS ? TY : 1]) {
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const bool a1 = !ec1(kk, r);
+        const double cself = sc[r];
+        const double lo = dpp_from_lower(cself);
+        const double hi = dpp_from_upper(cself);
+        const double xl = a1 ? cself : lo;
+        const double xr = a1 ? hi : cself;
+        double nb = cz * sm[r];
+        nb = nb + cy * (r == 0 ? sh[0] : sc[r == 0 ? 0 : r - 1]);
+        nb = nb + cx * xl;
+        nb = nb + cx * xr;
+        nb = nb + cy * (r == TY - 1 ? sh[1] : sc[r == TY - 1 ? r : r + 1]);
+        nb = nb + cz * sp[r];
+        const double t = (bo[r] - nb) * icc;
+        const double v = (1.0 - omega) * xo[r] + omega * t;
+        double ov[2];
+        ov[0] = a1 ? cself : v;
+        ov[1] = a1 ? v : cself;
+        if (out_ok && (row_ok >> r & 1u)) {
+          store_row<2>(xout, rix(base + ro[r]), ov, g.nt);
+          if constexpr (SUMS) {
+            double rv2[2];
+            rv2[0] = a1 ? bc1[r] : bo[r];
+            rv2[1] = a1 ? bo[r] : bc1[r];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const double t2 = ov[e] - mu;
+              acc[0] += t2;
+              acc[1] += t2 * t2;
+              acc[2] += t2 * rv2[e];
+              acc[3] += rv2[e];
+            }
+          }
+        }
+      }
+    };
+    const int wm = wid > 0 ? wid - 1 : wid, wp = wid < NW - 1 ? wid + 1 : wid;
+    auto put_x = [&](int par, const double (&v)[TY][2]) {
+      xch[par][0][wid][lane] = v[0][0];
+      xch[par][1][wid][lane] = v[0][1];
+      xch[par][2][wid][lane] = v[TY - 1][0];
+      xch[par][3][wid][lane] = v[TY - 1][1];
+    };
+    // Iteration k: loads of plane k+2 (x_s, coarse) and k+1 (b) go out, the barrier publishes
+    // what iteration k-1 wrote (the input rows -1 / TY of plane k+1, the c1 values of rows -1 / TY
+    // of plane k), then the second half at plane k-1, the prolongation of plane k+2 and the first
+    // half at plane k+1 (post_sweep_kernel's order).
+    double xq1[TY + 2][2];  // input, plane k+1, rows -1 .. TY
+    double xm[TY], x0[TY];  // input c2 values, planes k-1, k
+    double s1[4][TY];       // c1 values after the first half, planes k-2 .. k+1
+    double shp[2], shc[2];  // c1 values of rows -1 / TY: planes k-1, k
+    double bm[TY], b0[TY];
+    double bm1[SUMS ? TY : 1], b01[SUMS ? TY : 1];
+    {
+      double xa[TY][2], cv[2][NC];
+      ldx(xa, cv, kb - 2);
+      prolong(xa, cv);
+      c2of(xa, kb - 2, x0);
+      ldx(xa, cv, kb - 1);
+      prolong(xa, cv);
+      put_x((kb - 3) & 1, xa);
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        xq1[r + 1][0] = xa[r][0];
+        xq1[r + 1][1] = xa[r][1];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      xm[r] = bm[r] = b0[r] = 0.0;
+      s1[0][r] = s1[1][r] = s1[2][r] = 0.0;
+      if constexpr (SUMS) bm1[r] = b01[r] = 0.0;
+    }
+    shp[0] = shp[1] = 0.0;
+    // loads of one iteration: x_s and coarse values of plane k+2, b of plane k+1. PF = 2: issued
+    // one iteration earlier, into the other of two register sets (the loop is unrolled by two,
+    // so the sets swap roles without register copies, which would wait for the loads)
+    struct Ld {
+      double x[TY][2], cv[2][NC], b[TY][2];
+    };
+    auto step = [&](int k, Ld& cur, Ld& nxt) {
+      if constexpr (PF == 1) {
+        ldx(cur.x, cur.cv, k + 2);
+        ldb(cur.b, k + 1);
+      } else {
+        ldx(nxt.x, nxt.cv, k + 3);
+        ldb(nxt.b, k + 2);
+      }
+      __syncthreads();
+      {
+        const int rp = (k - 1) & 1;
+        xq1[0][0] = xch[rp][2][wm][lane];
+        xq1[0][1] = xch[rp][3][wm][lane];
+        xq1[TY + 1][0] = xch[rp][0][wp][lane];
+        xq1[TY + 1][1] = xch[rp][1][wp][lane];
+        shc[0] = xch[rp][5][wm][lane];
+        shc[1] = xch[rp][4][wp][lane];
+      }
+      if (k > kb) half2(k - 1, s1[0], s1[1], s1[2], shp, xm, bm, bm1);
+      prolong(cur.x, cur.cv);
+      put_x(k & 1, cur.x);
+      half1(x0, xq1, cur.x, cur.b, k + 1, s1[3]);
+      xch[k & 1][4][wid][lane] = s1[3][0];
+      xch[k & 1][5][wid][lane] = s1[3][TY - 1];
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        xm[r] = x0[r];
+        bm[r] = b0[r];
+        if constexpr (SUMS) bm1[r] = b01[r];
+        s1[0][r] = s1[1][r];
+        s1[1][r] = s1[2][r];
+        s1[2][r] = s1[3][r];
+      }
+      shp[0] = shc[0];
+      shp[1] = shc[1];
+      {
+        double own[TY][2];
+#pragma unroll
+        for (int r = 0; r < TY; ++r) {
+          own[r][0] = xq1[r + 1][0];
+          own[r][1] = xq1[r + 1][1];
+        }
+        c2of(own, k + 1, x0);
+      }
+      c2of(cur.b, k + 1, b0);
+      if constexpr (SUMS) c1of(cur.b, k + 1, b01);
+#pragma unroll
+      for (int r = 0; r < TY; ++r)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) xq1[r + 1][e] = cur.x[r][e];
+    };
+    int k = kb - 2;
+    if constexpr (PF == 1) {
+      Ld A;
+#pragma unroll 1
+      for (; k < ke; ++k) step(k, A, A);
+    } else {
+      Ld A, B;
+      ldx(A.x, A.cv, kb);
+      ldb(A.b, kb - 1);
+#pragma unroll 1
+      for (; k + 1 < ke; k += 2) {
+        step(k, A, B);
+        step(k + 1, B, A);
+      }
+      if (k < ke) step(k, A, B);
+    }
+    half2(ke - 1, s1[0], s1[1], s1[2], shp, xm, bm, bm1);
+  }
+  if constexpr (SUMS) block_partials<4>(acc, parts);
+}
+
+// ---------------------------------------------------------------------------------------------
+// post_sweep_xch_kernel with the plane loop unrolled by four (r03), as
+// presmooth_restrict_u4_kernel: the queues (input planes with their halo rows, first-half values,
+// c2 inputs and right-hand sides, halo first-half values) are rings of four or two register slots
+// whose roles rotate with the unrolled copy, and each copy knows its plane's parity (one rank,
+// even extents and origins), so the colour choices are register choices and each half-sweep
+// shifts one value per row. A chunk runs a whole number of four-plane steps (the last step's
+// extra planes store nothing). Same operations on the same operands: bit-identical.
+// ---------------------------------------------------------------------------------------------
+template <bool SUMS, int NW, int TY>
+__global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
+    Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
+    const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
+    double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
+  static_assert(TY % 2 == 0 && TY >= 2, "own rows start on an even fine row");
+  constexpr int RB = NW * TY;
+  constexpr int SB = RB - 4;
+  constexpr int NC = TY / 2 + 2;
+  __shared__ double xch[2][6][NW][64];  // as post_sweep_xch_kernel's
+  if (skip && *skip) return;
+  const double icc = 1.0 / cc;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const double mu = SUMS ? st->mu : 0.0;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int bid = xcd_block(g.remap);
+  const int seg = bid % g.nseg;
+  bid /= g.nseg;
+  const int tile = bid % g.ntile;
+  const int chunk = bid / g.ntile;
+  const int nx = g.nx, ny = g.ny, nz = g.nzl;
+  const int kb = chunk * g.kc;  // even (kc even)
+  const int ke = min(kb + g.kc, nz);
+  if (kb < nz) {
+    const int g0 = tile * SB - 2;
+    const int br0 = wid * TY;
+    const int j0 = g0 + br0;  // even
+    auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
+    int ip = seg * kSegOut + 2 * (lane - kSegLead);  // even
+    if (ip < 0) ip += nx;
+    if (ip >= nx) ip -= nx;
+    const int o = seg * kSegOut + 2 * (lane - kSegLead);
+    const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
+    int64_t ro[TY];
+    unsigned row_ok = 0;
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      ro[r] = (int64_t)wrap(j0 + r, ny) * nx;
+      const int brow = br0 + r;
+      if (brow >= 2 && brow < RB - 2 && g0 + brow < ny) row_ok |= 1u << r;
+    }
+    const unsigned boff = (unsigned)ip * 8u;
+    auto rix = [&](int64_t row) { return RowIx{row, boff}; };
+    auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+    auto pl = [&](int kk) -> int64_t { return (int64_t)wrapk(kk) * g.plane; };
+    int64_t crow[NC];
+#pragma unroll
+    for (int t = 0; t < NC; ++t) crow[t] = (int64_t)wrap((j0 >> 1) - 1 + t, cgeo.ncy) * cgeo.ncx;
+    const unsigned cboff = (unsigned)(ip >> 1) * 8u;
+    // x_s rows of plane kk into rows 1 .. TY of dst, and the coarse values under them
+    auto ldx = [&](double (&dst)[TY + 2][2], double (&cv)[2][NC], int kk) {
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 0; r < TY; ++r) load_row<2>(xs, rix(base + ro[r]), dst[r + 1]);
+      const int kw = wrapk(kk);
+      const int K = kw >> 1;
+      int fK = (kw & 1) ? K + 1 : K - 1;
+      if (fK < 0) fK += cgeo.ncz;
+      if (fK >= cgeo.ncz) fK -= cgeo.ncz;
+      const double* cn = xc + (int64_t)K * cgeo.cplane;
+      const double* cf = xc + (int64_t)fK * cgeo.cplane;
+#pragma unroll
+      for (int t = 0; t < NC; ++t) {
+        cv[0][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cn + crow[t]) + cboff);
+        cv[1][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cf + crow[t]) + cboff);
+      }
+    };
+    auto prolong = [&](double (&v)[TY + 2][2], const double (&cv)[2][NC]) {
+      double xi[2][NC][2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int t = 0; t < NC; ++t) {
+          const double c = cv[q][t];
+          xi[q][t][0] = 0.75 * c + 0.25 * dpp_from_lower(c);
+          xi[q][t][1] = 0.75 * c + 0.25 * dpp_from_upper(c);
+        }
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const int tJ = 1 + (r >> 1);
+        const int tf = (r & 1) ? tJ + 1 : tJ - 1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double vn = 0.75 * xi[0][tJ][e] + 0.25 * xi[0][tf][e];
+          const double vf = 0.75 * xi[1][tJ][e] + 0.25 * xi[1][tf][e];
+          v[r + 1][e] = v[r + 1][e] + (0.75 * vn + 0.25 * vf);
+        }
+      }
+    };
+    auto ldb = [&](double (&dst)[TY][2], int kk) {
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 0; r < TY; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
+    };
+    // element of the c1 (first-half) point of own row r on a plane of parity P: post_sweep_kernel's
+    // ec1 with ((i + j) & 1) = r & 1 and c1 = 1
+    auto e1 = [](int r, int P) { return ((r + P) & 1) ^ 1; };
+    auto half1 = [&](auto Pc, const double (&zmv)[TY], const double (&xcn)[TY + 2][2],
+                     const double (&xp)[TY + 2][2], const double (&bb)[TY][2],
+                     double (&out)[TY]) {
+      constexpr int P = decltype(Pc)::value;
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const int e = e1(r, P);
+        const double xl = e ? xcn[r + 1][0] : dpp_from_lower(xcn[r + 1][1]);
+        const double xr = e ? dpp_from_upper(xcn[r + 1][0]) : xcn[r + 1][1];
+        double nb = cz * zmv[r];
+        nb = nb + cy * xcn[r][e];
+        nb = nb + cx * xl;
+        nb = nb + cx * xr;
+        nb = nb + cy * xcn[r + 2][e];
+        nb = nb + cz * xp[r + 1][e];
+        const double t = (bb[r][e] - nb) * icc;
+        out[r] = (1.0 - omega) * xcn[r + 1][e] + omega * t;
+      }
+    };
+    auto half2 = [&](auto Pc, int kk, const double (&sm)[TY], const double (&sc)[TY],
+                     const double (&sp)[TY], const double (&sh)[2], const double (&xo)[TY],
+                     const double (&bo)[TY], const double (&bc1)[SUMS ? TY : 1]) {
+      constexpr int P = decltype(Pc)::value;
+      const int64_t base = pl(kk);
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const int e2 = e1(r, P) ^ 1;  // the second-colour point's element
+        const double cself = sc[r];
+        const double xl = e2 ? cself : dpp_from_lower(cself);
+        const double xr = e2 ? dpp_from_upper(cself) : cself;
+        double nb = cz * sm[r];
+        nb = nb + cy * (r == 0 ? sh[0] : sc[r == 0 ? 0 : r - 1]);
+        nb = nb + cx * xl;
+        nb = nb + cx * xr;
+        nb = nb + cy * (r == TY - 1 ? sh[1] : sc[r == TY - 1 ? r : r + 1]);
+        nb = nb + cz * sp[r];
+        const double t = (bo[r] - nb) * icc;
+        const double v = (1.0 - omega) * xo[r] + omega * t;
+        double ov[2];
+        ov[e2] = v;
+        ov[e2 ^ 1] = cself;
+        if (out_ok && (row_ok >> r & 1u)) {
+          store_row<2>(xout, rix(base + ro[r]), ov, g.nt);
+          if constexpr (SUMS) {
+            double rv2[2];
+            rv2[e2] = bo[r];
+            rv2[e2 ^ 1] = bc1[r];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const double t2 = ov[e] - mu;
+              acc[0] += t2;
+              acc[1] += t2 * t2;
+              acc[2] += t2 * rv2[e];
+              acc[3] += rv2[e];
+            }
+          }
+        }
+      }
+    };
+    const int wm = wid > 0 ? wid - 1 : wid, wp = wid < NW - 1 ? wid + 1 : wid;
+    auto put_x = [&](int par, const double (&v)[TY + 2][2]) {
+      xch[par][0][wid][lane] = v[1][0];
+      xch[par][1][wid][lane] = v[1][1];
+      xch[par][2][wid][lane] = v[TY][0];
+      xch[par][3][wid][lane] = v[TY][1];
+    };
+    double XQ[2][TY + 2][2];  // input planes k+1 (rows -1 .. TY), k+2 (own rows) at Q, Q+1
+    double XM[2][TY];         // input c2 values: planes k-1, k at Q, Q+1
+    double S1[4][TY];         // first-half values: planes k-2 .. k+1 at Q .. Q+3
+    double SH[2][2];          // first-half values of rows -1 / TY: planes k-1, k at Q, Q+1
+    double BB[2][TY];         // b at c2 points: planes k-1, k at Q, Q+1
+    double BB1[2][SUMS ? TY : 1];  // b at c1 points (sums only)
+    {
+      double cv[2][NC];
+      ldx(XQ[1], cv, kb - 2);  // plane kb-2 (even): its c2 values only
+      prolong(XQ[1], cv);
+#pragma unroll
+      for (int r = 0; r < TY; ++r) XM[1][r] = XQ[1][r + 1][e1(r, 0) ^ 1];
+      ldx(XQ[0], cv, kb - 1);
+      prolong(XQ[0], cv);
+      put_x(1, XQ[0]);  // as if iteration kb-3 (odd) had formed plane kb-1
+    }
+#pragma unroll
+    for (int r = 0; r < TY; ++r) {
+      XM[0][r] = BB[0][r] = BB[1][r] = 0.0;
+      S1[0][r] = S1[1][r] = S1[2][r] = 0.0;
+      if constexpr (SUMS) BB1[0][r] = BB1[1][r] = 0.0;
+    }
+    SH[0][0] = SH[0][1] = 0.0;
+    // one plane: k = kb - 2 + Q (mod 4), parity Q & 1
+    auto body = [&](auto Qc, int k) {
+      constexpr int Q = decltype(Qc)::value;
+      constexpr int KP = Q & 1;
+      double (&xq1)[TY + 2][2] = XQ[Q & 1];
+      double (&xq2)[TY + 2][2] = XQ[(Q + 1) & 1];
+      double (&xm)[TY] = XM[Q & 1];
+      double (&x0)[TY] = XM[(Q + 1) & 1];
+      double (&bm)[TY] = BB[Q & 1];
+      double (&b0)[TY] = BB[(Q + 1) & 1];
+      double (&bm1)[SUMS ? TY : 1] = BB1[Q & 1];
+      double (&b01)[SUMS ? TY : 1] = BB1[(Q + 1) & 1];
+      double (&shp)[2] = SH[Q & 1];
+      double (&shc)[2] = SH[(Q + 1) & 1];
+      double bq1[TY][2], cv[2][NC];
+      ldx(xq2, cv, k + 2);
+      ldb(bq1, k + 1);
+      __syncthreads();
+      {
+        constexpr int rp = KP ^ 1;
+        xq1[0][0] = xch[rp][2][wm][lane];
+        xq1[0][1] = xch[rp][3][wm][lane];
+        xq1[TY + 1][0] = xch[rp][0][wp][lane];
+        xq1[TY + 1][1] = xch[rp][1][wp][lane];
+        shc[0] = xch[rp][5][wm][lane];
+        shc[1] = xch[rp][4][wp][lane];
+      }
+      if (k > kb && k <= ke)
+        half2(std::integral_constant<int, KP ^ 1>{}, k - 1, S1[Q], S1[(Q + 1) & 3],
+              S1[(Q + 2) & 3], shp, xm, bm, bm1);
+      prolong(xq2, cv);
+      put_x(KP, xq2);
+      double (&s1n)[TY] = S1[(Q + 3) & 3];
+      half1(std::integral_constant<int, KP ^ 1>{}, x0, xq1, xq2, bq1, s1n);  // plane k+1
+      xch[KP][4][wid][lane] = s1n[0];
+      xch[KP][5][wid][lane] = s1n[TY - 1];
+      // plane k+1's c2 input values and right-hand side replace plane k-1's
+#pragma unroll
+      for (int r = 0; r < TY; ++r) {
+        const int e = e1(r, KP ^ 1);
+        xm[r] = xq1[r + 1][e ^ 1];
+        bm[r] = bq1[r][e ^ 1];
+        if constexpr (SUMS) bm1[r] = bq1[r][e];
+      }
+    };
+#pragma unroll 1
+    for (int k = kb - 2; k <= ke; k += 4) {
+      body(std::integral_constant<int, 0>{}, k);
+      body(std::integral_constant<int, 1>{}, k + 1);
+      body(std::integral_constant<int, 2>{}, k + 2);
+      body(std::integral_constant<int, 3>{}, k + 3);
+    }
+  }
+  if constexpr (SUMS) block_partials<4>(acc, parts);
+}
+
 // even extents, nx >= 128, >= 4 planes per rank: the fused sweep applies (else two half-sweeps)
 bool sor_sweep2_supported(const pb_grid* g) {
   return g->n[0] >= 128 && g->n[0] % 2 == 0 && g->n[1] % 2 == 0 && g->n[1] >= 8 &&
@@ -1040,10 +2087,57 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
   if (cg->n[0] * 2 != g->n[0] || cg->n[1] * 2 != g->n[1] || cg->nzl * 2 != g->nzl)
     return set_error(PB_ERR_ARG, "fused post-smoothing: coarse grid is not half the fine one");
   Sweep2Geo geo;
-  const int64_t nblocks = sweep2_geo(g, geo);
+  int64_t nblocks = sweep2_geo(g, geo);
   geo.split = 0;
   geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
   PostGeo cgeo{(int)cg->n[0], (int)cg->n[1], (int)cg->nzl, cg->plane};
+  // rows shared through LDS (post_sweep_xch_kernel): 1 = 8 waves x 4 rows, 2 = 16 x 2, 3 = 8 x 2;
+  // 4 .. 6: the same with the loads issued one iteration earlier (two register sets); 7 .. 9:
+  // the plane loop unrolled by four (post_sweep_u4_kernel: 8 x 4, 16 x 2, 8 x 2; its compile-time
+  // colours assume k0 = 0 and even chunk starts)
+  const int xv = env_int("PB_POSTX", 1);
+  if (xv >= 1 && xv <= 9) {
+    const int nw = (xv == 2 || xv == 5 || xv == 8) ? 16 : 8;
+    const int ty = (xv == 1 || xv == 4 || xv == 7) ? 4 : 2;
+    geo.ntile = (geo.ny + nw * ty - 5) / (nw * ty - 4);
+    const int columns = geo.nseg * geo.ntile;
+    const int target = env_int("PB_POSTX_WGCU", 4) * g->ctx->num_cus;
+    int nchunk = std::max(1, (target + columns - 1) / columns);
+    nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_POSTX_MINZ", 16)));
+    geo.kc = (geo.nzl + nchunk - 1) / nchunk;
+    geo.kc += geo.kc & 1;  // even chunk starts (the unrolled kernels' plane parities)
+    geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
+    nblocks = (int64_t)columns * geo.nchunk;
+    if (sums_st && nblocks * 4 > g->ctx->partials_cap)
+      return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
+                       (long long)nblocks);
+    decltype(&post_sweep_xch_kernel<true, 8, 4, 1>) kern;
+#define PB_POSTX_KERN(NW_, TY_, PF_) \
+  (sums_st ? post_sweep_xch_kernel<true, NW_, TY_, PF_> : post_sweep_xch_kernel<false, NW_, TY_, PF_>)
+    switch (xv) {
+      case 1: kern = PB_POSTX_KERN(8, 4, 1); break;
+      case 2: kern = PB_POSTX_KERN(16, 2, 1); break;
+      case 3: kern = PB_POSTX_KERN(8, 2, 1); break;
+      case 4: kern = PB_POSTX_KERN(8, 4, 2); break;
+      case 5: kern = PB_POSTX_KERN(16, 2, 2); break;
+      case 6: kern = PB_POSTX_KERN(8, 2, 2); break;
+#define PB_POSTU_KERN(NW_, TY_) \
+  (sums_st ? post_sweep_u4_kernel<true, NW_, TY_> : post_sweep_u4_kernel<false, NW_, TY_>)
+      case 7: kern = PB_POSTU_KERN(8, 4); break;
+      case 8: kern = PB_POSTU_KERN(16, 2); break;
+      default: kern = PB_POSTU_KERN(8, 2); break;
+    }
+#undef PB_POSTX_KERN
+#undef PB_POSTU_KERN
+    if (xv >= 7 && g->k0 != 0)
+      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: one rank only");
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo, cgeo,
+                       s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout, sums_st,
+                       sums_st ? g->ctx->d_partials : (double*)nullptr, skip);
+    if (sums_st && nparts) *nparts = (int)nblocks;
+    PB_HIP(hipGetLastError());
+    return PB_OK;
+  }
   if (sums_st) {
     if (nblocks * 4 > g->ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
@@ -1074,6 +2168,32 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
   sweep2_geo(g, geo);
   geo.split = 0;
   geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
+  // rows shared through LDS (presmooth_restrict_xch_kernel): 1 = 8 waves x 4 rows, 2 = 16 x 2
+  // (16 x 4 would need more than the 128 VGPRs a 1024-thread block can have); 3, 4: the same with
+  // the plane loop unrolled by four (presmooth_restrict_u4_kernel; its compile-time colours
+  // assume k0 = 0, which one rank has)
+  const int xv = env_int("PB_PRRX", 1);
+  if (xv >= 1 && xv <= 4) {
+    const int nw = (xv & 1) ? 8 : 16, ty = (xv & 1) ? 4 : 2;
+    geo.ntile = (geo.ny + nw * ty - 9) / (nw * ty - 8);
+    const int columns = geo.nseg * geo.ntile;
+    const int target = env_int("PB_PRRX_WGCU", 4) * g->ctx->num_cus;
+    int nchunk = std::max(1, (target + columns - 1) / columns);
+    nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_PRRX_MINZ", 16)));
+    geo.kc = (geo.nzl + nchunk - 1) / nchunk;
+    geo.kc += geo.kc & 1;
+    geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
+    const int64_t nblocks = (int64_t)columns * geo.nchunk;
+    if (g->k0 != 0) return set_error(PB_ERR_UNSUPPORTED, "fused restriction: one rank only");
+    auto kern = xv == 1   ? presmooth_restrict_xch_kernel<8, 4>
+                : xv == 2 ? presmooth_restrict_xch_kernel<16, 2>
+                : xv == 3 ? presmooth_restrict_u4_kernel<8, 4>
+                          : presmooth_restrict_u4_kernel<16, 2>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo,
+                       (int)cg->n[0], cg->plane, s.cx, s.cy, s.cz, s.cc, omega, b, xout, bc, skip);
+    PB_HIP(hipGetLastError());
+    return PB_OK;
+  }
   geo.ntile = (geo.ny + kWaves * kTYR - 1) / (kWaves * kTYR);
   // chunks of an even number of planes (the restriction pairs them); each chunk also forms S1 on
   // three planes and the residual on two planes outside it, so chunks stay long

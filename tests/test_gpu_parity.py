@@ -726,7 +726,10 @@ MG_KERNELS = {"default": {},
               "norestrict": {"PB_MG_PRESMOOTH_RESTRICT": "0", "PB_MG_ENGINE_MIN_PLANE": "0"},
               # short chunks: more z-chunk seams in the fused restriction
               "prrchunks": {"PB_PRR_WGCU": "64", "PB_PRR_MINZ": "2",
-                            "PB_MG_ENGINE_MIN_PLANE": "0"}}
+                            "PB_PRRX_WGCU": "64", "PB_PRRX_MINZ": "2",
+                            "PB_MG_ENGINE_MIN_PLANE": "0"},
+              # the per-wave fused sweeps (before rows were shared through LDS, r03)
+              "perwave": {"PB_PRRX": "0", "PB_POSTX": "0", "PB_MG_ENGINE_MIN_PLANE": "0"}}
 
 
 @pytest.mark.parametrize("kern", sorted(MG_KERNELS))
@@ -802,6 +805,85 @@ def test_cg_mg_fused_post_smoothing(ctx, monkeypatch, kern):
     check_history(hist, ho, bar=HIST_RTOL_PC)
     check_x(x.get_values(), xo)
     k.destroy()
+
+
+# fused post-smoothing kernels: rows shared between the waves of a block through LDS
+# (PB_POSTX 1 = 8 waves x 4 rows, 2 = 16 x 2, 3 = 8 x 2; 4-6 the same with loads one plane
+# further ahead; 7-9 = 8 x 4, 16 x 2, 8 x 2 with the plane loop unrolled by four) and the
+# per-wave kernel (0); y extents that are no multiple of a block's stored rows (28 / 12), one smaller than a block (8 rows:
+# the block's rows wrap several times), and the full-size test's 256^2 planes
+POSTX_SHAPES = [(256, 256, 32), (128, 40, 16), (256, 8, 8), (128, 96, 24)]
+
+
+@pytest.mark.parametrize("postx", ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9"])
+@pytest.mark.parametrize("n3", POSTX_SHAPES)
+def test_mg_post_sweep_variants_bit_exact(ctx, monkeypatch, postx, n3):
+    monkeypatch.setenv("PB_POSTX", postx)
+    monkeypatch.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
+    monkeypatch.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    r = O.fill_random(N, 5)
+    ref = O.mg_apply(r, n3, h, pc="mg")
+    da = pb.DA(ctx, n3)
+    P, A, _, _ = pb.initialise_linear_system(da, h)
+    k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
+    rv, zv = pb.Vec(da), pb.Vec(da)
+    rv.set_values(r)
+    k.pc_apply(rv, zv)
+    assert np.array_equal(zv.get_values(), ref)
+    k.destroy()
+
+
+@pytest.mark.parametrize("prrx", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("chunks", [False, True])
+@pytest.mark.parametrize("n3", POSTX_SHAPES)
+def test_mg_presmooth_restrict_variants_bit_exact(ctx, monkeypatch, prrx, chunks, n3):
+    """Fused pre-smoothing + residual + restriction: rows shared through LDS (PB_PRRX 1 = 8
+    waves x 4 rows, 2 = 16 x 2; 3, 4 the same with the plane loop unrolled by four) and the
+    per-wave kernel (0); short z chunks put chunk seams inside the restriction's plane pairs'
+    neighbourhood."""
+    monkeypatch.setenv("PB_PRRX", prrx)
+    monkeypatch.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
+    monkeypatch.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
+    if chunks:
+        for k_ in ("PB_PRR_WGCU", "PB_PRRX_WGCU"):
+            monkeypatch.setenv(k_, "64")
+        for k_ in ("PB_PRR_MINZ", "PB_PRRX_MINZ"):
+            monkeypatch.setenv(k_, "2")
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    r = O.fill_random(N, 6)
+    ref = O.mg_apply(r, n3, h, pc="mg")
+    da = pb.DA(ctx, n3)
+    P, A, _, _ = pb.initialise_linear_system(da, h)
+    k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
+    rv, zv = pb.Vec(da), pb.Vec(da)
+    rv.set_values(r)
+    k.pc_apply(rv, zv)
+    assert np.array_equal(zv.get_values(), ref)
+    k.destroy()
+
+
+@pytest.mark.parametrize("postx", ["1", "2", "3", "4", "5", "6", "7", "8", "9"])
+def test_cg_mg_post_sweep_xch_sums(ctx, monkeypatch, postx):
+    """The LDS-shared post-smoothing also takes CG's residual sums on level 0 (a partial per
+    block): CG + MG history / solution within the CG bar."""
+    monkeypatch.setenv("PB_POSTX", postx)
+    monkeypatch.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
+    monkeypatch.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
+    n3 = (128, 96, 24)
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(N, SEED), n3, h)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-10, pc="mg")
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(P, A, x, bv, ["-pc_type", "mg", "-ksp_rtol", "1e-10"])
+    assert reason == ro == 2 and its == itso
+    check_history(hist, ho, bar=HIST_RTOL_PC)
+    check_x(x.get_values(), xo)
 
 
 def test_cg_compact_operator_mg_pc(ctx):
