@@ -748,7 +748,8 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_xch_kernel(
   }
   const unsigned boff = (unsigned)ip * 8u;
   auto rix = [&](int64_t row) { return RowIx{row, boff}; };
-  auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+  // planes up to a few steps past the chunk (the last step's spare planes): any distance
+  auto wrapk = [&](int kk) { kk %= nz; return kk < 0 ? kk + nz : kk; };
   auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
   auto ldraw = [&](double (&dst)[TY][2], int kk) {
     const int64_t base = (int64_t)wrapk(kk) * g.plane;
@@ -950,16 +951,22 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_xch_kernel(
 // A chunk runs a whole number of four-plane steps (up to three planes more than it needs; they
 // store nothing). Same operations on the same operands: bit-identical.
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TY>
+template <int NW, int TY, bool EDGE>
 __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
     double omega, const double* __restrict__ b, double* __restrict__ xout,
     double* __restrict__ bc, const int* skip) {
   static_assert(TY % 2 == 0 && TY >= 2, "whole coarse rows per wave");
   constexpr int RB = NW * TY;
-  constexpr int SB = RB - 8;
+  // EDGE: the block's first and last waves also form the red values of the rows just outside
+  // the block (one more b row each), so the block loses two rows at each end instead of four
+  constexpr int LO = EDGE ? 2 : 4;  // first stored block row
+  constexpr int SB = RB - 2 * LO;
   constexpr int NCR = TY / 2;
-  __shared__ double xch[2][8][NW][64];  // as presmooth_restrict_xch_kernel's
+  // as presmooth_restrict_xch_kernel's; (EDGE) xe: the red values of the first and the last
+  // wave's edge rows
+  __shared__ double xch[2][8][NW][64];
+  __shared__ double xe[2][2][64];
   if (skip && *skip) return;
   const double icc = 1.0 / cc;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -972,7 +979,7 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
   const int ke = min(kb + g.kc, g.nzl);
   const int nx = g.nx, ny = g.ny, nz = g.nzl;
   if (kb >= nz) return;
-  const int g0 = tile * SB - 4;
+  const int g0 = tile * SB - LO;
   const int br0 = wid * TY;
   const int j0 = g0 + br0;  // even
   auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
@@ -987,11 +994,14 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
   for (int r = 0; r < TY; ++r) {
     ro[r] = (int64_t)wrap(j0 + r, ny) * nx;
     const int brow = br0 + r;
-    if (brow >= 4 && brow < RB - 4 && g0 + brow < ny) row_ok |= 1u << r;
+    if (brow >= LO && brow < RB - LO && g0 + brow < ny) row_ok |= 1u << r;
   }
+  const int er = wid == 0 ? -1 : TY;  // edge row (used by the first and the last wave)
+  const int64_t roe = (int64_t)wrap(j0 + er, ny) * nx;
   const unsigned boff = (unsigned)ip * 8u;
   auto rix = [&](int64_t row) { return RowIx{row, boff}; };
-  auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+  // planes up to a few steps past the chunk (the last step's spare planes): any distance
+  auto wrapk = [&](int kk) { kk %= nz; return kk < 0 ? kk + nz : kk; };
   auto ldraw = [&](double (&dst)[TY][2], int kk) {
     const int64_t base = (int64_t)wrapk(kk) * g.plane;
 #pragma unroll
@@ -1000,6 +1010,13 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
   // element holding the red point of own row r on a plane of parity P (pair origin i even, row
   // origin j0 even, k0 = 0): presmooth_restrict_kernel's ((i + j) & 1) + kpar != 0
   auto red_e = [](int r, int P) { return (r + P) & 1; };
+  auto ldedge = [&](double (&dst)[2], int kk) {
+    if constexpr (EDGE) load_row<2>(b, rix((int64_t)wrapk(kk) * g.plane + roe), dst);
+  };
+  auto rededge = [&](int P, const double (&v)[2]) -> double {  // the edge row's red value
+    const double t = (((er + P) & 1) ? v[1] : v[0]) - 0.0;
+    return (1.0 - omega) * 0.0 + omega * (t * icc);
+  };
   auto redv = [&](auto Pc, const double (&v)[TY][2], double (&red)[TY]) {
     constexpr int P = decltype(Pc)::value;
 #pragma unroll
@@ -1039,17 +1056,27 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
   double X[2][TY];     // residual x sums: planes k-1, k at slots Q, Q+1
   double H[2][2];      // red values of rows -1 / TY: planes k+1, k+2 at slots Q, Q+1
   double accA[NCR], accB[NCR];
+  double ev2[2], ev1[2];  // edge rows of planes kb-2, kb-1
   ldraw(B[3], kb - 3);
   redv(std::integral_constant<int, 1>{}, B[3], R[0]);  // planes kb-3 (odd), kb-2, kb-1
   ldraw(B[1], kb - 2);
+  ldedge(ev2, kb - 2);
   redv(std::integral_constant<int, 0>{}, B[1], R[1]);
   ldraw(B[2], kb - 1);
+  ldedge(ev1, kb - 1);
   redv(std::integral_constant<int, 1>{}, B[2], R[2]);
   xch[1][0][wid][lane] = R[1][0];
   xch[1][1][wid][lane] = R[1][TY - 1];
   __syncthreads();
   H[0][0] = xch[1][1][wm][lane];
   H[0][1] = xch[1][0][wp][lane];
+  if constexpr (EDGE) {
+    if (wid == 0) H[0][0] = rededge(0, ev2);
+    if (wid == NW - 1) H[0][1] = rededge(0, ev2);
+    const double v = rededge(1, ev1);
+    if (wid == 0) xe[0][0][lane] = v;
+    if (wid == NW - 1) xe[0][1][lane] = v;
+  }
   xch[0][0][wid][lane] = R[2][0];
   xch[0][1][wid][lane] = R[2][TY - 1];
 #pragma unroll
@@ -1079,12 +1106,19 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     double (&rh1)[2] = H[Q & 1];
     double (&rh2)[2] = H[(Q + 1) & 1];
     ldraw(raw, k + 3);
+    double rawe[2];
+    ldedge(rawe, k + 3);
     __syncthreads();
     double sh[2][2], sxh[2];
     {
       constexpr int rp = KP ^ 1;  // written by plane k-1
-      rh2[0] = xch[rp][1][wm][lane];
-      rh2[1] = xch[rp][0][wp][lane];
+      if constexpr (EDGE) {  // the edge waves' own edge rows
+        rh2[0] = wid == 0 ? xe[rp][0][lane] : xch[rp][1][wm][lane];
+        rh2[1] = wid == NW - 1 ? xe[rp][1][lane] : xch[rp][0][wp][lane];
+      } else {
+        rh2[0] = xch[rp][1][wm][lane];
+        rh2[1] = xch[rp][0][wp][lane];
+      }
       sh[0][0] = xch[rp][4][wm][lane];
       sh[0][1] = xch[rp][5][wm][lane];
       sh[1][0] = xch[rp][2][wp][lane];
@@ -1166,6 +1200,11 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     redv(std::integral_constant<int, KP ^ 1>{}, raw, rn);  // plane k+3
     xch[KP][0][wid][lane] = rn[0];
     xch[KP][1][wid][lane] = rn[TY - 1];
+    if constexpr (EDGE) {
+      const double v = rededge(KP ^ 1, rawe);
+      if (wid == 0) xe[KP][0][lane] = v;
+      if (wid == NW - 1) xe[KP][1][lane] = v;
+    }
   };
 #pragma unroll 1
   for (int k = kb - 3; k <= ke + 1; k += 4) {
@@ -1805,51 +1844,54 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
     }
     const unsigned boff = (unsigned)ip * 8u;
     auto rix = [&](int64_t row) { return RowIx{row, boff}; };
-    auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
+    // planes up to a few steps past the chunk (the last step's spare planes): any distance
+    auto wrapk = [&](int kk) { kk %= nz; return kk < 0 ? kk + nz : kk; };
     auto pl = [&](int kk) -> int64_t { return (int64_t)wrapk(kk) * g.plane; };
     int64_t crow[NC];
 #pragma unroll
     for (int t = 0; t < NC; ++t) crow[t] = (int64_t)wrap((j0 >> 1) - 1 + t, cgeo.ncy) * cgeo.ncx;
     const unsigned cboff = (unsigned)(ip >> 1) * 8u;
-    // x_s rows of plane kk into rows 1 .. TY of dst, and the coarse values under them
-    auto ldx = [&](double (&dst)[TY + 2][2], double (&cv)[2][NC], int kk) {
+    // x_s rows of plane kk into rows 1 .. TY of dst
+    auto ldx = [&](double (&dst)[TY + 2][2], int kk) {
       const int64_t base = pl(kk);
 #pragma unroll
       for (int r = 0; r < TY; ++r) load_row<2>(xs, rix(base + ro[r]), dst[r + 1]);
-      const int kw = wrapk(kk);
-      const int K = kw >> 1;
-      int fK = (kw & 1) ? K + 1 : K - 1;
-      if (fK < 0) fK += cgeo.ncz;
-      if (fK >= cgeo.ncz) fK -= cgeo.ncz;
-      const double* cn = xc + (int64_t)K * cgeo.cplane;
-      const double* cf = xc + (int64_t)fK * cgeo.cplane;
+    };
+    // coarse plane K (periodic) under the own rows
+    auto ldc = [&](double (&cv)[NC], int K) {
+      K %= cgeo.ncz;
+      if (K < 0) K += cgeo.ncz;
+      const double* cp = xc + (int64_t)K * cgeo.cplane;
+#pragma unroll
+      for (int t = 0; t < NC; ++t)
+        cv[t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cp + crow[t]) + cboff);
+    };
+    // one coarse plane interpolated in x, then in y onto each own row (post_sweep_kernel's
+    // prolong_p: the same operations, formed once per coarse plane instead of once per fine plane
+    // that reads it -- each serves the two fine planes it is near to and the two it is far from)
+    auto yinterp = [&](const double (&cv)[NC], double (&Y)[TY][2]) {
+      double xi[NC][2];
 #pragma unroll
       for (int t = 0; t < NC; ++t) {
-        cv[0][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cn + crow[t]) + cboff);
-        cv[1][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cf + crow[t]) + cboff);
+        const double c = cv[t];
+        xi[t][0] = 0.75 * c + 0.25 * dpp_from_lower(c);
+        xi[t][1] = 0.75 * c + 0.25 * dpp_from_upper(c);
       }
-    };
-    auto prolong = [&](double (&v)[TY + 2][2], const double (&cv)[2][NC]) {
-      double xi[2][NC][2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int t = 0; t < NC; ++t) {
-          const double c = cv[q][t];
-          xi[q][t][0] = 0.75 * c + 0.25 * dpp_from_lower(c);
-          xi[q][t][1] = 0.75 * c + 0.25 * dpp_from_upper(c);
-        }
 #pragma unroll
       for (int r = 0; r < TY; ++r) {
         const int tJ = 1 + (r >> 1);
         const int tf = (r & 1) ? tJ + 1 : tJ - 1;
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const double vn = 0.75 * xi[0][tJ][e] + 0.25 * xi[0][tf][e];
-          const double vf = 0.75 * xi[1][tJ][e] + 0.25 * xi[1][tf][e];
-          v[r + 1][e] = v[r + 1][e] + (0.75 * vn + 0.25 * vf);
-        }
+        for (int e = 0; e < 2; ++e) Y[r][e] = 0.75 * xi[tJ][e] + 0.25 * xi[tf][e];
       }
+    };
+    // x_s + P x_c on the own rows: Yn, Yf = the near / far coarse planes' interpolants
+    auto prolong = [&](double (&v)[TY + 2][2], const double (&Yn)[TY][2],
+                       const double (&Yf)[TY][2]) {
+#pragma unroll
+      for (int r = 0; r < TY; ++r)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) v[r + 1][e] = v[r + 1][e] + (0.75 * Yn[r][e] + 0.25 * Yf[r][e]);
     };
     auto ldb = [&](double (&dst)[TY][2], int kk) {
       const int64_t base = pl(kk);
@@ -1931,14 +1973,23 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
     double SH[2][2];          // first-half values of rows -1 / TY: planes k-1, k at Q, Q+1
     double BB[2][TY];         // b at c2 points: planes k-1, k at Q, Q+1
     double BB1[2][SUMS ? TY : 1];  // b at c1 points (sums only)
+    // coarse interpolants: slot K & 1 holds coarse plane K (kb a multiple of 4, K0 = kb / 2 even)
+    double YC[2][TY][2];
+    const int K0 = kb >> 1;
     {
-      double cv[2][NC];
-      ldx(XQ[1], cv, kb - 2);  // plane kb-2 (even): its c2 values only
-      prolong(XQ[1], cv);
+      double cv[NC];
+      ldc(cv, K0 - 2);
+      yinterp(cv, YC[0]);
+      ldc(cv, K0 - 1);
+      yinterp(cv, YC[1]);
+      ldx(XQ[1], kb - 2);  // plane kb-2 (even; near K0-1, far K0-2): its c2 values only
+      prolong(XQ[1], YC[1], YC[0]);
 #pragma unroll
       for (int r = 0; r < TY; ++r) XM[1][r] = XQ[1][r + 1][e1(r, 0) ^ 1];
-      ldx(XQ[0], cv, kb - 1);
-      prolong(XQ[0], cv);
+      ldc(cv, K0);
+      yinterp(cv, YC[0]);
+      ldx(XQ[0], kb - 1);  // plane kb-1 (near K0-1, far K0)
+      prolong(XQ[0], YC[1], YC[0]);
       put_x(1, XQ[0]);  // as if iteration kb-3 (odd) had formed plane kb-1
     }
 #pragma unroll
@@ -1962,8 +2013,12 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
       double (&b01)[SUMS ? TY : 1] = BB1[(Q + 1) & 1];
       double (&shp)[2] = SH[Q & 1];
       double (&shc)[2] = SH[(Q + 1) & 1];
-      double bq1[TY][2], cv[2][NC];
-      ldx(xq2, cv, k + 2);
+      // plane k+2 = kb + 4m + Q: even (Q even) -> near K, far K-1; odd -> near K, far K+1 (new),
+      // K = (k + 2) >> 1 = K0 + 2m + (Q >> 1)
+      constexpr int KN = Q >> 1;  // near coarse plane's slot (K0 even)
+      double bq1[TY][2], cv[NC];
+      ldx(xq2, k + 2);
+      if constexpr (Q & 1) ldc(cv, ((k + 2) >> 1) + 1);
       ldb(bq1, k + 1);
       __syncthreads();
       {
@@ -1978,7 +2033,8 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
       if (k > kb && k <= ke)
         half2(std::integral_constant<int, KP ^ 1>{}, k - 1, S1[Q], S1[(Q + 1) & 3],
               S1[(Q + 2) & 3], shp, xm, bm, bm1);
-      prolong(xq2, cv);
+      if constexpr (Q & 1) yinterp(cv, YC[KN ^ 1]);
+      prolong(xq2, YC[KN], YC[KN ^ 1]);
       put_x(KP, xq2);
       double (&s1n)[TY] = S1[(Q + 3) & 3];
       half1(std::integral_constant<int, KP ^ 1>{}, x0, xq1, xq2, bq1, s1n);  // plane k+1
@@ -2105,7 +2161,7 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     int nchunk = std::max(1, (target + columns - 1) / columns);
     nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_POSTX_MINZ", 16)));
     geo.kc = (geo.nzl + nchunk - 1) / nchunk;
-    geo.kc += geo.kc & 1;  // even chunk starts (the unrolled kernels' plane parities)
+    geo.kc = (geo.kc + 3) & ~3;  // chunk starts at multiples of 4 (the unrolled kernels' parities)
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
     nblocks = (int64_t)columns * geo.nchunk;
     if (sums_st && nblocks * 4 > g->ctx->partials_cap)
@@ -2173,9 +2229,10 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
   // the plane loop unrolled by four (presmooth_restrict_u4_kernel; its compile-time colours
   // assume k0 = 0, which one rank has)
   const int xv = env_int("PB_PRRX", 1);
-  if (xv >= 1 && xv <= 4) {
+  if (xv >= 1 && xv <= 5) {
     const int nw = (xv & 1) ? 8 : 16, ty = (xv & 1) ? 4 : 2;
-    geo.ntile = (geo.ny + nw * ty - 9) / (nw * ty - 8);
+    const int sb = nw * ty - (xv == 5 ? 4 : 8);  // 5: u4 8 x 4 with the edge rows' red values
+    geo.ntile = (geo.ny + sb - 1) / sb;
     const int columns = geo.nseg * geo.ntile;
     const int target = env_int("PB_PRRX_WGCU", 4) * g->ctx->num_cus;
     int nchunk = std::max(1, (target + columns - 1) / columns);
@@ -2187,8 +2244,9 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     if (g->k0 != 0) return set_error(PB_ERR_UNSUPPORTED, "fused restriction: one rank only");
     auto kern = xv == 1   ? presmooth_restrict_xch_kernel<8, 4>
                 : xv == 2 ? presmooth_restrict_xch_kernel<16, 2>
-                : xv == 3 ? presmooth_restrict_u4_kernel<8, 4>
-                          : presmooth_restrict_u4_kernel<16, 2>;
+                : xv == 3 ? presmooth_restrict_u4_kernel<8, 4, false>
+                : xv == 4 ? presmooth_restrict_u4_kernel<16, 2, false>
+                          : presmooth_restrict_u4_kernel<8, 4, true>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo,
                        (int)cg->n[0], cg->plane, s.cx, s.cy, s.cz, s.cc, omega, b, xout, bc, skip);
     PB_HIP(hipGetLastError());
