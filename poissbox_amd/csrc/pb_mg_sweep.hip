@@ -951,22 +951,17 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_xch_kernel(
 // A chunk runs a whole number of four-plane steps (up to three planes more than it needs; they
 // store nothing). Same operations on the same operands: bit-identical.
 // ---------------------------------------------------------------------------------------------
-template <int NW, int TY, bool EDGE>
+template <int NW, int TY>
 __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
     double omega, const double* __restrict__ b, double* __restrict__ xout,
     double* __restrict__ bc, const int* skip) {
   static_assert(TY % 2 == 0 && TY >= 2, "whole coarse rows per wave");
   constexpr int RB = NW * TY;
-  // EDGE: the block's first and last waves also form the red values of the rows just outside
-  // the block (one more b row each), so the block loses two rows at each end instead of four
-  constexpr int LO = EDGE ? 2 : 4;  // first stored block row
+  constexpr int LO = 4;  // first stored block row
   constexpr int SB = RB - 2 * LO;
   constexpr int NCR = TY / 2;
-  // as presmooth_restrict_xch_kernel's; (EDGE) xe: the red values of the first and the last
-  // wave's edge rows
-  __shared__ double xch[2][8][NW][64];
-  __shared__ double xe[2][2][64];
+  __shared__ double xch[2][8][NW][64];  // as presmooth_restrict_xch_kernel's
   if (skip && *skip) return;
   const double icc = 1.0 / cc;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -996,8 +991,6 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     const int brow = br0 + r;
     if (brow >= LO && brow < RB - LO && g0 + brow < ny) row_ok |= 1u << r;
   }
-  const int er = wid == 0 ? -1 : TY;  // edge row (used by the first and the last wave)
-  const int64_t roe = (int64_t)wrap(j0 + er, ny) * nx;
   const unsigned boff = (unsigned)ip * 8u;
   auto rix = [&](int64_t row) { return RowIx{row, boff}; };
   // planes up to a few steps past the chunk (the last step's spare planes): any distance
@@ -1010,13 +1003,7 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
   // element holding the red point of own row r on a plane of parity P (pair origin i even, row
   // origin j0 even, k0 = 0): presmooth_restrict_kernel's ((i + j) & 1) + kpar != 0
   auto red_e = [](int r, int P) { return (r + P) & 1; };
-  auto ldedge = [&](double (&dst)[2], int kk) {
-    if constexpr (EDGE) load_row<2>(b, rix((int64_t)wrapk(kk) * g.plane + roe), dst);
-  };
-  auto rededge = [&](int P, const double (&v)[2]) -> double {  // the edge row's red value
-    const double t = (((er + P) & 1) ? v[1] : v[0]) - 0.0;
-    return (1.0 - omega) * 0.0 + omega * (t * icc);
-  };
+
   auto redv = [&](auto Pc, const double (&v)[TY][2], double (&red)[TY]) {
     constexpr int P = decltype(Pc)::value;
 #pragma unroll
@@ -1056,27 +1043,17 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
   double X[2][TY];     // residual x sums: planes k-1, k at slots Q, Q+1
   double H[2][2];      // red values of rows -1 / TY: planes k+1, k+2 at slots Q, Q+1
   double accA[NCR], accB[NCR];
-  double ev2[2], ev1[2];  // edge rows of planes kb-2, kb-1
   ldraw(B[3], kb - 3);
   redv(std::integral_constant<int, 1>{}, B[3], R[0]);  // planes kb-3 (odd), kb-2, kb-1
   ldraw(B[1], kb - 2);
-  ldedge(ev2, kb - 2);
   redv(std::integral_constant<int, 0>{}, B[1], R[1]);
   ldraw(B[2], kb - 1);
-  ldedge(ev1, kb - 1);
   redv(std::integral_constant<int, 1>{}, B[2], R[2]);
   xch[1][0][wid][lane] = R[1][0];
   xch[1][1][wid][lane] = R[1][TY - 1];
   __syncthreads();
   H[0][0] = xch[1][1][wm][lane];
   H[0][1] = xch[1][0][wp][lane];
-  if constexpr (EDGE) {
-    if (wid == 0) H[0][0] = rededge(0, ev2);
-    if (wid == NW - 1) H[0][1] = rededge(0, ev2);
-    const double v = rededge(1, ev1);
-    if (wid == 0) xe[0][0][lane] = v;
-    if (wid == NW - 1) xe[0][1][lane] = v;
-  }
   xch[0][0][wid][lane] = R[2][0];
   xch[0][1][wid][lane] = R[2][TY - 1];
 #pragma unroll
@@ -1106,19 +1083,12 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     double (&rh1)[2] = H[Q & 1];
     double (&rh2)[2] = H[(Q + 1) & 1];
     ldraw(raw, k + 3);
-    double rawe[2];
-    ldedge(rawe, k + 3);
     __syncthreads();
     double sh[2][2], sxh[2];
     {
       constexpr int rp = KP ^ 1;  // written by plane k-1
-      if constexpr (EDGE) {  // the edge waves' own edge rows
-        rh2[0] = wid == 0 ? xe[rp][0][lane] : xch[rp][1][wm][lane];
-        rh2[1] = wid == NW - 1 ? xe[rp][1][lane] : xch[rp][0][wp][lane];
-      } else {
-        rh2[0] = xch[rp][1][wm][lane];
-        rh2[1] = xch[rp][0][wp][lane];
-      }
+      rh2[0] = xch[rp][1][wm][lane];
+      rh2[1] = xch[rp][0][wp][lane];
       sh[0][0] = xch[rp][4][wm][lane];
       sh[0][1] = xch[rp][5][wm][lane];
       sh[1][0] = xch[rp][2][wp][lane];
@@ -1200,11 +1170,6 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     redv(std::integral_constant<int, KP ^ 1>{}, raw, rn);  // plane k+3
     xch[KP][0][wid][lane] = rn[0];
     xch[KP][1][wid][lane] = rn[TY - 1];
-    if constexpr (EDGE) {
-      const double v = rededge(KP ^ 1, rawe);
-      if (wid == 0) xe[KP][0][lane] = v;
-      if (wid == NW - 1) xe[KP][1][lane] = v;
-    }
   };
 #pragma unroll 1
   for (int k = kb - 3; k <= ke + 1; k += 4) {
@@ -1495,7 +1460,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PB_POS
 // advance by NW TY - 4 rows. Same operations on the same operands as post_sweep_kernel (the
 // prolongation's per-coarse-row x stage, the half-sweeps' operand order): bit-identical.
 // ---------------------------------------------------------------------------------------------
-template <bool SUMS, int NW, int TY, int PF>
+template <bool SUMS, int NW, int TY>
 __global__ __launch_bounds__(64 * NW) void post_sweep_xch_kernel(
     Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
     const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
@@ -1714,20 +1679,13 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_xch_kernel(
       if constexpr (SUMS) bm1[r] = b01[r] = 0.0;
     }
     shp[0] = shp[1] = 0.0;
-    // loads of one iteration: x_s and coarse values of plane k+2, b of plane k+1. PF = 2: issued
-    // one iteration earlier, into the other of two register sets (the loop is unrolled by two,
-    // so the sets swap roles without register copies, which would wait for the loads)
+    // loads of one iteration: x_s and coarse values of plane k+2, b of plane k+1
     struct Ld {
       double x[TY][2], cv[2][NC], b[TY][2];
     };
-    auto step = [&](int k, Ld& cur, Ld& nxt) {
-      if constexpr (PF == 1) {
-        ldx(cur.x, cur.cv, k + 2);
-        ldb(cur.b, k + 1);
-      } else {
-        ldx(nxt.x, nxt.cv, k + 3);
-        ldb(nxt.b, k + 2);
-      }
+    auto step = [&](int k, Ld& cur) {
+      ldx(cur.x, cur.cv, k + 2);
+      ldb(cur.b, k + 1);
       __syncthreads();
       {
         const int rp = (k - 1) & 1;
@@ -1771,22 +1729,9 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_xch_kernel(
 #pragma unroll
         for (int e = 0; e < 2; ++e) xq1[r + 1][e] = cur.x[r][e];
     };
-    int k = kb - 2;
-    if constexpr (PF == 1) {
-      Ld A;
+    Ld A;
 #pragma unroll 1
-      for (; k < ke; ++k) step(k, A, A);
-    } else {
-      Ld A, B;
-      ldx(A.x, A.cv, kb);
-      ldb(A.b, kb - 1);
-#pragma unroll 1
-      for (; k + 1 < ke; k += 2) {
-        step(k, A, B);
-        step(k + 1, B, A);
-      }
-      if (k < ke) step(k, A, B);
-    }
+    for (int k = kb - 2; k < ke; ++k) step(k, A);
     half2(ke - 1, s1[0], s1[1], s1[2], shp, xm, bm, bm1);
   }
   if constexpr (SUMS) block_partials<4>(acc, parts);
@@ -2007,10 +1952,8 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
       double (&xq2)[TY + 2][2] = XQ[(Q + 1) & 1];
       double (&xm)[TY] = XM[Q & 1];
       double (&x0)[TY] = XM[(Q + 1) & 1];
-      double (&bm)[TY] = BB[Q & 1];
-      double (&b0)[TY] = BB[(Q + 1) & 1];
+      double (&bm)[TY] = BB[Q & 1];  // (plane k's sits in the other slot until the next copy)
       double (&bm1)[SUMS ? TY : 1] = BB1[Q & 1];
-      double (&b01)[SUMS ? TY : 1] = BB1[(Q + 1) & 1];
       double (&shp)[2] = SH[Q & 1];
       double (&shc)[2] = SH[(Q + 1) & 1];
       // plane k+2 = kb + 4m + Q: even (Q even) -> near K, far K-1; odd -> near K, far K+1 (new),
@@ -2147,17 +2090,15 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
   geo.split = 0;
   geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
   PostGeo cgeo{(int)cg->n[0], (int)cg->n[1], (int)cg->nzl, cg->plane};
-  // rows shared through LDS (post_sweep_xch_kernel): 1 = 8 waves x 4 rows, 2 = 16 x 2, 3 = 8 x 2;
-  // 4 .. 6: the same with the loads issued one iteration earlier (two register sets); 7 .. 9:
-  // the plane loop unrolled by four (post_sweep_u4_kernel: 8 x 4, 16 x 2, 8 x 2; its compile-time
-  // colours assume k0 = 0 and even chunk starts)
-  const int xv = env_int("PB_POSTX", 1);
-  if (xv >= 1 && xv <= 9) {
-    const int nw = (xv == 2 || xv == 5 || xv == 8) ? 16 : 8;
-    const int ty = (xv == 1 || xv == 4 || xv == 7) ? 4 : 2;
+  // rows shared through LDS: 1, 2 = post_sweep_xch_kernel with 8 waves x 4 / x 2 rows; 3, 4 = the
+  // same with the plane loop unrolled by four (post_sweep_u4_kernel; compile-time colours: k0 = 0,
+  // chunk starts at multiples of 4); 0 = the per-wave kernel below
+  const int xv = env_int("PB_POSTX", 4);
+  if (xv >= 1 && xv <= 4) {
+    const int nw = 8, ty = (xv & 1) ? 4 : 2;
     geo.ntile = (geo.ny + nw * ty - 5) / (nw * ty - 4);
     const int columns = geo.nseg * geo.ntile;
-    const int target = env_int("PB_POSTX_WGCU", 4) * g->ctx->num_cus;
+    const int target = env_int("PB_POSTX_WGCU", 8) * g->ctx->num_cus;
     int nchunk = std::max(1, (target + columns - 1) / columns);
     nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_POSTX_MINZ", 16)));
     geo.kc = (geo.nzl + nchunk - 1) / nchunk;
@@ -2167,26 +2108,15 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     if (sums_st && nblocks * 4 > g->ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
                        (long long)nblocks);
-    decltype(&post_sweep_xch_kernel<true, 8, 4, 1>) kern;
-#define PB_POSTX_KERN(NW_, TY_, PF_) \
-  (sums_st ? post_sweep_xch_kernel<true, NW_, TY_, PF_> : post_sweep_xch_kernel<false, NW_, TY_, PF_>)
-    switch (xv) {
-      case 1: kern = PB_POSTX_KERN(8, 4, 1); break;
-      case 2: kern = PB_POSTX_KERN(16, 2, 1); break;
-      case 3: kern = PB_POSTX_KERN(8, 2, 1); break;
-      case 4: kern = PB_POSTX_KERN(8, 4, 2); break;
-      case 5: kern = PB_POSTX_KERN(16, 2, 2); break;
-      case 6: kern = PB_POSTX_KERN(8, 2, 2); break;
-#define PB_POSTU_KERN(NW_, TY_) \
-  (sums_st ? post_sweep_u4_kernel<true, NW_, TY_> : post_sweep_u4_kernel<false, NW_, TY_>)
-      case 7: kern = PB_POSTU_KERN(8, 4); break;
-      case 8: kern = PB_POSTU_KERN(16, 2); break;
-      default: kern = PB_POSTU_KERN(8, 2); break;
-    }
-#undef PB_POSTX_KERN
-#undef PB_POSTU_KERN
-    if (xv >= 7 && g->k0 != 0)
+    if (xv >= 3 && g->k0 != 0)
       return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: one rank only");
+    decltype(&post_sweep_u4_kernel<true, 8, 4>) kern;
+    if (sums_st)
+      kern = xv == 1 ? post_sweep_xch_kernel<true, 8, 4> : xv == 2 ? post_sweep_xch_kernel<true, 8, 2>
+           : xv == 3 ? post_sweep_u4_kernel<true, 8, 4> : post_sweep_u4_kernel<true, 8, 2>;
+    else
+      kern = xv == 1 ? post_sweep_xch_kernel<false, 8, 4> : xv == 2 ? post_sweep_xch_kernel<false, 8, 2>
+           : xv == 3 ? post_sweep_u4_kernel<false, 8, 4> : post_sweep_u4_kernel<false, 8, 2>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo, cgeo,
                        s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout, sums_st,
                        sums_st ? g->ctx->d_partials : (double*)nullptr, skip);
@@ -2224,15 +2154,13 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
   sweep2_geo(g, geo);
   geo.split = 0;
   geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
-  // rows shared through LDS (presmooth_restrict_xch_kernel): 1 = 8 waves x 4 rows, 2 = 16 x 2
-  // (16 x 4 would need more than the 128 VGPRs a 1024-thread block can have); 3, 4: the same with
-  // the plane loop unrolled by four (presmooth_restrict_u4_kernel; its compile-time colours
-  // assume k0 = 0, which one rank has)
-  const int xv = env_int("PB_PRRX", 1);
-  if (xv >= 1 && xv <= 5) {
-    const int nw = (xv & 1) ? 8 : 16, ty = (xv & 1) ? 4 : 2;
-    const int sb = nw * ty - (xv == 5 ? 4 : 8);  // 5: u4 8 x 4 with the edge rows' red values
-    geo.ntile = (geo.ny + sb - 1) / sb;
+  // rows shared through LDS: 1 = presmooth_restrict_xch_kernel, 2 = the same with the plane loop
+  // unrolled by four (presmooth_restrict_u4_kernel; compile-time colours: k0 = 0, even chunk
+  // starts), both 8 waves x 4 rows; 0 = the per-wave kernel below
+  const int xv = env_int("PB_PRRX", 2);
+  if (xv == 1 || xv == 2) {
+    constexpr int nw = 8, ty = 4;
+    geo.ntile = (geo.ny + nw * ty - 9) / (nw * ty - 8);
     const int columns = geo.nseg * geo.ntile;
     const int target = env_int("PB_PRRX_WGCU", 4) * g->ctx->num_cus;
     int nchunk = std::max(1, (target + columns - 1) / columns);
@@ -2242,11 +2170,7 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
     const int64_t nblocks = (int64_t)columns * geo.nchunk;
     if (g->k0 != 0) return set_error(PB_ERR_UNSUPPORTED, "fused restriction: one rank only");
-    auto kern = xv == 1   ? presmooth_restrict_xch_kernel<8, 4>
-                : xv == 2 ? presmooth_restrict_xch_kernel<16, 2>
-                : xv == 3 ? presmooth_restrict_u4_kernel<8, 4, false>
-                : xv == 4 ? presmooth_restrict_u4_kernel<16, 2, false>
-                          : presmooth_restrict_u4_kernel<8, 4, true>;
+    auto kern = xv == 1 ? presmooth_restrict_xch_kernel<nw, ty> : presmooth_restrict_u4_kernel<nw, ty>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo,
                        (int)cg->n[0], cg->plane, s.cx, s.cy, s.cz, s.cc, omega, b, xout, bc, skip);
     PB_HIP(hipGetLastError());
