@@ -17,8 +17,8 @@ for c in "${CFGS[@]}"; do
   rc=$?; echo "solve [$c] rc=$rc"; cut -c1-420 gpurun_out/prrx_solve_$i.jsonl; [ $rc -eq 0 ] || exit $rc
   i=$((i+1))
 done
-if [ -n "${MG_TRACE:-}" ]; then
+if [ -n "${MG_TRACE:-}" ]; then  # kernel trace of the default V-cycle
   R=$(pwd)
-  (cd /tmp && export TMPDIR=/tmp && PB_TUNE_ROUNDS=1 PB_TUNE_CONFIGS="[{\"PB_PRRX\":\"3\",\"PB_POSTX\":\"${MG_TRACE}\"}]" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/mgtrace -o mg --output-format csv -- python3 $R/scripts/tune_mg.py > $R/gpurun_out/mgtrace.jsonl 2> $R/gpurun_out/mgtrace.err)
+  (cd /tmp && export TMPDIR=/tmp && PB_TUNE_ROUNDS=1 PB_TUNE_CONFIGS="[{}]" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/mgtrace -o mg --output-format csv -- python3 $R/scripts/tune_mg.py > $R/gpurun_out/mgtrace.jsonl 2> $R/gpurun_out/mgtrace.err)
   rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
