@@ -2098,9 +2098,13 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     const int nw = 8, ty = (xv & 1) ? 4 : 2;
     geo.ntile = (geo.ny + nw * ty - 5) / (nw * ty - 4);
     const int columns = geo.nseg * geo.ntile;
+    // z-chunks: every chunk re-reads two planes and runs up to five spare ones, so chunks stay
+    // >= 64 planes where the grid has 512 (measured: 0.733 -> 0.700 ms at 512^3 against 16) and
+    // >= nz / 8 on shallower grids, which need the workgroups
     const int target = env_int("PB_POSTX_WGCU", 8) * g->ctx->num_cus;
     int nchunk = std::max(1, (target + columns - 1) / columns);
-    nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_POSTX_MINZ", 16)));
+    const int minz = std::min(env_int("PB_POSTX_MINZ", 64), std::max(16, geo.nzl / 8));
+    nchunk = std::min(nchunk, std::max(1, geo.nzl / minz));
     geo.kc = (geo.nzl + nchunk - 1) / nchunk;
     geo.kc = (geo.kc + 3) & ~3;  // chunk starts at multiples of 4 (the unrolled kernels' parities)
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
@@ -2162,8 +2166,16 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     constexpr int nw = 8, ty = 4;
     geo.ntile = (geo.ny + nw * ty - 9) / (nw * ty - 8);
     const int columns = geo.nseg * geo.ntile;
-    const int target = env_int("PB_PRRX_WGCU", 4) * g->ctx->num_cus;
-    int nchunk = std::max(1, (target + columns - 1) / columns);
+    // z-chunks: each chunk forms red, black and residual values on five planes outside it, and
+    // the passes are latency-bound at two waves per SIMD, so (measured at 512^3, one box) few long
+    // chunks at most one workgroup per CU win (2 chunks of 256 planes, 220 workgroups: 0.503 ms)
+    // over many (10 of 52, 1100 workgroups: 0.566 ms) -- while a count just above one per CU
+    // leaves some CUs two workgroups (3 chunks of 172, 330 workgroups: 0.685 vs 0.609 on another
+    // box). So: at most one workgroup per CU when that keeps chunks of >= PB_PRRX_LONGZ planes,
+    // else ~4 per CU (256^3 and smaller grids)
+    int nchunk = std::max(1, g->ctx->num_cus / columns);
+    if (geo.nzl / nchunk < env_int("PB_PRRX_LONGZ", 128))
+      nchunk = std::max(1, (env_int("PB_PRRX_WGCU", 4) * g->ctx->num_cus + columns - 1) / columns);
     nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_PRRX_MINZ", 16)));
     geo.kc = (geo.nzl + nchunk - 1) / nchunk;
     geo.kc += geo.kc & 1;
