@@ -2093,7 +2093,7 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
   // rows shared through LDS: 1, 2 = post_sweep_xch_kernel with 8 waves x 4 / x 2 rows; 3, 4 = the
   // same with the plane loop unrolled by four (post_sweep_u4_kernel; compile-time colours: k0 = 0,
   // chunk starts at multiples of 4); 0 = the per-wave kernel below
-  const int xv = env_int("PB_POSTX", 4);
+  const int xv = env_int("PB_POSTX", 3);
   if (xv >= 1 && xv <= 4) {
     const int nw = 8, ty = (xv & 1) ? 4 : 2;
     geo.ntile = (geo.ny + nw * ty - 5) / (nw * ty - 4);
