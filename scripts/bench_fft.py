@@ -1,5 +1,5 @@
 """Spectral PC apply time (pb_ksp_pc_apply, -pc_type fft) per grid; one JSON line per grid with
-the knobs in the environment (PB_FFT_TL_X / _Y / _Z). usage: python scripts/bench_fft.py [n ...]"""
+the knobs in the environment (PB_FFT_TL_X / _Y / _Z). usage: python scripts/bench_fft.py [n | nx x ny x nz ...]"""
 import json
 import os
 import sys
@@ -12,11 +12,12 @@ import poissbox_amd as pb  # noqa: E402
 
 
 def main():
-    sizes = [int(a) for a in sys.argv[1:]] or [512]
+    sizes = sys.argv[1:] or ["512"]
     ctx = pb.Context(0)
-    for n in sizes:
-        n3 = (n, n, n)
-        h = (2 * np.pi / n,) * 3
+    for arg in sizes:
+        n3 = tuple(int(v) for v in arg.split("x")) if "x" in arg else (int(arg),) * 3
+        n = n3[0] if len(set(n3)) == 1 else "x".join(map(str, n3))
+        h = tuple(2 * np.pi / m for m in n3)
         da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
         P = pb.Mat(da, pb.COMPACT, h)
         k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
@@ -44,7 +45,8 @@ def main():
                 passes[nm] = round(t / c, 4)
         ctx.set_timing(False)
         cfg = {kk: v for kk, v in os.environ.items() if kk.startswith(("PB_FFT", "PB_LINES"))}
-        print(json.dumps({"n": n, "pc_apply_ms": ms, "GBps_80B": 80 * n ** 3 / ms / 1e6,
+        ndof = n3[0] * n3[1] * n3[2]
+        print(json.dumps({"n": n, "pc_apply_ms": ms, "GBps_80B": 80 * ndof / ms / 1e6,
                           "passes_ms": passes, "cfg": cfg}), flush=True)
         for o in (k, r, z, P):
             o.destroy()
