@@ -50,6 +50,7 @@ struct DhtPass {
   const double* in;   // tile source (X forward: r), else == out
   double* out;
   int64_t li, lo, es;  // element e of line (outer, inner) at outer*lo + inner*li + e*es
+  int64_t lo_out;      // the output's outer stride (Y passes into / out of the padded buffer)
   int ninner, nouter, ntiles_inner;
   const double* w;    // twiddles of the line axis: (re, im) of exp(-2 pi i k / n), k < n
   const double* tab;  // [Lx | Jx | Ly | Jy | Lz | Jz] (SCALE only)
@@ -57,6 +58,8 @@ struct DhtPass {
   double scale, thr;  // 1 / (nx ny nz) and the null-mode threshold (SCALE only)
   int remap;          // XCD-aware tile order (PB_FFT_REMAP, default on): consecutive tiles share an
                       // XCD; Z pass 1.35-1.36 vs 1.375-1.378 ms at 512^3 (ab_remap_fft.jsonl)
+  int order;          // strided passes: 0 = consecutive tiles are x-adjacent (same outer row),
+                      // 1 = consecutive tiles walk the outer rows (PB_FFT_ZORDER / _YORDER)
   // CG's residual sums taken by the last pass (X inverse) as it writes z: t = z - mu, over the
   // tile, against r = sr -> parts[block * 4 + (t, t^2, t r, r)] (cg_pc_sums_kernel's sums)
   const double* sr;
@@ -484,8 +487,13 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
   // tile t: lines [inner0, inner0 + nl) of row `outer`
   const int ntiles = p.ntiles_inner * p.nouter;
   auto tile_of = [&](int t, int64_t& outer, int& inner0, int& nl, int64_t& base) {
-    outer = t / p.ntiles_inner;
-    inner0 = (t % p.ntiles_inner) * TL;
+    if (p.order) {
+      outer = t % p.nouter;
+      inner0 = (t / p.nouter) * TL;
+    } else {
+      outer = t / p.ntiles_inner;
+      inner0 = (t % p.ntiles_inner) * TL;
+    }
     nl = min(TL, p.ninner - inner0);  // even: every extent is
     base = outer * p.lo + (int64_t)inner0 * p.li;
   };
@@ -624,7 +632,7 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
           v.x = lds[l * LP + lpad(e)];
           v.y = lds[l * LP + lpad(e + 1)];
         }
-        const int64_t a = base + l * p.li + e * p.es;
+        const int64_t a = base + outer * (p.lo_out - p.lo) + l * p.li + e * p.es;
         if (PB_FFT_ABLATE_TRAFFIC) {
           if (v.x == 12345.678) p.out[a] = v.y;  // keeps the LDS reads (never true on real data)
           continue;
@@ -969,6 +977,14 @@ struct FftPc {
   double* tw[3] = {nullptr, nullptr, nullptr};
   double* tab = nullptr;
   double* ybuf = nullptr;  // split grids: one y-slab field + the transpose aux space
+  // one rank: the Y forward pass writes into zbuf, whose planes are `zplane` = nx ny + PB_FFT_ZPAD
+  // (default 32) doubles apart, the Z pass runs there and the Y inverse pass reads it back: the Z
+  // pass's elements are then not 2^k bytes apart (512^3: 2 MiB), which measured 13-23 % slower per
+  // DoF than 1.5 / 2.5 MiB (profiles/r03/fft_plane_stride.jsonl). Z pass 0.649 -> 0.502 ms at
+  // 512^3, 6.75 -> 6.21 ms at 1024^3 (fft_zpad.jsonl; a 16 KiB pad measured 0.99 ms: not every
+  // pad breaks the aliasing)
+  double* zbuf = nullptr;
+  int64_t zplane = 0;
   double thr = 0.0;
 };
 
@@ -1065,6 +1081,15 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
       delete f;
       return set_error(PB_ERR_ALLOC, "fft pc y-slab buffer: out of device memory");
     }
+  } else if (const int64_t pad = env_int("PB_FFT_ZPAD", 32);
+             pad > 0 && g->plane >= env_int("PB_FFT_ZPAD_MIN_PLANE", 512 * 512)) {
+    // (256^3, 512 KiB planes: no gain, 0.079 -> 0.083 ms; so only from 2 MiB planes up)
+    f->zplane = g->plane + pad;
+    if (hipMalloc(&f->zbuf, (size_t)(f->zplane * g->nzl) * sizeof(double)) != hipSuccess) {
+      (void)hipFree(f->dev);
+      delete f;
+      return set_error(PB_ERR_ALLOC, "fft pc padded buffer: out of device memory");
+    }
   }
   *out = f;
   return PB_OK;
@@ -1074,7 +1099,8 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
 static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, const double* in,
                     double* out, const int* skip, int j0 = 0, const double* sr = nullptr,
                     const CgState* st = nullptr, int* np = nullptr,
-                    const RUpdate* ru = nullptr) {
+                    const RUpdate* ru = nullptr, int64_t pl_in = 0, int64_t pl_out = 0) {
+  // pl_in / pl_out: plane strides of in / out (0: nx ny; the Y and Z passes of the padded buffer)
   static const char* names[3] = {"pc_fft_x", "pc_fft_y", "pc_fft_z"};
   ScopedTimer tm(ctx, names[axis]);
   DhtPass p{};
@@ -1089,6 +1115,7 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   if (axis == 0) {  // contiguous lines: inner = j, outer = k
     p.li = nx;
     p.lo = nx * ny;
+    p.lo_out = p.lo;
     p.es = 1;
     p.ninner = (int)ny;
     p.nouter = (int)nz;
@@ -1112,18 +1139,22 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   }
   if (axis == 1) {  // inner = i, outer = k, elements along j
     p.li = 1;
-    p.lo = nx * ny;
+    p.lo = pl_in ? pl_in : nx * ny;
+    p.lo_out = pl_out ? pl_out : nx * ny;
     p.es = nx;
     p.ninner = (int)nx;
     p.nouter = (int)nz;
+    p.order = env_int("PB_FFT_YORDER", 0);
     return launch_dht<0, 0>(ctx, ny, p, skip);
   }
   // axis 2 with the scaling: inner = i, outer = j, elements along k
   p.li = 1;
   p.lo = nx;
-  p.es = nx * ny;
+  p.lo_out = nx;
+  p.es = pl_in ? pl_in : nx * ny;  // in place: pl_out == pl_in
   p.ninner = (int)nx;
   p.nouter = (int)ny;
+  p.order = env_int("PB_FFT_ZORDER", 0);
   p.tab = f->tab;
   p.nx = (int)f->g->n[0];
   p.ny = (int)f->g->n[1];
@@ -1147,19 +1178,28 @@ int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgS
   ScopedTimer tm(ctx, "pc_fft");
   const int64_t b[3] = {g->n[0], g->n[1], g->nzl};
   PB_TRY(dht_axis(ctx, f, b, 0, r, z, skip, 0, nullptr, nullptr, nullptr, ru));
-  PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
-  if (!grid_split(g)) {
-    PB_TRY(dht_axis(ctx, f, b, 2, z, z, skip));
+  if (f->zbuf) {  // Y forward into the padded buffer, Z there, Y inverse back into z
+    PB_TRY(dht_axis(ctx, f, b, 1, z, f->zbuf, skip, 0, nullptr, nullptr, nullptr, nullptr, 0,
+                    f->zplane));
+    PB_TRY(dht_axis(ctx, f, b, 2, f->zbuf, f->zbuf, skip, 0, nullptr, nullptr, nullptr, nullptr,
+                    f->zplane, f->zplane));
+    PB_TRY(dht_axis(ctx, f, b, 1, f->zbuf, z, skip, 0, nullptr, nullptr, nullptr, nullptr,
+                    f->zplane, 0));
   } else {
-    YSlabPlan yp;
-    double* fy = f->ybuf;
-    PB_TRY(yslab_begin(g, fy + yslab_len(g), &yp));
-    PB_TRY(yslab_to(g, yp, z, fy));
-    const int64_t by[3] = {g->n[0], yp.ny_me, g->n[2]};
-    PB_TRY(dht_axis(ctx, f, by, 2, fy, fy, skip, (int)yp.j0[ctx->rank]));
-    PB_TRY(yslab_from(g, yp, fy, z));
+    PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
+    if (!grid_split(g)) {
+      PB_TRY(dht_axis(ctx, f, b, 2, z, z, skip));
+    } else {
+      YSlabPlan yp;
+      double* fy = f->ybuf;
+      PB_TRY(yslab_begin(g, fy + yslab_len(g), &yp));
+      PB_TRY(yslab_to(g, yp, z, fy));
+      const int64_t by[3] = {g->n[0], yp.ny_me, g->n[2]};
+      PB_TRY(dht_axis(ctx, f, by, 2, fy, fy, skip, (int)yp.j0[ctx->rank]));
+      PB_TRY(yslab_from(g, yp, fy, z));
+    }
+    PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
   }
-  PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
   // with sums_st: the residual sums of CG (PB_FFT_SUMS, default on) are taken by the last pass
   static const int fused = env_int("PB_FFT_SUMS", 1);
   if (sums_st && nparts && fused) return dht_axis(ctx, f, b, 0, z, z, skip, 0, r, sums_st, nparts);
@@ -1171,6 +1211,7 @@ void fftpc_destroy(FftPc* f) {
   (void)wait_stream(f->g->ctx, f->g->ctx->stream, "fftpc_destroy");
   if (f->dev) (void)hipFree(f->dev);
   if (f->ybuf) (void)hipFree(f->ybuf);
+  if (f->zbuf) (void)hipFree(f->zbuf);
   delete f;
 }
 

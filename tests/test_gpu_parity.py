@@ -1095,6 +1095,31 @@ def test_fft_pc_apply_vs_oracle(ctx, n3, compact):
     k.destroy()
 
 
+@pytest.mark.parametrize("pad", [1, 512, 65536])
+@pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 256), (96, 96, 96), (64, 64, 512),
+                                (512, 32, 64)])
+def test_fft_pc_padded_z_buffer_bit_identical(ctx, monkeypatch, n3, pad):
+    """PB_FFT_ZPAD: the Y forward pass writes a buffer with padded planes, the Z pass runs there
+    and the Y inverse pass reads it back; the same operations on the same values, so the PC
+    apply is bit-identical to the in-place passes (and so within the oracle bar)."""
+    N = int(np.prod(n3))
+    h, kind = _fft_case(n3, True)
+    r = O.fill_random(N, 23)
+    outs = []
+    for zp in ("0", str(pad)):
+        monkeypatch.setenv("PB_FFT_ZPAD", zp)
+        monkeypatch.setenv("PB_FFT_ZPAD_MIN_PLANE", "0")
+        da = pb.DA(ctx, n3)
+        P = pb.Mat(da, kind, h)
+        k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
+        rv, zv = pb.Vec(da), pb.Vec(da)
+        rv.set_values(r)
+        k.pc_apply(rv, zv)
+        outs.append(zv.get_values())
+        k.destroy()
+    assert np.array_equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 128), (512, 64, 64)])
 def test_cg_fft_pc_matches_oracle(ctx, n3, compact):
