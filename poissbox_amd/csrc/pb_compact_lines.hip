@@ -557,7 +557,7 @@ __device__ __forceinline__ void x_direct_line(const LinePass& p, int64_t line, d
 template <int C, bool DOT = false>
 __global__ __launch_bounds__(256) void compact_lines_x_direct(LinePass p, int64_t nlines) {
   if (p.skip && *p.skip) return;
-  constexpr int LP = Lds<C>::LP, CP = Lds<C>::CP;
+  constexpr int LP = Lds<C>::LP;
   __shared__ double strip[4][2 * LP];
   __shared__ double red[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;

@@ -754,6 +754,27 @@ def test_pc_apply_bit_exact(ctx, monkeypatch, kern, pc, n3, levels):
     k.destroy()
 
 
+@pytest.mark.parametrize("m", [64, 128])
+def test_cg_compact_fft_padded_bit_identical(ctx, monkeypatch, m):
+    """Config 5's CG (compact A, spectral PC, fused passes) with the PC's padded Z buffer:
+    reason, iterations, history and x bit-identical to the unpadded run."""
+    n3 = (m, m, m)
+    h = (2 * np.pi / m,) * 3
+    b = O.lapl(O.fill_random(m ** 3, SEED), n3, h)
+    monkeypatch.setenv("PB_FFT_ZPAD_MIN_PLANE", "0")
+    res = []
+    for pad in ("0", "32"):
+        monkeypatch.setenv("PB_FFT_ZPAD", pad)
+        da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+        A = pb.Mat(da, pb.COMPACT, h)
+        x, bv = pb.Vec(da), pb.Vec(da)
+        bv.set_values(b)
+        reason, its, hist = pb.solve(A, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "1e-10"])
+        res.append((reason, its, np.asarray(hist), x.get_values()))
+    assert res[0][:2] == res[1][:2] and res[0][0] == 2
+    assert np.array_equal(res[0][2], res[1][2]) and np.array_equal(res[0][3], res[1][3])
+
+
 @pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("pc,n", [("sor", 32), ("mg", 32), ("mg", 64)])
 def test_cg_sor_mg_matches_oracle(ctx, monkeypatch, kern, pc, n):
