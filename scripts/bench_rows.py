@@ -42,6 +42,19 @@ def timed(ctx, fn, reps, name):
     return ms / max(cnt, 1)
 
 
+def gpu_wall(ctx, fn, reps):
+    """ms per call of a GPU op over `reps` back-to-back calls, host clock between two syncs (no
+    HIP events: at 256^3 the per-pass event records inside a multi-launch op added ~65 us per
+    call to the event-timed figure, profiles/r03/close2/rows.jsonl vs compact.jsonl)"""
+    fn()
+    ctx.sync()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    ctx.sync()
+    return (time.perf_counter() - t) * 1e3 / reps
+
+
 def wall(fn, reps):
     fn()
     t = time.perf_counter()
@@ -99,7 +112,7 @@ def main():
     A = pb.Mat(da, pb.STAR7)
     x, y = pb.Vec(da), pb.Vec(da)
     x.set_random(1)
-    ms = timed(ctx, lambda: A.mult(x, y), 20, "stencil")
+    ms = gpu_wall(ctx, lambda: A.mult(x, y), 50)
     n64 = (128, 128, 128)
     xs = O.fill_random(128 ** 3, 1)
     t1 = wall(lambda: O.stencil(xs, n64, (1 / 128,) * 3, faithful=True), 1)
@@ -149,7 +162,7 @@ def main():
         f, out = pb.Vec(da), pb.Vec(da)
         f.set_random(5)
         h = da.spacing
-        ms = timed(ctx, lambda: pb.compact_lapl_fast(da, h, f, out), 5, "compact_lapl_fast")
+        ms = gpu_wall(ctx, lambda: pb.compact_lapl_fast(da, h, f, out), 20)
         cpu = None
         if m == 256:
             fc = O.fill_random(64 ** 3, 5)
