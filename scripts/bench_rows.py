@@ -42,19 +42,6 @@ def timed(ctx, fn, reps, name):
     return ms / max(cnt, 1)
 
 
-def gpu_wall(ctx, fn, reps):
-    """ms per call of a GPU op over `reps` back-to-back calls, host clock between two syncs (no
-    HIP events: at 256^3 the per-pass event records inside a multi-launch op added ~65 us per
-    call to the event-timed figure, profiles/r03/close2/rows.jsonl vs compact.jsonl)"""
-    fn()
-    ctx.sync()
-    t = time.perf_counter()
-    for _ in range(reps):
-        fn()
-    ctx.sync()
-    return (time.perf_counter() - t) * 1e3 / reps
-
-
 def wall(fn, reps):
     fn()
     t = time.perf_counter()
@@ -112,7 +99,7 @@ def main():
     A = pb.Mat(da, pb.STAR7)
     x, y = pb.Vec(da), pb.Vec(da)
     x.set_random(1)
-    ms = gpu_wall(ctx, lambda: A.mult(x, y), 50)
+    ms = timed(ctx, lambda: A.mult(x, y), 20, "stencil")
     n64 = (128, 128, 128)
     xs = O.fill_random(128 ** 3, 1)
     t1 = wall(lambda: O.stencil(xs, n64, (1 / 128,) * 3, faithful=True), 1)
@@ -162,7 +149,7 @@ def main():
         f, out = pb.Vec(da), pb.Vec(da)
         f.set_random(5)
         h = da.spacing
-        ms = gpu_wall(ctx, lambda: pb.compact_lapl_fast(da, h, f, out), 20)
+        ms = timed(ctx, lambda: pb.compact_lapl_fast(da, h, f, out), 5, "compact_lapl_fast")
         cpu = None
         if m == 256:
             fc = O.fill_random(64 ** 3, 5)
