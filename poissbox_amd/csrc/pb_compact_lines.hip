@@ -98,28 +98,41 @@ static LineOp make_line_op(int kind, int C, double h) {
 }
 
 __device__ __forceinline__ double lane_shfl(double v, int src) { return __shfl(v, src & 63, 64); }
+// the wave rotations by one lane as DPP moves (VALU, no LDS round trip like __shfl's
+// ds_bpermute): lane l <- lane l-1 (lane 0 <- 63: wave_ror:1) / lane l+1 (lane 63 <- 0: wave_rol:1).
+// The same values as lane_shfl(v, lane -/+ 1), so the results do not change.
+template <int CTRL>
+__device__ __forceinline__ double lane_rot(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double lane_from_lower(double v) { return lane_rot<0x13C>(v); }
+__device__ __forceinline__ double lane_from_upper(double v) { return lane_rot<0x134>(v); }
 
 // d <- explicit RHS of x (stagger -1: cell -> vertex, +1: vertex -> cell), eval_1d_rhs order
 template <int C>
 __device__ __forceinline__ void line_rhs(const double (&x)[C], double (&d)[C], const LineOp& o,
                                          int stagger, int lane) {
   double xm2, xm1, xp0, xp1;  // x at local offsets -2, -1, C, C+1
-  xm1 = lane_shfl(x[C - 1], lane - 1);
-  xp0 = lane_shfl(x[0], lane + 1);
+  (void)lane;
+  xm1 = lane_from_lower(x[C - 1]);
+  xp0 = lane_from_upper(x[0]);
   if constexpr (C >= 2) {
     if (stagger < 0) {
-      xm2 = lane_shfl(x[C - 2], lane - 1);
+      xm2 = lane_from_lower(x[C - 2]);
       xp1 = 0.0;
     } else {
-      xp1 = lane_shfl(x[1], lane + 1);
+      xp1 = lane_from_upper(x[1]);
       xm2 = 0.0;
     }
   } else {
     if (stagger < 0) {
-      xm2 = lane_shfl(x[0], lane - 2);
+      xm2 = lane_from_lower(xm1);
       xp1 = 0.0;
     } else {
-      xp1 = lane_shfl(x[0], lane + 2);
+      xp1 = lane_from_upper(xp0);
       xm2 = 0.0;
     }
   }
@@ -148,18 +161,22 @@ __device__ __forceinline__ void line_solve(double (&d)[C], const LineOp& o, int 
 #pragma unroll
   for (int m = 1; m < C; ++m) d[m] = d[m] + mq * d[m - 1];
   double T = d[C - 1];
-  for (int s = 0; s < o.nsteps; ++s) T = T + o.gs[s] * lane_shfl(T, lane - (1 << s));
+  // the scan's distance-1 step and the carries as DPP rotations (chains of them for distances 2
+  // and 4 measured no faster than ds_bpermute, profiles/r03/compact_dpp_*.jsonl)
+  if (o.nsteps > 0) T = T + o.gs[0] * lane_from_lower(T);
+  for (int s = 1; s < o.nsteps; ++s) T = T + o.gs[s] * lane_shfl(T, lane - (1 << s));
   T *= o.corr;
-  double cin = lane_shfl(T, lane - 1);
+  double cin = lane_from_lower(T);
 #pragma unroll
   for (int m = 0; m < C; ++m) d[m] = d[m] + o.pw[m] * cin;
   // anti-causal sweep z_i = y_i - q z_{i+1}
 #pragma unroll
   for (int m = C - 2; m >= 0; --m) d[m] = d[m] + mq * d[m + 1];
   T = d[0];
-  for (int s = 0; s < o.nsteps; ++s) T = T + o.gs[s] * lane_shfl(T, lane + (1 << s));
+  if (o.nsteps > 0) T = T + o.gs[0] * lane_from_upper(T);
+  for (int s = 1; s < o.nsteps; ++s) T = T + o.gs[s] * lane_shfl(T, lane + (1 << s));
   T *= o.corr;
-  cin = lane_shfl(T, lane + 1);
+  cin = lane_from_upper(T);
 #pragma unroll
   for (int m = 0; m < C; ++m) d[m] = (d[m] + o.pw[C - 1 - m] * cin) * o.inv_kappa;
 }
