@@ -832,9 +832,10 @@ def test_cg_mg_fused_post_smoothing(ctx, monkeypatch, kern):
 # (PB_POSTX 1, 2 = 8 waves x 4 / x 2 rows; 3, 4 the same with the plane loop unrolled by four) and
 # the per-wave kernel (0); y extents that are no multiple of a block's stored rows (28 / 12), one
 # smaller than a block (8 rows: the block's rows wrap several times), four planes (the unrolled
-# kernels' spare planes wrap around the grid more than once), and the full-size test's 256^2
-# planes
-POSTX_SHAPES = [(256, 256, 32), (128, 40, 16), (256, 8, 8), (128, 96, 24), (256, 16, 4)]
+# kernels' spare planes wrap around the grid more than once), plane counts that are no multiple
+# of the unrolled loop's four (6, 12), and the full-size test's 256^2 planes
+POSTX_SHAPES = [(256, 256, 32), (128, 40, 16), (256, 8, 8), (128, 96, 24), (256, 16, 4),
+                (128, 24, 6), (256, 16, 12)]
 
 
 @pytest.mark.parametrize("postx", ["0", "1", "2", "3", "4"])
