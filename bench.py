@@ -204,6 +204,222 @@ def cpu_baseline(mode="full"):
             "host": info, "rows": rows, "skipped_rows": skipped, "variants": cpu_variants(T)}
 
 
+# Workloads measured by whole solves (--workload): a step is one KSPSolve to rtol 1e-10 from x0 = 0
+# (the solves take 1-13 iterations, so a fixed-iteration step would run past convergence).
+#   compact-fft: BASELINE config 5's operator -- the compact-scheme Laplacian as A = P
+#     (src/compact_schemes.f90:17-37, A != 7-point as src/poissbox.f90:226-228,294) -- with the
+#     spectral -pc_type fft that inverts its symbol (the substitute for the V-cycle of
+#     config 5's text, which cannot precondition the compact operator's Nyquist null modes);
+#     default strong scaling of 512^3 (config 5: 512^3 on 8 GPUs).
+#   star7-mg: the README's recommended solver shape (README.md:40-45, CG + multigrid with SOR
+#     smoothing) on the 7-point operator: -pc_type mg, geometric V(1,1) red-black SOR; weak scaling.
+# roofline: the kernel, its algorithmic bytes per owned DoF (N = 1 / N > 1: on a split grid MG's
+# post-smoothing runs as prolongation 17 + fused sweep 24) and a description.
+SOLVE_WORKLOADS = {
+    "compact-fft": {
+        "ops": ("compact", "compact"),
+        "argv": ["-ksp_type", "cg", "-pc_type", "fft", "-ksp_rtol", "1e-10"],
+        "scaling": "strong",
+        "roof": ("pc_fft_z", (16, 16),
+                 "pc_fft_z (spectral PC Z pass: forward FFT of z-lines, 1/(N lambda) of the compact "
+                 "symbol, inverse FFT; read + write 16 B/DoF; on N > 1 ranks on y-slabs)"),
+        # (the PC's X passes also carry CG's x / r update and residual sums: no fixed bytes)
+        "kernels": {"pc_fft_x": None, "pc_fft_y": 16, "pc_fft_z": 16, "compact_lines_x": None,
+                    "compact_lines_y": None, "compact_lines_z": None, "pc_fft": None,
+                    "alltoallv": None, "allreduce": None},
+        "describe": "fp64 CG, compact-scheme Laplacian A = P (src/compact_schemes.f90:17-37), "
+                    "spectral PC (-pc_type fft), rtol 1e-10",
+    },
+    "star7-mg": {
+        "ops": ("star7", "assembled"),
+        "argv": ["-ksp_type", "cg", "-pc_type", "mg", "-ksp_rtol", "1e-10"],
+        "scaling": "weak",
+        "roof": ("mg_fine_prolong_post", (25, 41),
+                 "mg_fine_prolong_post (finest level: prolongation + correction + both red-black "
+                 "SOR post-smoothing half-sweeps; 25 B/DoF fused on one rank, 17 + 24 on a split "
+                 "grid)"),
+        "kernels": {"mg_apply": None, "mg_fine_smooth_first": 17, "mg_fine_prolong_post": None,
+                    "mg_coarse_levels": None, "cg_pass_a": None, "cg_pass_b": None,
+                    "halo": None, "allreduce": None},
+        "describe": "fp64 CG + geometric multigrid V(1,1), red-black SOR smoothing "
+                    "(-pc_type mg), 7-pt periodic Laplacian, rtol 1e-10",
+    },
+}
+
+
+def cpu_solve_baseline(workload, budget_s=None, m=128):
+    """cpu_baseline of a solve workload: the oracle's restatement of the same KSPSolve (PETSc
+    KSPCG sequence + the same preconditioner) on a grid it finishes in seconds (128^3), repeated
+    for about budget_s (PB_CPU_BUDGET_S, default 20 s) on the GPU box's host cores."""
+    from oracle import oracle as O
+    info = host_info()
+    T = int(os.environ.get("PB_CPU_THREADS", info["usable_cores"]))
+    budget = budget_s or float(os.environ.get("PB_CPU_SOLVE_BUDGET_S", "20"))
+    n3 = (m, m, m)
+    N = m ** 3
+    h = (1.0 / m,) * 3
+    xt = O.fill_random(N, SEED)
+    if workload == "compact-fft":
+        b = O.lapl(xt, n3, h)
+        kw = dict(pc="fft", op="compact")
+        what = ("compact lapl in the reference's operation order (1 thread) + spectral PC "
+                f"(naive Hartley sums, OpenMP {T} threads)")
+    else:
+        b = O.stencil(xt, n3, h, nthreads=T)
+        kw = dict(pc="mg", nthreads=T)
+        what = "7-point CG + geometric MG V(1,1) red-black SOR (the pb_mg.hip restatement)"
+    kw.setdefault("nthreads", T)
+    solves, its_total, el = 0, 0, 0.0
+    reason = None
+    while el < budget or solves == 0:
+        t0 = time.perf_counter()
+        _, reason, its, _ = O.cg_solve(b, n3, h, rtol=1e-10, **kw)
+        el += time.perf_counter() - t0
+        solves += 1
+        its_total += its
+    return {"value": N * its_total / el, "unit": "DoF-updates/s", "cores": T, "kind": "port",
+            "solves_per_s": solves / el, "its_per_solve": its_total / solves,
+            "reason": reason, "host": info,
+            "sample": f"{m}^3 grid, {solves} solve(s) to rtol 1e-10 of oracle/pb_oracle.c "
+                      f"({what}; PETSc KSPCG sequence, constant null space) in {el:.1f} s on the "
+                      f"GPU box host"}
+
+
+def run_solve_workload(args, pb, ctx, da, n, rank, world, dist, comm_transport, comm_nranks,
+                       json_fd):
+    """One step = one KSPSolve to rtol 1e-10 (SOLVE_WORKLOADS). Timed region: K solves after W
+    warm-up solves, barrier + device sync on both sides, max over ranks. HIP events bracket only
+    the roofline kernel inside it; the other kernels are timed in one further solve."""
+    W = SOLVE_WORKLOADS[args.workload]
+    h = da.spacing
+    kinds = {"compact": pb.COMPACT, "star7": pb.STAR7, "assembled": pb.ASSEMBLED27}
+    A = pb.Mat(da, kinds[W["ops"][0]], h)
+    P = A if W["ops"][1] == W["ops"][0] else pb.Mat(da, kinds[W["ops"][1]], h)
+    x, b, xt = pb.Vec(da), pb.Vec(da), pb.Vec(da)
+    xt.set_random(SEED)      # synthetic x_true (SURVEY §8d), decomposition independent
+    A.mult(xt, b)            # b = A x_true (src/example.f90:70-72)
+    ksp = pb.KSP(A, P, pb.ksp_options(W["argv"]))
+    for _ in range(args.warmup):
+        ksp.solve(b, x)
+    roof, roof_bytes_np, roof_desc = W["roof"]
+    roof_bytes = roof_bytes_np[0] if world == 1 else roof_bytes_np[1]
+    ctx.sync()
+    ctx.barrier()
+    if dist:
+        dist.barrier()
+    os.environ["PB_TIMING_ONLY"] = roof
+    os.environ["PB_TIMING_EVERY"] = "1"
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    its_seen = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        reason, its, hist = ksp.solve(b, x)
+        its_seen.append(its)
+    ctx.sync()
+    t1 = time.perf_counter()
+    ctx.barrier()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    ms_roof, cnt_roof = ctx.timing(roof)
+    ctx.set_timing(False)
+    os.environ.pop("PB_TIMING_ONLY", None)
+    os.environ.pop("PB_TIMING_EVERY", None)
+    # diagnostics: one more solve with every phase timed
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    ksp.solve(b, x)
+    ctx.sync()
+    nloc = da.nlocal
+    kern = {}
+    comm = {"rank": rank, "device": ctx_device(ctx), "transport": comm_transport,
+            "comm_nranks": comm_nranks}
+    for nm, bpd in W["kernels"].items():
+        ms_, cnt_ = ctx.timing(nm)
+        if cnt_ == 0:
+            continue
+        row = {"avg_ms": ms_ / cnt_, "launches_per_solve": cnt_}
+        if bpd:
+            t_ = ms_ / cnt_ / 1e3
+            row.update(GBps=bpd * nloc / t_ / 1e9, frac=bpd * nloc / t_ / 1e9 / HBM_PEAK_GBS,
+                       bytes_per_dof=bpd)
+        kern[nm] = row
+        if nm in ("alltoallv", "allreduce", "halo", "halo_comm"):
+            comm[f"{nm}_ms_per_solve"] = ms_
+            comm[f"{nm}_calls"] = cnt_
+    ctx.set_timing(False)
+    # true residual of the last solve: ||b - A x|| / ||b||
+    r = pb.Vec(da)
+    A.mult(x, r)
+    r.axpy(-1.0, b)
+    rel = r.norm() / b.norm()
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, comm)
+    else:
+        per_rank = [comm]
+    t_roof = ms_roof / max(cnt_roof, 1) / 1e3
+    achieved = roof_bytes * nloc / t_roof / 1e9 if t_roof > 0 else 0.0
+    N = n[0] * n[1] * n[2]
+    its_total = int(sum(its_seen))
+    if rank == 0:
+        out = {
+            "metric": "CG iter/s and DoF-updates/s at 512^3; achieved HBM GB/s vs peak",
+            "value": N * its_total / elapsed,
+            "unit": "DoF-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": args.scaling_eff,
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (x_true = SplitMix64 U[-1,1], b = A x_true, x0 = 0)",
+            "config": {"workload": f"{W['describe']}, {n[0]}x{n[1]}x{n[2]} grid",
+                       "workload_key": args.workload,
+                       "step": "one KSPSolve to rtol 1e-10 from x0 = 0",
+                       "grid": list(n), "global_dofs": N, "per_gpu_dofs": nloc,
+                       "parallelism": f"z-slab x{world}" + (
+                           f" ({'RCCL' if args.transport == 'rccl' else 'gloo host'})"
+                           if world > 1 else ""),
+                       "ksp": " ".join(W["argv"]) + ", constant null space"},
+            "iter_per_s": its_total / elapsed,
+            "solves_per_s": args.steps / elapsed,
+            "its_per_solve": its_total / max(args.steps, 1),
+            "roofline": {"bound": "hbm", "kernel": roof_desc, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "bytes_per_dof": roof_bytes,
+                         "avg_launch_ms": t_roof * 1e3, "launches_timed": cnt_roof},
+            "kernels": kern,
+            "launcher": os.environ.get("PB_BENCH_LAUNCHER",
+                                       "torch.distributed.run" if dist else "none"),
+            "transport": comm_transport,
+            "rccl_nranks": comm_nranks if comm_transport == "rccl" else None,
+            "per_rank_comm": per_rank if world > 1 else None,
+            "ksp_state": {"reason": pb.REASONS.get(reason, reason), "its": its,
+                          "rnorm0": float(hist[0]), "rnorm_last": float(hist[-1]),
+                          "true_residual_rel": rel},
+        }
+        if world == 1 and not args.no_cpu_baseline and args.cpu_baseline != "none":
+            out["cpu_baseline"] = cpu_solve_baseline(args.workload)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    for o in (ksp, r, xt, x, b):
+        o.destroy()
+    if P is not A:
+        P.destroy()
+    A.destroy()
+
+
+def ctx_device(ctx):
+    return getattr(ctx, "device", None)
+
+
 def sustained_row(samples, nloc, gbs):
     """The sustained matvec row from per-launch durations (ms): average, median, and the first /
     last ten launches' averages (drift under sustained load)."""
@@ -296,6 +512,7 @@ def dry_run(args):
         dist.all_gather_object(seen, (rank, local_rank, os.getpid()))
     n = global_grid(world, args.base) if args.scaling == "weak" else (args.base,) * 3
     out = {"dry_run": True, "n_gpus": world, "grid": list(n), "ranks": seen,
+           "workload": args.workload, "scaling": args.scaling_eff,
            "launcher": os.environ.get("PB_BENCH_LAUNCHER", "env" if dist else "none")}
     if dist:
         dist.destroy_process_group()
@@ -324,7 +541,16 @@ def main():
                          "(lets several ranks share one GPU for testing)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch and join the ranks, print the plan; no GPU work")
+    ap.add_argument("--workload", choices=("star7-jacobi",) + tuple(SOLVE_WORKLOADS),
+                    default="star7-jacobi",
+                    help="star7-jacobi (default, BASELINE configs 2-4: fixed CG + Jacobi "
+                         "iterations); compact-fft (config 5: compact A = P, spectral PC, whole "
+                         "solves, strong scaling by default); star7-mg (CG + MG V-cycle solves)")
     args = ap.parse_args()
+    # --scaling defaults to the workload's own (config 5 is a strong-scaling case)
+    if args.workload in SOLVE_WORKLOADS and "--scaling" not in " ".join(sys.argv):
+        args.scaling = SOLVE_WORKLOADS[args.workload]["scaling"]
+    args.scaling_eff = "strong" if (args.scaling == "strong" and not args.grid) else "weak"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -368,10 +594,18 @@ def main():
     ctx = pb.Context(device, rank, world, uid)
     if dist and args.transport == "host":
         tr = GlooTransport(dist)
-        ctx.set_host_transport(tr.sendrecv, tr.allreduce)
+        ctx.set_host_transport(tr.sendrecv, tr.allreduce, tr.alltoallv)
     # what the transport itself reports (RCCL: ncclCommCount / ncclCommUserRank)
     comm_transport, comm_nranks, comm_rank = ctx.comm_info()
     da = pb.initialise_grid(ctx, n)
+    if args.workload in SOLVE_WORKLOADS:
+        run_solve_workload(args, pb, ctx, da, n, rank, world, dist, comm_transport, comm_nranks,
+                           json_fd)
+        da.destroy()
+        ctx.destroy()
+        if dist:
+            dist.destroy_process_group()
+        return
     h = da.spacing
     P, A, x, b = pb.initialise_linear_system(da, h)
     xt = pb.Vec(da)
@@ -486,11 +720,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if (args.scaling == "strong" and not args.grid) else "weak",
+            "scaling": args.scaling_eff,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (x_true = SplitMix64 U[-1,1], b = A x_true, x0 = 0)",
-            "config": {"workload": f"fp64 CG + Jacobi, 7-pt periodic Laplacian, "
+            "config": {"workload_key": "star7-jacobi",
+                       "workload": f"fp64 CG + Jacobi, 7-pt periodic Laplacian, "
                                    f"{n[0]}x{n[1]}x{n[2]} grid ({args.base}^3 DoF per GPU)",
                        "grid": list(n), "global_dofs": N, "per_gpu_dofs": nloc,
                        "parallelism": f"z-slab x{world}" + (

@@ -62,6 +62,7 @@ class Context:
         h = C.c_void_p()
         L.call("pb_ctx_create", int(device), int(rank), int(nranks), uid, C.byref(h))
         self.h = h
+        self.device = device
         self.rank, self.nranks = rank, nranks
         self._keep = []
 
@@ -73,6 +74,7 @@ class Context:
         h = C.c_void_p()
         L.call("pb_ctx_create_from_env", int(device), C.byref(h))
         self.h = h
+        self.device = device
         r, n = C.c_int(), C.c_int()
         L.call("pb_ctx_get_rank", h, C.byref(r), C.byref(n))
         self.rank, self.nranks = r.value, n.value

@@ -98,3 +98,25 @@ def test_sustained_row():
     assert r["launches"] == 100 and r["first10_ms"] == 1.0 and r["last10_ms"] == 2.0
     assert abs(r["avg_ms"] - 1.5) < 1e-12 and r["median_ms"] == 1.5
     assert bench.sustained_row([], 1, gbs) is None
+
+
+def test_solve_workload_dry_run_and_cpu_rows():
+    """--workload compact-fft defaults to strong scaling (config 5: 512^3 over the GPUs); its CPU
+    baseline (the oracle's compact CG + spectral PC) and star7-mg's run on small grids here."""
+    import json
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--dry-run",
+                        "--workload", "compact-fft"], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["workload"] == "compact-fft" and out["scaling"] == "strong"
+    assert out["grid"] == [512, 512, 512]
+    for wl in ("compact-fft", "star7-mg"):
+        cb = bench.cpu_solve_baseline(wl, budget_s=0.01, m=16)
+        assert cb["reason"] == 2 and cb["value"] > 0 and cb["its_per_solve"] >= 1
+        assert cb["kind"] == "port" and cb["cores"] >= 1

@@ -159,6 +159,63 @@ def test_config5_compact_fft_solve_512(ctx):
     da.destroy()
 
 
+def test_config5_eight_ranks_512():
+    """BASELINE config 5's decomposition: 512^3 over 8 ranks (512x512x64 z-slabs, the Z passes on
+    64-row y-slabs through all-to-all transposes), 8 contexts on the one GPU joined by the
+    in-process host transport. Against the 1-rank run of the same problem: A x_true (compact
+    operator) and the spectral PC apply bit-identical on every slab; the CG solve to rtol 1e-10
+    with the same reason and iteration count, x within the CG bar (the dot products sum per-rank
+    partials in another order, so x differs at rounding level) and ||b - A x|| / ||b|| < 1e-12."""
+    from test_gpu_parity import run_ranks
+    n = (512, 512, 512)
+    plane = n[0] * n[1]
+    h = tuple(2 * np.pi / m for m in n)
+    argv = ["-ksp_type", "cg", "-pc_type", "fft", "-ksp_rtol", "1e-10"]
+
+    def system(ctx):
+        da = pb.DA(ctx, n, (2 * np.pi,) * 3)
+        A = pb.Mat(da, pb.COMPACT, h)
+        x, b, xt, z = pb.Vec(da), pb.Vec(da), pb.Vec(da), pb.Vec(da)
+        xt.set_random(SEED)
+        A.mult(xt, b)
+        k = pb.KSP(A, A, pb.ksp_options(argv))
+        k.pc_apply(b, z)
+        return da, A, x, b, xt, z, k
+
+    ctx1 = pb.Context(0)
+    da, A, x, b, xt, z, k = system(ctx1)
+    reason1, its1, _ = k.solve(b, x)
+    ref_b, ref_z, ref_x = b.get_values(), z.get_values(), x.get_values()
+    for o in (k, A, x, b, xt, z):
+        o.destroy()
+    da.destroy()
+    ctx1.destroy()
+    assert reason1 == 2 and its1 <= 3
+    xscale = float(np.max(np.abs(ref_x)))
+
+    def body(ctx, rank):
+        da, A, x, b, xt, z, k = system(ctx)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        sl = slice(k0 * plane, (k0 + nk) * plane)
+        same_b = bool(np.array_equal(b.get_values(), ref_b[sl]))
+        same_z = bool(np.array_equal(z.get_values(), ref_z[sl]))
+        reason, its, _ = k.solve(b, x)
+        xerr = float(np.max(np.abs(x.get_values() - ref_x[sl]))) / xscale
+        res = _true_residual(A, x, b)  # collective: every rank takes part
+        for o in (k, A, x, b, xt, z):
+            o.destroy()
+        da.destroy()
+        return k0, nk, same_b, same_z, reason, its, xerr, res
+
+    out = run_ranks(8, body)
+    assert [(r[0], r[1]) for r in out] == [(64 * q, 64) for q in range(8)]
+    for k0, nk, same_b, same_z, reason, its, xerr, res in out:
+        assert same_b and same_z, (k0, same_b, same_z)
+        assert (reason, its) == (reason1, its1)
+        assert xerr <= 1e-10, xerr  # parity_bars.X_RTOL
+        assert res < 1e-12, res
+
+
 def test_mg_pc_apply_512_bit_exact(ctx):
     """One V-cycle (8 levels, fused sweeps on the 512^3 and 256^3 levels) bit-identical to the
     oracle's over the whole grid."""

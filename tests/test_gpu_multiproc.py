@@ -130,6 +130,35 @@ def test_config4_geometry_eight_ranks():
         check_history(hist, ho)
 
 
+@pytest.mark.parametrize("workload,extra", [("compact-fft", ["--base", "64"]),
+                                            ("star7-mg", ["--base", "32"])])
+def test_bench_solve_workload_self_launch(workload, extra):
+    """bench.py --workload (whole KSPSolves) through the self-launch path with no
+    launcher in the environment: 2 rank processes on the one GPU over the gloo host transport
+    (config 5 strong-scaled: the compact operator's transposes run as host all-to-alls)."""
+    import json
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = REPO
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--workload", workload, "--transport", "host"] + extra
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["launcher"] == "self" and d["transport"] == "host"
+    assert d["config"]["workload_key"] == workload
+    assert d["ksp_state"]["reason"] == "CONVERGED_RTOL"
+    assert d["ksp_state"]["true_residual_rel"] < 1e-8
+    assert d["value"] > 0 and d["roofline"]["launches_timed"] > 0
+    if workload == "compact-fft":
+        assert d["scaling"] == "strong" and d["config"]["grid"] == [64, 64, 64]
+        assert all("alltoallv_calls" in r for r in d["per_rank_comm"])
+    else:
+        assert d["scaling"] == "weak" and d["config"]["grid"] == [32, 32, 64]
+
+
 def test_bench_two_ranks_host_transport():
     """bench.py's multi-rank orchestration (torch.distributed.run, barrier, max-over-ranks,
     weak-scaling grid) on one GPU through the host transport, at a small per-GPU size."""

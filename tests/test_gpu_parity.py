@@ -1217,12 +1217,13 @@ def test_multirank_fft_pc(nranks, n3, compact):
         assert err < FFT_PC_RTOL, err
 
 
-@pytest.mark.parametrize("nranks", [2, 3, 4])
-def test_multirank_cg_compact_fft(nranks):
+@pytest.mark.parametrize("nranks,n3", [(2, (64, 64, 64)), (3, (64, 64, 64)), (4, (64, 64, 64)),
+                                       (8, (64, 64, 64)), (8, (128, 64, 128))])
+def test_multirank_cg_compact_fft(nranks, n3):
     """Config 5 decomposed: compact A = P on z-slabs (Z passes on y-slabs via all-to-all
     transposes), spectral PC, CG to rtol 1e-10 -- reason / its equal to the single-grid oracle,
-    x within the CG bar on every rank."""
-    n3 = (64, 64, 64)
+    x within the CG bar on every rank. 8 ranks: config 5's GPU count (8-plane / 16-plane slabs,
+    8-row y-slabs)."""
     N = int(np.prod(n3))
     h = tuple(2 * np.pi / m for m in n3)
     b = O.lapl(O.fill_random(N, SEED), n3, h)
