@@ -174,3 +174,10 @@ def test_bench_two_ranks_host_transport():
     assert len(line) == 1
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["config"]["grid"] == [48, 48, 96] and d["value"] > 0
+    # the default run also measures the solve workloads (config 5 strong-scaled, CG + MG)
+    sec = d["secondary"]
+    assert sec["compact-fft"]["config"]["grid"] == [48, 48, 48]
+    assert sec["star7-mg"]["config"]["grid"] == [48, 48, 96]
+    for wl in ("compact-fft", "star7-mg"):
+        assert sec[wl]["ksp_state"]["reason"] == "CONVERGED_RTOL", sec[wl]
+        assert sec[wl]["value"] > 0
