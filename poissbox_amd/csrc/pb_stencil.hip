@@ -106,11 +106,15 @@ struct StoreY {
 // becomes read-only (16 B/DoF) and pass B reads 2 / writes 2 arrays (32 B/DoF), same 48 B/DoF.
 // Read-only (STORE = false): 4-row tiles, one workgroup per CU (z-chunks of half the slab at
 // 512^3), measured 0.378 vs 0.391 ms for 8-row tiles (profiles/r02/ab_pst_defer_512.jsonl).
+#ifndef PB_PASSA_TALL
+#define PB_PASSA_TALL 0
+#endif
 template <bool STORE>
 struct PassAT {
   static constexpr int NS = 1, NE = 0;
-  static constexpr bool RAW = false, TALL = STORE;  // put() takes the Laplacian; 8-row tiles
+  static constexpr bool RAW = false, TALL = STORE || PB_PASSA_TALL;  // put() takes the Laplacian; 8-row tiles
   static constexpr int WGCU = STORE ? 3 : 1;        // (4-row tiles; 1 with 8 rows)
+  static constexpr bool CAP = !STORE, WIDE8 = !STORE;
   static constexpr bool PREFETCH = true;
   double* __restrict__ p_new;
   int nt_p;  // non-temporal p stores (PB_PASSA_NT, default on; cached stores, which pass B could
@@ -153,6 +157,7 @@ struct PassB {
   // one workgroup per CU (z-chunks of half the slab at 512^3): 8-10 % faster than 3 per CU
   static constexpr int WGCU = PST ? PB_PSTB_WGCU : 1;
   static constexpr bool TALL = PST && XU == 0 && PB_PSTB_TALL;  // (A/B builds)
+  static constexpr bool CAP = true, WIDE8 = PST && XU == 0;
   static constexpr bool PREFETCH = true;
   double* __restrict__ x;
   double* __restrict__ r;
@@ -606,6 +611,17 @@ static int pick_ty(int ny) {
   return 1;
 }
 
+// Epi::CAP (optional trait): keep at most WGCU workgroups resident per CU (launch_t)
+template <class E, class = void>
+struct CapOf {
+  static constexpr bool v = false;
+};
+template <class E>
+struct CapOf<E, std::void_t<decltype(E::CAP)>> {
+  static constexpr bool v = E::CAP;
+};
+constexpr size_t kLdsPerCu = 160 * 1024;
+
 template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                     const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev,
@@ -617,8 +633,18 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
   if ((part_off + nblocks) * NS > g->ctx->partials_cap)
     return set_error(PB_ERR_UNSUPPORTED, "stencil grid of %lld blocks exceeds partials capacity",
                      (long long)nblocks);
-  hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads), 0,
-                     g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
+  // Residency cap (Epi::CAP, the CG passes): a grid with more columns than the epilogue's WGCU
+  // workgroups per CU (planes of 1024^2 points: 512 columns of 4-row tiles, twice the 1-per-CU
+  // count) would run two workgroups per CU side by side; an LDS request no kernel uses keeps it at
+  // WGCU resident per CU, the rest following as slots free. 1024x1024x128 (config 4's per-GPU
+  // slab): pass B 0.847 -> 0.772 ms, iteration 1.47 -> 1.40 ms (profiles/r04/shapes_r4.txt).
+  size_t lds = 0;
+  if constexpr (CapOf<Epi>::v) {
+    const int w = wgcu > 0 ? wgcu : Epi::WGCU;
+    if (nblocks > (int64_t)w * g->ctx->num_cus) lds = kLdsPerCu / (size_t)(w + 1) + 4096;
+  }
+  hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads),
+                     lds, g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
                      g->ctx->d_partials + (int64_t)part_off * NS, skip, fold);
   PB_HIP(hipGetLastError());
   if (nb_out) *nb_out = (int)nblocks;
@@ -637,6 +663,20 @@ struct TallOf<E, std::void_t<decltype(E::TALL)>> {
   static constexpr bool v = E::TALL;
 };
 
+// Epi::WIDE8 (optional trait): 8 rows per wave when 4-row tiles would leave more columns than
+// WGCU workgroups per CU (planes 1024 or more points wide): the CG passes then run one column per
+// CU as at 512^3. 1024x1024x128: pass A 0.412 -> 0.389 ms, pass B 0.759 -> 0.720 ms, iteration
+// 1.39 -> 1.33 ms, the 512^3 rate; at 512^3 itself 4-row tiles stay faster
+// (profiles/r04/shapes_r4b.txt)
+template <class E, class = void>
+struct Wide8Of {
+  static constexpr bool v = false;
+};
+template <class E>
+struct Wide8Of<E, std::void_t<decltype(E::WIDE8)>> {
+  static constexpr bool v = E::WIDE8;
+};
+
 template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                       const Epi& ep, const int* skip, int mode = PLANES_ALL, int part_off = 0,
@@ -644,6 +684,13 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
                       const Fold& fold = Fold{}) {
   const bool vec2 = (g->n[0] % 2) == 0;
   const int ty = pick_ty((int)g->n[1]);
+  if constexpr (Wide8Of<Epi>::v) {
+    const int64_t cols4 = ((g->n[0] + 127) / 128) * ((g->n[1] + kWaves * 4 - 1) / (kWaves * 4));
+    const int w = wgcu > 0 ? wgcu : Epi::WGCU;
+    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && !getenv("PB_STENCIL_TY") &&
+        cols4 > (int64_t)w * g->ctx->num_cus)
+      return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
+  }
   if constexpr (TallOf<Epi>::v) {
     const int tall = env_int("PB_STENCIL_TALL", 1);  // read per launch (A/B tuning)
     const int64_t tall_min = env_int("PB_STENCIL_TALL_MIN_PLANE", 512 * 512);
