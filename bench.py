@@ -26,10 +26,10 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X spec (MI355X_MICROARCH.md "Chip-level parameters")
 PASS_B_X_NAME = {0: "cg_pass_b", 2: "cg_pass_b_odd", 4: "cg_pass_b_x4"}
-# Algorithmic bytes per DoF of each CG pass, by where p is stored (PB_CG_PSTORE_B, library
-# default 1, pb_solver.cpp):
+# Algorithmic bytes per DoF of each CG pass, by where p is stored (tuning parameter cg_pstore_b,
+# library default 1, pb_solver.cpp):
 #  pstore 0: pass A reads r, p_old, writes p (24); pass B reads p (stencil), r, writes r (24);
-#            the x update every D-th iteration (PB_CG_DEFER_X = D, default 4) adds x read/write
+#            the x update every D-th iteration (cg_defer_x = D, default 4) adds x read/write
 #            and p_{i-1} .. p_{i-D+1}
 #  pstore 1: pass A reads r, p_old (16, p.Ap only); pass B re-forms p from r, p_old, writes p and
 #            r into the other residual buffer (32); the x update adds x read/write and
@@ -41,9 +41,9 @@ PASS_BYTES = {
 MATVEC_BYTES = 16            # y = A x: read x, write y
 
 
-def pstore_mode():
-    """The library's p-store placement (PB_CG_PSTORE_B, default 1)."""
-    return 0 if os.environ.get("PB_CG_PSTORE_B", "1") == "0" else 1
+def pstore_mode(setting=None):
+    """The library's p-store placement from the cg_pstore_b tuning setting (None: default 1)."""
+    return 0 if setting == 0 else 1
 
 
 def cg_iter_bytes(defer, pstore=1):
@@ -314,9 +314,7 @@ def run_solve_workload(args, pb, ctx, workload, scaling, steps, warmup, rank, wo
     ctx.barrier()
     if dist:
         dist.barrier()
-    os.environ["PB_TIMING_ONLY"] = roof
-    os.environ["PB_TIMING_EVERY"] = "1"
-    ctx.set_timing(True)
+    ctx.set_timing(True, only=roof, every=1)
     ctx.reset_timing()
     its_seen = []
     t0 = time.perf_counter()
@@ -331,8 +329,6 @@ def run_solve_workload(args, pb, ctx, workload, scaling, steps, warmup, rank, wo
     elapsed = t1 - t0
     ms_roof, cnt_roof = ctx.timing(roof)
     ctx.set_timing(False)
-    os.environ.pop("PB_TIMING_ONLY", None)
-    os.environ.pop("PB_TIMING_EVERY", None)
     # diagnostics: one more solve with every phase timed
     ctx.set_timing(True)
     ctx.reset_timing()
@@ -600,6 +596,9 @@ def main():
                     help="star7-jacobi (default, BASELINE configs 2-4: fixed CG + Jacobi "
                          "iterations); compact-fft (config 5: compact A = P, spectral PC, whole "
                          "solves, strong scaling by default); star7-mg (CG + MG V-cycle solves)")
+    ap.add_argument("--tune", default="",
+                    help="A/B runs: name=value[,name=value] tuning settings (pb_tune_set, "
+                         "INTEGRATION.md) applied before the run")
     ap.add_argument("--secondary", type=int, choices=(0, 1), default=1,
                     help="default run: also measure the compact-fft (config 5) and star7-mg "
                          "solve workloads after the headline, under \"secondary\" (1, default)")
@@ -630,8 +629,11 @@ def main():
 
     import poissbox_amd as pb
     from poissbox_amd.dist import GlooTransport, broadcast_uid, init_from_env
+    for kv in filter(None, args.tune.split(",")):
+        k_, v_ = kv.split("=", 1)
+        pb.tune_set(k_.strip(), int(v_))
 
-    dx = int(os.environ.get("PB_CG_DEFER_X", "4"))  # the solver's deferral depth (pb_solver.cpp)
+    dx = pb.tune_get("cg_defer_x")  # the solver's deferral depth (pb_solver.cpp, default 4)
     defer = 0 if dx == 0 else (2 if dx == 2 else 4)
     rank, world, local_rank, dist = init_from_env("gloo")   # control plane only
     uid = None
@@ -683,12 +685,10 @@ def main():
     # timed region: HIP events around the roofline kernel only, on every 4th launch (events
     # around every launch add ~2 % of gaps to the measured step; around every pass A ~0.7 %).
     # The roofline kernel is the one with the largest share of the step: pass A when it stores p
-    # (PB_CG_PSTORE_B=0), otherwise pass B without the x update (3 of 4 iterations at D = 4)
-    pstore = pstore_mode()
+    # (cg_pstore_b = 0), otherwise pass B without the x update (3 of 4 iterations at D = 4)
+    pstore = pstore_mode(pb.tune_get("cg_pstore_b"))
     roof = "cg_pass_b_even" if (pstore and defer == 4) else "cg_pass_a"
-    os.environ["PB_TIMING_ONLY"] = roof
-    os.environ["PB_TIMING_EVERY"] = "4"
-    ctx.set_timing(True)
+    ctx.set_timing(True, only=roof, every=4)
     ctx.reset_timing()
     t0 = time.perf_counter()
     ksp.iterate(args.steps)
@@ -700,8 +700,6 @@ def main():
     elapsed = t1 - t0
     ms_roof, cnt_roof = ctx.timing(roof)
     ctx.set_timing(False)
-    os.environ.pop("PB_TIMING_ONLY", None)
-    os.environ.pop("PB_TIMING_EVERY", None)
     # per-kernel diagnostics of the other passes: a few more iterations, every launch timed
     ctx.set_timing(True)
     ctx.reset_timing()

@@ -110,6 +110,10 @@ int pb_ctx_comm_info(const pb_ctx* ctx, int* transport, int* comm_nranks, int* c
 int pb_ctx_destroy(pb_ctx* ctx);
 /* Per-kernel timing with HIP events on the context's stream (off by default). */
 int pb_ctx_set_timing(pb_ctx* ctx, int enable);
+/* Timing restricted to the comma-separated phase names in `only` (NULL or "": every phase), and
+ * to one launch in `every` of each such phase: a timed region keeps its event records off the
+ * other launches (bench.py times its roofline kernel inside the timed steps this way). */
+int pb_ctx_set_timing_filter(pb_ctx* ctx, int enable, const char* only, int every);
 /* name: "stencil", "cg_pass_a", "cg_pass_b", ...; returns total ms and launch count since reset */
 int pb_ctx_get_timing(pb_ctx* ctx, const char* name, double* total_ms, int64_t* count);
 /* The per-launch durations behind pb_ctx_get_timing (the first 65536 since the last reset):
@@ -118,6 +122,17 @@ int pb_ctx_get_timing(pb_ctx* ctx, const char* name, double* total_ms, int64_t* 
 int pb_ctx_get_timing_samples(pb_ctx* ctx, const char* name, float* ms, int64_t cap,
                               int64_t* count);
 int pb_ctx_reset_timing(pb_ctx* ctx);
+
+/* ---- tuning (kernel selection and launch shapes; no reference counterpart) ----
+ * Process-wide table of the launchers' parameters (INTEGRATION.md lists the names: z-march
+ * alternation, tile heights, multigrid kernel thresholds, spectral-PC tile shapes, ...). Unset
+ * names take the measured defaults; every setting selects kernels that give the same results to
+ * the bits (or, for tile heights, to the reduction order of the CG sums), so it is a speed knob,
+ * never a correctness one. The library reads no such setting from the environment. Unknown names
+ * return PB_ERR_ARG. Set before the calls it should affect; not thread-safe against running calls. */
+int pb_tune_set(const char* name, int value);
+int pb_tune_get(const char* name, int* value, int* is_set);
+int pb_tune_reset(void);
 
 /* ---- slab partition (replaces DMDACreate3d's PETSC_DECIDE split, src/poissbox.f90:191-202) ---- */
 /* Pure host function: remainder planes go to the low ranks (README.md:30-32's 22/21/21). */

@@ -59,6 +59,10 @@ _SIGS = {
     "pb_ctx_allreduce_host": [c_p, P_d, C.c_int],
     "pb_ctx_destroy": [c_p],
     "pb_ctx_set_timing": [c_p, C.c_int],
+    "pb_ctx_set_timing_filter": [c_p, C.c_int, C.c_char_p, C.c_int],
+    "pb_tune_set": [C.c_char_p, C.c_int],
+    "pb_tune_get": [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+    "pb_tune_reset": [],
     "pb_ctx_get_timing": [c_p, C.c_char_p, P_d, P_i64],
     "pb_ctx_get_timing_samples": [c_p, C.c_char_p, C.POINTER(C.c_float), c_i64, P_i64],
     "pb_ctx_reset_timing": [c_p],

@@ -54,6 +54,22 @@ def slab_partition(nz, nranks, rank):
     return k0.value, nk.value
 
 
+def tune_set(name, value):
+    """pb_tune_set: a kernel-selection / launch-shape parameter (INTEGRATION.md lists them)."""
+    L.call("pb_tune_set", name.encode(), int(value))
+
+
+def tune_get(name):
+    """The value set for a tuning parameter, or None when it runs at its measured default."""
+    v, s = C.c_int(), C.c_int()
+    L.call("pb_tune_get", name.encode(), C.byref(v), C.byref(s))
+    return v.value if s.value else None
+
+
+def tune_reset():
+    L.call("pb_tune_reset")
+
+
 class Context:
     """One GPU, one rank. nranks > 1 needs either an RCCL unique id (uid, from rank 0's
     comm_unique_id()) or a host transport (set_host_transport) before the grid is created."""
@@ -165,8 +181,13 @@ class Context:
         L.call("pb_ctx_comm_info", self.h, C.byref(t), C.byref(n), C.byref(r))
         return self.TRANSPORTS.get(t.value, t.value), n.value, r.value
 
-    def set_timing(self, on=True):
-        L.call("pb_ctx_set_timing", self.h, int(bool(on)))
+    def set_timing(self, on=True, only=None, every=1):
+        """HIP-event timing of the library's phases; only: phase names (str or list) to time,
+        every: time one launch in `every` of each (pb_ctx_set_timing_filter)."""
+        if isinstance(only, (list, tuple)):
+            only = ",".join(only)
+        L.call("pb_ctx_set_timing_filter", self.h, int(bool(on)),
+               only.encode() if only else None, int(every))
 
     def timing(self, name):
         ms, cnt = C.c_double(), C.c_int64()

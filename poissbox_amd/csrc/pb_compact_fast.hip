@@ -231,7 +231,7 @@ static int launch_pass(pb_ctx* ctx, FastPass& p) {
 // complete: the caller's grid on one rank, the y-slab of the transposed data for the Z pass on N
 // ranks. Register line solves where n = 64*C supports them, the LDS-PCR kernel otherwise. ----
 static bool reg_lines(int64_t n) {
-  static const bool lines_ok = env_int("PB_COMPACT_LINES", 1) != 0;
+  const bool lines_ok = tune("compact_lines", 1) != 0;
   return lines_ok && compact_lines_supported(n);
 }
 

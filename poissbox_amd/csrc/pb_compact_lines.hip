@@ -697,11 +697,14 @@ static LineOp make_solve_op(double alpha, int C) {
 // the CgFuse passes apply: one rank (no z-slab <-> y-slab transposes), register line solves in
 // every direction, the Z pass with prefetch (lines of <= 512 points) on an even x extent, default
 // launch shapes
+// (the same conditions the Z and X passes test below and in compact_pass_*: the solver falls back
+// to the unfused iteration when a pass reports it did not fuse)
 bool compact_cg_fusable(const pb_grid* g) {
-  return !grid_split(g) && compact_lines_supported(g->n[0]) && compact_lines_supported(g->n[1]) &&
+  return !grid_split(g) && !g->ctx->split && tune("compact_lines", 1) &&
+         compact_lines_supported(g->n[0]) && compact_lines_supported(g->n[1]) &&
          compact_lines_supported(g->n[2]) && g->n[2] <= 512 && g->n[0] % 2 == 0 &&
-         !env_int("PB_LINES_CFG", 0) && env_int("PB_LINES_XDIRECT", 1) &&
-         env_int("PB_CG_FUSE", 1);
+         !tune("lines_cfg", 0) && tune("lines_xdirect", 1) &&
+         tune("cg_fuse", 1);
 }
 
 bool compact_lines_supported(int64_t n) {
@@ -749,7 +752,7 @@ static int launch_lines_k(pb_ctx* ctx, LinePass& p, int64_t nouter) {
 // selects an alternative shape (tuning, C = 4 and 8).
 template <int C, int LAYOUT, int PASS>
 static int launch_lines_c(pb_ctx* ctx, LinePass& p, int64_t nouter) {
-  static const int cfg = env_int("PB_LINES_CFG", 0);
+  const int cfg = tune("lines_cfg", 0);
   if constexpr (C == 4 || C == 8) {
     switch (cfg) {
       case 1: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 1>>(ctx, p, nouter);
@@ -810,8 +813,8 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
   ScopedTimer tm(ctx, names[axis]);
   LinePass p{};
   p.skip = ctx->op_skip;
-  p.remap = env_int("PB_LINES_REMAP", 0);
-  static const int ablate = env_int("PB_LINES_ABLATE", 0);
+  p.remap = tune("lines_remap", 0);
+  const int ablate = PB_ABLATE_LINES;
   p.ablate = ablate;
   p.in0 = in0;
   p.in1 = in1;
@@ -826,7 +829,7 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
     p.ninner = (int)nx;
     CgFuse* cf = ctx->cg_fuse;
     if (cf && cf->z && C <= 8 && nx % 2 == 0 && ((uintptr_t)cf->z & 15) == 0 &&
-        ((uintptr_t)out0 & 15) == 0 && !env_int("PB_LINES_CFG", 0)) {
+        ((uintptr_t)out0 & 15) == 0 && !tune("lines_cfg", 0)) {
       // CG's p formed by the Z pass from z and p_old (CgFuse); in0 is not read
       p.in0 = cf->z;
       p.in1 = cf->p_old;
@@ -858,7 +861,7 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
   p.lo = nx * ny;
   p.es = 1;
   p.ninner = (int)ny;
-  static const int xdirect = env_int("PB_LINES_XDIRECT", 1);
+  const int xdirect = tune("lines_xdirect", 1);
   if (xdirect) {
     switch (C) {
       case 1: return launch_x_direct<1>(ctx, p, ny * nz);
@@ -884,7 +887,7 @@ int lines_solve_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_str
   const int C = (int)(n / 64);
   LinePass p{};
   p.skip = ctx->op_skip;
-  p.remap = env_int("PB_LINES_REMAP", 0);
+  p.remap = tune("lines_remap", 0);
   p.in0 = d;
   p.out0 = d;
   p.J = make_solve_op(alpha, C);

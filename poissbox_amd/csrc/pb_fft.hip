@@ -880,7 +880,7 @@ int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
   }
   // persistent passes: one resident round of blocks (PB_FFT_BLOCKS_PER_CU overrides, tuning);
   // the others one tile per block
-  static const int bpc = env_int("PB_FFT_BLOCKS_PER_CU", 0);
+  const int bpc = tune("fft_blocks_per_cu", 0);
   int64_t nblocks = (int64_t)(bpc > 0 ? bpc : occ) * ctx->num_cus;
   const bool persist = N <= 512 && (LAYOUT == 1 || PFS);
   if (!persist || nblocks > ntiles) nblocks = ntiles;
@@ -903,7 +903,7 @@ int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
 // PB_FFT_PF_STRIDED=1 selects those); PB_FFT_TL_Z = 32 (512-point lines): 32-line Z tiles, 256-B
 // pieces, one block per CU (measured no faster).
 static bool reg_x_on() {
-  static const int reg = env_int("PB_FFT_REG", 1);
+  const int reg = tune("fft_reg", 1);
   return reg != 0;
 }
 
@@ -920,9 +920,9 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   if constexpr (LAYOUT == 1) {
     return launch_dht_k<N, TL, 1, MODE, false>(ctx, p, skip);
   } else {
-    static const int pfs = env_int("PB_FFT_PF_STRIDED", 0);
+    const int pfs = tune("fft_pf_strided", 0);
     if constexpr (N == 512 && MODE == 1) {
-      static const int tlz = env_int("PB_FFT_TL_Z", 16);
+      const int tlz = tune("fft_tl_z", 16);
       if (tlz == 32)
         return pfs ? launch_dht_k<N, 32, 0, 1, true>(ctx, p, skip)
                    : launch_dht_k<N, 32, 0, 1, false>(ctx, p, skip);
@@ -931,7 +931,7 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
       if (pfs) return launch_dht_k<N, TL, 0, MODE, true>(ctx, p, skip);
     if constexpr (N > 512) {
       // PB_FFT_TL_LONG=8 / 16: the tile width on 768 / 1024-point lines (A/B)
-      static const int tll = env_int("PB_FFT_TL_LONG", 0);
+      const int tll = tune("fft_tl_long", 0);
       if (tll == 16 && TL != 16) return launch_dht_k<N, 16, 0, MODE, false>(ctx, p, skip);
       if (tll == 8 && TL != 8) return launch_dht_k<N, 8, 0, MODE, false>(ctx, p, skip);
     }
@@ -1081,8 +1081,8 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
       delete f;
       return set_error(PB_ERR_ALLOC, "fft pc y-slab buffer: out of device memory");
     }
-  } else if (const int64_t pad = env_int("PB_FFT_ZPAD", 32);
-             pad > 0 && g->plane >= env_int("PB_FFT_ZPAD_MIN_PLANE", 512 * 512)) {
+  } else if (const int64_t pad = tune("fft_zpad", 32);
+             pad > 0 && g->plane >= tune("fft_zpad_min_plane", 512 * 512)) {
     // (256^3, 512 KiB planes: no gain, 0.079 -> 0.083 ms; so only from 2 MiB planes up)
     f->zplane = g->plane + pad;
     if (hipMalloc(&f->zbuf, (size_t)(f->zplane * g->nzl) * sizeof(double)) != hipSuccess) {
@@ -1104,9 +1104,9 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   static const char* names[3] = {"pc_fft_x", "pc_fft_y", "pc_fft_z"};
   ScopedTimer tm(ctx, names[axis]);
   DhtPass p{};
-  p.remap = env_int("PB_FFT_REMAP", 1);
-  p.ablate = env_int("PB_FFT_ABLATE", 0);
-  p.stagger = env_int("PB_FFT_STAGGER", 0);
+  p.remap = tune("fft_remap", 1);
+  p.ablate = PB_ABLATE_FFT;
+  p.stagger = tune("fft_stagger", 0);
   p.ncu = ctx->num_cus;
   p.in = in;
   p.out = out;
@@ -1144,7 +1144,7 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
     p.es = nx;
     p.ninner = (int)nx;
     p.nouter = (int)nz;
-    p.order = env_int("PB_FFT_YORDER", 0);
+    p.order = tune("fft_yorder", 0);
     return launch_dht<0, 0>(ctx, ny, p, skip);
   }
   // axis 2 with the scaling: inner = i, outer = j, elements along k
@@ -1154,7 +1154,7 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   p.es = pl_in ? pl_in : nx * ny;  // in place: pl_out == pl_in
   p.ninner = (int)nx;
   p.nouter = (int)ny;
-  p.order = env_int("PB_FFT_ZORDER", 0);
+  p.order = tune("fft_zorder", 0);
   p.tab = f->tab;
   p.nx = (int)f->g->n[0];
   p.ny = (int)f->g->n[1];
@@ -1201,7 +1201,7 @@ int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgS
     PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
   }
   // with sums_st: the residual sums of CG (PB_FFT_SUMS, default on) are taken by the last pass
-  static const int fused = env_int("PB_FFT_SUMS", 1);
+  const int fused = tune("fft_sums", 1);
   if (sums_st && nparts && fused) return dht_axis(ctx, f, b, 0, z, z, skip, 0, r, sums_st, nparts);
   return dht_axis(ctx, f, b, 0, z, z, skip);
 }

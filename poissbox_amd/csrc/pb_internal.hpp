@@ -315,17 +315,25 @@ int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_d
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----
 int64_t compact_fast_work_len(const pb_grid* g);
 int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* out, double* work);
-// integer tuning knob from the environment (PB_*), dflt when unset
+// integer user setting from the environment (the PB_* variables INTEGRATION.md lists), dflt when
+// unset
 inline int env_int(const char* name, int dflt) {
   const char* s = getenv(name);
   return s ? atoi(s) : dflt;
 }
-// Field-sized device allocations (vectors, KSP work vectors). PB_ALLOC_CONTIGUOUS=1 asks for
-// physically contiguous memory (hipDeviceMallocContiguous): fewer translation misses when a
-// kernel streams many 1 GiB arrays at once (A/B knob for the x-update pass).
-// PB_ALLOC_STAGGER=b: the n-th field starts (n % 8) * b bytes into its allocation (b a multiple
-// of 256), so arrays a kernel streams at the same offsets do not hit the same HBM channel / bank
-// at the same time (A/B knob). Free with field_free.
+// Kernel-selection / launch-shape parameter: the value a caller set with pb_tune_set (tests and
+// A/B runs), else dflt -- the measured default at the call site. Never read from the environment.
+int tune(const char* name, int dflt);
+bool tune_is_set(const char* name);
+// Timing-only ablations (they skip traffic and give wrong results): compile-time only, for
+// scripts/build_variant.sh builds, never in the product library
+#ifndef PB_ABLATE_FFT
+#define PB_ABLATE_FFT 0
+#endif
+#ifndef PB_ABLATE_LINES
+#define PB_ABLATE_LINES 0
+#endif
+// Field-sized device allocations (vectors, KSP work vectors). Free with field_free.
 hipError_t field_alloc(void** p, size_t bytes);
 void field_free(void* p);
 template <class T>

@@ -566,8 +566,8 @@ __global__ __launch_bounds__(512) void mg_tail_kernel(TailArgs A, const int* ski
 // chunks of coarse planes for the z-marching transfer kernels: ~16 resident waves per CU, at
 // least 4 coarse planes per chunk
 static int transfer_chunk(pb_ctx* ctx, int64_t cols, int64_t nzl, int64_t* nchunk_out) {
-  const int64_t tpc = env_int("PB_MG_TRANSFER_TPC", 1024);  // threads per CU
-  const int64_t minz = env_int("PB_MG_TRANSFER_MINZ", 4);   // coarse planes per chunk, at least
+  const int64_t tpc = tune("mg_transfer_tpc", 1024);  // threads per CU
+  const int64_t minz = tune("mg_transfer_minz", 4);   // coarse planes per chunk, at least
   int64_t nchunk = ((int64_t)ctx->num_cus * tpc + cols - 1) / cols;
   nchunk = std::max<int64_t>(1, std::min<int64_t>(nchunk, nzl / minz));
   const int kc = (int)((nzl + nchunk - 1) / nchunk);
@@ -675,7 +675,7 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
     return set_error(PB_ERR_UNSUPPORTED, "multigrid: more than 2^32 points on one GPU");
   // PETSc PCSORSetOmega rejects omega outside (0, 2); PB_SOR_OMEGA_ANY=1 (diagnostics) accepts
   // it -- an indefinite SOR preconditioner, e.g. to exercise KSP_DIVERGED_INDEFINITE_PC
-  if (!(omega > 0.0 && omega < 2.0) && !env_int("PB_SOR_OMEGA_ANY", 0))
+  if (!(omega > 0.0 && omega < 2.0) && !tune("sor_omega_any", 0))
     return set_error(PB_ERR_ARG, "SOR omega must be in (0, 2)");
   Mg* mg = new Mg();
   mg->ctx = ctx;
@@ -685,8 +685,8 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
   mg->lv.resize(L);
   int64_t total = 0;
   // levels that take the fused post-smoothing (PB_MG_POST_FUSED, one rank): an xs array each
-  const bool want_post = !ctx->split && env_int("PB_MG_POST_FUSED", 1) != 0;
-  const int64_t post_min_plane = env_int("PB_MG_ENGINE_MIN_PLANE", 256 * 256);
+  const bool want_post = !ctx->split && tune("mg_post_fused", 1) != 0;
+  const int64_t post_min_plane = tune("mg_engine_min_plane", 256 * 256);
   auto takes_post = [&](const MgLevel& lv, int l) {
     return want_post && l < L - 1 && lv.g->plane >= post_min_plane && sor_sweep2_supported(lv.g);
   };
@@ -742,7 +742,7 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
 static bool post_fused(const Mg* mg, int l) {
   const MgLevel& F = mg->lv[l];
   if (!F.xs || l + 1 >= (int)mg->lv.size() || F.g->plane < mg->engine_min_plane ||
-      !env_int("PB_MG_PRESMOOTH_FUSED", 1) || !env_int("PB_MG_POST_FUSED", 1) ||
+      !tune("mg_presmooth_fused", 1) || !tune("mg_post_fused", 1) ||
       mg->prolong_cell != 2)
     return false;
   const MgLevel& C = mg->lv[l + 1];
@@ -754,18 +754,18 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
   if (nparts) *nparts = 0;
   ScopedTimer tm(mg->ctx, "mg_apply");
   mg->skip = skip;
-  mg->engine_min_plane = env_int("PB_MG_ENGINE_MIN_PLANE", 256 * 256);
-  mg->prolong_cell = env_int("PB_MG_PROLONG_CELL", 2);
-  mg->restrict_z = env_int("PB_MG_RESTRICT_Z", 1);
-  mg->restrict_z_min_cols = env_int("PB_MG_RESTRICT_Z_MIN_COLS", 4096);
+  mg->engine_min_plane = tune("mg_engine_min_plane", 256 * 256);
+  mg->prolong_cell = tune("mg_prolong_cell", 2);
+  mg->restrict_z = tune("mg_restrict_z", 1);
+  mg->restrict_z_min_cols = tune("mg_restrict_z_min_cols", 4096);
   const int L = (int)mg->lv.size();
   mg->lv[0].b = const_cast<double*>(r);
   mg->lv[0].x = z;
   pb_ctx* ctx = mg->ctx;
   // the coarse tail in one launch (one rank): levels Lt .. L-1 of <= PB_MG_TAIL_MAX points
   int Lt = L;
-  if (!ctx->split && env_int("PB_MG_TAIL", 1)) {
-    const int64_t tail_max = env_int("PB_MG_TAIL_MAX", 8192);
+  if (!ctx->split && tune("mg_tail", 1)) {
+    const int64_t tail_max = tune("mg_tail_max", 8192);
     Lt = L - 1;
     while (Lt > 1 && mg->lv[Lt - 1].g->nlocal <= tail_max) --Lt;
     if (Lt < 1 || mg->lv[Lt].g->nlocal > tail_max || L - Lt > kTailMax) Lt = L;
@@ -776,10 +776,10 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     MgLevel& Cl = mg->lv[l + 1];
     // large level: zero-start red + black half-sweeps and the residual in one pass
     const bool fused = F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g) &&
-                       env_int("PB_MG_PRESMOOTH_FUSED", 1);
+                       tune("mg_presmooth_fused", 1);
     // one rank: the restriction too (the residual is never stored)
     const bool fused_r = fused && !ctx->split && F.g->nzl % 2 == 0 &&
-                         env_int("PB_MG_PRESMOOTH_RESTRICT", 1);
+                         tune("mg_presmooth_restrict", 1);
     if (fused_r) {
       ScopedTimer t1(ctx, l == 0 ? "mg_fine_smooth_first" : "mg_coarse_levels");
       PB_TRY(launch_presmooth_restrict(F.g, F.s, Cl.g, F.b, post_fused(mg, l) ? F.xs : F.x, Cl.b,

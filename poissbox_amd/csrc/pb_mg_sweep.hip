@@ -2006,7 +2006,7 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
 // even extents, nx >= 128, >= 4 planes per rank: the fused sweep applies (else two half-sweeps)
 bool sor_sweep2_supported(const pb_grid* g) {
   return g->n[0] >= 128 && g->n[0] % 2 == 0 && g->n[1] % 2 == 0 && g->n[1] >= 8 &&
-         g->nzl >= 4 && env_int("PB_MG_SWEEP2", 1) != 0;
+         g->nzl >= 4 && tune("mg_sweep2", 1) != 0;
 }
 
 // N ranks: two-deep ghosts of xin (and, when b is another array, one-deep ghosts of b)
@@ -2038,12 +2038,12 @@ static int64_t sweep2_geo(pb_grid* g, Sweep2Geo& geo) {
   geo.nseg = (geo.nx + kSegOut - 1) / kSegOut;
   geo.ntile = (geo.ny + kWaves * kTY2 - 1) / (kWaves * kTY2);
   geo.k0 = (int)g->k0;
-  geo.remap = env_int("PB_XCD_REMAP", 1);
-  geo.nt = env_int("PB_STENCIL_NT", 1);
+  geo.remap = tune("xcd_remap", 1);
+  geo.nt = tune("stencil_nt", 1);
   const int columns = geo.nseg * geo.ntile;
   // chunks: ~PB_SWEEP2_WGCU (16) workgroups per CU (many rounds: the loop is latency-bound),
   // at least 16 planes per chunk
-  const int target = env_int("PB_SWEEP2_WGCU", 16) * g->ctx->num_cus;
+  const int target = tune("sweep2_wgcu", 16) * g->ctx->num_cus;
   int nchunk = std::max(1, (target + columns - 1) / columns);
   nchunk = std::min(nchunk, std::max(1, geo.nzl / 16));
   geo.kc = (geo.nzl + nchunk - 1) / nchunk;
@@ -2093,7 +2093,7 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
   // rows shared through LDS: 1, 2 = post_sweep_xch_kernel with 8 waves x 4 / x 2 rows; 3, 4 = the
   // same with the plane loop unrolled by four (post_sweep_u4_kernel; compile-time colours: k0 = 0,
   // chunk starts at multiples of 4); 0 = the per-wave kernel below
-  const int xv = env_int("PB_POSTX", 3);
+  const int xv = tune("postx", 3);
   if (xv >= 1 && xv <= 4) {
     const int nw = 8, ty = (xv & 1) ? 4 : 2;
     geo.ntile = (geo.ny + nw * ty - 5) / (nw * ty - 4);
@@ -2101,9 +2101,9 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     // z-chunks: every chunk re-reads two planes and runs up to five spare ones, so chunks stay
     // >= 64 planes where the grid has 512 (measured: 0.733 -> 0.700 ms at 512^3 against 16) and
     // >= nz / 8 on shallower grids, which need the workgroups
-    const int target = env_int("PB_POSTX_WGCU", 8) * g->ctx->num_cus;
+    const int target = tune("postx_wgcu", 8) * g->ctx->num_cus;
     int nchunk = std::max(1, (target + columns - 1) / columns);
-    const int minz = std::min(env_int("PB_POSTX_MINZ", 64), std::max(16, geo.nzl / 8));
+    const int minz = std::min(tune("postx_minz", 64), std::max(16, geo.nzl / 8));
     nchunk = std::min(nchunk, std::max(1, geo.nzl / minz));
     geo.kc = (geo.nzl + nchunk - 1) / nchunk;
     geo.kc = (geo.kc + 3) & ~3;  // chunk starts at multiples of 4 (the unrolled kernels' parities)
@@ -2161,7 +2161,7 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
   // rows shared through LDS: 1 = presmooth_restrict_xch_kernel, 2 = the same with the plane loop
   // unrolled by four (presmooth_restrict_u4_kernel; compile-time colours: k0 = 0, even chunk
   // starts), both 8 waves x 4 rows; 0 = the per-wave kernel below
-  const int xv = env_int("PB_PRRX", 2);
+  const int xv = tune("prrx", 2);
   if (xv == 1 || xv == 2) {
     constexpr int nw = 8, ty = 4;
     geo.ntile = (geo.ny + nw * ty - 9) / (nw * ty - 8);
@@ -2174,9 +2174,9 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     // box). So: at most one workgroup per CU when that keeps chunks of >= PB_PRRX_LONGZ planes,
     // else ~4 per CU (256^3 and smaller grids)
     int nchunk = std::max(1, g->ctx->num_cus / columns);
-    if (geo.nzl / nchunk < env_int("PB_PRRX_LONGZ", 128))
-      nchunk = std::max(1, (env_int("PB_PRRX_WGCU", 4) * g->ctx->num_cus + columns - 1) / columns);
-    nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_PRRX_MINZ", 16)));
+    if (geo.nzl / nchunk < tune("prrx_longz", 128))
+      nchunk = std::max(1, (tune("prrx_wgcu", 4) * g->ctx->num_cus + columns - 1) / columns);
+    nchunk = std::min(nchunk, std::max(1, geo.nzl / tune("prrx_minz", 16)));
     geo.kc = (geo.nzl + nchunk - 1) / nchunk;
     geo.kc += geo.kc & 1;
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
@@ -2192,9 +2192,9 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
   // chunks of an even number of planes (the restriction pairs them); each chunk also forms S1 on
   // three planes and the residual on two planes outside it, so chunks stay long
   const int columns = geo.nseg * geo.ntile;
-  const int target = env_int("PB_PRR_WGCU", 4) * g->ctx->num_cus;
+  const int target = tune("prr_wgcu", 4) * g->ctx->num_cus;
   int nchunk = std::max(1, (target + columns - 1) / columns);
-  nchunk = std::min(nchunk, std::max(1, geo.nzl / env_int("PB_PRR_MINZ", 32)));
+  nchunk = std::min(nchunk, std::max(1, geo.nzl / tune("prr_minz", 32)));
   geo.kc = (geo.nzl + nchunk - 1) / nchunk;
   geo.kc += geo.kc & 1;
   geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
@@ -2214,7 +2214,7 @@ int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double
   Sweep2Geo geo;
   const int64_t nblocks = sweep2_geo(g, geo);
   PB_TRY(sweep2_ghosts(g, b, b, geo));
-  if (env_int("PB_MG_PRESMOOTH_SLIM", 1)) {  // one double per pair in the x queue
+  if (tune("mg_presmooth_slim", 1)) {  // one double per pair in the x queue
     auto kern = geo.split ? presmooth_resid_kernel<true> : presmooth_resid_kernel<false>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0, g->ctx->stream, geo,
                        s.cx, s.cy, s.cz, s.cc, omega, b, x, res, skip);

@@ -19,39 +19,47 @@
 namespace pb {
 
 // ---- field allocations (pb_internal.hpp) ----
-namespace {
-std::mutex g_field_mu;
-std::unordered_map<void*, void*> g_field_base;  // staggered pointer -> allocation base
-unsigned g_field_count = 0;
-}  // namespace
-
-hipError_t field_alloc(void** p, size_t bytes) {
-  static const int contiguous = env_int("PB_ALLOC_CONTIGUOUS", 0);
-  static const size_t stagger = (size_t)std::max(0, env_int("PB_ALLOC_STAGGER", 0)) & ~(size_t)255;
-  std::lock_guard<std::mutex> lk(g_field_mu);
-  const size_t off = stagger * (g_field_count++ % 8);
-  void* base = nullptr;
-  const hipError_t e = contiguous
-                           ? hipExtMallocWithFlags(&base, bytes + off, hipDeviceMallocContiguous)
-                           : hipMalloc(&base, bytes + off);
-  if (e != hipSuccess) return e;
-  *p = static_cast<char*>(base) + off;
-  if (off) g_field_base[*p] = base;
-  return hipSuccess;
-}
+hipError_t field_alloc(void** p, size_t bytes) { return hipMalloc(p, bytes); }
 
 void field_free(void* p) {
-  if (!p) return;
-  void* base = p;
-  {
-    std::lock_guard<std::mutex> lk(g_field_mu);
-    auto it = g_field_base.find(p);
-    if (it != g_field_base.end()) {
-      base = it->second;
-      g_field_base.erase(it);
-    }
-  }
-  (void)hipFree(base);
+  if (p) (void)hipFree(p);
+}
+
+// ---- tuning table (pb_tune_set; pb_internal.hpp tune()) ----
+namespace {
+std::mutex g_tune_mu;
+std::unordered_map<std::string, int> g_tune;
+// every name a kernel launcher consults; the defaults live at the call sites (the measured
+// choices), the table only holds values a caller set
+const char* const kTuneNames[] = {
+    "cg_defer_x", "cg_fold", "cg_fuse", "cg_pstore_b", "compact_lines", "fft_blocks_per_cu",
+    "fft_pf_strided", "fft_poll", "fft_reg", "fft_remap", "fft_rupd", "fft_stagger", "fft_sums",
+    "fft_tl_long", "fft_tl_z", "fft_yorder", "fft_zorder", "fft_zpad", "fft_zpad_min_plane",
+    "force_comm", "ksp_event_all", "ksp_lazy0", "lines_cfg", "lines_remap", "lines_xdirect",
+    "mg_engine_min_plane", "mg_post_fused", "mg_presmooth_fused", "mg_presmooth_restrict",
+    "mg_presmooth_slim", "mg_prolong_cell", "mg_restrict_z", "mg_restrict_z_min_cols",
+    "mg_sweep2", "mg_tail", "mg_tail_max", "mg_transfer_minz", "mg_transfer_tpc", "passa_nt",
+    "pcr_lines", "postx", "postx_minz", "postx_wgcu", "prr_minz", "prr_wgcu", "prrx", "prrx_longz",
+    "prrx_minz", "prrx_wgcu", "sor_omega_any", "stencil_blocks", "stencil_kcmin", "stencil_nt",
+    "stencil_tall", "stencil_tall_min_plane", "stencil_ty", "sweep2_wgcu", "tall_wgcu",
+    "xcd_remap", "zalt"};
+bool tune_known(const char* name) {
+  for (const char* n : kTuneNames)
+    if (strcmp(n, name) == 0) return true;
+  return false;
+}
+}  // namespace
+
+int tune(const char* name, int dflt) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  if (g_tune.empty()) return dflt;
+  auto it = g_tune.find(name);
+  return it == g_tune.end() ? dflt : it->second;
+}
+
+bool tune_is_set(const char* name) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  return g_tune.count(name) != 0;
 }
 
 static thread_local char g_err[1024] = "";
@@ -565,7 +573,7 @@ int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb
     rc = comm_init_bounded(ctx, nranks, id, rank);
   }
   ctx->split = nranks > 1;
-  if (rc == PB_OK && nranks == 1 && env_int("PB_FORCE_COMM", 0)) {
+  if (rc == PB_OK && nranks == 1 && tune("force_comm", 0)) {
     ncclUniqueId id;
     const ncclResult_t r = ncclGetUniqueId(&id);
     rc = r == ncclSuccess ? comm_init_bounded(ctx, 1, id, 0)
@@ -666,15 +674,43 @@ int pb_ctx_destroy(pb_ctx* ctx) {
   return PB_OK;
 }
 
+int pb_tune_set(const char* name, int value) {
+  PB_CHECK_ARG(name, "tuning name is NULL");
+  if (!tune_known(name)) return set_error(PB_ERR_ARG, "unknown tuning parameter '%s'", name);
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tune[name] = value;
+  return PB_OK;
+}
+
+int pb_tune_get(const char* name, int* value, int* is_set) {
+  PB_CHECK_ARG(name && value, "bad tuning args");
+  if (!tune_known(name)) return set_error(PB_ERR_ARG, "unknown tuning parameter '%s'", name);
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  auto it = g_tune.find(name);
+  if (is_set) *is_set = it != g_tune.end();
+  if (it != g_tune.end()) *value = it->second;
+  return PB_OK;
+}
+
+int pb_tune_reset(void) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tune.clear();
+  return PB_OK;
+}
+
 int pb_ctx_set_timing(pb_ctx* ctx, int enable) {
+  return pb_ctx_set_timing_filter(ctx, enable, nullptr, 1);
+}
+
+int pb_ctx_set_timing_filter(pb_ctx* ctx, int enable, const char* only, int every) {
   PB_CHECK_ARG(ctx, "ctx is NULL");
   ctx->timing = enable != 0;
-  // PB_TIMING_ONLY (comma-separated phase names): record events around those phases only, so a
-  // timed region is not perturbed by event records around every kernel
+  // only (comma-separated phase names, or NULL / ""): record events around those phases only, and
+  // of each such phase around one launch in `every`, so a timed region is not perturbed by event
+  // records around every kernel
   ctx->timing_only.clear();
   ctx->timer_calls.clear();
-  ctx->timing_every = std::max(1, env_int("PB_TIMING_EVERY", 1));
-  const char* only = getenv("PB_TIMING_ONLY");
+  ctx->timing_every = std::max(1, every);
   if (enable && only && *only) {
     std::string cur;
     for (const char* c = only;; ++c) {

@@ -279,7 +279,7 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   if ((k->opts.pc_type == PB_PC_SOR || k->opts.pc_type == PB_PC_MG ||
        k->opts.pc_type == PB_PC_FFT) && k->opts.check_every > 2)
     k->opts.check_every = 2;
-  if (k->opts.pc_type == PB_PC_FFT) k->opts.check_every = std::max(1, env_int("PB_FFT_POLL", 1));
+  if (k->opts.pc_type == PB_PC_FFT) k->opts.check_every = std::max(1, tune("fft_poll", 1));
   const int pc = k->opts.pc_type;
   if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG &&
       pc != PB_PC_FFT)
@@ -368,14 +368,14 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   // depth 4 (default): 58 instead of 60 B/DoF per iteration, measured 3 % faster at 512^3
   // (profiles/r01/ab_defer_x.txt); the x update sums four alpha p terms instead of adding them
   // one per iteration (rounding-level difference in x only: the history is unaffected)
-  const int dx = env_int("PB_CG_DEFER_X", 4);
+  const int dx = tune("cg_defer_x", 4);
   k->defer_x = dx == 0 ? 0 : (dx == 2 ? 2 : 4);
   if (!fused_kind(k->A->kind)) k->defer_x = 0;  // generic path: x every iteration
   st.defer_x = k->defer_x;
   // p stored by pass B (default): pass A read-only, 56 instead of 58 B/DoF per iteration and
   // the passes closer to their patterns' rates -- 1.29 vs 1.36 ms/iteration at 512^3 on one box
   // (profiles/r02/ab_pst_defer_512.jsonl); PB_CG_PSTORE_B=0 stores p in pass A
-  k->pst = env_int("PB_CG_PSTORE_B", 1) != 0 && fused_kind(k->A->kind) && !k->stored_z();
+  k->pst = tune("cg_pstore_b", 1) != 0 && fused_kind(k->A->kind) && !k->stored_z();
   if (k->pst && !k->r2) {
     const size_t vb = (size_t)g->nlocal * sizeof(double);
     if (field_alloc(&k->r2, vb) != hipSuccess)
@@ -390,7 +390,7 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   // stored z with an operator without a stencil engine (compact A): r0 = b, x0 = 0 and p0 = 0 are
   // implicit -- the setup reads b in place of r, and the first iteration writes p = z, x = alpha p
   // and r = b - alpha w without reading them (three vector passes fewer)
-  k->lazy0 = k->stored_z() && !fused_kind(k->A->kind) && env_int("PB_KSP_LAZY0", 1) != 0;
+  k->lazy0 = k->stored_z() && !fused_kind(k->A->kind) && tune("ksp_lazy0", 1) != 0;
   if (k->stored_z()) {
     // r = b, x = 0, p = 0; z = M^-1 r; sums of z (KSPSolve_CG setup, PC_LEFT)
     const size_t vb = (size_t)g->nlocal * sizeof(double);
@@ -462,10 +462,15 @@ static int enqueue_pc_iteration(pb_ksp* k) {
       ctx->cg_fuse = &cf;
       PB_TRY(op_apply_raw(k->A, p, k->w));
     }
-    if (!cf.fused_z || !cf.fused_dot)
-      return set_error(PB_ERR_STATE, "compact CG fusion did not apply (z %d, dot %d)",
-                       (int)cf.fused_z, (int)cf.fused_dot);
     np = cf.nparts;
+    if (!cf.fused_z) {
+      // a pass did not take the fusion (a launch shape the predicate cannot see): the operator
+      // ran on p_old -- form p and apply again, unfused
+      PB_TRY(launch_cg_generic_p(g, k->z, p, k->d_st, first));
+      OpApplySkip guard(ctx, &k->d_st->done);
+      PB_TRY(op_apply_raw(k->A, p, k->w));
+    }
+    if (!cf.fused_z || !cf.fused_dot) PB_TRY(launch_cg_generic_dot(g, p, k->w, k->d_st, &np));
   } else {
     PB_TRY(launch_cg_generic_p(g, k->z, p, k->d_st, first));  // dinv = 1: z - mu
     {
@@ -476,7 +481,7 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   }
   PB_TRY(cg_finalize_pass_a(ctx, np, k->d_st));
   const double* r_in = first ? k->b->d : k->r;
-  const int rupd = env_int("PB_FFT_RUPD", 1);
+  const int rupd = tune("fft_rupd", 1);
   if (k->fft && rupd && fftpc_fuses_r_update(k->fft)) {
     // r = r_in - alpha w formed by the spectral PC's first pass as it loads r, x = x + alpha p
     // beside it (8 B/DoF and one vector pass fewer)
@@ -587,7 +592,7 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
   // one rank, Jacobi, fused operator: the finalize steps ride in the passes' prologues
   // (PB_CG_FOLD=0 keeps the separate finalize launches)
   const bool fold = C >= 2 && !ctx->split && fused_kind(k->A->kind) && !k->stored_z() &&
-                    env_int("PB_CG_FOLD", 1) != 0;
+                    tune("cg_fold", 1) != 0;
   int64_t n = 0;
   for (; n < iters && !k->stopped; ++n) {
     PB_TRY(enqueue_iteration(k, fold, fold && n > 0));
@@ -595,7 +600,7 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
     // only the iterations the poll below waits for get an event (j = 0 mod C; folded j + 1): an
     // event record between two kernels costs the stream ~6 us of idle time (measured 5.9 us per
     // iteration with one record per iteration; profiles/r02/cg_gaps_*.txt)
-    static const bool every = env_int("PB_KSP_EVENT_ALL", 0) != 0;  // (A/B: one per iteration)
+    const bool every = tune("ksp_event_all", 0) != 0;  // (A/B: one per iteration)
     if (every || hi % C == (fold ? 1 : 0) % C)
       PB_HIP(hipEventRecord(k->ring[hi % R], ctx->stream));
     // lagged, rank-consistent poll: decide on the flag of iteration hi + 1 - C only (folded:

@@ -558,7 +558,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 // exchange of a multi-rank step overlap the interior.
 static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   Geo geo;
-  geo.rev = env_int("PB_ZALT", 1) ? rev : 0;
+  geo.rev = tune("zalt", 1) ? rev : 0;
   geo.k0 = (int)g->k0;
   geo.wrap = 0;
   geo.nx = (int)g->n[0];
@@ -566,8 +566,8 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   geo.nzl = (int)g->nzl;
   geo.plane = g->plane;
   geo.ty = TY;
-  geo.remap = env_int("PB_XCD_REMAP", 1);
-  geo.nt = env_int("PB_STENCIL_NT", 1);
+  geo.remap = tune("xcd_remap", 1);
+  geo.nt = tune("stencil_nt", 1);
   geo.nsegx = (geo.nx + 64 * V - 1) / (64 * V);
   geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
   if (mode == PLANES_BOUNDARY) {
@@ -585,13 +585,13 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   // wgcu (the epilogue's WGCU) workgroups per CU: long z-chunks, few chunk-boundary re-reads.
   // Measured at 512^3: 3 per CU for the matvec and pass A (768 blocks beat 512 even where the
   // registers allow only 2 resident), 1 per CU for pass B
-  int target = env_int("PB_STENCIL_BLOCKS", wgcu * g->ctx->num_cus);
+  int target = tune("stencil_blocks", wgcu * g->ctx->num_cus);
   int nchunk = (target + columns - 1) / columns;
   // z-chunks shorter than PB_STENCIL_KCMIN (64) planes re-read too many boundary planes (2 per
   // chunk): use fewer, longer chunks, but keep at least one workgroup per CU (256^3: 8 chunks of
   // 32 planes instead of 24 of 11, measured 8-15 % faster)
-  const int kcmin = env_int("PB_STENCIL_KCMIN", 64);
-  if (!getenv("PB_STENCIL_BLOCKS") && kcmin > 0 && nk / nchunk < kcmin) {
+  const int kcmin = tune("stencil_kcmin", 64);
+  if (!tune_is_set("stencil_blocks") && kcmin > 0 && nk / nchunk < kcmin) {
     const int floor_cu = (g->ctx->num_cus + columns - 1) / columns;
     nchunk = std::max(nk / kcmin, floor_cu);
   }
@@ -604,7 +604,7 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
 }
 
 static int pick_ty(int ny) {
-  int forced = env_int("PB_STENCIL_TY", 0);
+  int forced = tune("stencil_ty", 0);
   if ((forced == 1 || forced == 2 || forced == 4) && ny % forced == 0) return forced;
   if (ny % 4 == 0) return 4;
   if (ny % 2 == 0) return 2;
@@ -687,17 +687,17 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
   if constexpr (Wide8Of<Epi>::v) {
     const int64_t cols4 = ((g->n[0] + 127) / 128) * ((g->n[1] + kWaves * 4 - 1) / (kWaves * 4));
     const int w = wgcu > 0 ? wgcu : Epi::WGCU;
-    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && !getenv("PB_STENCIL_TY") &&
+    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && !tune_is_set("stencil_ty") &&
         cols4 > (int64_t)w * g->ctx->num_cus)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
   }
   if constexpr (TallOf<Epi>::v) {
-    const int tall = env_int("PB_STENCIL_TALL", 1);  // read per launch (A/B tuning)
-    const int64_t tall_min = env_int("PB_STENCIL_TALL_MIN_PLANE", 512 * 512);
-    if (vec2 && ty == 4 && tall && !getenv("PB_STENCIL_TY") && g->n[1] % 8 == 0 &&
+    const int tall = tune("stencil_tall", 1);  // read per launch (A/B tuning)
+    const int64_t tall_min = tune("stencil_tall_min_plane", 512 * 512);
+    if (vec2 && ty == 4 && tall && !tune_is_set("stencil_ty") && g->n[1] % 8 == 0 &&
         g->plane >= tall_min)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev,
-                            wgcu > 0 ? wgcu : env_int("PB_TALL_WGCU", 1), fold);
+                            wgcu > 0 ? wgcu : tune("tall_wgcu", 1), fold);
   }
   if (vec2) {
     switch (ty) {
@@ -1185,7 +1185,7 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
                      int* nblocks, bool store) {
   ScopedTimer tm(g->ctx,
                  timer_name(mode, "cg_pass_a", "cg_pass_a_interior", "cg_pass_a_boundary"));
-  const int nt_p = env_int("PB_PASSA_NT", 1);  // read per launch (A/B tuning)
+  const int nt_p = tune("passa_nt", 1);  // read per launch (A/B tuning)
   const CombineLoad ld{r, p_old, st, 0.0, 0.0, 0.0};
   if (!store)
     return launch_any(g, s, ld, gp, PassAT<false>{p_new, nt_p}, &st->done, mode, part_off, nblocks);
@@ -1212,7 +1212,7 @@ int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const do
   f.hist = hist;
   f.h_done = h_done;
   f.host_iter = host_iter - 1;  // stage 2 of the previous iteration
-  const int nt_p = env_int("PB_PASSA_NT", 1);
+  const int nt_p = tune("passa_nt", 1);
   const CombineLoad ld{r, p_old, nullptr, 0.0, 0.0, 0.0};
   if (!store)
     return launch_any(g, s, ld, gp, PassAT<false>{p_new, nt_p}, nullptr, PLANES_ALL, 0, nblocks, 0,

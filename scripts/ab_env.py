@@ -1,9 +1,9 @@
-"""A/B environment knobs on the bench: runs `bench.py --no-cpu-baseline` once per (config, rep),
+"""A/B tuning settings on the bench: runs `bench.py --no-cpu-baseline --tune CFG` once per (config, rep),
 interleaved (rep-major) so box drift hits every config alike, and prints one JSON line per run with
 ms/step and the per-kernel averages.
 
-usage: python scripts/ab_env.py REPS 'NAME=VAL[,NAME=VAL]' ['...' ...] [-- extra bench args]
-('-' = no extra variables)"""
+usage: python scripts/ab_env.py REPS 'name=val[,name=val]' ['...' ...] [-- extra bench args]
+('-' = defaults; names as pb_tune_set takes them)"""
 import json
 import os
 import subprocess
@@ -19,12 +19,9 @@ reps, cfgs = int(args[0]), args[1:]
 for rep in range(reps):
     for cfg in cfgs:
         env = dict(os.environ)
-        if cfg != "-":
-            for kv in cfg.split(","):
-                k, v = kv.split("=", 1)
-                env[k] = v
+        tune = [] if cfg == "-" else ["--tune", cfg]
         p = subprocess.run([sys.executable, os.path.join(here, "bench.py"), "--no-cpu-baseline",
-                            "--steps", "100", "--warmup", "10"] + extra,
+                            "--secondary", "0", "--steps", "100", "--warmup", "10"] + tune + extra,
                            env=env, capture_output=True, text=True, timeout=300)
         if p.returncode != 0:
             print(json.dumps({"cfg": cfg, "rep": rep, "rc": p.returncode,

@@ -1,5 +1,5 @@
 """Fast compact Laplacian (pb_compact_lapl_fast, 3-pass factorisation) apply time per grid, with
-per-pass averages (HIP events around each line pass); one JSON line per grid with the PB_LINES_*
+per-pass averages (HIP events around each line pass); one JSON line per grid with the
 knobs in the environment. usage: python scripts/bench_compact.py [n ...]"""
 import json
 import os
@@ -41,7 +41,7 @@ def main():
             if c:
                 passes[nm] = {"ms": round(t / c, 4), "GBps": round(bpd * n ** 3 / (t / c) / 1e6, 1)}
         ctx.set_timing(False)
-        cfg = {kk: v for kk, v in os.environ.items() if kk.startswith("PB_LINES")}
+        cfg = {}
         print(json.dumps({"n": n, "lapl_ms": ms, "GBps_80B": 80 * n ** 3 / ms / 1e6,
                           "frac": 80 * n ** 3 / ms / 1e6 / 8000.0, "passes": passes, "cfg": cfg}),
               flush=True)

@@ -1,5 +1,5 @@
 """Spectral PC apply time (pb_ksp_pc_apply, -pc_type fft) per grid; one JSON line per grid with
-the knobs in the environment (PB_FFT_TL_X / _Y / _Z). usage: python scripts/bench_fft.py [n | nx x ny x nz ...]"""
+the tuning settings. usage: python scripts/bench_fft.py [n | nx x ny x nz ...]"""
 import json
 import os
 import sys
@@ -44,7 +44,7 @@ def main():
             if c:
                 passes[nm] = round(t / c, 4)
         ctx.set_timing(False)
-        cfg = {kk: v for kk, v in os.environ.items() if kk.startswith(("PB_FFT", "PB_LINES"))}
+        cfg = {}
         ndof = n3[0] * n3[1] * n3[2]
         print(json.dumps({"n": n, "pc_apply_ms": ms, "GBps_80B": 80 * ndof / ms / 1e6,
                           "passes_ms": passes, "cfg": cfg}), flush=True)

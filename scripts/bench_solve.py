@@ -80,7 +80,7 @@ def main():
                    "rel_residual": r.norm() / b.norm(),
                    "pc_apply_ms": pc_t["avg_ms"] if pc_t else None,
                    "pc_applies": pc_t, "per_launch": parts}
-            out["cfg"] = {k: v for k, v in os.environ.items() if k.startswith("PB_")}
+            out["cfg"] = {}
             print(json.dumps(out), flush=True)
             r.destroy()
             k.destroy()

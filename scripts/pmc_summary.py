@@ -16,7 +16,7 @@ import sys
 from collections import defaultdict
 
 # bench.py kernel roles -> kernel-name pattern (template arguments of pb::star7_kernel), by where
-# CG stores p: pass A (PB_CG_PSTORE_B=0, key <grid>) or pass B (default, key <grid>/pstore_b)
+# CG stores p: pass A (tuning cg_pstore_b = 0, key <grid>) or pass B (default, key <grid>/pstore_b)
 ROLES = {
     "": {
         "matvec_star7": r"star7_kernel<.*PlainLoad, pb::StoreY>",

@@ -1,7 +1,7 @@
 """A/B the V-cycle kernel knobs at 512^3 on one GPU: PC applies (-pc_type mg) with per-phase
 HIP-event timing, interleaved rounds in ONE process.
 
-PB_TUNE_CONFIGS: JSON list of env dicts. Prints one JSON line per config (median over rounds).
+PB_TUNE_CONFIGS: JSON list of tuning dicts (pb_tune_set names, e.g. {"mg_tail": 0}). Prints one JSON line per config (median over rounds).
 """
 import json
 import os
@@ -23,15 +23,11 @@ k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
 r, z = pb.Vec(da), pb.Vec(da)
 r.set_random(3)
 acc = {i: {nm: [] for nm in names} for i in range(len(configs))}
-base_env = dict(os.environ)
 for rnd in range(rounds):
     for i, cfg in enumerate(configs):
-        for key in set().union(*configs):
-            if key in base_env:
-                os.environ[key] = base_env[key]
-            else:
-                os.environ.pop(key, None)
-        os.environ.update({key: str(v) for key, v in cfg.items()})
+        pb.tune_reset()
+        for key, v in cfg.items():  # tuning table (pb_tune_set), not the environment
+            pb.tune_set(key[3:].lower() if key.startswith("PB_") else key, int(v))
         k.pc_apply(r, z)
         ctx.sync()
         ctx.set_timing(True)

@@ -1,6 +1,6 @@
 """A/B the stencil launch knobs at 512^3 on one GPU, interleaved rounds in ONE process.
 
-PB_TUNE_CONFIGS: JSON list of env dicts (e.g. [{"PB_STENCIL_TY":"4","PB_XCD_REMAP":"0"}, ...]).
+PB_TUNE_CONFIGS: JSON list of tuning dicts (pb_tune_set names, e.g. [{"stencil_ty": 4, "xcd_remap": 0}, ...]).
 Per config and round: 20 matvecs + 16 CG iterations with HIP-event kernel timing.
 Prints one JSON line per config with min/median over rounds.
 """
@@ -25,15 +25,11 @@ A.mult(xt, b)
 y = pb.Vec(da)
 N = da.nlocal
 acc = {i: {"mv": [], "a": [], "b": [], "be": [], "it": []} for i in range(len(configs))}
-base_env = dict(os.environ)
 for rnd in range(rounds):
     for i, cfg in enumerate(configs):
-        for k in set().union(*configs):  # every key any config sets: back to the base env
-            if k in base_env:
-                os.environ[k] = base_env[k]
-            else:
-                os.environ.pop(k, None)
-        os.environ.update({k: str(v) for k, v in cfg.items()})
+        pb.tune_reset()
+        for key, v in cfg.items():  # tuning table (pb_tune_set), not the environment
+            pb.tune_set(key[3:].lower() if key.startswith("PB_") else key, int(v))
         for _ in range(3):
             A.mult(xt, y)
         ctx.sync()
@@ -67,7 +63,7 @@ for rnd in range(rounds):
         acc[i]["it"].append(it_ms)
 for i, cfg in enumerate(configs):
     out = {"cfg": cfg}
-    dfx = int(os.environ.get("PB_CG_DEFER_X", "4"))
+    dfx = int(cfg.get("cg_defer_x", cfg.get("PB_CG_DEFER_X", 4)))
     bx, it_b = {0: (40, 64), 2: (48, 60)}.get(dfx, (64, 58))
     for key, nbytes in (("mv", 16), ("a", 24), ("b", bx), ("be", 24), ("it", it_b)):
         v = acc[i][key]

@@ -24,3 +24,29 @@ def ctx():
     c = pb.Context(0)
     yield c
     c.destroy()
+
+
+class Tuning:
+    """pb_tune_set from tests: the launchers' kernel-selection / launch-shape parameters, named as
+    the library names them ("mg_engine_min_plane") or in the env-style spelling the tests used
+    before the table existed ("PB_MG_ENGINE_MIN_PLANE")."""
+
+    def __init__(self, pb):
+        self.pb = pb
+
+    @staticmethod
+    def name(n):
+        return n[3:].lower() if n.startswith("PB_") else n
+
+    def set(self, name, value):
+        self.pb.tune_set(self.name(name), int(value))
+
+    setenv = set
+
+
+@pytest.fixture
+def tune():
+    import poissbox_amd as pb
+    pb.tune_reset()
+    yield Tuning(pb)
+    pb.tune_reset()

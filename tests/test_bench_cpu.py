@@ -20,11 +20,10 @@ def test_cg_iter_bytes():
     assert bench.cg_iter_bytes(0, 0) == 64
 
 
-def test_pstore_mode_env(monkeypatch):
-    monkeypatch.delenv("PB_CG_PSTORE_B", raising=False)
-    assert bench.pstore_mode() == 1
-    monkeypatch.setenv("PB_CG_PSTORE_B", "0")
-    assert bench.pstore_mode() == 0
+def test_pstore_mode_setting():
+    assert bench.pstore_mode() == 1          # cg_pstore_b unset: the library default
+    assert bench.pstore_mode(1) == 1
+    assert bench.pstore_mode(0) == 0
 
 
 def test_host_info_fields():

@@ -208,11 +208,11 @@ def test_cg_pc_none_and_max_it(ctx):
 
 @pytest.mark.parametrize("defer", ["0", "2", "4"])
 @pytest.mark.parametrize("max_it", [1, 2, 3, 8, 9, 10, 11])
-def test_cg_deferred_x_update(ctx, monkeypatch, defer, max_it):
-    """The solution update deferred over D iterations (PB_CG_DEFER_X = D; 4 is the default):
+def test_cg_deferred_x_update(ctx, defer, max_it, tune):
+    """The solution update deferred over D iterations (tuning cg_defer_x = D; 4 is the default):
     stopping at every position of the cycle (0-3 updates still pending, flushed at the end)
     gives the oracle's x (summation order differs: rounding level) and the same history."""
-    monkeypatch.setenv("PB_CG_DEFER_X", defer)
+    tune.setenv("PB_CG_DEFER_X", defer)
     n3 = (32, 24, 16)
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
@@ -231,7 +231,7 @@ def test_cg_deferred_x_update(ctx, monkeypatch, defer, max_it):
 
 @pytest.mark.parametrize("case", ["rtol", "rtol_tight", "max_it1", "max_it2", "max_it9",
                                   "split_iterate", "check1"])
-def test_cg_folded_finalize_bit_identical(ctx, monkeypatch, case):
+def test_cg_folded_finalize_bit_identical(ctx, case, tune):
     """One-rank Jacobi CG with the finalize steps folded into the passes' prologues (default)
     against the separate finalize launches (PB_CG_FOLD=0): same reason, iteration count,
     history and x, bit for bit -- stopping at every kind of place (rtol inside a poll interval,
@@ -248,7 +248,7 @@ def test_cg_folded_finalize_bit_identical(ctx, monkeypatch, case):
             "split_iterate": ["-ksp_rtol", "1e-7"], "check1": ["-ksp_rtol", "1e-6"]}[case]
     out = {}
     for fold in ("1", "0"):
-        monkeypatch.setenv("PB_CG_FOLD", fold)
+        tune.setenv("PB_CG_FOLD", fold)
         da = pb.DA(ctx, n3)
         P, A, x, bv = pb.initialise_linear_system(da, h)
         bv.set_values(b)
@@ -279,7 +279,7 @@ def test_cg_folded_finalize_bit_identical(ctx, monkeypatch, case):
 @pytest.mark.parametrize("n3", [(64, 32, 16), (512, 512, 8)])
 @pytest.mark.parametrize("fold", ["1", "0"])
 @pytest.mark.parametrize("defer", ["4", "2", "0"])
-def test_cg_pass_b_pstore_bit_identical(ctx, monkeypatch, n3, fold, defer):
+def test_cg_pass_b_pstore_bit_identical(ctx, n3, fold, defer, tune):
     """PB_CG_PSTORE_B=1: pass A only takes p.Ap, pass B re-forms p from (r, p_old), stores it and
     writes the residual into a second buffer. Same arithmetic per value, so reason, iteration count,
     history and x are bit-identical to the default split (p stored by pass A), with and without
@@ -291,11 +291,11 @@ def test_cg_pass_b_pstore_bit_identical(ctx, monkeypatch, n3, fold, defer):
     h = tuple(1.0 / m for m in n3)
     b = O.stencil(O.fill_random(N, SEED), n3, h)
     opts = ["-ksp_rtol", "1e-9", "-ksp_max_it", "60"]
-    monkeypatch.setenv("PB_CG_FOLD", fold)
-    monkeypatch.setenv("PB_CG_DEFER_X", defer)
+    tune.setenv("PB_CG_FOLD", fold)
+    tune.setenv("PB_CG_DEFER_X", defer)
     out = {}
     for pst in ("1", "0"):
-        monkeypatch.setenv("PB_CG_PSTORE_B", pst)
+        tune.setenv("PB_CG_PSTORE_B", pst)
         da = pb.DA(ctx, n3)
         P, A, x, bv = pb.initialise_linear_system(da, h)
         bv.set_values(b)
@@ -736,9 +736,9 @@ MG_KERNELS = {"default": {},
 @pytest.mark.parametrize("pc,n3,levels", [("sor", (16, 12, 8), 0), ("mg", (32, 32, 32), 0),
                                           ("mg", (64, 48, 32), 0), ("mg", (32, 16, 24), 2),
                                           ("mg", (8, 8, 8), 0), ("mg", (256, 256, 32), 0)])
-def test_pc_apply_bit_exact(ctx, monkeypatch, kern, pc, n3, levels):
+def test_pc_apply_bit_exact(ctx, kern, pc, n3, levels, tune):
     for k_, v_ in MG_KERNELS[kern].items():
-        monkeypatch.setenv(k_, v_)
+        tune.setenv(k_, v_)
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
     r = O.fill_random(N, 11)
@@ -755,16 +755,16 @@ def test_pc_apply_bit_exact(ctx, monkeypatch, kern, pc, n3, levels):
 
 
 @pytest.mark.parametrize("m", [64, 128])
-def test_cg_compact_fft_padded_bit_identical(ctx, monkeypatch, m):
+def test_cg_compact_fft_padded_bit_identical(ctx, m, tune):
     """Config 5's CG (compact A, spectral PC, fused passes) with the PC's padded Z buffer:
     reason, iterations, history and x bit-identical to the unpadded run."""
     n3 = (m, m, m)
     h = (2 * np.pi / m,) * 3
     b = O.lapl(O.fill_random(m ** 3, SEED), n3, h)
-    monkeypatch.setenv("PB_FFT_ZPAD_MIN_PLANE", "0")
+    tune.setenv("PB_FFT_ZPAD_MIN_PLANE", "0")
     res = []
     for pad in ("0", "32"):
-        monkeypatch.setenv("PB_FFT_ZPAD", pad)
+        tune.setenv("PB_FFT_ZPAD", pad)
         da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
         A = pb.Mat(da, pb.COMPACT, h)
         x, bv = pb.Vec(da), pb.Vec(da)
@@ -777,11 +777,11 @@ def test_cg_compact_fft_padded_bit_identical(ctx, monkeypatch, m):
 
 @pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("pc,n", [("sor", 32), ("mg", 32), ("mg", 64)])
-def test_cg_sor_mg_matches_oracle(ctx, monkeypatch, kern, pc, n):
+def test_cg_sor_mg_matches_oracle(ctx, kern, pc, n, tune):
     """CG + SOR / MG. 'engine': every level on the stencil-engine kernels, so the last half-sweep
     of each PC apply also takes the CG residual sums (no separate pass)."""
     for k_, v_ in MG_KERNELS[kern].items():
-        monkeypatch.setenv(k_, v_)
+        tune.setenv(k_, v_)
     n3 = (n, n, n)
     N = n ** 3
     h = (1.0 / n,) * 3
@@ -800,12 +800,12 @@ def test_cg_sor_mg_matches_oracle(ctx, monkeypatch, kern, pc, n):
 
 @pytest.mark.parametrize("kern", ["default", "engine", "legacy", "unfused", "nopost",
                                   "norestrict"])
-def test_cg_mg_fused_post_smoothing(ctx, monkeypatch, kern):
+def test_cg_mg_fused_post_smoothing(ctx, kern, tune):
     """x extent >= 128: the V-cycle's post-smoothing runs as ONE fused two-colour pass (out of
     place, with CG's residual sums on level 0); history / solution within the CG bar, PC apply
     bit-identical to the oracle."""
     for k_, v_ in MG_KERNELS[kern].items():
-        monkeypatch.setenv(k_, v_)
+        tune.setenv(k_, v_)
     n3 = (128, 128, 32)
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
@@ -840,10 +840,10 @@ POSTX_SHAPES = [(256, 256, 32), (128, 40, 16), (256, 8, 8), (128, 96, 24), (256,
 
 @pytest.mark.parametrize("postx", ["0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("n3", POSTX_SHAPES)
-def test_mg_post_sweep_variants_bit_exact(ctx, monkeypatch, postx, n3):
-    monkeypatch.setenv("PB_POSTX", postx)
-    monkeypatch.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
-    monkeypatch.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
+def test_mg_post_sweep_variants_bit_exact(ctx, postx, n3, tune):
+    tune.setenv("PB_POSTX", postx)
+    tune.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
+    tune.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
     r = O.fill_random(N, 5)
@@ -861,18 +861,18 @@ def test_mg_post_sweep_variants_bit_exact(ctx, monkeypatch, postx, n3):
 @pytest.mark.parametrize("prrx", ["0", "1", "2"])
 @pytest.mark.parametrize("chunks", [False, True])
 @pytest.mark.parametrize("n3", POSTX_SHAPES)
-def test_mg_presmooth_restrict_variants_bit_exact(ctx, monkeypatch, prrx, chunks, n3):
+def test_mg_presmooth_restrict_variants_bit_exact(ctx, prrx, chunks, n3, tune):
     """Fused pre-smoothing + residual + restriction: rows shared through LDS (PB_PRRX 1 = 8
     waves x 4 rows, 2 = the same with the plane loop unrolled by four) and the per-wave kernel
     (0); short z chunks put chunk seams inside the restriction's plane pairs' neighbourhood."""
-    monkeypatch.setenv("PB_PRRX", prrx)
-    monkeypatch.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
-    monkeypatch.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
+    tune.setenv("PB_PRRX", prrx)
+    tune.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
+    tune.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
     if chunks:
         for k_ in ("PB_PRR_WGCU", "PB_PRRX_WGCU"):
-            monkeypatch.setenv(k_, "64")
+            tune.setenv(k_, "64")
         for k_ in ("PB_PRR_MINZ", "PB_PRRX_MINZ"):
-            monkeypatch.setenv(k_, "2")
+            tune.setenv(k_, "2")
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
     r = O.fill_random(N, 6)
@@ -888,12 +888,12 @@ def test_mg_presmooth_restrict_variants_bit_exact(ctx, monkeypatch, prrx, chunks
 
 
 @pytest.mark.parametrize("postx", ["1", "2", "3", "4"])
-def test_cg_mg_post_sweep_xch_sums(ctx, monkeypatch, postx):
+def test_cg_mg_post_sweep_xch_sums(ctx, postx, tune):
     """The LDS-shared post-smoothing also takes CG's residual sums on level 0 (a partial per
     block): CG + MG history / solution within the CG bar."""
-    monkeypatch.setenv("PB_POSTX", postx)
-    monkeypatch.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
-    monkeypatch.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
+    tune.setenv("PB_POSTX", postx)
+    tune.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
+    tune.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
     n3 = (128, 96, 24)
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
@@ -927,7 +927,7 @@ def test_cg_compact_operator_mg_pc(ctx):
 
 
 @pytest.mark.parametrize("pc", ["fft", "mg"])
-def test_cg_compact_lazy_initial_state(ctx, monkeypatch, pc):
+def test_cg_compact_lazy_initial_state(ctx, pc, tune):
     """Stored-z CG on the compact operator leaves r0 = b, x0 = 0 and p0 = 0 implicit
     (PB_KSP_LAZY0, default on): the setup reads b in place of r and the first iteration writes
     p = z, x = alpha p, r = b - alpha w without reading them. Same reason, iterations, history and
@@ -946,7 +946,7 @@ def test_cg_compact_lazy_initial_state(ctx, monkeypatch, pc):
     x, bv = pb.Vec(da), pb.Vec(da)
     res = {}
     for lazy in ("1", "0"):
-        monkeypatch.setenv("PB_KSP_LAZY0", lazy)
+        tune.setenv("PB_KSP_LAZY0", lazy)
         x.set_random(99)  # stale content
         bv.set_values(b)
         reason, its, hist = pb.solve(Pm, A, x, bv, opts)
@@ -954,7 +954,7 @@ def test_cg_compact_lazy_initial_state(ctx, monkeypatch, pc):
     (r1, i1, h1, x1), (r0, i0, h0, x0) = res["1"], res["0"]
     assert (r1, i1) == (r0, i0) and r1 == 2 and i1 >= 1
     assert np.array_equal(h1, h0) and np.array_equal(x1, x0)
-    monkeypatch.setenv("PB_KSP_LAZY0", "1")
+    tune.setenv("PB_KSP_LAZY0", "1")
     x.set_random(99)
     bv.set_values(np.zeros(N))
     reason, its, hist = pb.solve(Pm, A, x, bv, opts)
@@ -963,7 +963,7 @@ def test_cg_compact_lazy_initial_state(ctx, monkeypatch, pc):
 
 
 @pytest.mark.parametrize("pc,m", [("fft", 64), ("fft", 128), ("mg", 64), ("sor", 64)])
-def test_cg_compact_fused_passes(ctx, monkeypatch, pc, m):
+def test_cg_compact_fused_passes(ctx, pc, m, tune):
     """Stored-z CG on the compact operator with the CgFuse passes (default): the compact Z pass
     forms p = (z - mu) + beta/beta_old p_old (cg_gen_p_kernel's arithmetic) and the X pass takes
     the p . w partial sums. Against PB_CG_FUSE=0 (separate p and dot passes): same reason and
@@ -987,11 +987,11 @@ def test_cg_compact_fused_passes(ctx, monkeypatch, pc, m):
     x, bv = pb.Vec(da), pb.Vec(da)
     res = {}
     for fuse in ("1", "0"):
-        monkeypatch.setenv("PB_CG_FUSE", fuse)
+        tune.setenv("PB_CG_FUSE", fuse)
         bv.set_values(b)
         reason, its, hist = pb.solve(Pm, A, x, bv, opts)
         res[fuse] = (reason, its, np.asarray(hist), x.get_values())
-    monkeypatch.setenv("PB_CG_FUSE", "1")
+    tune.setenv("PB_CG_FUSE", "1")
     (r1, i1, h1, x1), (r0, i0, h0, x0) = res["1"], res["0"]
     assert (r1, i1) == (r0, i0)
     # with the spectral PC the converged norm is rounding noise (~1e-14 of the first): measured
@@ -1012,14 +1012,14 @@ def test_cg_compact_fused_passes(ctx, monkeypatch, pc, m):
 @pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("pc,omega,n3", [("sor", 2.5, (16, 12, 8)), ("mg", 2.2, (16, 16, 16)),
                                          ("mg", 2.2, (32, 32, 32))])
-def test_cg_indefinite_pc(ctx, monkeypatch, kern, pc, omega, n3):
+def test_cg_indefinite_pc(ctx, kern, pc, omega, n3, tune):
     """KSP_DIVERGED_INDEFINITE_PC (PETSc KSPSolve_CG: beta*betaold < 0 at the top of an
     iteration), reached from src/poissbox.f90:296 with -pc_type sor|mg and an SOR factor outside
     (0, 2): same reason, iteration and logged history as the oracle; no norm is logged for the
     iteration that stopped (history length = its)."""
     for k_, v_ in MG_KERNELS[kern].items():
-        monkeypatch.setenv(k_, v_)
-    monkeypatch.setenv("PB_SOR_OMEGA_ANY", "1")  # PETSc's PCSOR would reject omega >= 2
+        tune.setenv(k_, v_)
+    tune.setenv("PB_SOR_OMEGA_ANY", "1")  # PETSc's PCSOR would reject omega >= 2
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
     b = O.stencil(O.fill_random(N, SEED), n3, h)
@@ -1046,13 +1046,13 @@ def test_mg_rejects_odd_extents(ctx):
 @pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("nranks,n", [(2, (16, 16, 32)), (4, (16, 16, 32)), (3, (16, 16, 12)),
                                         (2, (128, 16, 32)), (3, (128, 8, 12))])
-def test_multirank_mg_bit_exact_and_cg(monkeypatch, kern, nranks, n):
+def test_multirank_mg_bit_exact_and_cg(kern, nranks, n, tune):
     """Slab-decomposed V-cycle (halo exchanges per level) equals the single-grid restatement.
 
     nx = 128 cases take the fused two-colour sweeps on the fine level (two-deep z ghosts,
     nzl = 16 and 4 planes per rank)."""
     for k_, v_ in MG_KERNELS[kern].items():
-        monkeypatch.setenv(k_, v_)
+        tune.setenv(k_, v_)
     N = int(np.prod(n))
     h = tuple(1.0 / m for m in n)
     r = O.fill_random(N, 3)
@@ -1120,7 +1120,7 @@ def test_fft_pc_apply_vs_oracle(ctx, n3, compact):
 @pytest.mark.parametrize("pad", [1, 512, 65536])
 @pytest.mark.parametrize("n3", [(64, 64, 64), (128, 64, 256), (96, 96, 96), (64, 64, 512),
                                 (512, 32, 64)])
-def test_fft_pc_padded_z_buffer_bit_identical(ctx, monkeypatch, n3, pad):
+def test_fft_pc_padded_z_buffer_bit_identical(ctx, n3, pad, tune):
     """PB_FFT_ZPAD: the Y forward pass writes a buffer with padded planes, the Z pass runs there
     and the Y inverse pass reads it back; the same operations on the same values, so the PC
     apply is bit-identical to the in-place passes (and so within the oracle bar)."""
@@ -1129,8 +1129,8 @@ def test_fft_pc_padded_z_buffer_bit_identical(ctx, monkeypatch, n3, pad):
     r = O.fill_random(N, 23)
     outs = []
     for zp in ("0", str(pad)):
-        monkeypatch.setenv("PB_FFT_ZPAD", zp)
-        monkeypatch.setenv("PB_FFT_ZPAD_MIN_PLANE", "0")
+        tune.setenv("PB_FFT_ZPAD", zp)
+        tune.setenv("PB_FFT_ZPAD_MIN_PLANE", "0")
         da = pb.DA(ctx, n3)
         P = pb.Mat(da, kind, h)
         k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
@@ -1167,7 +1167,7 @@ def test_cg_fft_pc_matches_oracle(ctx, n3, compact):
 
 
 @pytest.mark.parametrize("n3", [(512, 64, 64), (1024, 32, 64)])
-def test_cg_fft_r_update_fused(ctx, monkeypatch, n3):
+def test_cg_fft_r_update_fused(ctx, n3, tune):
     """512- and 1024-point x lines: the spectral PC's first (register-edge) X pass forms CG's
     residual r = r_in - alpha w as it loads it (PB_FFT_RUPD, default on) with cg_pc_xr_kernel's
     rounding, and x is updated on its own: reason, iterations, history and x bit-identical to the
@@ -1180,7 +1180,7 @@ def test_cg_fft_r_update_fused(ctx, monkeypatch, n3):
     x, bv = pb.Vec(da), pb.Vec(da)
     res = {}
     for rupd in ("1", "0"):
-        monkeypatch.setenv("PB_FFT_RUPD", rupd)
+        tune.setenv("PB_FFT_RUPD", rupd)
         x.set_random(5)
         bv.set_values(b)
         reason, its, hist = pb.solve(A, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "1e-12"])
@@ -1402,16 +1402,14 @@ def test_multirank_cg_compact_operator_mg():
         check_x(xs, xo.reshape(32, -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
 
 
-def test_rccl_code_paths_one_rank_communicator(monkeypatch):
-    """PB_FORCE_COMM=1 gives a 1-rank context an RCCL communicator and the decomposed code paths:
+def test_rccl_code_paths_one_rank_communicator(tune):
+    """force_comm = 1 gives a 1-rank context an RCCL communicator and the decomposed code paths:
     the halo exchange (ncclSend/ncclRecv to self, interior/boundary overlap split), the RCCL
     allreduce of the CG sums, the compact transposes and the MG level halos -- the paths the
     multi-GPU driver runs, exercised on one GPU (two ranks cannot share a device under RCCL)."""
-    os.environ["PB_FORCE_COMM"] = "1"
-    try:
-        ctx = pb.Context(0)
-    finally:
-        del os.environ["PB_FORCE_COMM"]
+    tune.set("force_comm", 1)
+    ctx = pb.Context(0)
+    tune.set("force_comm", 0)
     n3 = (32, 24, 16)
     N = int(np.prod(n3))
     h = tuple(1.0 / m for m in n3)
@@ -1453,7 +1451,7 @@ def test_rccl_code_paths_one_rank_communicator(monkeypatch):
     r = O.fill_random(N, 3)
     ref = O.mg_apply(r, n3, h, pc="mg")
     for k_, v_ in MG_KERNELS["engine"].items():
-        monkeypatch.setenv(k_, v_)
+        tune.setenv(k_, v_)
     da = pb.DA(ctx, n3)
     P, A, _, _ = pb.initialise_linear_system(da, h)
     k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
@@ -1464,16 +1462,14 @@ def test_rccl_code_paths_one_rank_communicator(monkeypatch):
     ctx.destroy()
 
 
-def test_split_apply_timers_cover_whole_applies():
+def test_split_apply_timers_cover_whole_applies(tune):
     """On a decomposed grid a matvec / CG pass A is two launches (interior planes, then the
     boundary planes after the halo exchange). The "stencil" and "cg_pass_a" timers that bench.py
     prices against all owned DoF count one entry per complete apply; the launches keep their own
     "_interior" / "_boundary" names."""
-    os.environ["PB_FORCE_COMM"] = "1"
-    try:
-        ctx = pb.Context(0)
-    finally:
-        del os.environ["PB_FORCE_COMM"]
+    tune.set("force_comm", 1)
+    ctx = pb.Context(0)
+    tune.set("force_comm", 0)
     n3 = (64, 64, 16)
     h = tuple(1.0 / m for m in n3)
     da = pb.DA(ctx, n3)
