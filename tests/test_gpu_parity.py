@@ -1009,6 +1009,34 @@ def test_cg_compact_fused_passes(ctx, pc, m, tune):
     check_x(x1, xo, scale=np.max(np.abs(xo)))
 
 
+@pytest.mark.parametrize("pc", ["fft", "mg"])
+def test_cg_compact_lines_off(ctx, pc, tune):
+    """with the register line solves off (compact_lines = 0: the LDS-PCR passes, which
+    take no CgFuse) stored-z CG on the compact operator must take the unfused iteration, not fail
+    -- reason / its / x against the oracle (fixed 6 iterations for MG)."""
+    m = 64
+    n3 = (m, m, m)
+    h = (2 * np.pi / m,) * 3
+    b = O.lapl(O.fill_random(m ** 3, SEED), n3, h)
+    tune.set("compact_lines", 0)
+    da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+    P = pb.Mat(da, pb.ASSEMBLED27, h)
+    A = pb.Mat(da, pb.COMPACT, h)
+    if pc == "fft":
+        opts, kw = ["-pc_type", pc, "-ksp_rtol", "1e-10"], dict(rtol=1e-10)
+    else:
+        opts = ["-pc_type", pc, "-ksp_rtol", "0", "-ksp_atol", "0", "-ksp_max_it", "6",
+                "-ksp_divtol", "1e300"]
+        kw = dict(rtol=0.0, atol=0.0, dtol=1e300, max_it=6)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    bv.set_values(b)
+    reason, its, hist = pb.solve(A if pc == "fft" else P, A, x, bv, opts)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, pc=pc, op="compact", pc_compact=(pc == "fft"),
+                                  nthreads=8, **kw)
+    assert (reason, its) == (ro, itso)
+    check_x(x.get_values(), xo, scale=np.max(np.abs(xo)))
+
+
 @pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("pc,omega,n3", [("sor", 2.5, (16, 12, 8)), ("mg", 2.2, (16, 16, 16)),
                                          ("mg", 2.2, (32, 32, 32))])
