@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -83,6 +84,14 @@ struct pb_ctx {
   // later collective call returns PB_ERR_COMM at once
   int64_t comm_timeout_ms = 180000;
   bool comm_failed = false;
+  // device-side communication progress: an event after every 4th group of RCCL operations
+  // (pb::CommScope). A wait times out only while such a mark is pending and no mark has completed
+  // for longer than comm_timeout_ms -- local queued work with no communication behind it never
+  // counts, however long it runs
+  std::deque<hipEvent_t> comm_marks;
+  std::vector<hipEvent_t> mark_pool;
+  int64_t comm_groups = 0;
+  int* h_stall = nullptr;  // test hook (tuning "comm_stall_test_ms"): released by comm_fail
   void* shm = nullptr;  // built-in shared-memory host transport (pb_transport.cpp), if attached
   // host transport (tests)
   pb_sendrecv_fn h_sendrecv = nullptr;
@@ -217,6 +226,18 @@ int wait_event(pb_ctx* ctx, hipEvent_t ev, const char* what);
 // mark the context's communication as failed (aborting RCCL) and return PB_ERR_COMM
 int comm_fail(pb_ctx* ctx, const char* fmt, ...);
 #define PB_SYNC(ctx, what) PB_TRY(::pb::wait_stream((ctx), (ctx)->stream, (what)))
+// a group of RCCL operations enqueued on `s`; every 4th (and every forced one) gets an event
+// after it: the progress marks the bounded waits watch (pb_ctx::comm_marks)
+struct CommScope {
+  pb_ctx* ctx;
+  hipStream_t s;
+  bool mark;
+  CommScope(pb_ctx* c, hipStream_t st, bool force = false);
+  ~CommScope();
+};
+// test hook: a kernel on `s` that waits for ctx->h_stall (a peer that never answers), bounded by
+// `ms` of device time so it always ends
+int launch_comm_stall(pb_ctx* ctx, hipStream_t s, int ms);
 #define PB_COMM_OK(ctx)                                                                     \
   do {                                                                                      \
     if ((ctx)->comm_failed)                                                                 \

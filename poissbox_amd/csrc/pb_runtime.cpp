@@ -35,7 +35,7 @@ const char* const kTuneNames[] = {
     "cg_defer_x", "cg_fold", "cg_fuse", "cg_pstore_b", "compact_lines", "fft_blocks_per_cu",
     "fft_pf_strided", "fft_poll", "fft_reg", "fft_remap", "fft_rupd", "fft_stagger", "fft_sums",
     "fft_tl_long", "fft_tl_z", "fft_yorder", "fft_zorder", "fft_zpad", "fft_zpad_min_plane",
-    "force_comm", "ksp_event_all", "ksp_lazy0", "lines_cfg", "lines_remap", "lines_xdirect",
+    "comm_mark_every", "comm_stall_test_ms", "force_comm", "ksp_event_all", "ksp_lazy0", "lines_cfg", "lines_remap", "lines_xdirect",
     "mg_engine_min_plane", "mg_post_fused", "mg_presmooth_fused", "mg_presmooth_restrict",
     "mg_presmooth_slim", "mg_prolong_cell", "mg_restrict_z", "mg_restrict_z_min_cols",
     "mg_sweep2", "mg_tail", "mg_tail_max", "mg_transfer_minz", "mg_transfer_tpc", "passa_nt",
@@ -141,6 +141,7 @@ int comm_fail(pb_ctx* ctx, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+  if (ctx->h_stall) __atomic_store_n(ctx->h_stall, 1, __ATOMIC_RELEASE);  // (test hook)
   if (!ctx->comm_failed) {
     ctx->comm_failed = true;
     fprintf(stderr, "[poissbox rank %d] communication failure: %s\n", ctx->rank, g_err);
@@ -153,12 +154,62 @@ int comm_fail(pb_ctx* ctx, const char* fmt, ...) {
   return PB_ERR_COMM;
 }
 
+static int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+static hipEvent_t take_mark_event(pb_ctx* ctx) {
+  if (!ctx->mark_pool.empty()) {
+    hipEvent_t e = ctx->mark_pool.back();
+    ctx->mark_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  return e;
+}
+
+// retire completed marks; returns how many completed
+static int comm_marks_poll(pb_ctx* ctx) {
+  int done = 0;
+  for (auto it = ctx->comm_marks.begin(); it != ctx->comm_marks.end();) {
+    if (hipEventQuery(*it) == hipSuccess) {
+      ctx->mark_pool.push_back(*it);
+      it = ctx->comm_marks.erase(it);
+      ++done;
+    } else {
+      ++it;
+    }
+  }
+  return done;
+}
+
+CommScope::CommScope(pb_ctx* c, hipStream_t st, bool force) : ctx(c), s(st), mark(false) {
+  const int every = std::max(1, tune("comm_mark_every", 4));
+  mark = force || ctx->comm_groups++ % every == every - 1;
+  if (mark && ctx->comm_marks.size() > 64) (void)comm_marks_poll(ctx);
+}
+
+CommScope::~CommScope() {
+  if (!mark) return;
+  hipEvent_t e = take_mark_event(ctx);
+  (void)hipEventRecord(e, s);
+  ctx->comm_marks.push_back(e);
+}
+
+// Waits for query() to report completion. On a split context the wait is bounded: it fails with
+// PB_ERR_COMM when a communication mark (CommScope) is pending and none has completed for longer
+// than PB_COMM_TIMEOUT_MS (a dead or stalled peer), or on an RCCL asynchronous error. Local work
+// queued ahead of the wait with no communication behind it does not count, however long it runs.
 template <class Query>
 static int bounded_wait(pb_ctx* ctx, Query query, const char* what) {
-  using clk = std::chrono::steady_clock;
-  const auto t0 = clk::now();
+  const int64_t t0 = now_ms();
   // after a failure, drain for a short while only (never block teardown on a dead peer)
   const int64_t limit_ms = ctx->comm_failed ? 5000 : ctx->comm_timeout_ms;
+  (void)comm_marks_poll(ctx);
+  int64_t progress_ms = t0;  // the last time communication was seen to progress (or none pending)
   for (int64_t spin = 0;; ++spin) {
     const hipError_t e = query();
     if (e == hipSuccess) return ctx->comm_failed ? set_error(PB_ERR_COMM, "%s after a "
@@ -173,15 +224,16 @@ static int bounded_wait(pb_ctx* ctx, Query query, const char* what) {
             ar != ncclInProgress)
           return comm_fail(ctx, "%s: RCCL asynchronous error: %s", what, ncclGetErrorString(ar));
       }
-      const int64_t ms =
-          std::chrono::duration_cast<std::chrono::milliseconds>(clk::now() - t0).count();
-      if (ms > limit_ms) {
-        if (ctx->comm_failed)
+      if (ctx->comm_failed) {
+        if (now_ms() - t0 > limit_ms)
           return set_error(PB_ERR_COMM, "%s: still pending after a communication failure", what);
-        // the bound covers everything queued ahead of the wait, local kernels included
-        return comm_fail(ctx, "%s: not done after %lld ms (PB_COMM_TIMEOUT_MS bounds every wait "
-                         "on a multi-rank context, queued local work included); a peer rank is "
-                         "dead or stalled", what, (long long)ms);
+      } else {
+        const int64_t now = now_ms();
+        if (comm_marks_poll(ctx) > 0 || ctx->comm_marks.empty()) progress_ms = now;
+        if (now - progress_ms > limit_ms)
+          return comm_fail(ctx, "%s: communication pending with no progress for %lld ms "
+                           "(PB_COMM_TIMEOUT_MS); a peer rank is dead or stalled", what,
+                           (long long)(now - progress_ms));
       }
     }
     if (spin > 4096) {  // past the first few hundred microseconds: back off
@@ -237,6 +289,7 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi) {
   // Two phases whose issue order pairs correctly even when down == up (2 ranks):
   //   (1) send my lowest plane down, receive the plane above me from up  -> ghost_hi
   //   (2) send my highest plane up,  receive the plane below me from down -> ghost_lo
+  CommScope cs(ctx, ctx->stream);
   PB_NCCL(ncclGroupStart());
   PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->stream));
   PB_NCCL(ncclRecv(g->ghost_hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->stream));
@@ -279,6 +332,7 @@ int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, doub
     return PB_OK;
   }
   // the two-phase order of halo_exchange (pairs correctly when down == up)
+  CommScope cs(ctx, ctx->stream);
   PB_NCCL(ncclGroupStart());
   PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->stream));
   PB_NCCL(ncclRecv(rhi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->stream));
@@ -301,12 +355,15 @@ int halo_begin(pb_grid* g, const double* lo, const double* hi) {
   hipEvent_t tev = nullptr;
   const bool timed = ctx->timing && timer_wanted(ctx, "halo_comm");
   if (timed) timer_begin(ctx, "halo_comm", &tev, ctx->comm_stream);
-  PB_NCCL(ncclGroupStart());
-  PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
-  PB_NCCL(ncclRecv(g->ghost_hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
-  PB_NCCL(ncclSend(hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
-  PB_NCCL(ncclRecv(g->ghost_lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
-  PB_NCCL(ncclGroupEnd());
+  {
+    CommScope cs(ctx, ctx->comm_stream);
+    PB_NCCL(ncclGroupStart());
+    PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
+    PB_NCCL(ncclRecv(g->ghost_hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
+    PB_NCCL(ncclSend(hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
+    PB_NCCL(ncclRecv(g->ghost_lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
+    PB_NCCL(ncclGroupEnd());
+  }
   if (timed) timer_end(ctx, "halo_comm", tev, ctx->comm_stream);
   PB_HIP(hipEventRecord(ctx->ev_done, ctx->comm_stream));
   return PB_OK;
@@ -336,6 +393,7 @@ int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, dou
     return PB_OK;
   }
   if (ctx->comm) {
+    CommScope cs(ctx, ctx->stream);
     PB_NCCL(ncclGroupStart());
     for (int p = 0; p < P; ++p) {
       if (p == ctx->rank) continue;
@@ -390,6 +448,10 @@ int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
   PB_COMM_OK(ctx);
   ScopedTimer tm(ctx, "allreduce");
   if (ctx->h_allreduce) {
+    if (const int stall = tune("comm_stall_test_ms", 0)) {  // test hook: a peer that never answers
+      CommScope cs(ctx, ctx->stream, true);
+      PB_TRY(launch_comm_stall(ctx, ctx->stream, stall));
+    }
     PB_HIP(hipMemcpyAsync(ctx->h_scalars + 16, d_vals, count * sizeof(double), hipMemcpyDeviceToHost,
                           ctx->stream));
     PB_SYNC(ctx, "allreduce staging");
@@ -400,6 +462,7 @@ int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
     PB_SYNC(ctx, "allreduce staging");  // staging buffer is reused by the next call
     return PB_OK;
   }
+  CommScope cs(ctx, ctx->stream);
   PB_NCCL(ncclAllReduce(d_vals, d_vals, (size_t)count, ncclDouble, ncclSum, ctx->comm, ctx->stream));
   return PB_OK;
 }
@@ -659,6 +722,9 @@ int pb_ctx_destroy(pb_ctx* ctx) {
   (void)wait_stream(ctx, ctx->comm_stream, "pb_ctx_destroy");
   if (!ctx->comm_failed) timers_collect(ctx);
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->comm_marks) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->mark_pool) (void)hipEventDestroy(e);
+  if (ctx->h_stall) (void)hipHostFree(ctx->h_stall);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->h_a2a) (void)hipHostFree(ctx->h_a2a);

@@ -276,10 +276,11 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   // iteration with the spectral PC (1-3 iterations per solve: an iteration enqueued ahead of the
   // poll costs its skipped launches, ~0.15 ms of a 512^3 config-5 solve, more than the idle
   // stream time of waiting for each iteration)
-  if ((k->opts.pc_type == PB_PC_SOR || k->opts.pc_type == PB_PC_MG ||
-       k->opts.pc_type == PB_PC_FFT) && k->opts.check_every > 2)
+  // (only clamped down: a caller's explicit smaller interval stands -- ADVICE r03)
+  if ((k->opts.pc_type == PB_PC_SOR || k->opts.pc_type == PB_PC_MG) && k->opts.check_every > 2)
     k->opts.check_every = 2;
-  if (k->opts.pc_type == PB_PC_FFT) k->opts.check_every = std::max(1, tune("fft_poll", 1));
+  if (k->opts.pc_type == PB_PC_FFT)
+    k->opts.check_every = std::min(k->opts.check_every, std::max(1, tune("fft_poll", 1)));
   const int pc = k->opts.pc_type;
   if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG &&
       pc != PB_PC_FFT)

@@ -125,4 +125,25 @@ int vec_reduce(pb_ctx* ctx, int kind, const double* x, const double* y, int64_t 
   return PB_OK;
 }
 
+// Test hook for the bounded waits (tuning "comm_stall_test_ms"): one wave polls a host-mapped
+// flag, as a kernel waiting for a peer that never sends would, until comm_fail sets it -- or, so
+// the kernel always ends, until `ms` of device time have passed (s_memrealtime: 100 MHz).
+__global__ void comm_stall_kernel(const int* flag, uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+         __builtin_amdgcn_s_memrealtime() - t0 < ticks)
+    __builtin_amdgcn_s_sleep(64);
+}
+
+int launch_comm_stall(pb_ctx* ctx, hipStream_t s, int ms) {
+  if (!ctx->h_stall) PB_HIP(hipHostMalloc(&ctx->h_stall, sizeof(int), hipHostMallocMapped));
+  __atomic_store_n(ctx->h_stall, 0, __ATOMIC_RELEASE);
+  int* dflag = nullptr;
+  PB_HIP(hipHostGetDevicePointer((void**)&dflag, ctx->h_stall, 0));
+  hipLaunchKernelGGL(comm_stall_kernel, dim3(1), dim3(64), 0, s, (const int*)dflag,
+                     (uint64_t)ms * 100000ull);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
+}
+
 }  // namespace pb

@@ -49,10 +49,10 @@ def test_failing_host_callback_is_an_error_and_poisons_the_context():
 
 
 @pytest.mark.gpu
-def test_wait_timeout_is_an_error(monkeypatch):
-    """PB_COMM_TIMEOUT_MS bounds every wait of a split context: with 1 ms, waiting for ~1000
-    queued vector updates of a 512x512x128 slab (~0.15 ms each) must fail with PB_ERR_COMM
-    instead of blocking, and the failed context refuses further collectives."""
+def test_long_local_work_is_not_a_comm_timeout(monkeypatch):
+    """PB_COMM_TIMEOUT_MS bounds communication in flight, not local work: with a
+    1 ms bound, waiting for ~1000 queued vector updates of a 512x512x256 slab (~0.3 ms each) on a
+    split context completes, and the context stays usable."""
     monkeypatch.setenv("PB_COMM_TIMEOUT_MS", "1")
     loop = lambda lo, hi: (hi.copy(), lo.copy())  # noqa: E731 - loop-back halo
     ctx = _split_ctx(loop, lambda v: v)
@@ -62,15 +62,44 @@ def test_wait_timeout_is_an_error(monkeypatch):
         y.set_random(1)
         for _ in range(1000):
             x.axpy(1e-3, y)
+        ctx.sync()
+        assert not ctx.comm_failed
+        assert x.norm() > 0
+        for o in (x, y, da):
+            o.destroy()
+    finally:
+        ctx.destroy()
+
+
+@pytest.mark.gpu
+def test_stalled_peer_times_out(monkeypatch, tune):
+    """A communication that starts and never finishes -- the test hook comm_stall_test_ms puts a
+    kernel that waits for a peer's data (a host-mapped flag) inside the allreduce's
+    communication scope -- fails the wait with PB_ERR_COMM after PB_COMM_TIMEOUT_MS (200 ms), the
+    failure releases the waiting kernel, and the failed context refuses further collectives."""
+    import time
+    monkeypatch.setenv("PB_COMM_TIMEOUT_MS", "200")
+    loop = lambda lo, hi: (hi.copy(), lo.copy())  # noqa: E731 - loop-back halo
+    ctx = _split_ctx(loop, lambda v: v)
+    try:
+        da = pb.initialise_grid(ctx, (64, 64, 32))
+        x = pb.Vec(da)
+        x.set_random(1)
+        assert x.norm() > 0                        # the hook off: a normal allreduce
+        tune.set("comm_stall_test_ms", 20000)      # (the kernel ends by itself after 20 s)
+        t0 = time.monotonic()
         with pytest.raises(PbError) as e:
-            ctx.sync()
+            x.norm()
+        took = time.monotonic() - t0
         assert e.value.code == PB_ERR_COMM and "PB_COMM_TIMEOUT_MS" in str(e.value)
+        assert 0.15 < took < 10.0, took            # the bound, not the kernel's own 20 s
         assert ctx.comm_failed
+        tune.set("comm_stall_test_ms", 0)
         with pytest.raises(PbError) as e2:
             x.norm()
         assert e2.value.code == PB_ERR_COMM
-        for o in (x, y, da):
-            o.destroy()
+        x.destroy()
+        da.destroy()
     finally:
         ctx.destroy()
     # a fresh context is unaffected
