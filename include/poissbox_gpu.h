@@ -57,7 +57,11 @@ int pb_lapl_star_coeffs(double dx, double dy, double dz, double c[27]);
 int pb_comm_unique_id(unsigned char uid[128]);
 /* nranks == 1: uid may be NULL. nranks > 1: uid from rank 0's pb_comm_unique_id. The RCCL
  * communicator init is bounded by PB_COMM_TIMEOUT_MS: if not every rank joins in time (a peer
- * died during start-up, or holds another id) the call returns PB_ERR_COMM instead of blocking. */
+ * died during start-up, or holds another id) the call returns PB_ERR_COMM instead of blocking.
+ * The init then still runs on a helper thread inside RCCL's start-up handshake (RCCL's blocking
+ * init cannot be cancelled; its non-blocking form would make every later RCCL call of the hot
+ * path asynchronous): after PB_ERR_COMM from pb_ctx_create the process should exit rather than
+ * retry in-process. */
 int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb_ctx** ctx);
 /* Test transport: route halo exchange and allreduce through host callbacks instead of RCCL
  * (lets several ranks share one GPU in tests). Must be called before any grid is created.
@@ -85,7 +89,9 @@ int pb_ctx_get_rank(const pb_ctx* ctx, int* rank, int* nranks);
  *     a file PB_RENDEZVOUS_DIR/pb_uid_<job> (default /tmp; job = PB_JOB_ID, else MASTER_PORT,
  *     plus torchrun's TORCHELASTIC_RESTART_COUNT), removed once the communicator is up; a file
  *     last written more than PB_RENDEZVOUS_SLACK_S (120) before the reading process started is
- *     a crashed run's leftover and is ignored (likewise the shm segment below);
+ *     taken for a crashed run's leftover and ignored, with a line on stderr -- until the reader
+ *     itself has waited longer than the slack, when it takes the file (a rank started late; a
+ *     stale id then fails the bounded init with PB_ERR_COMM) (likewise the shm segment below);
  *   PB_TRANSPORT=shm (default when ranks outnumber GPUs): a built-in POSIX shared-memory host
  *     transport (halo planes and scalar sums; ranks may share one GPU; no all-to-all, so the
  *     compact operators need RCCL or a host alltoallv callback on a split grid). */

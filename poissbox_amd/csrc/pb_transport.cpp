@@ -96,18 +96,32 @@ double process_start_epoch_s() {
 // an earlier run that died before cleaning up: ignore it. "Before this launch" = more than
 // PB_RENDEZVOUS_SLACK_S (default 120) before this process started (the ranks of one launch start
 // within that of each other).
-bool fresh_enough(const struct stat& st) {
-  static const double start = process_start_epoch_s();
-  if (start <= 0.0) return true;
-  const double slack = std::max(0, env_int("PB_RENDEZVOUS_SLACK_S", 120));
-  const double mtime = (double)st.st_mtim.tv_sec + 1e-9 * (double)st.st_mtim.tv_nsec;
-  return mtime >= start - slack;
-}
-
 int64_t now_ms() {
   return std::chrono::duration_cast<std::chrono::milliseconds>(
              std::chrono::steady_clock::now().time_since_epoch())
       .count();
+}
+
+// ... unless this rank has already waited longer than the slack itself: a rank that
+// starts more than the slack after rank 0 (slow container start, staggered scheduler, a clock
+// that disagrees with the file system's) then takes the file it sees, with a warning -- at worst
+// a stale id, which the bounded communicator init reports as PB_ERR_COMM. `waited_ms`: how long
+// the caller has been waiting for this object; `what` names it in the log line (once per object).
+bool fresh_enough(const struct stat& st, int64_t waited_ms, const char* what) {
+  static const double start = process_start_epoch_s();
+  if (start <= 0.0) return true;
+  const double slack = std::max(0, env_int("PB_RENDEZVOUS_SLACK_S", 120));
+  const double mtime = (double)st.st_mtim.tv_sec + 1e-9 * (double)st.st_mtim.tv_nsec;
+  if (mtime >= start - slack) return true;
+  static std::string logged;
+  const bool accept = (double)waited_ms > 1000.0 * slack;
+  if (logged != std::string(what) + (accept ? "+" : "-")) {
+    logged = std::string(what) + (accept ? "+" : "-");
+    fprintf(stderr, "[poissbox] rendezvous: %s was written %.0f s before this process started "
+            "(PB_RENDEZVOUS_SLACK_S %.0f): %s\n", what, start - mtime, slack,
+            accept ? "accepted after waiting the slack out" : "ignored as stale for now");
+  }
+  return accept;
 }
 
 void nap() {
@@ -211,7 +225,8 @@ int shm_attach(pb_ctx* ctx, const std::string& key, Shm** out) {
     for (;;) {  // rank 0 creates the segment and sizes it; wait for both
       fd = shm_open(name.c_str(), O_RDWR, 0600);
       struct stat st;
-      if (fd >= 0 && fstat(fd, &st) == 0 && (size_t)st.st_size == bytes && fresh_enough(st))
+      if (fd >= 0 && fstat(fd, &st) == 0 && (size_t)st.st_size == bytes &&
+          fresh_enough(st, now_ms() - t0, name.c_str()))
         break;
       if (fd >= 0) close(fd);
       fd = -1;
@@ -284,7 +299,7 @@ int uid_rendezvous(int rank, const std::string& key, unsigned char uid[128], int
     FILE* f = fopen(path.c_str(), "rb");
     if (f) {
       struct stat st;
-      const bool fresh = fstat(fileno(f), &st) == 0 && fresh_enough(st);
+      const bool fresh = fstat(fileno(f), &st) == 0 && fresh_enough(st, now_ms() - t0, path.c_str());
       const size_t got = fresh ? fread(uid, 1, 128, f) : 0;
       fclose(f);
       if (got == 128) return PB_OK;
