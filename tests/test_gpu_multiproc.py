@@ -181,3 +181,33 @@ def test_bench_two_ranks_host_transport():
     for wl in ("compact-fft", "star7-mg"):
         assert sec[wl]["ksp_state"]["reason"] == "CONVERGED_RTOL", sec[wl]
         assert sec[wl]["value"] > 0
+
+
+def test_bench_eight_ranks_default_run_host_transport():
+    """Rehearsal of the driver's N = 8 scaling run on one GPU: `bench.py --gpus 8` with no launcher
+    (self-launch: 8 rank processes), the default workload plus its secondaries (config 5's compact
+    operator with the spectral PC strong-scaled over 8 slabs -- all-to-all transposes on 8 ranks --
+    and CG + MG), over the gloo host transport in place of RCCL (which refuses two ranks on one
+    GPU). One JSON line; every workload converges and reports 8 ranks."""
+    import json
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = REPO
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "4",
+           "--warmup", "1", "--base", "32", "--matvecs", "2", "--sustained", "2",
+           "--transport", "host"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 8 and d["launcher"] == "self" and d["config"]["grid"] == [64, 64, 64]
+    assert len(d["per_rank_comm"]) == 8 and d["value"] > 0
+    sec = d["secondary"]
+    assert "error" not in sec, sec.get("error")
+    assert sec["compact-fft"]["config"]["grid"] == [32, 32, 32]
+    for wl in ("compact-fft", "star7-mg"):
+        assert sec[wl]["n_gpus"] == 8
+        assert sec[wl]["ksp_state"]["reason"] == "CONVERGED_RTOL", sec[wl]
+        assert sec[wl]["ksp_state"]["true_residual_rel"] < 1e-8
+    assert all(r["alltoallv_calls"] > 0 for r in sec["compact-fft"]["per_rank_comm"])
