@@ -8,7 +8,7 @@ O=$R/gpurun_out/close
 mkdir -p $O
 cd $R && PYTEST_ARGS="--timeout 300 --timeout-method thread" bash scripts/gpu_check.sh || exit $?
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 $R/bench.py --steps 50 --warmup 5 --no-cpu-baseline > $O/bench_prof.json 2> $O/bench_prof.err
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 $R/bench.py --steps 50 --warmup 5 --no-cpu-baseline --secondary 0 > $O/bench_prof.json 2> $O/bench_prof.err
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R && bash scripts/gpu_pmc.sh || exit $?
 cd /tmp
