@@ -1073,12 +1073,13 @@ def test_mg_rejects_odd_extents(ctx):
 
 @pytest.mark.parametrize("kern", ["default", "engine"])
 @pytest.mark.parametrize("nranks,n", [(2, (16, 16, 32)), (4, (16, 16, 32)), (3, (16, 16, 12)),
-                                        (2, (128, 16, 32)), (3, (128, 8, 12))])
+                                        (2, (128, 16, 32)), (3, (128, 8, 12)),
+                                        (8, (32, 32, 64)), (8, (128, 16, 64))])
 def test_multirank_mg_bit_exact_and_cg(kern, nranks, n, tune):
     """Slab-decomposed V-cycle (halo exchanges per level) equals the single-grid restatement.
 
     nx = 128 cases take the fused two-colour sweeps on the fine level (two-deep z ghosts,
-    nzl = 16 and 4 planes per rank)."""
+    nzl = 16, 8 and 4 planes per rank); 8 ranks: the GPU count of the driver's scaling runs."""
     for k_, v_ in MG_KERNELS[kern].items():
         tune.setenv(k_, v_)
     N = int(np.prod(n))
