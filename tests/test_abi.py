@@ -65,3 +65,36 @@ def test_options_parse_petsc_names():
     assert (d.rtol, d.atol, d.dtol, d.max_it, d.pc_type) == (1e-5, 1e-50, 1e5, 10000, pb.PC_JACOBI)
     with pytest.raises(pb.PbError):
         pb.ksp_options(["-ksp_type", "gmres"])
+
+
+def test_tuning_table_round_trip():
+    """pb_tune_set / pb_tune_get / pb_tune_reset (host-only): set values read back, unset names
+    report None (the launcher's measured default), unknown names are an error."""
+    pb.tune_reset()
+    assert pb.tune_get("cg_defer_x") is None
+    pb.tune_set("cg_defer_x", 2)
+    pb.tune_set("mg_engine_min_plane", 0)
+    assert pb.tune_get("cg_defer_x") == 2 and pb.tune_get("mg_engine_min_plane") == 0
+    with pytest.raises(pb.PbError):
+        pb.tune_set("no_such_knob", 1)
+    with pytest.raises(pb.PbError):
+        pb.tune_get("PB_CG_DEFER_X")  # the environment spelling is not a tuning name
+    pb.tune_reset()
+    assert pb.tune_get("cg_defer_x") is None
+
+
+def test_library_reads_only_the_documented_environment():
+    """The product library's getenv sites name only the user settings INTEGRATION.md lists (plus
+    the launcher's rank variables): kernel variants are tuning-table entries, not environment
+    knobs."""
+    csrc = os.path.join(REPO, "poissbox_amd", "csrc")
+    names = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".hpp")):
+            src = open(os.path.join(csrc, f)).read()
+            names |= set(re.findall(r'(?:getenv|env_int)\("(PB_[A-Z0-9_]+)"', src))
+    documented = {"PB_COMM_TIMEOUT_MS", "PB_DEVICE", "PB_TRANSPORT", "PB_SHM_SLOT_DOUBLES",
+                  "PB_RENDEZVOUS_DIR", "PB_RENDEZVOUS_SLACK_S", "PB_ROCTX"}
+    assert names <= documented, names - documented
+    integ = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    assert all(f"`{n}" in integ for n in documented)
