@@ -410,6 +410,15 @@ def run_solve_workload(args, pb, ctx, workload, scaling, steps, warmup, rank, wo
                           "rnorm0": float(hist[0]), "rnorm_last": float(hist[-1]),
                           "true_residual_rel": rel},
         }
+        traffic_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        key = f"{n[0]}x{n[1]}x{n[2]}/{workload}"
+        try:
+            tr = json.load(open(traffic_file)) if world == 1 else {}
+            if roof in tr.get(key, {}):  # PMC bytes per launch of the roofline kernel (one GPU)
+                out["roofline"]["traffic"] = tr[key][roof]["bytes_per_launch"]
+                out["roofline"]["traffic_source"] = tr[key][roof].get("source")
+        except Exception:
+            pass
         if world == 1 and not args.no_cpu_baseline and args.cpu_baseline != "none":
             out["cpu_baseline"] = cpu_solve_baseline(workload, cpu_budget_s)
     for o in (ksp, r, xt, x, b):
