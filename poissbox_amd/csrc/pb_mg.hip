@@ -66,6 +66,7 @@ struct Mg {
   int prolong_cell = 2;
   int restrict_z = 1;    // restriction marching in z per coarse column (PB_MG_RESTRICT_Z) on
   int64_t restrict_z_min_cols = 4096;  // coarse levels of >= this many columns
+  bool tail_attr = false;  // mg_tail_kernel's dynamic-LDS limit raised
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -509,57 +510,86 @@ struct TailLevel {
   double* b;
   double* res;
   Star s;
+  int64_t ox, ob, ores;  // LDS offsets (doubles) of x, b, res when the tail runs in LDS
 };
 static constexpr int kTailMax = 12;
+static constexpr size_t kTailLdsMax = 144 * 1024;  // LDS the tail may take (of 160 KB per CU)
 struct TailArgs {
   TailLevel lv[kTailMax];
   int nl;           // levels in the tail; lv[nl-1] is the coarsest
   int coarse_its;
   int prolong_cell;
   double omega;
+  int lds;          // 1: every tail array lives in LDS (lv[0].b copied in, lv[0].x copied out)
 };
 
 __device__ __forceinline__ const double* wrap_lo(const MgGeo& G, const double* v) {
   return v + (int64_t)(G.nzl - 1) * G.plane;  // one rank: plane -1 is the last plane
 }
 
+// With A.lds the tail's arrays live in the workgroup's LDS (the 16^3, 8^3, 4^3 levels of a 512^3
+// hierarchy: 109 KB): lv[0].b is copied in, lv[0].x copied out at the end, and every step in
+// between reads and writes LDS through the same bodies (generic pointers) -- same operations on
+// the same values, so the same bits; LDS instead of L2 latency on each of the ~35 dependent steps.
 __global__ __launch_bounds__(512) void mg_tail_kernel(TailArgs A, const int* skip) {
   if (skip && *skip) return;
+  extern __shared__ __attribute__((aligned(16))) double tl[];
   const int64_t t0 = threadIdx.x, ts = blockDim.x;
   const double w = A.omega;
-  auto smooth = [&](const TailLevel& L, int color, int mode) {
-    const double* v = mode == 1 ? L.b : L.x;
-    mg_smooth_body(L.G, L.x, L.b, wrap_lo(L.G, v), v, L.s, w, color, mode, t0, ts);
+  // level t's arrays (LDS or global); computed per use, so no array of pointers goes to scratch
+  auto X = [&](int t) { return A.lds ? tl + A.lv[t].ox : A.lv[t].x; };
+  auto Bv = [&](int t) { return A.lds ? tl + A.lv[t].ob : A.lv[t].b; };
+  auto RES = [&](int t) { return A.lds ? tl + A.lv[t].ores : A.lv[t].res; };
+  if (A.lds) {
+    const double* src = A.lv[0].b;
+    double* dst = Bv(0);
+    for (int64_t i = t0; i < A.lv[0].G.nlocal; i += ts) dst[i] = src[i];
+    __syncthreads();
+  }
+  auto smooth = [&](int t, int color, int mode) {
+    const TailLevel& L = A.lv[t];
+    double* x = X(t);
+    const double* b = Bv(t);
+    const double* v = mode == 1 ? b : x;
+    mg_smooth_body(L.G, x, b, wrap_lo(L.G, v), v, L.s, w, color, mode, t0, ts);
     __syncthreads();
   };
   for (int t = 0; t + 1 < A.nl; ++t) {  // down: pre-smooth, residual, restrict
     const TailLevel& F = A.lv[t];
-    smooth(F, 0, 1);
-    mg_residual_body(F.G, F.x, F.b, wrap_lo(F.G, F.x), F.x, F.s, F.res, t0, ts);
+    smooth(t, 0, 1);
+    double* x = X(t);
+    double* res = RES(t);
+    mg_residual_body(F.G, x, Bv(t), wrap_lo(F.G, x), x, F.s, res, t0, ts);
     __syncthreads();
-    mg_restrict_body(F.G, F.res, wrap_lo(F.G, F.res), F.res, A.lv[t + 1].G, A.lv[t + 1].b, t0,
-                     ts);
+    mg_restrict_body(F.G, res, wrap_lo(F.G, res), res, A.lv[t + 1].G, Bv(t + 1), t0, ts);
     __syncthreads();
   }
   {  // coarsest: `coarse_its` symmetric red-black sweeps from zero (coarse_solve's order)
-    const TailLevel& L = A.lv[A.nl - 1];
-    smooth(L, 0, 1);
-    smooth(L, 0, 0);
+    const int c = A.nl - 1;
+    smooth(c, 0, 1);
+    smooth(c, 0, 0);
     for (int it = 1; it < A.coarse_its; ++it) {
-      smooth(L, 1, 0);
-      smooth(L, 0, 0);
+      smooth(c, 1, 0);
+      smooth(c, 0, 0);
     }
   }
   for (int t = A.nl - 2; t >= 0; --t) {  // up: prolongate + correct, post-smooth
     const TailLevel& F = A.lv[t];
     const TailLevel& Cl = A.lv[t + 1];
+    double* xf = X(t);
+    const double* xc = X(t + 1);
     if (A.prolong_cell)
-      mg_prolong_cell_body(F.G, F.x, Cl.G, Cl.x, wrap_lo(Cl.G, Cl.x), Cl.x, t0, ts);
+      mg_prolong_cell_body(F.G, xf, Cl.G, xc, wrap_lo(Cl.G, xc), xc, t0, ts);
     else
-      mg_prolong_body(F.G, F.x, Cl.G, Cl.x, wrap_lo(Cl.G, Cl.x), Cl.x, t0, ts);
+      mg_prolong_body(F.G, xf, Cl.G, xc, wrap_lo(Cl.G, xc), xc, t0, ts);
     __syncthreads();
-    smooth(F, 1, 0);
-    smooth(F, 0, 0);
+    smooth(t, 1, 0);
+    smooth(t, 0, 0);
+  }
+  if (A.lds) {
+    const double* src = X(0);
+    double* dst = A.lv[0].x;
+    for (int64_t i = t0; i < A.lv[0].G.nlocal; i += ts) dst[i] = src[i];
   }
 }
 
@@ -830,11 +860,26 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     A.coarse_its = mg->coarse_its;
     A.prolong_cell = mg->prolong_cell;
     A.omega = mg->omega;
+    int64_t off = 0;
     for (int t = 0; t < A.nl; ++t) {
       const MgLevel& lv = mg->lv[Lt + t];
-      A.lv[t] = TailLevel{lv.geo(), lv.x, lv.b, lv.res, lv.s};
+      A.lv[t] = TailLevel{lv.geo(), lv.x, lv.b, lv.res, lv.s, 0, 0, 0};
+      const int64_t n = (lv.g->nlocal + 1) & ~(int64_t)1;  // 16-byte aligned arrays
+      A.lv[t].ox = off;
+      A.lv[t].ob = off + n;
+      A.lv[t].ores = off + 2 * n;
+      off += (t + 1 < A.nl ? 3 : 2) * n;
     }
-    hipLaunchKernelGGL(mg_tail_kernel, dim3(1), dim3(512), 0, ctx->stream, A, mg->skip);
+    // the tail in LDS when it fits (512^3: 109 KB of the 160 KB per CU)
+    const size_t lds = (size_t)off * sizeof(double);
+    A.lds = tune("mg_tail_lds", 1) && lds <= kTailLdsMax;
+    if (A.lds && !mg->tail_attr) {
+      PB_HIP(hipFuncSetAttribute((const void*)mg_tail_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTailLdsMax));
+      mg->tail_attr = true;
+    }
+    hipLaunchKernelGGL(mg_tail_kernel, dim3(1), dim3(512), A.lds ? lds : 0, ctx->stream, A,
+                       mg->skip);
     PB_HIP(hipGetLastError());
   } else {
     ScopedTimer t3(ctx, L > 1 ? "mg_coarse_levels" : "mg_fine_smooth_first");
