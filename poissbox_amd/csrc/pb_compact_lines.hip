@@ -400,7 +400,9 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
       if (PASS == 0 || PASS == 3) {
         if (tn < ntiles) {
           tile_fetch(p, p.in0, base_n, nl_n, pre);
-          if constexpr (CGP) tile_fetch(p, p.in1, base_n, nl_n, pold);
+          // (the first iteration of a lazy-start solve has no p_old: p = z - mu, 8 B/DoF fewer)
+          if constexpr (CGP)
+            if (!p.first) tile_fetch(p, p.in1, base_n, nl_n, pold);
         }
       } else {
         tile_fetch(p, p.in1, base, nl, pre);
@@ -488,7 +490,8 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
       int n0;
       tile_of(t, b0, n0);
       tile_fetch(p, p.in0, b0, n0, pre);
-      if constexpr (CGP) tile_fetch(p, p.in1, b0, n0, pold);
+      if constexpr (CGP)
+        if (!p.first) tile_fetch(p, p.in1, b0, n0, pold);
     }
     for (; t < ntiles; t += gridDim.x) step(t, pre, t + gridDim.x);
   }
