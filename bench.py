@@ -589,9 +589,9 @@ def main():
                     help="back-to-back matvecs of the sustained-rate row (SURVEY §8(d) (i))")
     ap.add_argument("--grid", default=None,
                     help="nx,ny,nz global grid override (diagnostics; default: weak scaling)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak (default): base^3 DoF per GPU; strong: the base^3 grid split "
-                         "over all GPUs (e.g. --base 512 or 1024)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
+                    help="weak (star7-jacobi / star7-mg default): base^3 DoF per GPU; strong "
+                         "(compact-fft default): the base^3 grid split over all GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline", choices=("full", "quick", "none"), default="full",
                     help="SURVEY §8(d) CPU rows: full (default), quick (512^3 only) or none")
@@ -613,8 +613,9 @@ def main():
                          "solve workloads after the headline, under \"secondary\" (1, default)")
     args = ap.parse_args()
     # --scaling defaults to the workload's own (config 5 is a strong-scaling case)
-    if args.workload in SOLVE_WORKLOADS and "--scaling" not in " ".join(sys.argv):
-        args.scaling = SOLVE_WORKLOADS[args.workload]["scaling"]
+    if args.scaling is None:
+        args.scaling = SOLVE_WORKLOADS[args.workload]["scaling"] \
+            if args.workload in SOLVE_WORKLOADS else "weak"
     args.scaling_eff = "strong" if (args.scaling == "strong" and not args.grid) else "weak"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
