@@ -45,6 +45,7 @@ struct Sweep2Geo {
   // N ranks (split): xin's planes -2, -1, nzl, nzl+1 at xg[0..3], b's planes -1 / nzl at
   // bg_lo / bg_hi; one rank reads the periodic wrap in place
   int split;
+  int wsplit = 0;  // > 0: planes per workgroup of the balanced work split (the u4 kernels)
   const double* xg;
   const double* bg_lo;
   const double* bg_hi;
@@ -951,27 +952,19 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_xch_kernel(
 // A chunk runs a whole number of four-plane steps (up to three planes more than it needs; they
 // store nothing). Same operations on the same operands: bit-identical.
 // ---------------------------------------------------------------------------------------------
+// one z-range [kb, ke) of one column (x-segment seg, row tile) of presmooth_restrict_u4_kernel
 template <int NW, int TY>
-__global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
-    Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
+__device__ __forceinline__ void presmooth_restrict_u4_range(
+    const Sweep2Geo& g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
     double omega, const double* __restrict__ b, double* __restrict__ xout,
-    double* __restrict__ bc, const int* skip) {
+    double* __restrict__ bc, int seg, int tile, int kb, int ke, double (&xch)[2][8][NW][64]) {
   static_assert(TY % 2 == 0 && TY >= 2, "whole coarse rows per wave");
   constexpr int RB = NW * TY;
   constexpr int LO = 4;  // first stored block row
   constexpr int SB = RB - 2 * LO;
   constexpr int NCR = TY / 2;
-  __shared__ double xch[2][8][NW][64];  // as presmooth_restrict_xch_kernel's
-  if (skip && *skip) return;
   const double icc = 1.0 / cc;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int bid = xcd_block(g.remap);
-  const int seg = bid % g.nseg;
-  bid /= g.nseg;
-  const int tile = bid % g.ntile;
-  const int chunk = bid / g.ntile;
-  const int kb = chunk * g.kc;  // even (kc even)
-  const int ke = min(kb + g.kc, g.nzl);
   const int nx = g.nx, ny = g.ny, nz = g.nzl;
   if (kb >= nz) return;
   const int g0 = tile * SB - LO;
@@ -1178,6 +1171,45 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     body(std::integral_constant<int, 2>{}, k + 2);
     body(std::integral_constant<int, 3>{}, k + 3);
   }
+}
+
+// Work split (g.wsplit > 0): the columns' planes laid end to end (column-major: column c owns
+// [c nz, (c + 1) nz)) and cut into equal pieces of g.wsplit planes, one per workgroup, so every
+// CU gets the same number of planes whatever the column count (a piece may end one column and
+// start the next: two z-ranges, each with its own few warm-up planes). 512^3: 110 columns of
+// 512 planes as 2 chunks each left 36 of 256 CUs idle. wsplit = 0: g.nchunk chunks of g.kc.
+__device__ __forceinline__ int64_t split_total(const Sweep2Geo& g) {
+  return (int64_t)g.nseg * g.ntile * g.nzl;
+}
+
+template <int NW, int TY>
+__global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
+    Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
+    double omega, const double* __restrict__ b, double* __restrict__ xout,
+    double* __restrict__ bc, const int* skip) {
+  __shared__ double xch[2][8][NW][64];  // as presmooth_restrict_xch_kernel's
+  if (skip && *skip) return;
+  int bid = xcd_block(g.remap);
+  if (g.wsplit > 0) {
+    const int64_t e = min(split_total(g), (int64_t)(bid + 1) * g.wsplit);
+    for (int64_t s = (int64_t)bid * g.wsplit; s < e;) {
+      const int col = (int)(s / g.nzl);
+      const int kb = (int)(s - (int64_t)col * g.nzl);  // even (wsplit, nzl even)
+      const int ke = (int)min((int64_t)g.nzl, kb + (e - s));
+      presmooth_restrict_u4_range<NW, TY>(g, ncx, cplane, cx, cy, cz, cc, omega, b, xout, bc,
+                                          col % g.nseg, col / g.nseg, kb, ke, xch);
+      s += ke - kb;
+      __syncthreads();  // the next range rewrites the exchange slots
+    }
+    return;
+  }
+  const int seg = bid % g.nseg;
+  bid /= g.nseg;
+  const int tile = bid % g.ntile;
+  const int chunk = bid / g.ntile;
+  const int kb = chunk * g.kc;  // even (kc even)
+  presmooth_restrict_u4_range<NW, TY>(g, ncx, cplane, cx, cy, cz, cc, omega, b, xout, bc, seg,
+                                      tile, kb, min(kb + g.kc, g.nzl), xch);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1746,29 +1778,21 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_xch_kernel(
 // shifts one value per row. A chunk runs a whole number of four-plane steps (the last step's
 // extra planes store nothing). Same operations on the same operands: bit-identical.
 // ---------------------------------------------------------------------------------------------
+// one z-range [kb, ke) (kb a multiple of 4) of one column of post_sweep_u4_kernel; CG's
+// residual sums accumulate into acc
 template <bool SUMS, int NW, int TY>
-__global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
-    Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
-    const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
-    double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
+__device__ __forceinline__ void post_sweep_u4_range(
+    const Sweep2Geo& g, const PostGeo& cgeo, double cx, double cy, double cz, double cc,
+    double omega, const double* __restrict__ xs, const double* __restrict__ xc,
+    const double* __restrict__ b, double* __restrict__ xout, double mu, int seg, int tile, int kb,
+    int ke, double (&xch)[2][6][NW][64], double (&acc)[4]) {
   static_assert(TY % 2 == 0 && TY >= 2, "own rows start on an even fine row");
   constexpr int RB = NW * TY;
   constexpr int SB = RB - 4;
   constexpr int NC = TY / 2 + 2;
-  __shared__ double xch[2][6][NW][64];  // as post_sweep_xch_kernel's
-  if (skip && *skip) return;
   const double icc = 1.0 / cc;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  const double mu = SUMS ? st->mu : 0.0;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int bid = xcd_block(g.remap);
-  const int seg = bid % g.nseg;
-  bid /= g.nseg;
-  const int tile = bid % g.ntile;
-  const int chunk = bid / g.ntile;
   const int nx = g.nx, ny = g.ny, nz = g.nzl;
-  const int kb = chunk * g.kc;  // even (kc even)
-  const int ke = min(kb + g.kc, nz);
   if (kb < nz) {
     const int g0 = tile * SB - 2;
     const int br0 = wid * TY;
@@ -2000,6 +2024,40 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
       body(std::integral_constant<int, 3>{}, k + 3);
     }
   }
+}
+
+// g.wsplit > 0: the balanced work split of presmooth_restrict_u4_kernel (pieces of a multiple of
+// 4 planes, so every z-range starts on a multiple of 4)
+template <bool SUMS, int NW, int TY>
+__global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
+    Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
+    const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
+    double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
+  __shared__ double xch[2][6][NW][64];  // as post_sweep_xch_kernel's
+  if (skip && *skip) return;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const double mu = SUMS ? st->mu : 0.0;
+  int bid = xcd_block(g.remap);
+  if (g.wsplit > 0) {
+    const int64_t e = min(split_total(g), (int64_t)(bid + 1) * g.wsplit);
+    for (int64_t s = (int64_t)bid * g.wsplit; s < e;) {
+      const int col = (int)(s / g.nzl);
+      const int kb = (int)(s - (int64_t)col * g.nzl);
+      const int ke = (int)min((int64_t)g.nzl, kb + (e - s));
+      post_sweep_u4_range<SUMS, NW, TY>(g, cgeo, cx, cy, cz, cc, omega, xs, xc, b, xout, mu,
+                                        col % g.nseg, col / g.nseg, kb, ke, xch, acc);
+      s += ke - kb;
+      __syncthreads();  // the next range rewrites the exchange slots
+    }
+  } else {
+    const int seg = bid % g.nseg;
+    bid /= g.nseg;
+    const int tile = bid % g.ntile;
+    const int chunk = bid / g.ntile;
+    const int kb = chunk * g.kc;
+    post_sweep_u4_range<SUMS, NW, TY>(g, cgeo, cx, cy, cz, cc, omega, xs, xc, b, xout, mu, seg,
+                                      tile, kb, min(kb + g.kc, g.nzl), xch, acc);
+  }
   if constexpr (SUMS) block_partials<4>(acc, parts);
 }
 
@@ -2077,6 +2135,20 @@ int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double
   return PB_OK;
 }
 
+// The u4 kernels' balanced work split (Sweep2Geo::wsplit): per_cu workgroups per CU, pieces of a
+// multiple of `align` planes (the kernels' chunk-start parity); per_cu = 0 keeps the chunks.
+// Returns the workgroup count.
+static int64_t balanced_split(const pb_grid* g, Sweep2Geo& geo, int per_cu, int align,
+                              int64_t nblocks) {
+  geo.wsplit = 0;
+  if (per_cu <= 0 || geo.nzl % align) return nblocks;
+  const int64_t total = (int64_t)geo.nseg * geo.ntile * geo.nzl;
+  int64_t w = (total + (int64_t)per_cu * g->ctx->num_cus - 1) / ((int64_t)per_cu * g->ctx->num_cus);
+  w = (w + align - 1) / align * align;
+  geo.wsplit = (int)w;
+  return (total + w - 1) / w;
+}
+
 int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double* xs,
                       const double* xc, const double* b, double* xout, double omega,
                       const int* skip, const CgState* sums_st, int* nparts) {
@@ -2109,11 +2181,12 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     geo.kc = (geo.kc + 3) & ~3;  // chunk starts at multiples of 4 (the unrolled kernels' parities)
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
     nblocks = (int64_t)columns * geo.nchunk;
+    if (xv >= 3 && g->k0 != 0)
+      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: one rank only");
+    if (xv >= 3) nblocks = balanced_split(g, geo, tune("postx_split", 0), 4, nblocks);
     if (sums_st && nblocks * 4 > g->ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
                        (long long)nblocks);
-    if (xv >= 3 && g->k0 != 0)
-      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: one rank only");
     decltype(&post_sweep_u4_kernel<true, 8, 4>) kern;
     if (sums_st)
       kern = xv == 1 ? post_sweep_xch_kernel<true, 8, 4> : xv == 2 ? post_sweep_xch_kernel<true, 8, 2>
@@ -2180,8 +2253,9 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     geo.kc = (geo.nzl + nchunk - 1) / nchunk;
     geo.kc += geo.kc & 1;
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
-    const int64_t nblocks = (int64_t)columns * geo.nchunk;
+    int64_t nblocks = (int64_t)columns * geo.nchunk;
     if (g->k0 != 0) return set_error(PB_ERR_UNSUPPORTED, "fused restriction: one rank only");
+    if (xv == 2) nblocks = balanced_split(g, geo, tune("prrx_split", 0), 2, nblocks);
     auto kern = xv == 1 ? presmooth_restrict_xch_kernel<nw, ty> : presmooth_restrict_u4_kernel<nw, ty>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo,
                        (int)cg->n[0], cg->plane, s.cx, s.cy, s.cz, s.cc, omega, b, xout, bc, skip);

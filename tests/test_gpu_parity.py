@@ -887,11 +887,40 @@ def test_mg_presmooth_restrict_variants_bit_exact(ctx, prrx, chunks, n3, tune):
     k.destroy()
 
 
-@pytest.mark.parametrize("postx", ["1", "2", "3", "4"])
-def test_cg_mg_post_sweep_xch_sums(ctx, postx, tune):
+@pytest.mark.parametrize("split", [1, 2, 7, 64])
+@pytest.mark.parametrize("n3", POSTX_SHAPES)
+def test_mg_u4_balanced_split_bit_exact(ctx, split, n3, tune):
+    """The unrolled fused passes with the balanced work split (prrx_split / postx_split =
+    workgroups per CU): the columns' planes cut into equal pieces, so one workgroup may run the
+    end of one column and the start of the next, or several columns (64 per CU: pieces of 2 or 4
+    planes, shorter than the passes' warm-up) -- PC apply bit-identical to the oracle."""
+    tune.set("prrx_split", split)
+    tune.set("postx_split", split)
+    tune.set("mg_engine_min_plane", 0)
+    tune.set("mg_restrict_z_min_cols", 0)
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    r = O.fill_random(N, 8)
+    ref = O.mg_apply(r, n3, h, pc="mg")
+    da = pb.DA(ctx, n3)
+    P, A, _, _ = pb.initialise_linear_system(da, h)
+    k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
+    rv, zv = pb.Vec(da), pb.Vec(da)
+    rv.set_values(r)
+    k.pc_apply(rv, zv)
+    assert np.array_equal(zv.get_values(), ref)
+    k.destroy()
+
+
+@pytest.mark.parametrize("postx,split", [("1", 0), ("2", 0), ("3", 0), ("4", 0), ("3", 1),
+                                         ("3", 7)])
+def test_cg_mg_post_sweep_xch_sums(ctx, postx, split, tune):
     """The LDS-shared post-smoothing also takes CG's residual sums on level 0 (a partial per
-    block): CG + MG history / solution within the CG bar."""
+    block; split > 0: a partial per balanced-split workgroup, whatever ranges it ran): CG + MG
+    history / solution within the CG bar."""
     tune.setenv("PB_POSTX", postx)
+    tune.set("postx_split", split)
+    tune.set("prrx_split", split)
     tune.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
     tune.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
     n3 = (128, 96, 24)
@@ -1297,6 +1326,67 @@ def test_multirank_cg_compact_fft_register_edges():
     for k0, nk, reason, its, hist, xs in run_ranks(2, body):
         assert (reason, its) == (ro, itso)
         assert abs(hist[0] - ho[0]) / ho[0] < 1e-12
+        check_x(xs, xo.reshape(n3[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
+
+
+def _compact_star_symbol_case(n3):
+    """Config 5's operator with the spectral PC of the 7-point symbol (P = STAR7): the symbols
+    part at the multi-Nyquist modes (compact A near zero there, the star not), so CG runs many
+    iterations -- a long history of the fused compact passes and the spectral PC, which the
+    config-5 solve (A = P, one iteration) cannot give. Fixed iteration count, no convergence
+    test; measured oracle-vs-oracle (1 vs 8 threads) history spread 2.6e-13 at 64^3."""
+    N = int(np.prod(n3))
+    h = tuple(2 * np.pi / m for m in n3)
+    b = O.lapl(O.fill_random(N, SEED), n3, h)
+    return h, b
+
+
+@pytest.mark.parametrize("n3,its", [((32, 32, 32), 40), ((64, 64, 64), 24)])
+def test_cg_compact_star_symbol_fft_history(ctx, n3, its):
+    """Compact A, spectral PC of the 7-point P, fixed iterations: reason, iterations, the whole
+    ||z_k|| history and x against the oracle's same KSPSolve."""
+    h, b = _compact_star_symbol_case(n3)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=its, pc="fft",
+                                  op="compact", pc_compact=False, nthreads=8)
+    assert ro == -3 and itso == its and ho[-1] < 1e-3 * ho[0]
+    da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+    A = pb.Mat(da, pb.COMPACT, h)
+    P = pb.Mat(da, pb.STAR7, h)
+    x, bv = pb.Vec(da), pb.Vec(da)
+    bv.set_values(b)
+    reason, its_g, hist = pb.solve(P, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "0", "-ksp_atol",
+                                                 "0", "-ksp_max_it", str(its), "-ksp_divtol",
+                                                 "1e300"])
+    assert (reason, its_g) == (ro, itso)
+    check_history(hist, ho, bar=HIST_RTOL_PC)
+    check_x(x.get_values(), xo)
+
+
+@pytest.mark.parametrize("nranks,n3", [(2, (32, 32, 32)), (8, (64, 64, 64))])
+def test_multirank_cg_compact_star_symbol_fft_history(nranks, n3):
+    """The same decomposed: z-slab ranks, compact Z passes and the PC's Z pass on y-slabs through
+    the all-to-all transposes (8 ranks: config 5's count), 20 fixed iterations -- every rank's
+    history and x slab against the single-grid oracle."""
+    its = 20
+    h, b = _compact_star_symbol_case(n3)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=its, pc="fft",
+                                  op="compact", pc_compact=False, nthreads=8)
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        A = pb.Mat(da, pb.COMPACT, h)
+        P = pb.Mat(da, pb.STAR7, h)
+        x, bv = pb.Vec(da), pb.Vec(da)
+        bv.set_values(b.reshape(n3[2], -1)[k0:k0 + nk])
+        reason, its_g, hist = pb.solve(P, A, x, bv, ["-pc_type", "fft", "-ksp_rtol", "0",
+                                                     "-ksp_atol", "0", "-ksp_max_it", str(its),
+                                                     "-ksp_divtol", "1e300"])
+        return k0, nk, reason, its_g, hist, x.get_values()
+
+    for k0, nk, reason, its_g, hist, xs in run_ranks(nranks, body):
+        assert (reason, its_g) == (ro, itso)
+        check_history(hist, ho, bar=HIST_RTOL_PC)
         check_x(xs, xo.reshape(n3[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
 
 
