@@ -1173,13 +1173,32 @@ __device__ __forceinline__ void presmooth_restrict_u4_range(
   }
 }
 
-// Work split (g.wsplit > 0): the columns' planes laid end to end (column-major: column c owns
-// [c nz, (c + 1) nz)) and cut into equal pieces of g.wsplit planes, one per workgroup, so every
-// CU gets the same number of planes whatever the column count (a piece may end one column and
-// start the next: two z-ranges, each with its own few warm-up planes). 512^3: 110 columns of
-// 512 planes as 2 chunks each left 36 of 256 CUs idle. wsplit = 0: g.nchunk chunks of g.kc.
-__device__ __forceinline__ int64_t split_total(const Sweep2Geo& g) {
-  return (int64_t)g.nseg * g.ntile * g.nzl;
+// Work split (g.wsplit = W > 0): every workgroup gets W planes of work whatever the column count
+// (512^3: 110 columns of 512 planes as 2 chunks each leave 36 of 256 CUs idle). Bands first:
+// band t = planes [t W, (t + 1) W) of every column, one workgroup per column and band, so the
+// workgroups running together stay at a few z-positions (pieces at scattered planes were 30 %
+// slower at 512^3); then the last, lower band [T W, nz) of all columns laid end to end
+// (column-major) and cut into pieces of W planes -- a piece may run the end of one column and
+// the start of the next, each z-range with its own few warm-up planes. fn(col, kb, ke) per range.
+template <class F>
+__device__ __forceinline__ void split_ranges(const Sweep2Geo& g, int bid, F&& fn) {
+  const int ncol = g.nseg * g.ntile, W = g.wsplit, T = g.nzl / W;
+  if (bid < T * ncol) {
+    const int kb = (bid / ncol) * W;
+    fn(bid % ncol, kb, kb + W);
+    return;
+  }
+  const int k0 = T * W, h = g.nzl - k0;
+  if (h <= 0) return;
+  const int64_t total = (int64_t)ncol * h;
+  const int64_t e = min(total, (int64_t)(bid - T * ncol + 1) * W);
+  for (int64_t s = (int64_t)(bid - T * ncol) * W; s < e;) {
+    const int col = (int)(s / h);
+    const int kb = (int)(s - (int64_t)col * h);
+    const int ke = (int)min((int64_t)h, kb + (e - s));
+    fn(col, k0 + kb, k0 + ke);
+    s += ke - kb;
+  }
 }
 
 template <int NW, int TY>
@@ -1190,17 +1209,12 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
   __shared__ double xch[2][8][NW][64];  // as presmooth_restrict_xch_kernel's
   if (skip && *skip) return;
   int bid = xcd_block(g.remap);
-  if (g.wsplit > 0) {
-    const int64_t e = min(split_total(g), (int64_t)(bid + 1) * g.wsplit);
-    for (int64_t s = (int64_t)bid * g.wsplit; s < e;) {
-      const int col = (int)(s / g.nzl);
-      const int kb = (int)(s - (int64_t)col * g.nzl);  // even (wsplit, nzl even)
-      const int ke = (int)min((int64_t)g.nzl, kb + (e - s));
+  if (g.wsplit > 0) {  // ranges start on even planes (W, nzl even)
+    split_ranges(g, bid, [&](int col, int kb, int ke) {
       presmooth_restrict_u4_range<NW, TY>(g, ncx, cplane, cx, cy, cz, cc, omega, b, xout, bc,
                                           col % g.nseg, col / g.nseg, kb, ke, xch);
-      s += ke - kb;
       __syncthreads();  // the next range rewrites the exchange slots
-    }
+    });
     return;
   }
   const int seg = bid % g.nseg;
@@ -2026,8 +2040,8 @@ __device__ __forceinline__ void post_sweep_u4_range(
   }
 }
 
-// g.wsplit > 0: the balanced work split of presmooth_restrict_u4_kernel (pieces of a multiple of
-// 4 planes, so every z-range starts on a multiple of 4)
+// g.wsplit > 0: the balanced work split of presmooth_restrict_u4_kernel (split_ranges; W a
+// multiple of 4, so every z-range starts on a multiple of 4)
 template <bool SUMS, int NW, int TY>
 __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
     Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
@@ -2038,17 +2052,12 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const double mu = SUMS ? st->mu : 0.0;
   int bid = xcd_block(g.remap);
-  if (g.wsplit > 0) {
-    const int64_t e = min(split_total(g), (int64_t)(bid + 1) * g.wsplit);
-    for (int64_t s = (int64_t)bid * g.wsplit; s < e;) {
-      const int col = (int)(s / g.nzl);
-      const int kb = (int)(s - (int64_t)col * g.nzl);
-      const int ke = (int)min((int64_t)g.nzl, kb + (e - s));
+  if (g.wsplit > 0) {  // ranges start on multiples of 4 (W, nzl multiples of 4)
+    split_ranges(g, bid, [&](int col, int kb, int ke) {
       post_sweep_u4_range<SUMS, NW, TY>(g, cgeo, cx, cy, cz, cc, omega, xs, xc, b, xout, mu,
                                         col % g.nseg, col / g.nseg, kb, ke, xch, acc);
-      s += ke - kb;
       __syncthreads();  // the next range rewrites the exchange slots
-    }
+    });
   } else {
     const int seg = bid % g.nseg;
     bid /= g.nseg;
@@ -2142,11 +2151,12 @@ static int64_t balanced_split(const pb_grid* g, Sweep2Geo& geo, int per_cu, int 
                               int64_t nblocks) {
   geo.wsplit = 0;
   if (per_cu <= 0 || geo.nzl % align) return nblocks;
-  const int64_t total = (int64_t)geo.nseg * geo.ntile * geo.nzl;
+  const int64_t ncol = (int64_t)geo.nseg * geo.ntile, total = ncol * geo.nzl;
   int64_t w = (total + (int64_t)per_cu * g->ctx->num_cus - 1) / ((int64_t)per_cu * g->ctx->num_cus);
-  w = (w + align - 1) / align * align;
+  w = std::min<int64_t>((w + align - 1) / align * align, geo.nzl);
   geo.wsplit = (int)w;
-  return (total + w - 1) / w;
+  const int64_t T = geo.nzl / w, h = geo.nzl - T * w;  // split_ranges: T bands, then the rest
+  return T * ncol + (ncol * h + w - 1) / w;
 }
 
 int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double* xs,
@@ -2255,7 +2265,15 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
     int64_t nblocks = (int64_t)columns * geo.nchunk;
     if (g->k0 != 0) return set_error(PB_ERR_UNSUPPORTED, "fused restriction: one rank only");
-    if (xv == 2) nblocks = balanced_split(g, geo, tune("prrx_split", 0), 2, nblocks);
+    // balanced split (prrx_split workgroups per CU; default: 1 where the chunks above need more
+    // than one round of workgroups -- this pass runs one per CU (254 VGPRs): 512^3's 256^3 level,
+    // 528 workgroups, 0.405 -> 0.382 ms for the coarse levels; on the 512^3 level itself, 220
+    // workgroups in one round, the split was slower, 0.506 -> 0.521 ms, r04/mg/split_ab.jsonl)
+    if (xv == 2) {
+      const int ps = tune("prrx_split", -1);
+      nblocks = balanced_split(g, geo, ps >= 0 ? ps : (nblocks > g->ctx->num_cus ? 1 : 0), 2,
+                               nblocks);
+    }
     auto kern = xv == 1 ? presmooth_restrict_xch_kernel<nw, ty> : presmooth_restrict_u4_kernel<nw, ty>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo,
                        (int)cg->n[0], cg->plane, s.cx, s.cy, s.cz, s.cc, omega, b, xout, bc, skip);
