@@ -187,6 +187,28 @@ def test_cg_matches_petsc_semantics(ctx, n, rtol):
     assert r.norm() <= 1e3 * rtol * np.linalg.norm(b) + 1e-9
 
 
+def test_cg_wide_planes_vs_oracle(ctx):
+    """Planes of 1024 x 1024 (config 4's per-GPU slab width) on one rank: the CG passes run
+    8-row tiles (WIDE8) with the residency cap -- against the oracle: 20 fixed iterations'
+    history, x. (r04 also measured 4 points per lane on 4-row tiles there: no faster,
+    profiles/r04/shapes/slab_v4_ab.jsonl.)"""
+    n3 = (1024, 1024, 16)
+    its = 20
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(N, SEED), n3, h, nthreads=8)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=its,
+                                  nthreads=8)
+    da = pb.DA(ctx, n3)
+    P, A, x, bv = pb.initialise_linear_system(da, h)
+    bv.set_values(b)
+    reason, it, hist = pb.solve(P, A, x, bv, ["-ksp_rtol", "0", "-ksp_atol", "0", "-ksp_max_it",
+                                              str(its), "-ksp_divtol", "1e300"])
+    assert (reason, it) == (ro, itso) == (reason, its)
+    check_history(hist, ho)
+    check_x(x.get_values(), xo)
+
+
 def test_cg_pc_none_and_max_it(ctx):
     n3 = (16, 16, 16)
     h = (1 / 16,) * 3
