@@ -40,7 +40,7 @@ const char* const kTuneNames[] = {
     "mg_presmooth_slim", "mg_prolong_cell", "mg_restrict_z", "mg_restrict_z_min_cols",
     "mg_sweep2", "mg_tail", "mg_tail_lds", "mg_tail_max", "mg_transfer_minz", "mg_transfer_tpc", "passa_nt",
     "pcr_lines", "postx", "postx_minz", "postx_split", "postx_wgcu", "prr_minz", "prr_wgcu", "prrx",
-    "prrx_longz", "prrx_minz", "prrx_split", "prrx_wgcu", "sor_omega_any", "stencil_blocks", "stencil_kcmin", "stencil_nt",
+    "prrx_longz", "prrx_minz", "prrx_split", "prrx_wgcu", "slab_rows", "sor_omega_any", "stencil_blocks", "stencil_kcmin", "stencil_nt",
     "stencil_tall", "stencil_tall_min_plane", "stencil_ty", "sweep2_wgcu", "tall_wgcu",
     "xcd_remap", "zalt"};
 bool tune_known(const char* name) {
