@@ -142,6 +142,14 @@ int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p) {
   return PB_OK;
 }
 
+bool yslab_blocked(const YSlabPlan& p) {
+  const int64_t n = p.nyl.empty() ? 0 : p.nyl[0];
+  if (n <= 0 || (n & (n - 1))) return false;
+  for (int64_t v : p.nyl)
+    if (v != n) return false;
+  return true;
+}
+
 int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy) {
   pb_ctx* ctx = g->ctx;
   {

@@ -51,6 +51,11 @@ struct DhtPass {
   double* out;
   int64_t li, lo, es;  // element e of line (outer, inner) at outer*lo + inner*li + e*es
   int64_t lo_out;      // the output's outer stride (Y passes into / out of the padded buffer)
+  // blocked elements (decomposed Y passes writing / reading the all-to-all buffer directly):
+  // element e of the input at (e >> esh_in) * ebs_in + (e & (2^esh_in - 1)) * es (esh_in = 0:
+  // plain e * es); likewise the output with esh_out / ebs_out / es_out (es_out = 0: es)
+  int esh_in, esh_out;
+  int64_t ebs_in, ebs_out, es_out;
   int ninner, nouter, ntiles_inner;
   const double* w;    // twiddles of the line axis: (re, im) of exp(-2 pi i k / n), k < n
   const double* tab;  // [Lx | Jx | Ly | Jy | Lz | Jz] (SCALE only)
@@ -503,6 +508,18 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
   constexpr int NS = WAVE ? 64 : NT;
   constexpr int NR = (NP + NS - 1) / NS;    // pairs per thread (the last round may be partial)
   const int fid = WAVE ? lane : (int)threadIdx.x;
+  // element offsets (blocked layouts: the decomposed Y passes, strided LAYOUT 0 only)
+  auto eoff_in = [&](int e) -> int64_t {
+    if (LAYOUT == 0 && p.esh_in)
+      return (int64_t)(e >> p.esh_in) * p.ebs_in + (int64_t)(e & ((1 << p.esh_in) - 1)) * p.es;
+    return (int64_t)e * p.es;
+  };
+  const int64_t es_o = p.es_out ? p.es_out : p.es;
+  auto eoff_out = [&](int e) -> int64_t {
+    if (LAYOUT == 0 && p.esh_out)
+      return (int64_t)(e >> p.esh_out) * p.ebs_out + (int64_t)(e & ((1 << p.esh_out) - 1)) * es_o;
+    return (int64_t)e * es_o;
+  };
   // (l, e) of the thread's q-th pair; l = TL (no line) past the tile's pairs
   // (the thread index goes through an empty asm per use: recomputing (l, e) costs a few VALU
   // ops, while letting the compiler hoist every pair's coordinates and addresses out of the tile
@@ -537,7 +554,7 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
     const bool ok = l < nl;
     const int lc = ok ? l : 0, ec = ok ? e : 0;  // selects, not a branch around the load
     if (PB_FFT_ABLATE_TRAFFIC) return dv2{0.0, 0.0};
-    return __builtin_nontemporal_load((const dv2*)(p.in + base + lc * p.li + ec * p.es));
+    return __builtin_nontemporal_load((const dv2*)(p.in + base + lc * p.li + eoff_in(ec)));
   };
   auto fetch = [&](int t) {
     int64_t outer, base;
@@ -632,7 +649,7 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
           v.x = lds[l * LP + lpad(e)];
           v.y = lds[l * LP + lpad(e + 1)];
         }
-        const int64_t a = base + outer * (p.lo_out - p.lo) + l * p.li + e * p.es;
+        const int64_t a = base + outer * (p.lo_out - p.lo) + l * p.li + eoff_out(e);
         if (PB_FFT_ABLATE_TRAFFIC) {
           if (v.x == 12345.678) p.out[a] = v.y;  // keeps the LDS reads (never true on real data)
           continue;
@@ -1098,10 +1115,13 @@ int fftpc_create(pb_grid* g, const double deltas[3], int compact, FftPc** out) {
 }
 
 // one DHT along an axis of the box b (b[2] = planes), in place or from `in`
+// blk (Y passes of a decomposed grid): the output (blk_dir 1) or the input (blk_dir 2) is the
+// y-slab all-to-all buffer, rank blocks [kl][jl][i] in rank order (yslab_blocked)
 static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, const double* in,
                     double* out, const int* skip, int j0 = 0, const double* sr = nullptr,
                     const CgState* st = nullptr, int* np = nullptr,
-                    const RUpdate* ru = nullptr, int64_t pl_in = 0, int64_t pl_out = 0) {
+                    const RUpdate* ru = nullptr, int64_t pl_in = 0, int64_t pl_out = 0,
+                    const YSlabPlan* blk = nullptr, int blk_dir = 0) {
   // pl_in / pl_out: plane strides of in / out (0: nx ny; the Y and Z passes of the padded buffer)
   static const char* names[3] = {"pc_fft_x", "pc_fft_y", "pc_fft_z"};
   ScopedTimer tm(ctx, names[axis]);
@@ -1147,6 +1167,20 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
     p.ninner = (int)nx;
     p.nouter = (int)nz;
     p.order = tune("fft_yorder", 0);
+    if (blk) {  // row (kl, j) of the z-slab lives at block j / nyl, row kl * nyl + j % nyl
+      const int64_t nyl = blk->nyl[0];
+      int sh = 0;
+      while (((int64_t)1 << sh) < nyl) ++sh;
+      if (blk_dir == 1) {
+        p.lo_out = nyl * nx;
+        p.esh_out = sh;
+        p.ebs_out = nz * nyl * nx;
+      } else {
+        p.lo = nyl * nx;
+        p.esh_in = sh;
+        p.ebs_in = nz * nyl * nx;
+      }
+    }
     return launch_dht<0, 0>(ctx, ny, p, skip);
   }
   // axis 2 with the scaling: inner = i, outer = j, elements along k
@@ -1187,20 +1221,32 @@ int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgS
                     f->zplane, f->zplane));
     PB_TRY(dht_axis(ctx, f, b, 1, f->zbuf, z, skip, 0, nullptr, nullptr, nullptr, nullptr,
                     f->zplane, 0));
-  } else {
+  } else if (!grid_split(g)) {
     PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
-    if (!grid_split(g)) {
-      PB_TRY(dht_axis(ctx, f, b, 2, z, z, skip));
+    PB_TRY(dht_axis(ctx, f, b, 2, z, z, skip));
+    PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
+  } else {
+    YSlabPlan yp;
+    double* fy = f->ybuf;
+    PB_TRY(yslab_begin(g, fy + yslab_len(g), &yp));
+    const int64_t by[3] = {g->n[0], yp.ny_me, g->n[2]};
+    if (yslab_blocked(yp) && tune("fft_fuse_transpose", 1)) {
+      // the Y passes write / read the all-to-all buffer in its blocked layout: no pack / unpack
+      // pass (two field copies per apply)
+      PB_TRY(dht_axis(ctx, f, b, 1, z, yp.stage, skip, 0, nullptr, nullptr, nullptr, nullptr, 0,
+                      0, &yp, 1));
+      PB_TRY(alltoallv_device(ctx, yp.stage, yp.zc.data(), fy, yp.yc.data()));
+      PB_TRY(dht_axis(ctx, f, by, 2, fy, fy, skip, (int)yp.j0[ctx->rank]));
+      PB_TRY(alltoallv_device(ctx, fy, yp.yc.data(), yp.stage, yp.zc.data()));
+      PB_TRY(dht_axis(ctx, f, b, 1, yp.stage, z, skip, 0, nullptr, nullptr, nullptr, nullptr, 0,
+                      0, &yp, 2));
     } else {
-      YSlabPlan yp;
-      double* fy = f->ybuf;
-      PB_TRY(yslab_begin(g, fy + yslab_len(g), &yp));
+      PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
       PB_TRY(yslab_to(g, yp, z, fy));
-      const int64_t by[3] = {g->n[0], yp.ny_me, g->n[2]};
       PB_TRY(dht_axis(ctx, f, by, 2, fy, fy, skip, (int)yp.j0[ctx->rank]));
       PB_TRY(yslab_from(g, yp, fy, z));
+      PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
     }
-    PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
   }
   // with sums_st: the residual sums of CG (PB_FFT_SUMS, default on) are taken by the last pass
   const int fused = tune("fft_sums", 1);

@@ -392,6 +392,9 @@ int64_t yslab_len(const pb_grid* g);
 int64_t yslab_aux_len(const pb_grid* g);
 int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p);  // aux: yslab_aux_len doubles
 int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy);
+// equal y-slabs of 2^k rows: a z-slab row (kl, j) sits in the all-to-all buffer at block j >> k,
+// row kl * nyl + (j & (nyl - 1)) -- producers / consumers may address it directly
+bool yslab_blocked(const YSlabPlan& p);
 int yslab_from(pb_grid* g, const YSlabPlan& p, const double* fy, double* f);
 // all-to-all with per-peer counts; blocks are contiguous in rank order on both sides
 int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,

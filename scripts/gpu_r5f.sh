@@ -1,0 +1,7 @@
+# kernel stats of the decomposed config-5 path (force_comm, one GPU)
+set -u
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r5f
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o cf -- python3 $R/bench.py --workload compact-fft --steps 4 --warmup 1 --no-cpu-baseline --tune force_comm=1 > $O/cf.json 2> $O/cf.err
