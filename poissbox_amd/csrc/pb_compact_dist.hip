@@ -172,7 +172,8 @@ int yslab_from(pb_grid* g, const YSlabPlan& p, const double* fy, double* f) {
 // y-slab fields fy, uy, vy and the transpose aux space
 int64_t compact_dist_work_len(const pb_grid* g) { return 3 * yslab_len(g) + yslab_aux_len(g); }
 
-int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double* v, double* work) {
+int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double* v, double* work,
+                        YSlabPlan* plan_out, bool* blocked) {
   const int64_t ny_slab = yslab_len(g);
   double* fy = work;
   double* uy = fy + ny_slab;
@@ -182,6 +183,15 @@ int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double
   PB_TRY(yslab_to(g, p, f, fy));
   const int64_t dy[3] = {g->n[0], p.ny_me, g->n[2]};
   PB_TRY(compact_pass_z(g->ctx, dy, h, fy, uy, vy));
+  if (blocked) *blocked = false;
+  if (plan_out && blocked && yslab_blocked(p) && tune("compact_fuse_transpose", 1)) {
+    // received straight into u, v (nlocal doubles each) in the all-to-all layout
+    PB_TRY(alltoallv_device(g->ctx, uy, p.yc.data(), u, p.zc.data()));
+    PB_TRY(alltoallv_device(g->ctx, vy, p.yc.data(), v, p.zc.data()));
+    *plan_out = p;
+    *blocked = true;
+    return PB_OK;
+  }
   PB_TRY(yslab_from(g, p, uy, u));
   return yslab_from(g, p, vy, v);
 }

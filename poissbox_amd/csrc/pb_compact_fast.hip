@@ -262,10 +262,11 @@ int compact_pass_z(pb_ctx* ctx, const int64_t d[3], double h, const double* f, d
 
 // Y: s = Jy u, t = Ly u + Jy v
 int compact_pass_y(pb_ctx* ctx, const int64_t d[3], double h, const double* u, const double* v,
-                   double* s_, double* t) {
+                   double* s_, double* t, const YSlabPlan* blk_in) {
   const int64_t nx = d[0], ny = d[1], nz = d[2];
   if (ny > kTile) return set_error(PB_ERR_UNSUPPORTED, "compact fast path: n > %d", kTile);
-  if (reg_lines(ny)) return compact_lines_pass(ctx, d, 1, h, u, v, s_, t);
+  if (reg_lines(ny)) return compact_lines_pass(ctx, d, 1, h, u, v, s_, t, blk_in);
+  if (blk_in) return set_error(PB_ERR_ARG, "compact Y pass: blocked input needs the line solves");
   FastPass p{};  // lines along j; tile = consecutive i for fixed k
   p.n = (int)ny;
   p.layout = 0;
@@ -330,7 +331,14 @@ int compact_lapl_fast(pb_grid* g, const double dx[3], const double* f, double* o
   if (!g->ctx->split) {
     PB_TRY(compact_pass_z(g->ctx, d, dx[2], f, u, v));
   } else {  // z-lines span the slabs: transpose to y-slabs, Z pass, transpose u, v back
-    PB_TRY(compact_dist_pass_z(g, dx[2], f, u, v, work + 4 * N));
+    // (with the register line solves on y the Y pass reads u, v straight from the all-to-all
+    // layout: no unpack passes)
+    YSlabPlan bp;
+    bool blocked = false;
+    PB_TRY(compact_dist_pass_z(g, dx[2], f, u, v, work + 4 * N, reg_lines(d[1]) ? &bp : nullptr,
+                               &blocked));
+    PB_TRY(compact_pass_y(g->ctx, d, dx[1], u, v, s_, t, blocked ? &bp : nullptr));
+    return compact_pass_x(g->ctx, d, dx[0], s_, t, out);
   }
   PB_TRY(compact_pass_y(g->ctx, d, dx[1], u, v, s_, t));
   return compact_pass_x(g->ctx, d, dx[0], s_, t, out);

@@ -60,6 +60,10 @@ struct LinePass {
   int first;
   const double* dot_p;
   double* parts;
+  // blocked inputs (lo_in > 0): the decomposed Y pass reads the all-to-all receive buffers --
+  // outer stride lo_in, element e at (e >> esh_in) * ebs_in + (e & (2^esh_in - 1)) * es
+  int64_t lo_in, ebs_in;
+  int esh_in;
 };
 
 static LineOp make_line_op(int kind, int C, double h) {
@@ -247,6 +251,11 @@ __device__ __forceinline__ void tile_fetch(const LinePass& p, const double* __re
                                            int64_t base, int nl, TileRegs<C, LAYOUT, TL, V, NT>& t) {
   using T = TileRegs<C, LAYOUT, TL, V, NT>;
   if (PB_LINES_ABLATE_TRAFFIC) return;
+  int64_t b_in = base;  // base is the output layout's
+  if (p.lo_in) {
+    const int64_t outer = base / p.lo;
+    b_in = outer * p.lo_in + (base - outer * p.lo);
+  }
 #pragma unroll
   for (int r = 0; r < T::R; ++r) {
     int l, e;
@@ -254,7 +263,10 @@ __device__ __forceinline__ void tile_fetch(const LinePass& p, const double* __re
     tile_coord<C, LAYOUT, TL, V>(f, l, e);
     const bool ok = (T::NF % NT == 0 || f < T::NF) && l < nl;
     const int lc = ok ? l : 0, ec = ok ? e : 0;  // selects, not a branch around the load
-    const double* a = src + base + lc * p.li + ec * p.es;
+    const int64_t eo = p.esh_in ? (int64_t)(ec >> p.esh_in) * p.ebs_in +
+                                      (int64_t)(ec & ((1 << p.esh_in) - 1)) * p.es
+                                : (int64_t)ec * p.es;
+    const double* a = src + b_in + lc * p.li + eo;
     if (V == 2) {
       const dv2 w = __builtin_nontemporal_load((const dv2*)a);
       t.v[r][0] = w.x;
@@ -808,7 +820,7 @@ static int launch_lines(pb_ctx* ctx, LinePass& p, int64_t n, int64_t nouter) {
 
 // One pass of the factorised Laplacian with register line solves. axis: 2 = Z, 1 = Y, 0 = X.
 int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, const double* in0,
-                       const double* in1, double* out0, double* out1) {
+                       const double* in1, double* out0, double* out1, const YSlabPlan* blk_in) {
   const int64_t nx = dims[0], ny = dims[1], nz = dims[2];
   const int64_t n = axis == 2 ? nz : (axis == 1 ? ny : nx);
   const int C = (int)(n / 64);
@@ -858,8 +870,17 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
     p.lo = nx * ny;
     p.es = nx;
     p.ninner = (int)nx;
+    if (blk_in) {  // row (kl, j) at block j >> k, row kl * nyl + (j & (nyl - 1))
+      const int64_t nyl = blk_in->nyl[0];
+      int sh = 0;
+      while (((int64_t)1 << sh) < nyl) ++sh;
+      p.lo_in = nyl * nx;
+      p.esh_in = sh;
+      p.ebs_in = nz * nyl * nx;
+    }
     return launch_lines<0, 1>(ctx, p, n, nz);
   }
+  if (blk_in) return set_error(PB_ERR_ARG, "compact lines: blocked input on the Y pass only");
   p.li = nx;
   p.lo = nx * ny;
   p.es = 1;

@@ -365,20 +365,27 @@ inline hipError_t field_alloc(T** p, size_t bytes) {
 // ---- register-resident line solves (pb_compact_lines.hip) ----
 bool compact_lines_supported(int64_t n);
 bool compact_cg_fusable(const pb_grid* g);  // CgFuse applies to the compact operator on g
+struct YSlabPlan;
+// blk_in (Y pass of a decomposed grid): in0 / in1 are the all-to-all receive buffers in their
+// blocked layout (yslab_blocked), not z-slab fields
 int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, const double* in0,
-                       const double* in1, double* out0, double* out1);
+                       const double* in1, double* out0, double* out1,
+                       const YSlabPlan* blk_in = nullptr);
 // batched periodic (alpha,1,alpha) solve in registers (n = 64*C); PB_ERR_UNSUPPORTED otherwise
 int lines_solve_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_stride,
                         int64_t elem_stride, double alpha, double* d);
 // the three passes of the factorised compact Laplacian on a box with complete lines
 int compact_pass_z(pb_ctx* ctx, const int64_t d[3], double h, const double* f, double* u, double* v);
 int compact_pass_y(pb_ctx* ctx, const int64_t d[3], double h, const double* u, const double* v,
-                   double* s, double* t);
+                   double* s, double* t, const YSlabPlan* blk_in = nullptr);
 int compact_pass_x(pb_ctx* ctx, const int64_t d[3], double h, const double* s, const double* t,
                    double* out);
 // ---- multi-rank Z pass: z-slab <-> y-slab all-to-all transposes (compact_dist.cpp) ----
 int64_t compact_dist_work_len(const pb_grid* g);
-int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double* v, double* work);
+// plan_out != nullptr: on equal 2^k-row y-slabs u, v are left in the all-to-all layout (the plan
+// in *plan_out, *blocked = true) for a Y pass that reads them so; otherwise unpacked as z-slabs
+int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double* v, double* work,
+                        YSlabPlan* plan_out = nullptr, bool* blocked = nullptr);
 // z-slab <-> y-slab transposes (rank r holds rows [j0_r, j0_r + nyl_r) of every plane: complete
 // z-lines) for line operations along z on a split grid; pb_compact_dist.hip
 struct YSlabPlan {

@@ -32,7 +32,7 @@ std::unordered_map<std::string, int> g_tune;
 // every name a kernel launcher consults; the defaults live at the call sites (the measured
 // choices), the table only holds values a caller set
 const char* const kTuneNames[] = {
-    "cg_defer_x", "cg_fold", "cg_fuse", "cg_pstore_b", "compact_lines", "fft_blocks_per_cu", "fft_fuse_transpose",
+    "cg_defer_x", "cg_fold", "cg_fuse", "cg_pstore_b", "compact_fuse_transpose", "compact_lines", "fft_blocks_per_cu", "fft_fuse_transpose",
     "fft_pf_strided", "fft_poll", "fft_reg", "fft_remap", "fft_rupd", "fft_stagger", "fft_sums",
     "fft_tl_long", "fft_tl_z", "fft_yorder", "fft_zorder", "fft_zpad", "fft_zpad_min_plane",
     "comm_mark_every", "comm_stall_test_ms", "force_comm", "ksp_event_all", "ksp_lazy0", "lines_cfg", "lines_remap", "lines_xdirect",
