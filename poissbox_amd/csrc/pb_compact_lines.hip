@@ -246,13 +246,15 @@ struct TileRegs {
 #ifndef PB_LINES_ABLATE_TRAFFIC
 #define PB_LINES_ABLATE_TRAFFIC 0  // timing builds only: no global loads / stores in tiled passes
 #endif
-template <int C, int LAYOUT, int TL, int V, int NT>
+// BLK: the input is an all-to-all receive buffer in its blocked layout (LinePass::lo_in, esh_in,
+// ebs_in; the decomposed Y pass, PASS 4); base is the output layout's
+template <bool BLK = false, int C, int LAYOUT, int TL, int V, int NT>
 __device__ __forceinline__ void tile_fetch(const LinePass& p, const double* __restrict__ src,
                                            int64_t base, int nl, TileRegs<C, LAYOUT, TL, V, NT>& t) {
   using T = TileRegs<C, LAYOUT, TL, V, NT>;
   if (PB_LINES_ABLATE_TRAFFIC) return;
-  int64_t b_in = base;  // base is the output layout's
-  if (p.lo_in) {
+  int64_t b_in = base;
+  if constexpr (BLK) {
     const int64_t outer = base / p.lo;
     b_in = outer * p.lo_in + (base - outer * p.lo);
   }
@@ -263,9 +265,9 @@ __device__ __forceinline__ void tile_fetch(const LinePass& p, const double* __re
     tile_coord<C, LAYOUT, TL, V>(f, l, e);
     const bool ok = (T::NF % NT == 0 || f < T::NF) && l < nl;
     const int lc = ok ? l : 0, ec = ok ? e : 0;  // selects, not a branch around the load
-    const int64_t eo = p.esh_in ? (int64_t)(ec >> p.esh_in) * p.ebs_in +
-                                      (int64_t)(ec & ((1 << p.esh_in) - 1)) * p.es
-                                : (int64_t)ec * p.es;
+    int64_t eo = (int64_t)ec * p.es;
+    if constexpr (BLK)
+      eo = (int64_t)(ec >> p.esh_in) * p.ebs_in + (int64_t)(ec & ((1 << p.esh_in) - 1)) * p.es;
     const double* a = src + b_in + lc * p.li + eo;
     if (V == 2) {
       const dv2 w = __builtin_nontemporal_load((const dv2*)a);
@@ -378,8 +380,11 @@ struct LineCfg {
 // CGP (PASS 0, V = 2): in0 = z, in1 = p_old; the tile's input is p = (dinv z - mu) + beta/
 // beta_old p_old (cg_gen_p_kernel's operations, unfused roundings: bit-identical), also stored to
 // p_out as it goes into LDS
-template <int C, int LAYOUT, int PASS, class K, int V, bool CGP = false>
+// PASS_ 4: PASS 1 with its inputs read from the all-to-all receive buffers (tile_fetch BLK)
+template <int C, int LAYOUT, int PASS_, class K, int V, bool CGP = false>
 __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
+  constexpr bool BLK = PASS_ == 4;
+  constexpr int PASS = BLK ? 1 : PASS_;
   static_assert(!CGP || (PASS == 0 && V == 2 && K::PF == 1), "CGP: Z pass, pairs, prefetch");
   if (p.skip && *p.skip) return;
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -404,20 +409,20 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
     tile_of(t, base, nl);
     if (K::PF && tn < ntiles) tile_of(tn, base_n, nl_n);
     __syncthreads();  // previous tile's LDS reads are done
-    if (!K::PF) tile_fetch(p, p.in0, base, nl, pre);
+    if (!K::PF) tile_fetch<BLK>(p, p.in0, base, nl, pre);
     if constexpr (CGP) cg_form_p<C, LAYOUT, TL, V, NT>(p, base, nl, pre, pold);
     tile_put(lds, nl, pre);
     __syncthreads();
     if (K::PF) {
       if (PASS == 0 || PASS == 3) {
         if (tn < ntiles) {
-          tile_fetch(p, p.in0, base_n, nl_n, pre);
+          tile_fetch<BLK>(p, p.in0, base_n, nl_n, pre);
           // (the first iteration of a lazy-start solve has no p_old: p = z - mu, 8 B/DoF fewer)
           if constexpr (CGP)
-            if (!p.first) tile_fetch(p, p.in1, base_n, nl_n, pold);
+            if (!p.first) tile_fetch<BLK>(p, p.in1, base_n, nl_n, pold);
         }
       } else {
-        tile_fetch(p, p.in1, base, nl, pre);
+        tile_fetch<BLK>(p, p.in1, base, nl, pre);
       }
     }
 #pragma unroll
@@ -460,10 +465,10 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
       tile_store<C, LAYOUT, TL, V, NT>(p, p.out0, lds, base, nl);
       __syncthreads();
     }
-    if (!K::PF) tile_fetch(p, p.in1, base, nl, pre);
+    if (!K::PF) tile_fetch<BLK>(p, p.in1, base, nl, pre);
     tile_put(lds, nl, pre);
     __syncthreads();
-    if (K::PF && tn < ntiles) tile_fetch(p, p.in0, base_n, nl_n, pre);
+    if (K::PF && tn < ntiles) tile_fetch<BLK>(p, p.in0, base_n, nl_n, pre);
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
       const int l = wave * LPW + j;
@@ -485,10 +490,10 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
     int64_t b0;
     int n0;
     tile_of(t, b0, n0);
-    tile_fetch(p, p.in0, b0, n0, ra);
+    tile_fetch<BLK>(p, p.in0, b0, n0, ra);
     if (t + G < ntiles) {
       tile_of(t + G, b0, n0);
-      tile_fetch(p, p.in0, b0, n0, rb);
+      tile_fetch<BLK>(p, p.in0, b0, n0, rb);
     }
     for (; t < ntiles; t += 2 * G) {
       step(t, ra, t + 2 * G);
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(K::NT) void compact_lines_kernel(LinePass p) {
       int64_t b0;
       int n0;
       tile_of(t, b0, n0);
-      tile_fetch(p, p.in0, b0, n0, pre);
+      tile_fetch<BLK>(p, p.in0, b0, n0, pre);
       if constexpr (CGP)
         if (!p.first) tile_fetch(p, p.in1, b0, n0, pold);
     }
@@ -768,7 +773,7 @@ static int launch_lines_k(pb_ctx* ctx, LinePass& p, int64_t nouter) {
 template <int C, int LAYOUT, int PASS>
 static int launch_lines_c(pb_ctx* ctx, LinePass& p, int64_t nouter) {
   const int cfg = tune("lines_cfg", 0);
-  if constexpr (C == 4 || C == 8) {
+  if constexpr ((C == 4 || C == 8) && PASS != 4) {  // (A/B configs: not for the blocked Y pass)
     switch (cfg) {
       case 1: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 1>>(ctx, p, nouter);
       case 2: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 8, 1>>(ctx, p, nouter);
@@ -877,6 +882,7 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
       p.lo_in = nyl * nx;
       p.esh_in = sh;
       p.ebs_in = nz * nyl * nx;
+      return launch_lines<0, 4>(ctx, p, n, nz);
     }
     return launch_lines<0, 1>(ctx, p, n, nz);
   }
