@@ -67,6 +67,17 @@ struct Mg {
   int restrict_z = 1;    // restriction marching in z per coarse column (PB_MG_RESTRICT_Z) on
   int64_t restrict_z_min_cols = 4096;  // coarse levels of >= this many columns
   bool tail_attr = false;  // mg_tail_kernel's dynamic-LDS limit raised
+  // Decomposed grids (r04): the coarse levels [La, L) are gathered onto every rank once per
+  // V-cycle (one all-to-all of level La's right-hand side) and run there as the one-launch tail
+  // on full-grid arrays -- instead of a latency-bound halo exchange per half-sweep, residual and
+  // transfer on levels of a few thousand points. La = 0: none. Every rank computes the same
+  // coarse correction (same kernels, same inputs) and prolongates from its own planes of it.
+  int La = 0;
+  double* agg = nullptr;                   // full-grid x, b, res of levels La .. L-1; send staging
+  std::vector<MgGeo> ageo;                 // their full-grid geometry (k0 = 0)
+  std::vector<double*> ax, ab, ares;
+  double* agg_send = nullptr;              // P copies of this rank's level-La slab
+  std::vector<int64_t> agg_sc, agg_rc;     // all-to-all counts (send: own slab; recv: rank q's)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -690,7 +701,56 @@ void mg_destroy(Mg* mg) {
   for (auto& L : mg->lv)
     if (L.own) pb_grid_destroy(L.g);
   if (mg->mem) (void)hipFree(mg->mem);
+  if (mg->agg) (void)hipFree(mg->agg);
   delete mg;
+}
+
+// the agglomerated coarse levels of a decomposed grid (Mg::La): the first level whose whole grid
+// fits the one-launch tail (<= PB_MG_TAIL_MAX points, as on one rank), at least level 1
+static int mg_agglomerate_setup(Mg* mg) {
+  pb_ctx* ctx = mg->ctx;
+  const int L = (int)mg->lv.size();
+  mg->La = 0;
+  if (!ctx->split || L < 2 || !tune("mg_agglomerate", 1)) return PB_OK;
+  const int64_t tail_max = tune("mg_tail_max", 8192);
+  int La = L;
+  for (int l = L - 1; l >= 1; --l) {
+    const MgLevel& v = mg->lv[l];
+    if (v.n[0] * v.n[1] * v.n[2] <= tail_max) La = l;
+    else break;
+  }
+  if (La >= L || L - La > kTailMax) return PB_OK;
+  const int P = ctx->nranks;
+  const MgLevel& A0 = mg->lv[La];
+  int64_t total = 0;
+  for (int l = La; l < L; ++l) {
+    const MgLevel& v = mg->lv[l];
+    total += 3 * ((v.n[0] * v.n[1] * v.n[2] + 1) & ~(int64_t)1);
+  }
+  const int64_t slab = A0.g->nlocal;
+  total += P * slab;
+  if (hipMalloc(&mg->agg, (size_t)total * sizeof(double)) != hipSuccess)
+    return set_error(PB_ERR_ALLOC, "multigrid coarse levels: out of device memory");
+  double* q = mg->agg;
+  for (int l = La; l < L; ++l) {
+    const MgLevel& v = mg->lv[l];
+    const int64_t n = v.n[0] * v.n[1] * v.n[2], n2 = (n + 1) & ~(int64_t)1;
+    mg->ageo.push_back(MgGeo{(int)v.n[0], (int)v.n[1], (int)v.n[2], v.n[0] * v.n[1], n, 0});
+    mg->ax.push_back(q);
+    mg->ab.push_back(q + n2);
+    mg->ares.push_back(q + 2 * n2);
+    q += 3 * n2;
+  }
+  mg->agg_send = q;
+  mg->agg_sc.assign(P, slab);
+  mg->agg_rc.resize(P);
+  for (int r = 0; r < P; ++r) {
+    int64_t k0 = 0, nz = 0;
+    pb_slab_partition(mg->lv[0].g->n[2], P, r, &k0, &nz);
+    mg->agg_rc[r] = (nz >> La) * A0.n[0] * A0.n[1];
+  }
+  mg->La = La;
+  return PB_OK;
 }
 
 int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, int coarse_its,
@@ -763,6 +823,10 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
       p += lv.g->nlocal;
     }
   }
+  if (const int rc = mg_agglomerate_setup(mg); rc != PB_OK) {
+    mg_destroy(mg);
+    return rc;
+  }
   *out = mg;
   return PB_OK;
 }
@@ -794,7 +858,8 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
   pb_ctx* ctx = mg->ctx;
   // the coarse tail in one launch (one rank): levels Lt .. L-1 of <= PB_MG_TAIL_MAX points
   int Lt = L;
-  if (!ctx->split && tune("mg_tail", 1)) {
+  if (mg->La > 0) Lt = mg->La;  // decomposed grid: the agglomerated levels run as the tail
+  else if (!ctx->split && tune("mg_tail", 1)) {
     const int64_t tail_max = tune("mg_tail_max", 8192);
     Lt = L - 1;
     while (Lt > 1 && mg->lv[Lt - 1].g->nlocal <= tail_max) --Lt;
@@ -853,6 +918,16 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     }
     PB_HIP(hipGetLastError());
   }
+  const bool agg = mg->La > 0;
+  if (agg) {  // gather level La's right-hand side onto every rank (P copies out, P slabs in)
+    ScopedTimer tg(ctx, "mg_coarse_levels");
+    const MgLevel& A0 = mg->lv[mg->La];
+    const size_t bytes = (size_t)A0.g->nlocal * sizeof(double);
+    for (int r = 0; r < ctx->nranks; ++r)
+      PB_HIP(hipMemcpyAsync(mg->agg_send + (int64_t)r * A0.g->nlocal, A0.b, bytes,
+                            hipMemcpyDeviceToDevice, ctx->stream));
+    PB_TRY(alltoallv_device(ctx, mg->agg_send, mg->agg_sc.data(), mg->ab[0], mg->agg_rc.data()));
+  }
   if (Lt < L) {
     ScopedTimer t3(ctx, "mg_coarse_levels");
     TailArgs A{};
@@ -863,8 +938,9 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     int64_t off = 0;
     for (int t = 0; t < A.nl; ++t) {
       const MgLevel& lv = mg->lv[Lt + t];
-      A.lv[t] = TailLevel{lv.geo(), lv.x, lv.b, lv.res, lv.s, 0, 0, 0};
-      const int64_t n = (lv.g->nlocal + 1) & ~(int64_t)1;  // 16-byte aligned arrays
+      A.lv[t] = agg ? TailLevel{mg->ageo[t], mg->ax[t], mg->ab[t], mg->ares[t], lv.s, 0, 0, 0}
+                    : TailLevel{lv.geo(), lv.x, lv.b, lv.res, lv.s, 0, 0, 0};
+      const int64_t n = ((agg ? mg->ageo[t].nlocal : lv.g->nlocal) + 1) & ~(int64_t)1;  // 16-byte aligned arrays
       A.lv[t].ox = off;
       A.lv[t].ob = off + n;
       A.lv[t].ores = off + 2 * n;
@@ -897,7 +973,15 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
       continue;
     }
     const double *lo, *hi;
-    PB_TRY(ghosts(Cl, Cl.x, &lo, &hi));
+    const double* xc = Cl.x;
+    if (agg && l + 1 == mg->La) {  // this rank's planes of the full coarse correction
+      const int64_t pc = Cl.g->plane, nzc = Cl.n[2], k0c = Cl.g->k0, nzl = Cl.g->nzl;
+      xc = mg->ax[0] + k0c * pc;
+      lo = mg->ax[0] + ((k0c - 1 + nzc) % nzc) * pc;
+      hi = mg->ax[0] + ((k0c + nzl) % nzc) * pc;
+    } else {
+      PB_TRY(ghosts(Cl, Cl.x, &lo, &hi));
+    }
     const MgGeo G = F.geo(), CG = Cl.geo();
     const int64_t cols = (int64_t)CG.nx * CG.ny;
     bool fused = false;
@@ -908,14 +992,14 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
       // pass back into F.x (which also takes CG's residual sums on level 0)
       fused = F.res && F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g);
       hipLaunchKernelGGL(mg_prolong_z_kernel, dim3(mg_blocks(ctx, cols * nchunk)), dim3(256), 0,
-                         ctx->stream, G, (const double*)F.x, fused ? F.res : F.x, CG, kc,
-                         (const double*)Cl.x, lo, hi, mg->skip);
+                         ctx->stream, G, (const double*)F.x, fused ? F.res : F.x, CG, kc, xc, lo,
+                         hi, mg->skip);
     } else if (mg->prolong_cell)
       hipLaunchKernelGGL(mg_prolong_cell_kernel, dim3(mg_blocks(ctx, CG.nlocal)), dim3(256), 0,
-                         ctx->stream, G, F.x, CG, (const double*)Cl.x, lo, hi, mg->skip);
+                         ctx->stream, G, F.x, CG, xc, lo, hi, mg->skip);
     else
       hipLaunchKernelGGL(mg_prolong_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0,
-                         ctx->stream, G, F.x, CG, (const double*)Cl.x, lo, hi, mg->skip);
+                         ctx->stream, G, F.x, CG, xc, lo, hi, mg->skip);
     PB_HIP(hipGetLastError());
     if (fused) {
       PB_TRY(launch_sor_sweep2(F.g, F.s, F.res, F.b, F.x, mg->omega, 1, mg->skip,

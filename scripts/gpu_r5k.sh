@@ -1,0 +1,13 @@
+# decomposed MG: coarse levels gathered onto every rank -- tests, phase probe, force_comm solves
+set -u
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r5k
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread -k "mg or rccl_code_paths or multiproc" > $O/tests.log 2>&1
+rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/probe_mg_decomposed.py > $O/mg.jsonl 2> $O/err || exit $?
+for t in "force_comm=1,mg_agglomerate=0" "force_comm=1" "force_comm=1,mg_agglomerate=0" "force_comm=1"; do
+  timeout -k 10 300 python bench.py --workload star7-mg --steps 6 --warmup 2 --no-cpu-baseline --tune $t > $O/w.json 2>> $O/err || exit $?
+  python3 -c "import json,sys; d=json.loads(open('$O/w.json').read()); print(sys.argv[1], round(d['ms_per_step'],3))" "$t" >> $O/ab.txt
+done

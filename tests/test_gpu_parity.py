@@ -751,7 +751,10 @@ MG_KERNELS = {"default": {},
                             "PB_PRRX_WGCU": "64", "PB_PRRX_MINZ": "2",
                             "PB_MG_ENGINE_MIN_PLANE": "0"},
               # the per-wave fused sweeps (before rows were shared through LDS, r03)
-              "perwave": {"PB_PRRX": "0", "PB_POSTX": "0", "PB_MG_ENGINE_MIN_PLANE": "0"}}
+              "perwave": {"PB_PRRX": "0", "PB_POSTX": "0", "PB_MG_ENGINE_MIN_PLANE": "0"},
+              # decomposed grids: coarse levels with halo exchanges instead of gathered onto
+              # every rank (the pre-r04 N > 1 path)
+              "noagg": {"PB_MG_AGGLOMERATE": "0"}}
 
 
 @pytest.mark.parametrize("kern", sorted(MG_KERNELS))
@@ -1122,12 +1125,14 @@ def test_mg_rejects_odd_extents(ctx):
         pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
 
 
-@pytest.mark.parametrize("kern", ["default", "engine"])
+@pytest.mark.parametrize("kern", ["default", "engine", "noagg"])
 @pytest.mark.parametrize("nranks,n", [(2, (16, 16, 32)), (4, (16, 16, 32)), (3, (16, 16, 12)),
                                         (2, (128, 16, 32)), (3, (128, 8, 12)),
                                         (8, (32, 32, 64)), (8, (128, 16, 64))])
 def test_multirank_mg_bit_exact_and_cg(kern, nranks, n, tune):
-    """Slab-decomposed V-cycle (halo exchanges per level) equals the single-grid restatement.
+    """Slab-decomposed V-cycle equals the single-grid restatement: halo exchanges on the
+    decomposed levels, the coarse levels gathered onto every rank and run as the one-launch tail
+    (default since r04; "noagg": halo exchanges on every level).
 
     nx = 128 cases take the fused two-colour sweeps on the fine level (two-deep z ghosts,
     nzl = 16, 8 and 4 planes per rank); 8 ranks: the GPU count of the driver's scaling runs."""
