@@ -706,13 +706,14 @@ void mg_destroy(Mg* mg) {
 }
 
 // the agglomerated coarse levels of a decomposed grid (Mg::La): the first level whose whole grid
-// fits the one-launch tail (<= PB_MG_TAIL_MAX points, as on one rank), at least level 1
+// fits the one-launch tail (<= mg_agglomerate_max points, default PB_MG_TAIL_MAX as on one
+// rank), at least level 1
 static int mg_agglomerate_setup(Mg* mg) {
   pb_ctx* ctx = mg->ctx;
   const int L = (int)mg->lv.size();
   mg->La = 0;
   if (!ctx->split || L < 2 || !tune("mg_agglomerate", 1)) return PB_OK;
-  const int64_t tail_max = tune("mg_tail_max", 8192);
+  const int64_t tail_max = tune("mg_agglomerate_max", tune("mg_tail_max", 8192));
   int La = L;
   for (int l = L - 1; l >= 1; --l) {
     const MgLevel& v = mg->lv[l];

@@ -36,7 +36,7 @@ const char* const kTuneNames[] = {
     "fft_pf_strided", "fft_poll", "fft_reg", "fft_remap", "fft_rupd", "fft_stagger", "fft_sums",
     "fft_tl_long", "fft_tl_z", "fft_yorder", "fft_zorder", "fft_zpad", "fft_zpad_min_plane",
     "comm_mark_every", "comm_stall_test_ms", "force_comm", "ksp_event_all", "ksp_lazy0", "lines_cfg", "lines_remap", "lines_xdirect",
-    "mg_agglomerate", "mg_engine_min_plane", "mg_post_fused", "mg_presmooth_fused", "mg_presmooth_restrict",
+    "mg_agglomerate", "mg_agglomerate_max", "mg_engine_min_plane", "mg_post_fused", "mg_presmooth_fused", "mg_presmooth_restrict",
     "mg_presmooth_slim", "mg_prolong_cell", "mg_restrict_z", "mg_restrict_z_min_cols",
     "mg_sweep2", "mg_tail", "mg_tail_lds", "mg_tail_max", "mg_transfer_minz", "mg_transfer_tpc", "passa_nt",
     "pcr_lines", "postx", "postx_minz", "postx_split", "postx_wgcu", "prr_minz", "prr_wgcu", "prrx",
