@@ -139,8 +139,9 @@ struct pb_grid {
   double* bnd_lo = nullptr;
   double* bnd_hi = nullptr;
   double* h_stage = nullptr;  // pinned host staging for the host transport (4 planes)
-  // two-deep ghosts for the fused multigrid sweeps on N ranks (allocated on first use):
-  // ghost2 = [planes -2, -1 | nzl, nzl+1], h_stage2 = host staging (8 planes)
+  // deep ghosts for the fused multigrid sweeps on N ranks (allocated on first use, six planes):
+  // two deep = [planes -2, -1 | nzl, nzl+1], three deep = [-3 .. -1 | nzl .. nzl+2];
+  // h_stage2 = host staging (12 planes)
   double* ghost2 = nullptr;
   double* h_stage2 = nullptr;
   // z-slab <-> y-slab rank tables (j -> rank, j0, nyl; pb_compact_dist.hip), uploaded once on

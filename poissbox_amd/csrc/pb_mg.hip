@@ -776,7 +776,10 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
   mg->lv.resize(L);
   int64_t total = 0;
   // levels that take the fused post-smoothing (PB_MG_POST_FUSED, one rank): an xs array each
-  const bool want_post = !ctx->split && tune("mg_post_fused", 1) != 0;
+  // (N ranks: the unrolled fused passes with deep ghost planes, r04; mg_split_fused = 0 keeps
+  // the decomposed V-cycle on the per-pass kernels)
+  const bool split_ok = !ctx->split || tune("mg_split_fused", 1) != 0;
+  const bool want_post = split_ok && tune("mg_post_fused", 1) != 0;
   const int64_t post_min_plane = tune("mg_engine_min_plane", 256 * 256);
   auto takes_post = [&](const MgLevel& lv, int l) {
     return want_post && l < L - 1 && lv.g->plane >= post_min_plane && sor_sweep2_supported(lv.g);
@@ -841,6 +844,10 @@ static bool post_fused(const Mg* mg, int l) {
       mg->prolong_cell != 2)
     return false;
   const MgLevel& C = mg->lv[l + 1];
+  // N ranks: the unrolled kernel with deep ghosts (even slab origin, >= 2 planes per slab)
+  if (mg->ctx->split && (!tune("mg_split_fused", 1) || tune("postx", 3) < 3 || F.g->k0 % 2 ||
+                         F.g->nzl < 2 || C.g->nzl < 2))
+    return false;
   return C.g->n[0] * C.g->n[1] >= mg->restrict_z_min_cols;
 }
 
@@ -874,8 +881,9 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     const bool fused = F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g) &&
                        tune("mg_presmooth_fused", 1);
     // one rank: the restriction too (the residual is never stored)
-    const bool fused_r = fused && !ctx->split && F.g->nzl % 2 == 0 &&
-                         tune("mg_presmooth_restrict", 1);
+    const bool fused_r = fused && F.g->nzl % 2 == 0 && tune("mg_presmooth_restrict", 1) &&
+                         (!ctx->split || (tune("mg_split_fused", 1) && F.g->nzl >= 3 &&
+                                          F.g->k0 % 2 == 0 && tune("prrx", 2) == 2));
     if (fused_r) {
       ScopedTimer t1(ctx, l == 0 ? "mg_fine_smooth_first" : "mg_coarse_levels");
       PB_TRY(launch_presmooth_restrict(F.g, F.s, Cl.g, F.b, post_fused(mg, l) ? F.xs : F.x, Cl.b,
@@ -969,7 +977,9 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     ScopedTimer t4(ctx, l == 0 ? "mg_fine_prolong_post" : "mg_coarse_levels");
     if (post_fused(mg, l)) {
       // prolongation + correction + both post-smoothing half-sweeps in one pass, xs -> x
-      PB_TRY(launch_post_sweep(F.g, F.s, Cl.g, F.xs, Cl.x, F.b, F.x, mg->omega, mg->skip,
+      // (agglomerated coarse level: this rank's planes of the full coarse correction)
+      const double* xcp = agg && l + 1 == mg->La ? mg->ax[0] + Cl.g->k0 * Cl.g->plane : Cl.x;
+      PB_TRY(launch_post_sweep(F.g, F.s, Cl.g, F.xs, xcp, F.b, F.x, mg->omega, mg->skip,
                                l == 0 ? sums_st : nullptr, l == 0 ? nparts : nullptr));
       continue;
     }

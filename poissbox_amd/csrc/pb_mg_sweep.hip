@@ -988,10 +988,19 @@ __device__ __forceinline__ void presmooth_restrict_u4_range(
   auto rix = [&](int64_t row) { return RowIx{row, boff}; };
   // planes up to a few steps past the chunk (the last step's spare planes): any distance
   auto wrapk = [&](int kk) { kk %= nz; return kk < 0 ? kk + nz : kk; };
+  // b's plane kk: one rank wraps periodically; N ranks (g.split) read planes -3 .. -1 and
+  // nz .. nz+2 from the ghost buffer g.xg (six planes, in that order) -- the spare planes of the
+  // last unrolled step beyond those clamp (their values are never stored)
+  auto bplane = [&](int kk) -> const double* {
+    if (!g.split) return b + (int64_t)wrapk(kk) * g.plane;
+    if (kk >= 0 && kk < nz) return b + (int64_t)kk * g.plane;
+    const int gi = kk < 0 ? max(kk + 3, 0) : 3 + min(kk - nz, 2);
+    return g.xg + (int64_t)gi * g.plane;
+  };
   auto ldraw = [&](double (&dst)[TY][2], int kk) {
-    const int64_t base = (int64_t)wrapk(kk) * g.plane;
+    const double* src = bplane(kk);
 #pragma unroll
-    for (int r = 0; r < TY; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
+    for (int r = 0; r < TY; ++r) load_row<2>(src, rix(ro[r]), dst[r]);
   };
   // element holding the red point of own row r on a plane of parity P (pair origin i even, row
   // origin j0 even, k0 = 0): presmooth_restrict_kernel's ((i + j) & 1) + kpar != 0
@@ -1239,8 +1248,12 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
 // coarse-value prefetch in registers.
 // ---------------------------------------------------------------------------------------------
 struct PostGeo {
-  int ncx, ncy, ncz;   // coarse extents (one rank: the whole coarse grid)
+  int ncx, ncy, ncz;   // coarse extents (one rank: the whole coarse grid; N ranks: the slab)
   int64_t cplane;
+  // N ranks (post_sweep_u4_kernel): the coarse correction's planes -2, -1, ncz, ncz+1 (in that
+  // order) in cgh; the fine x_s ghosts (-2, -1, nz, nz+1) in Sweep2Geo::xg, b's in bg_lo / bg_hi
+  int split;
+  const double* cgh;
 };
 
 #ifndef PB_POST_WPE
@@ -1835,16 +1848,32 @@ __device__ __forceinline__ void post_sweep_u4_range(
     for (int t = 0; t < NC; ++t) crow[t] = (int64_t)wrap((j0 >> 1) - 1 + t, cgeo.ncy) * cgeo.ncx;
     const unsigned cboff = (unsigned)(ip >> 1) * 8u;
     // x_s rows of plane kk into rows 1 .. TY of dst
+    // N ranks (g.split): planes outside the slab from the ghost buffers (x_s two deep, b one
+    // deep, the coarse correction two deep); the last unrolled step's spare planes clamp
+    auto xsplane = [&](int kk) -> const double* {
+      if (!g.split) return xs + pl(kk);
+      if (kk >= 0 && kk < nz) return xs + (int64_t)kk * g.plane;
+      const int gi = kk < 0 ? max(kk + 2, 0) : 2 + min(kk - nz, 1);
+      return g.xg + (int64_t)gi * g.plane;
+    };
     auto ldx = [&](double (&dst)[TY + 2][2], int kk) {
-      const int64_t base = pl(kk);
+      const double* src = xsplane(kk);
 #pragma unroll
-      for (int r = 0; r < TY; ++r) load_row<2>(xs, rix(base + ro[r]), dst[r + 1]);
+      for (int r = 0; r < TY; ++r) load_row<2>(src, rix(ro[r]), dst[r + 1]);
     };
     // coarse plane K (periodic) under the own rows
     auto ldc = [&](double (&cv)[NC], int K) {
-      K %= cgeo.ncz;
-      if (K < 0) K += cgeo.ncz;
-      const double* cp = xc + (int64_t)K * cgeo.cplane;
+      const double* cp;
+      if (!cgeo.split) {
+        K %= cgeo.ncz;
+        if (K < 0) K += cgeo.ncz;
+        cp = xc + (int64_t)K * cgeo.cplane;
+      } else if (K >= 0 && K < cgeo.ncz) {
+        cp = xc + (int64_t)K * cgeo.cplane;
+      } else {
+        const int gi = K < 0 ? max(K + 2, 0) : 2 + min(K - cgeo.ncz, 1);
+        cp = cgeo.cgh + (int64_t)gi * cgeo.cplane;
+      }
 #pragma unroll
       for (int t = 0; t < NC; ++t)
         cv[t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cp + crow[t]) + cboff);
@@ -1877,9 +1906,11 @@ __device__ __forceinline__ void post_sweep_u4_range(
         for (int e = 0; e < 2; ++e) v[r + 1][e] = v[r + 1][e] + (0.75 * Yn[r][e] + 0.25 * Yf[r][e]);
     };
     auto ldb = [&](double (&dst)[TY][2], int kk) {
-      const int64_t base = pl(kk);
+      const double* src = !g.split ? b + pl(kk)
+                          : (kk >= 0 && kk < nz ? b + (int64_t)kk * g.plane
+                                                : (kk < 0 ? g.bg_lo : g.bg_hi));
 #pragma unroll
-      for (int r = 0; r < TY; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
+      for (int r = 0; r < TY; ++r) load_row<2>(src, rix(ro[r]), dst[r]);
     };
     // element of the c1 (first-half) point of own row r on a plane of parity P: post_sweep_kernel's
     // ec1 with ((i + j) & 1) = r & 1 and c1 = 1
@@ -2076,13 +2107,19 @@ bool sor_sweep2_supported(const pb_grid* g) {
          g->nzl >= 4 && tune("mg_sweep2", 1) != 0;
 }
 
+// the six-plane deep-ghost buffer of a grid (pb_grid::ghost2)
+static int ensure_ghost2(pb_grid* g) {
+  if (!g->ghost2 && hipMalloc(&g->ghost2, 6 * (size_t)g->plane * sizeof(double)) != hipSuccess)
+    return set_error(PB_ERR_ALLOC, "deep ghost planes: out of device memory");
+  return PB_OK;
+}
+
 // N ranks: two-deep ghosts of xin (and, when b is another array, one-deep ghosts of b)
 static int sweep2_ghosts(pb_grid* g, const double* xin, const double* b, Sweep2Geo& geo) {
   geo.split = g->ctx->split ? 1 : 0;
   geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
   if (!geo.split) return PB_OK;
-  if (!g->ghost2 && hipMalloc(&g->ghost2, 4 * (size_t)g->plane * sizeof(double)) != hipSuccess)
-    return set_error(PB_ERR_ALLOC, "two-deep ghost planes: out of device memory");
+  PB_TRY(ensure_ghost2(g));
   PB_TRY(halo_exchange_n(g, xin, xin + (g->nzl - 2) * g->plane, 2, g->ghost2,
                          g->ghost2 + 2 * g->plane));
   geo.xg = g->ghost2;
@@ -2163,7 +2200,9 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
                       const double* xc, const double* b, double* xout, double omega,
                       const int* skip, const CgState* sums_st, int* nparts) {
   ScopedTimer tm(g->ctx, "mg_post_sweep");
-  if (g->ctx->split) return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: one rank only");
+  const bool split = g->ctx->split;
+  if (split && tune("postx", 3) < 3)
+    return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing on N ranks: unrolled kernels only");
   if (xs == xout) return set_error(PB_ERR_ARG, "fused post-smoothing must run out of place");
   if (cg->n[0] * 2 != g->n[0] || cg->n[1] * 2 != g->n[1] || cg->nzl * 2 != g->nzl)
     return set_error(PB_ERR_ARG, "fused post-smoothing: coarse grid is not half the fine one");
@@ -2171,7 +2210,25 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
   int64_t nblocks = sweep2_geo(g, geo);
   geo.split = 0;
   geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
-  PostGeo cgeo{(int)cg->n[0], (int)cg->n[1], (int)cg->nzl, cg->plane};
+  PostGeo cgeo{(int)cg->n[0], (int)cg->n[1], (int)cg->nzl, cg->plane, 0, nullptr};
+  if (split) {  // x_s two deep, b one deep, the coarse correction two deep
+    pb_grid* gc = const_cast<pb_grid*>(cg);
+    if (g->nzl < 2 || gc->nzl < 2)
+      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: slabs of < 2 planes");
+    PB_TRY(ensure_ghost2(g));
+    PB_TRY(ensure_ghost2(gc));
+    PB_TRY(halo_exchange_n(g, xs, xs + (g->nzl - 2) * g->plane, 2, g->ghost2,
+                           g->ghost2 + 2 * g->plane));
+    PB_TRY(halo_exchange(g, b, b + (g->nzl - 1) * g->plane));
+    PB_TRY(halo_exchange_n(gc, xc, xc + (gc->nzl - 2) * gc->plane, 2, gc->ghost2,
+                           gc->ghost2 + 2 * gc->plane));
+    geo.split = 1;
+    geo.xg = g->ghost2;
+    geo.bg_lo = g->ghost_lo;
+    geo.bg_hi = g->ghost_hi;
+    cgeo.split = 1;
+    cgeo.cgh = gc->ghost2;
+  }
   // rows shared through LDS: 1, 2 = post_sweep_xch_kernel with 8 waves x 4 / x 2 rows; 3, 4 = the
   // same with the plane loop unrolled by four (post_sweep_u4_kernel; compile-time colours: k0 = 0,
   // chunk starts at multiples of 4); 0 = the per-wave kernel below
@@ -2191,8 +2248,10 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     geo.kc = (geo.kc + 3) & ~3;  // chunk starts at multiples of 4 (the unrolled kernels' parities)
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
     nblocks = (int64_t)columns * geo.nchunk;
-    if (xv >= 3 && g->k0 != 0)
-      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: one rank only");
+    if (xv >= 3 && g->k0 % 2 != 0)  // (the unrolled kernels' compile-time colours)
+      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: odd slab origin");
+    if (split && xv < 3)
+      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing on N ranks: unrolled kernels only");
     if (xv >= 3) nblocks = balanced_split(g, geo, tune("postx_split", 0), 4, nblocks);
     if (sums_st && nblocks * 4 > g->ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
@@ -2231,7 +2290,9 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
 int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, const double* b,
                               double* xout, double* bc, double omega, const int* skip) {
   ScopedTimer tm(g->ctx, "mg_presmooth_restrict");
-  if (g->ctx->split) return set_error(PB_ERR_UNSUPPORTED, "fused restriction: one rank only");
+  const bool split = g->ctx->split;
+  if (split && (tune("prrx", 2) != 2 || g->nzl < 3))
+    return set_error(PB_ERR_UNSUPPORTED, "fused restriction on N ranks: unrolled kernel, >= 3 planes");
   if (b == xout) return set_error(PB_ERR_ARG, "fused pre-smoothing must run out of place");
   if (!sor_sweep2_supported(g) || g->nzl % 2)
     return set_error(PB_ERR_UNSUPPORTED, "fused restriction: grid not supported");
@@ -2241,6 +2302,13 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
   sweep2_geo(g, geo);
   geo.split = 0;
   geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
+  if (split) {  // b three deep (planes -3 .. -1 | nzl .. nzl+2)
+    PB_TRY(ensure_ghost2(g));
+    PB_TRY(halo_exchange_n(g, b, b + (g->nzl - 3) * g->plane, 3, g->ghost2,
+                           g->ghost2 + 3 * g->plane));
+    geo.split = 1;
+    geo.xg = g->ghost2;
+  }
   // rows shared through LDS: 1 = presmooth_restrict_xch_kernel, 2 = the same with the plane loop
   // unrolled by four (presmooth_restrict_u4_kernel; compile-time colours: k0 = 0, even chunk
   // starts), both 8 waves x 4 rows; 0 = the per-wave kernel below
@@ -2264,7 +2332,8 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     geo.kc += geo.kc & 1;
     geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
     int64_t nblocks = (int64_t)columns * geo.nchunk;
-    if (g->k0 != 0) return set_error(PB_ERR_UNSUPPORTED, "fused restriction: one rank only");
+    if (g->k0 % 2 != 0)  // (the unrolled kernel's compile-time colours)
+      return set_error(PB_ERR_UNSUPPORTED, "fused restriction: odd slab origin");
     // balanced split (prrx_split workgroups per CU; default: 1 where the chunks above need more
     // than one round of workgroups -- this pass runs one per CU (254 VGPRs): 512^3's 256^3 level,
     // 528 workgroups, 0.405 -> 0.382 ms for the coarse levels; on the 512^3 level itself, 220

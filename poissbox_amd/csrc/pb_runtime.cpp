@@ -38,7 +38,7 @@ const char* const kTuneNames[] = {
     "comm_mark_every", "comm_stall_test_ms", "force_comm", "ksp_event_all", "ksp_lazy0", "lines_cfg", "lines_remap", "lines_xdirect",
     "mg_agglomerate", "mg_agglomerate_max", "mg_engine_min_plane", "mg_post_fused", "mg_presmooth_fused", "mg_presmooth_restrict",
     "mg_presmooth_slim", "mg_prolong_cell", "mg_restrict_z", "mg_restrict_z_min_cols",
-    "mg_sweep2", "mg_tail", "mg_tail_lds", "mg_tail_max", "mg_transfer_minz", "mg_transfer_tpc", "passa_nt",
+    "mg_split_fused", "mg_sweep2", "mg_tail", "mg_tail_lds", "mg_tail_max", "mg_transfer_minz", "mg_transfer_tpc", "passa_nt",
     "pcr_lines", "postx", "postx_minz", "postx_split", "postx_wgcu", "prr_minz", "prr_wgcu", "prrx",
     "prrx_longz", "prrx_minz", "prrx_split", "prrx_wgcu", "slab_rows", "sor_omega_any", "stencil_blocks", "stencil_kcmin", "stencil_nt",
     "stencil_tall", "stencil_tall_min_plane", "stencil_ty", "sweep2_wgcu", "tall_wgcu",
@@ -314,9 +314,9 @@ int halo_exchange_n(pb_grid* g, const double* lo, const double* hi, int np, doub
   const int down = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
   const int up = (ctx->rank + 1) % ctx->nranks;
   if (ctx->h_sendrecv) {
-    if (np > 2) return set_error(PB_ERR_UNSUPPORTED, "host halo of %d planes", np);
-    if (!g->h_stage2)
-      PB_HIP(hipHostMalloc(&g->h_stage2, 8 * (size_t)g->plane * sizeof(double),
+    if (np > 3) return set_error(PB_ERR_UNSUPPORTED, "host halo of %d planes", np);
+    if (!g->h_stage2)  // up to three planes each way (the fused MG pre-pass's b ghosts)
+      PB_HIP(hipHostMalloc(&g->h_stage2, 12 * (size_t)g->plane * sizeof(double),
                            hipHostMallocDefault));
     double* s_lo = g->h_stage2;
     double* s_hi = s_lo + cnt;

@@ -754,7 +754,12 @@ MG_KERNELS = {"default": {},
               "perwave": {"PB_PRRX": "0", "PB_POSTX": "0", "PB_MG_ENGINE_MIN_PLANE": "0"},
               # decomposed grids: coarse levels with halo exchanges instead of gathered onto
               # every rank (the pre-r04 N > 1 path)
-              "noagg": {"PB_MG_AGGLOMERATE": "0"}}
+              "noagg": {"PB_MG_AGGLOMERATE": "0"},
+              # decomposed grids: every level on the fused unrolled passes (deep ghost planes)
+              "splitfused": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
+              # ... and the pre-r04 decomposed V-cycle (per-pass kernels, halos on every level)
+              "nosplitfused": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_RESTRICT_Z_MIN_COLS": "0",
+                               "PB_MG_SPLIT_FUSED": "0", "PB_MG_AGGLOMERATE": "0"}}
 
 
 @pytest.mark.parametrize("kern", sorted(MG_KERNELS))
@@ -1125,7 +1130,7 @@ def test_mg_rejects_odd_extents(ctx):
         pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
 
 
-@pytest.mark.parametrize("kern", ["default", "engine", "noagg"])
+@pytest.mark.parametrize("kern", ["default", "engine", "noagg", "splitfused", "nosplitfused"])
 @pytest.mark.parametrize("nranks,n", [(2, (16, 16, 32)), (4, (16, 16, 32)), (3, (16, 16, 12)),
                                         (2, (128, 16, 32)), (3, (128, 8, 12)),
                                         (8, (32, 32, 64)), (8, (128, 16, 64))])
