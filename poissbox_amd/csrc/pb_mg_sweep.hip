@@ -501,7 +501,8 @@ __global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Pre-smoothing from x = 0, residual AND restriction in one pass (one rank): the residual is
+// Pre-smoothing from x = 0, residual AND restriction in one pass (one rank; the unrolled form also
+// on N ranks with three-deep ghosts of b, r04): the residual is
 // never stored -- each wave owns the two fine rows 2J, 2J+1 of one coarse row J and forms the
 // residual on the four rows 2J-1 .. 2J+2 that the restriction reads (so S1 on six rows, red values
 // on eight), then the restriction's x and y sums per fine plane and its z sum over the four planes
@@ -946,7 +947,8 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_xch_kernel(
 // presmooth_restrict_xch_kernel with the plane loop unrolled by four (r03). Its queues (red values,
 // smoothed pairs, b rows, x sums, halo values) become rings of four or two register slots whose
 // roles rotate with the unrolled copy, so no value is copied from one iteration to the next, and
-// each copy knows its plane's parity: with one rank (k0 = 0) and even extents, pair origins and
+// each copy knows its plane's parity: with an even slab origin k0 (one rank: 0; N ranks: the MG
+// plan keeps every level's slab origins even) and even extents, pair origins and
 // row origins, the colour of every element is known at compile time, so the colour choices are
 // register choices instead of selects and each half-sweep needs one DPP shift per row, not two.
 // A chunk runs a whole number of four-plane steps (up to three planes more than it needs; they
@@ -1003,7 +1005,7 @@ __device__ __forceinline__ void presmooth_restrict_u4_range(
     for (int r = 0; r < TY; ++r) load_row<2>(src, rix(ro[r]), dst[r]);
   };
   // element holding the red point of own row r on a plane of parity P (pair origin i even, row
-  // origin j0 even, k0 = 0): presmooth_restrict_kernel's ((i + j) & 1) + kpar != 0
+  // origin j0 even, k0 even): presmooth_restrict_kernel's ((i + j) & 1) + kpar != 0
   auto red_e = [](int r, int P) { return (r + P) & 1; };
 
   auto redv = [&](auto Pc, const double (&v)[TY][2], double (&red)[TY]) {
@@ -1236,7 +1238,8 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Post-smoothing with the prolongation folded in (one rank): the sweep's input
+// Post-smoothing with the prolongation folded in (one rank; the unrolled form also on N ranks with
+// deep ghost planes, r04): the sweep's input
 // xin = x_s + P x_c is formed as the planes arrive -- x_s (the pre-smoothed iterate) and the
 // coarse correction x_c are read, the prolongated input is never stored. Then both half-sweeps
 // (c1 = 1 first, then the other colour) out of place into xout, CG's residual sums optional.
@@ -1800,7 +1803,7 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_xch_kernel(
 // post_sweep_xch_kernel with the plane loop unrolled by four (r03), as
 // presmooth_restrict_u4_kernel: the queues (input planes with their halo rows, first-half values,
 // c2 inputs and right-hand sides, halo first-half values) are rings of four or two register slots
-// whose roles rotate with the unrolled copy, and each copy knows its plane's parity (one rank,
+// whose roles rotate with the unrolled copy, and each copy knows its plane's parity (even k0,
 // even extents and origins), so the colour choices are register choices and each half-sweep
 // shifts one value per row. A chunk runs a whole number of four-plane steps (the last step's
 // extra planes store nothing). Same operations on the same operands: bit-identical.
@@ -2230,7 +2233,7 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     cgeo.cgh = gc->ghost2;
   }
   // rows shared through LDS: 1, 2 = post_sweep_xch_kernel with 8 waves x 4 / x 2 rows; 3, 4 = the
-  // same with the plane loop unrolled by four (post_sweep_u4_kernel; compile-time colours: k0 = 0,
+  // same with the plane loop unrolled by four (post_sweep_u4_kernel; compile-time colours: even k0,
   // chunk starts at multiples of 4); 0 = the per-wave kernel below
   const int xv = tune("postx", 3);
   if (xv >= 1 && xv <= 4) {
@@ -2310,7 +2313,7 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     geo.xg = g->ghost2;
   }
   // rows shared through LDS: 1 = presmooth_restrict_xch_kernel, 2 = the same with the plane loop
-  // unrolled by four (presmooth_restrict_u4_kernel; compile-time colours: k0 = 0, even chunk
+  // unrolled by four (presmooth_restrict_u4_kernel; compile-time colours: even k0, even chunk
   // starts), both 8 waves x 4 rows; 0 = the per-wave kernel below
   const int xv = tune("prrx", 2);
   if (xv == 1 || xv == 2) {
