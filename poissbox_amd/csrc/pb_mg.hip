@@ -705,6 +705,14 @@ void mg_destroy(Mg* mg) {
   delete mg;
 }
 
+// levels whose planes hold at least this many points run the fused / engine passes: 256^2 on one
+// rank (the 128^3 level's six per-level launches beat the fused passes there, 0.381 vs 0.409 ms);
+// 128^2 on decomposed grids, where every per-level pass costs a halo exchange (force_comm 512^3
+// MG-PCG 48.1 -> 47.75 ms, profiles/r04/decomposed/mg_engine_128_ab.txt)
+static int64_t mg_engine_min_plane_default(const pb_ctx* ctx) {
+  return ctx->split ? 128 * 128 : 256 * 256;
+}
+
 // the agglomerated coarse levels of a decomposed grid (Mg::La): the first level whose whole grid
 // fits the one-launch tail (<= mg_agglomerate_max points, default PB_MG_TAIL_MAX as on one
 // rank), at least level 1
@@ -780,7 +788,7 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
   // the decomposed V-cycle on the per-pass kernels)
   const bool split_ok = !ctx->split || tune("mg_split_fused", 1) != 0;
   const bool want_post = split_ok && tune("mg_post_fused", 1) != 0;
-  const int64_t post_min_plane = tune("mg_engine_min_plane", 256 * 256);
+  const int64_t post_min_plane = tune("mg_engine_min_plane", mg_engine_min_plane_default(ctx));
   auto takes_post = [&](const MgLevel& lv, int l) {
     return want_post && l < L - 1 && lv.g->plane >= post_min_plane && sor_sweep2_supported(lv.g);
   };
@@ -856,7 +864,7 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
   if (nparts) *nparts = 0;
   ScopedTimer tm(mg->ctx, "mg_apply");
   mg->skip = skip;
-  mg->engine_min_plane = tune("mg_engine_min_plane", 256 * 256);
+  mg->engine_min_plane = tune("mg_engine_min_plane", mg_engine_min_plane_default(mg->ctx));
   mg->prolong_cell = tune("mg_prolong_cell", 2);
   mg->restrict_z = tune("mg_restrict_z", 1);
   mg->restrict_z_min_cols = tune("mg_restrict_z_min_cols", 4096);
