@@ -225,6 +225,12 @@ typedef struct {
   int mg_levels;     /* -pc_mg_levels: multigrid levels (0 = as many as the grid allows)      */
   int mg_coarse_its; /* -pc_mg_coarse_its: symmetric red-black sweeps on the coarsest level (8) */
   double sor_omega;  /* -pc_sor_omega: SOR relaxation factor (1.0 = Gauss-Seidel)              */
+  int cg_single_reduction; /* -ksp_cg_single_reduction (PETSc KSPCGUseSingleReduction): the
+                        iteration of KSPSolve_CG_SingleReduction -- one reduction per iteration
+                        (z'z, z'r, z'Az together), p'w by its recurrence. Equal to KSPSolve_CG in
+                        exact arithmetic. Runs as two engine passes on the 7-point operator with
+                        -pc_type jacobi|none; with other operators / PCs the KSPSolve_CG iteration
+                        runs (default 0) */
 } pb_ksp_opts;
 typedef struct {
   int reason;
@@ -237,7 +243,7 @@ typedef struct {
 int pb_ksp_opts_default(pb_ksp_opts* opts);
 /* Parses PETSc-style options (-ksp_type, -pc_type, -ksp_rtol, -ksp_atol, -ksp_divtol,
  * -ksp_max_it, -ksp_monitor, -ksp_converged_reason, -pc_mg_levels, -pc_mg_coarse_its,
- * -pc_sor_omega); unknown options are ignored.
+ * -pc_sor_omega, -ksp_cg_single_reduction [true|false]); unknown options are ignored.
  * -pc_type sor: one symmetric red-black SOR sweep (PETSc PCSOR default: 1 local symmetric sweep,
  * here in red-black order). -pc_type mg (or gamg): geometric V(1,1) multigrid with red-black SOR
  * smoothing on the 7-point P (README.md:40-45 recommends GAMG + SOR). Both need even extents. */

@@ -41,7 +41,7 @@ class KspOpts(C.Structure):
                 ("max_it", C.c_int64), ("pc_type", C.c_int), ("nullspace", C.c_int),
                 ("op_kind", C.c_int), ("nthreads", C.c_int), ("mg_levels", C.c_int),
                 ("mg_coarse_its", C.c_int), ("omega", C.c_double), ("nranks", C.c_int),
-                ("pc_compact", C.c_int)]
+                ("pc_compact", C.c_int), ("single_reduction", C.c_int)]
 
 PC_CODES = {"none": 0, "jacobi": 1, "sor": 2, "mg": 3, "fft": 4}
 
@@ -104,9 +104,11 @@ def fill_random(count, seed, g0=0):
 
 def cg_solve(b, n, h, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
              nullspace=True, faithful=False, nthreads=1, op="star7", mg_levels=0,
-             mg_coarse_its=8, omega=1.0, nranks=1, pc_compact=None):
+             mg_coarse_its=8, omega=1.0, nranks=1, pc_compact=None, single_reduction=0):
     """KSPSolve(-ksp_type cg -pc_type jacobi|none|sor|mg|fft) with the constant null space.
     pc_compact: the fft PC inverts the compact operator's symbol (default: when op is compact).
+    single_reduction: 1 = PETSc KSPSolve_CG_SingleReduction (-ksp_cg_single_reduction), 2 = the
+    same iteration with w = A p recomputed (the GPU pass's arithmetic).
     Returns (x, reason, its, history): the norms KSPLogResidualHistory logged (its + 1 of them,
     its after a breakdown exit)."""
     b = np.ascontiguousarray(b, dtype=np.float64).reshape(-1)
@@ -120,7 +122,7 @@ def cg_solve(b, n, h, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi"
     if pc_compact is None:
         pc_compact = op == "compact"
     o = KspOpts(rtol, atol, dtol, max_it, PC_CODES[pc], int(nullspace), kind, nthreads,
-                mg_levels, mg_coarse_its, omega, nranks, int(pc_compact))
+                mg_levels, mg_coarse_its, omega, nranks, int(pc_compact), int(single_reduction))
     reason = lib().pbo_cg_solve(_n3(n), _h3(h), C.byref(o), _p(b), _p(x), _p(hist), C.byref(its),
                                 C.byref(nlog))
     return x, reason, its.value, hist[:nlog.value].copy()

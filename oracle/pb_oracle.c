@@ -567,8 +567,102 @@ static void pc_apply_any(const int64_t n[3], const double h[3], const pbo_ksp_op
   pc_apply(N, r, z, dinv, o->pc_type, o->nullspace, nt);
 }
 
+/* PETSc KSPSolve_CG_SingleReduction (cg.c, selected by -ksp_cg_single_reduction through
+ * KSPSetFromOptions, src/poissbox.f90:295; PETSc is external and absent -- restated from its
+ * published cg.c). KSP_NORM_PRECONDITIONED (KSPCG's default): identical to KSPSolve_CG in exact
+ * arithmetic, with S = A z formed right after z, delta = z'S and beta = z'r taken together
+ * (VecMDot), w = A p and p'w by recurrence:  w_i = s_i + (beta/betaold) w_{i-1},
+ * dpi = delta - beta^2 dpiold / betaold^2  (i > 0; i = 0: w = A p, dpi = p'w).
+ * form 2 keeps the recurrence for dpi and recomputes w = A p (the GPU pass's arithmetic). */
+static int cg_solve_single_reduction(const int64_t n[3], const double h[3], const pbo_ksp_opts* o,
+                                     const double* b, double* x, double* history,
+                                     int64_t* its_out, int64_t* nlog_out) {
+  const int64_t N = n[0] * n[1] * n[2];
+  const int nt = o->nthreads > 0 ? o->nthreads : 1;
+  const int recompute_w = o->single_reduction == 2;
+  double* R = (double*)malloc(sizeof(double) * N);
+  double* Z = (double*)malloc(sizeof(double) * N);
+  double* P = (double*)malloc(sizeof(double) * N);
+  double* S = (double*)malloc(sizeof(double) * N);
+  double* W = (double*)malloc(sizeof(double) * N);
+  const double dinv = 1.0 / pbo_diag(h);
+  int reason = KSP_CONVERGED_ITERATING;
+  int64_t its = 0, nlog = 0;
+  double dp, beta, betaold = 1.0, dpi = 0.0, dpiold, delta, ttol, rnorm0;
+
+  memset(x, 0, sizeof(double) * N); /* guess_zero */
+  memcpy(R, b, sizeof(double) * N); /* r = b */
+  pc_apply_any(n, h, o, R, Z, dinv, nt); /* z = B r */
+  dp = sqrt(vdot(N, Z, Z, nt));          /* VecNorm(Z) */
+  history[0] = dp;
+  nlog = 1;
+  if (dp != dp || isinf(dp)) { reason = KSP_DIVERGED_NANORINF; goto done; }
+  ttol = fmax(o->rtol * dp, o->atol);
+  rnorm0 = dp;
+  if (dp <= ttol) { reason = dp < o->atol ? KSP_CONVERGED_ATOL : KSP_CONVERGED_RTOL; goto done; }
+  op_apply(n, h, Z, S, o->op_kind, nt); /* S = A z */
+  delta = vdot(N, Z, S, nt);            /* delta = z'A z */
+  beta = vdot(N, Z, R, nt);             /* beta = z'r */
+  if (!isfinite(beta)) { reason = KSP_DIVERGED_NANORINF; goto done; } /* KSPCheckDot */
+
+  int64_t i = 0;
+  do {
+    its = i + 1;
+    if (beta == 0.0) { reason = KSP_CONVERGED_ATOL; break; }
+    if (i > 0 && beta * betaold < 0.0) { reason = KSP_DIVERGED_INDEFINITE_PC; break; }
+    double bb = 0.0;
+    if (i == 0) {
+      memcpy(P, Z, sizeof(double) * N);
+    } else {
+      bb = beta / betaold;
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+      for (int64_t t = 0; t < N; ++t) P[t] = Z[t] + bb * P[t]; /* VecAYPX(P, b, Z) */
+    }
+    dpiold = dpi;
+    if (i == 0 || recompute_w) {
+      op_apply(n, h, P, W, o->op_kind, nt); /* w = A p */
+      if (i == 0) dpi = vdot(N, P, W, nt);  /* dpi = p'w */
+    } else {
+      const double c = beta / betaold;
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+      for (int64_t t = 0; t < N; ++t) W[t] = S[t] + c * W[t]; /* VecAYPX(W, beta/betaold, S) */
+    }
+    if (i > 0) dpi = delta - beta * beta * dpiold / (betaold * betaold);
+    betaold = beta;
+    if (dpi == 0.0 || (i > 0 && dpi * dpiold <= 0.0)) {
+      reason = KSP_DIVERGED_INDEFINITE_MAT;
+      break;
+    }
+    const double a = beta / dpi;
+#pragma omp parallel for num_threads(nt) schedule(static) if (nt > 1)
+    for (int64_t t = 0; t < N; ++t) {
+      x[t] = x[t] + a * P[t];
+      R[t] = R[t] + (-a) * W[t];
+    }
+    pc_apply_any(n, h, o, R, Z, dinv, nt); /* z = B r */
+    op_apply(n, h, Z, S, o->op_kind, nt);  /* S = A z */
+    dp = sqrt(vdot(N, Z, Z, nt));
+    history[i + 1] = dp;
+    nlog = i + 2;
+    if (dp != dp || isinf(dp)) { reason = KSP_DIVERGED_NANORINF; break; }
+    if (dp <= ttol) { reason = dp < o->atol ? KSP_CONVERGED_ATOL : KSP_CONVERGED_RTOL; break; }
+    if (dp >= o->dtol * rnorm0) { reason = KSP_DIVERGED_DTOL; break; }
+    delta = vdot(N, Z, S, nt); /* VecMDot(Z, {S, R}) */
+    beta = vdot(N, Z, R, nt);
+    if (!isfinite(beta)) { reason = KSP_DIVERGED_NANORINF; break; } /* KSPCheckDot */
+    i++;
+  } while (i < o->max_it);
+  if (i >= o->max_it) reason = KSP_DIVERGED_ITS;
+done:
+  *its_out = its;
+  if (nlog_out) *nlog_out = nlog;
+  free(R); free(Z); free(P); free(S); free(W);
+  return reason;
+}
+
 int pbo_cg_solve(const int64_t n[3], const double h[3], const pbo_ksp_opts* o, const double* b,
                  double* x, double* history, int64_t* its_out, int64_t* nlog_out) {
+  if (o->single_reduction) return cg_solve_single_reduction(n, h, o, b, x, history, its_out, nlog_out);
   const int64_t N = n[0] * n[1] * n[2];
   const int nt = o->nthreads > 0 ? o->nthreads : 1;
   double* R = (double*)malloc(sizeof(double) * N);

@@ -62,6 +62,10 @@ typedef struct {
   int nranks;        /* slab count the GPU run uses (only changes the automatic level count) */
   int pc_compact;    /* pc 4 (fft): invert the compact operator's symbol (P = compact), else the
                         7-point star's */
+  int single_reduction; /* -ksp_cg_single_reduction: 1 = PETSc KSPSolve_CG_SingleReduction
+                           (w and p'w by recurrence); 2 = the same iteration with w = A p
+                           recomputed each iteration (the GPU kernels' form; equal in exact
+                           arithmetic) -- 0 = KSPSolve_CG */
 } pbo_ksp_opts;
 
 /* ---- red-black SOR / geometric multigrid preconditioner (our GPU design, poissbox_amd/csrc/

@@ -28,7 +28,8 @@ class KspOpts(C.Structure):
     _fields_ = [("rtol", c_d), ("atol", c_d), ("dtol", c_d), ("max_it", c_i64),
                 ("ksp_type", C.c_int), ("pc_type", C.c_int), ("nullspace", C.c_int),
                 ("monitor", C.c_int), ("converged_reason", C.c_int), ("check_every", C.c_int),
-                ("mg_levels", C.c_int), ("mg_coarse_its", C.c_int), ("sor_omega", c_d)]
+                ("mg_levels", C.c_int), ("mg_coarse_its", C.c_int), ("sor_omega", c_d),
+                ("cg_single_reduction", C.c_int)]
 
 
 class KspResult(C.Structure):

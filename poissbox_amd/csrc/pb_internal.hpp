@@ -91,6 +91,9 @@ struct pb_ctx {
   std::deque<hipEvent_t> comm_marks;
   std::vector<hipEvent_t> mark_pool;
   int64_t comm_groups = 0;
+  // groups enqueued after the last mark of ctx->stream / ctx->comm_stream: a bounded wait marks
+  // them first, so a stuck unmarked group counts as pending
+  bool unmarked_main = false, unmarked_comm = false;
   int* h_stall = nullptr;  // test hook (tuning "comm_stall_test_ms"): released by comm_fail
   void* shm = nullptr;  // built-in shared-memory host transport (pb_transport.cpp), if attached
   // host transport (tests)
@@ -298,6 +301,10 @@ struct CgState {
                  // breakdown exit (beta = 0, indefinite PC / matrix) that skips the last norm
   int reason, done, pc, nullspace, defer_x;
   double bbp;  // beta / betaold of the current pass A (stage 1), for pass B re-forming p
+  // single-reduction CG (-ksp_cg_single_reduction): delta = z'A z of the current z (taken with
+  // z'z, z'r in the one reduction per iteration); sr = 1 selects that iteration's scalar logic
+  double delta;
+  int sr;
 };
 int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p, CgState* st,
                    double dinv, double* hist, int* h_done);
@@ -333,6 +340,33 @@ int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
                             int defer, int* nparts_b, const PStore& ps = PStore{});
 int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_done,
                  int64_t host_iter);
+// Single-reduction CG (PETSc KSPSolve_CG_SingleReduction, -ksp_cg_single_reduction), two engine
+// passes per iteration and ONE reduction (pb_stencil.hip):
+//   pass P: prologue = [the previous iteration's residual-sum stage (folded, one rank)] + the top
+//     of the iteration (beta / betaold, p'w = delta - beta^2 dpiold / betaold^2, alpha); body:
+//     p = (dinv r - mu) + b p_old on load, w = A p, r_out = r - alpha w, store p and r_out, the
+//     deferred x update every defer-th iteration. Reads state slot `in`, writes slot `out`.
+//   pass S: t = dinv r_out - mu on load, s = A t; per-block sums t, t^2, t.r, r, t.s (5 wide)
+//     into ctx->d_partials + part_off * 5.
+// fold_sums: 1 = the prologue first reduces pass S's partials (nparts_s blocks at offset 0) and
+// runs their stage (history / done flag of host_iter - 1); 0 = the state in `in` is complete.
+struct SrFold {
+  int fold_sums = 0;
+  int nparts_s = 0;
+  const CgState* in = nullptr;
+  CgState* out = nullptr;
+  double* hist = nullptr;
+  int* h_done = nullptr;
+};
+int launch_cg_sr_pass_p(pb_grid* g, const Star& s, const double* r, const double* const* p_prev,
+                        double* p_new, double* x, double* r_out, const StencilPlanes& gp,
+                        const SrFold& f, int mode, int64_t host_iter, int defer);
+int launch_cg_sr_pass_s(pb_grid* g, const Star& s, const double* r, const StencilPlanes& gp,
+                        const CgState* st, int mode, int part_off, int* nblocks);
+// after pass S (unfolded): reduce its partials (+ allreduce on split grids) and run the
+// residual-sum stage on st in place (stage_delta0: the setup's delta = z0'A z0 only)
+int cg_sr_finalize(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done,
+                   int64_t host_iter, bool stage_delta0 = false);
 
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----
 int64_t compact_fast_work_len(const pb_grid* g);

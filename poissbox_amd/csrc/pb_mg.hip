@@ -715,12 +715,14 @@ static int64_t mg_engine_min_plane_default(const pb_ctx* ctx) {
 
 // the agglomerated coarse levels of a decomposed grid (Mg::La): the first level whose whole grid
 // fits the one-launch tail (<= mg_agglomerate_max points, default PB_MG_TAIL_MAX as on one
-// rank), at least level 1
+// rank), at least level 1. Only with an all-to-all to gather them (RCCL, or a host transport
+// with an alltoallv callback): the built-in shm transport keeps the halo-exchange levels
 static int mg_agglomerate_setup(Mg* mg) {
   pb_ctx* ctx = mg->ctx;
   const int L = (int)mg->lv.size();
   mg->La = 0;
   if (!ctx->split || L < 2 || !tune("mg_agglomerate", 1)) return PB_OK;
+  if (!ctx->comm && !ctx->h_alltoallv) return PB_OK;
   const int64_t tail_max = tune("mg_agglomerate_max", tune("mg_tail_max", 8192));
   int La = L;
   for (int l = L - 1; l >= 1; --l) {

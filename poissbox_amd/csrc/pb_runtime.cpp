@@ -40,7 +40,7 @@ const char* const kTuneNames[] = {
     "mg_presmooth_slim", "mg_prolong_cell", "mg_restrict_z", "mg_restrict_z_min_cols",
     "mg_split_fused", "mg_sweep2", "mg_tail", "mg_tail_lds", "mg_tail_max", "mg_transfer_minz", "mg_transfer_tpc", "passa_nt",
     "pcr_lines", "postx", "postx_minz", "postx_split", "postx_wgcu", "prr_minz", "prr_wgcu", "prrx",
-    "prrx_longz", "prrx_minz", "prrx_split", "prrx_wgcu", "slab_rows", "sor_omega_any", "stencil_blocks", "stencil_kcmin", "stencil_nt",
+    "prrx_longz", "prrx_minz", "prrx_split", "prrx_wgcu", "slab_rows", "sor_omega_any", "sr_s_shape", "stencil_blocks", "stencil_kcmin", "stencil_nt",
     "stencil_tall", "stencil_tall_min_plane", "stencil_ty", "sweep2_wgcu", "tall_wgcu",
     "xcd_remap", "zalt"};
 bool tune_known(const char* name) {
@@ -192,11 +192,27 @@ CommScope::CommScope(pb_ctx* c, hipStream_t st, bool force) : ctx(c), s(st), mar
   if (mark && ctx->comm_marks.size() > 64) (void)comm_marks_poll(ctx);
 }
 
-CommScope::~CommScope() {
-  if (!mark) return;
+static bool& unmarked_flag(pb_ctx* ctx, hipStream_t s) {
+  return s == ctx->comm_stream ? ctx->unmarked_comm : ctx->unmarked_main;
+}
+
+static void push_mark(pb_ctx* ctx, hipStream_t s) {
   hipEvent_t e = take_mark_event(ctx);
   (void)hipEventRecord(e, s);
   ctx->comm_marks.push_back(e);
+  unmarked_flag(ctx, s) = false;
+}
+
+CommScope::~CommScope() {
+  if (mark) push_mark(ctx, s);
+  else unmarked_flag(ctx, s) = true;
+}
+
+// before a host wait: a mark after the groups enqueued since each stream's last mark, so every
+// enqueued group is behind some pending mark until it completes
+static void mark_unmarked(pb_ctx* ctx) {
+  if (ctx->unmarked_main) push_mark(ctx, ctx->stream);
+  if (ctx->unmarked_comm) push_mark(ctx, ctx->comm_stream);
 }
 
 // Waits for query() to report completion. On a split context the wait is bounded: it fails with
@@ -208,6 +224,7 @@ static int bounded_wait(pb_ctx* ctx, Query query, const char* what) {
   const int64_t t0 = now_ms();
   // after a failure, drain for a short while only (never block teardown on a dead peer)
   const int64_t limit_ms = ctx->comm_failed ? 5000 : ctx->comm_timeout_ms;
+  mark_unmarked(ctx);
   (void)comm_marks_poll(ctx);
   int64_t progress_ms = t0;  // the last time communication was seen to progress (or none pending)
   for (int64_t spin = 0;; ++spin) {
@@ -448,9 +465,11 @@ int allreduce_device(pb_ctx* ctx, double* d_vals, int count) {
   PB_COMM_OK(ctx);
   ScopedTimer tm(ctx, "allreduce");
   if (ctx->h_allreduce) {
-    if (const int stall = tune("comm_stall_test_ms", 0)) {  // test hook: a peer that never answers
-      CommScope cs(ctx, ctx->stream, true);
-      PB_TRY(launch_comm_stall(ctx, ctx->stream, stall));
+    // test hook: a peer that never answers (ms < 0: inside an unforced group, which carries a
+    // progress mark only as every comm_mark_every-th group does)
+    if (const int stall = tune("comm_stall_test_ms", 0)) {
+      CommScope cs(ctx, ctx->stream, stall > 0);
+      PB_TRY(launch_comm_stall(ctx, ctx->stream, stall > 0 ? stall : -stall));
     }
     PB_HIP(hipMemcpyAsync(ctx->h_scalars + 16, d_vals, count * sizeof(double), hipMemcpyDeviceToHost,
                           ctx->stream));

@@ -59,7 +59,15 @@ struct pb_ksp {
   bool begun = false;
   int defer_x = 4;  // x updated every defer_x-th iteration (PB_CG_DEFER_X = 0, 2 or 4)
   int pslots() const { return defer_x == 4 ? 4 : 2; }
+  // single-reduction iteration (-ksp_cg_single_reduction on the fused operator, Jacobi / none):
+  // the state alternates between the two slots d_st[0..1] within a pb_ksp_iterate batch (pass P
+  // of the batch's n-th iteration reads slot n & 1 and writes the other); sr_nparts = pass S's
+  // partial-sum blocks of the last iteration (folded: reduced by the next pass P's prologue)
+  bool sr = false;
+  int sr_nparts = 0;
 };
+
+static int sr_pass_s(pb_ksp* k, const double* r, const CgState* st, int* nparts);
 
 extern "C" {
 
@@ -202,6 +210,7 @@ int pb_ksp_opts_default(pb_ksp_opts* o) {
   o->mg_levels = 0;
   o->mg_coarse_its = 8;
   o->sor_omega = 1.0;
+  o->cg_single_reduction = 0;
   return PB_OK;
 }
 
@@ -243,6 +252,15 @@ int pb_ksp_opts_parse(pb_ksp_opts* o, int argc, const char* const* argv) {
     } else if (!strcmp(a, "-pc_sor_omega") && v) {
       o->sor_omega = atof(v);
       ++i;
+    } else if (!strcmp(a, "-ksp_cg_single_reduction")) {
+      // PetscOptionsBool: a bare flag is true; an explicit value may follow
+      o->cg_single_reduction = 1;
+      if (v && (!strcmp(v, "true") || !strcmp(v, "1") || !strcmp(v, "yes"))) {
+        ++i;
+      } else if (v && (!strcmp(v, "false") || !strcmp(v, "0") || !strcmp(v, "no"))) {
+        o->cg_single_reduction = 0;
+        ++i;
+      }
     } else if (!strcmp(a, "-ksp_monitor")) {
       o->monitor = 1;
     } else if (!strcmp(a, "-ksp_converged_reason")) {
@@ -377,6 +395,11 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   // the passes closer to their patterns' rates -- 1.29 vs 1.36 ms/iteration at 512^3 on one box
   // (profiles/r02/ab_pst_defer_512.jsonl); PB_CG_PSTORE_B=0 stores p in pass A
   k->pst = tune("cg_pstore_b", 1) != 0 && fused_kind(k->A->kind) && !k->stored_z();
+  // single reduction: the fused operator with Jacobi / no PC (pass P forms p from r on load);
+  // elsewhere the KSPSolve_CG iteration runs (equal in exact arithmetic; pb_ksp_opts)
+  k->sr = k->opts.cg_single_reduction != 0 && fused_kind(k->A->kind) && !k->stored_z();
+  st.sr = k->sr ? 1 : 0;
+  if (k->sr) k->pst = true;  // r ping-pongs between r and r2 (pass P reads r_i, writes r_i+1)
   if (k->pst && !k->r2) {
     const size_t vb = (size_t)g->nlocal * sizeof(double);
     if (field_alloc(&k->r2, vb) != hipSuccess)
@@ -408,6 +431,12 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   } else {
     PB_TRY(launch_cg_init(g, b->d, x->d, k->r, k->pb[0], k->d_st, st.dinv, k->d_hist,
                           k->h_done_dev));
+    if (k->sr) {
+      // KSPSolve_CG_SingleReduction's setup: S = A z, delta = z'S (pass S over r0 = b)
+      int np = 0;
+      PB_TRY(sr_pass_s(k, k->r, k->d_st, &np));
+      PB_TRY(cg_sr_finalize(ctx, np, k->d_st, k->d_hist, k->h_done_dev, -1, true));
+    }
   }
   PB_SYNC(ctx, "pb_ksp_begin");
   k->b = b;
@@ -495,6 +524,87 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   }
   if (np == 0) PB_TRY(launch_cg_pc_sums(g, k->z, k->r, k->d_st, &np));
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
+}
+
+// pass S over r (t = dinv r - mu of state st): split grids exchange r's boundary planes (raw;
+// the loader transforms ghosts too) under the interior planes
+static int sr_pass_s(pb_ksp* k, const double* r, const CgState* st, int* nparts) {
+  pb_grid* g = k->A->grid;
+  pb_ctx* ctx = g->ctx;
+  Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};
+  StencilPlanes gp;
+  if (!ctx->split) {
+    gp.ghost_lo = gp.ghost_hi = nullptr;
+    gp.wrap = true;
+    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, 0, nparts);
+  }
+  gp.ghost_lo = g->ghost_lo;
+  gp.ghost_hi = g->ghost_hi;
+  const double* hi = r + (g->nzl - 1) * g->plane;
+  if (g->nzl < 3) {
+    PB_TRY(halo_exchange(g, r, hi));
+    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, 0, nparts);
+  }
+  int nb1 = 0, nb2 = 0;
+  ScopedTimer tm(ctx, "cg_sr_s");
+  PB_TRY(halo_begin(g, r, hi));
+  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_INTERIOR, 0, &nb1));
+  PB_TRY(halo_end(g));
+  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_BOUNDARY, nb1, &nb2));
+  *nparts = nb1 + nb2;
+  return PB_OK;
+}
+
+// One single-reduction iteration (PETSc KSPSolve_CG_SingleReduction): pass P, pass S, and -- unless
+// folded into the next pass P's prologue (one rank) -- the reduction + residual-sum stage.
+// n = the iteration's index inside this pb_ksp_iterate batch (state slot parity).
+static int enqueue_sr_iteration(pb_ksp* k, bool fold, int64_t n) {
+  pb_grid* g = k->A->grid;
+  pb_ctx* ctx = g->ctx;
+  Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};
+  const int64_t i = k->host_iter;
+  const int ns = k->pslots();
+  const double* p_prev[3] = {k->pb[i % ns], k->pb[(i + ns - 1) % ns], k->pb[(i + ns - 2) % ns]};
+  double* p_new = k->pb[(i + 1) % ns];
+  double* r = k->rbuf(i);
+  double* r_out = k->rbuf(i + 1);
+  CgState* st_in = k->d_st + (n & 1);
+  CgState* st_out = k->d_st + ((n + 1) & 1);
+  SrFold f;
+  f.fold_sums = fold && n > 0;
+  f.nparts_s = k->sr_nparts;
+  f.in = st_in;
+  f.out = st_out;
+  f.hist = k->d_hist;
+  f.h_done = k->h_done_dev;
+  StencilPlanes gp;
+  if (!ctx->split) {
+    gp.ghost_lo = gp.ghost_hi = nullptr;
+    gp.wrap = true;
+    PB_TRY(launch_cg_sr_pass_p(g, s, r, p_prev, p_new, k->x->d, r_out, gp, f, PLANES_ALL, i,
+                               k->defer_x));
+  } else {
+    // p's boundary planes (b from the completed state in st_in) -> halo, under the interior
+    gp.ghost_lo = g->ghost_lo;
+    gp.ghost_hi = g->ghost_hi;
+    PB_TRY(launch_cg_boundary(g, r, p_prev[0], st_in));
+    if (g->nzl < 3) {
+      PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
+      PB_TRY(launch_cg_sr_pass_p(g, s, r, p_prev, p_new, k->x->d, r_out, gp, f, PLANES_ALL, i,
+                                 k->defer_x));
+    } else {
+      ScopedTimer tm(ctx, "cg_sr_p_split");
+      PB_TRY(halo_begin(g, g->bnd_lo, g->bnd_hi));
+      PB_TRY(launch_cg_sr_pass_p(g, s, r, p_prev, p_new, k->x->d, r_out, gp, f, PLANES_INTERIOR,
+                                 i, k->defer_x));
+      PB_TRY(halo_end(g));
+      PB_TRY(launch_cg_sr_pass_p(g, s, r, p_prev, p_new, k->x->d, r_out, gp, f, PLANES_BOUNDARY,
+                                 i, k->defer_x));
+    }
+  }
+  PB_TRY(sr_pass_s(k, r_out, st_out, &k->sr_nparts));
+  if (!fold) PB_TRY(cg_sr_finalize(ctx, k->sr_nparts, st_out, k->d_hist, k->h_done_dev, i));
+  return PB_OK;
 }
 
 // fold: the finalize steps run in the passes' prologues (one rank, Jacobi; fold_a = pass A also
@@ -596,7 +706,8 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
                     tune("cg_fold", 1) != 0;
   int64_t n = 0;
   for (; n < iters && !k->stopped; ++n) {
-    PB_TRY(enqueue_iteration(k, fold, fold && n > 0));
+    if (k->sr) PB_TRY(enqueue_sr_iteration(k, fold, n));
+    else PB_TRY(enqueue_iteration(k, fold, fold && n > 0));
     const int64_t hi = k->host_iter++;
     // only the iterations the poll below waits for get an event (j = 0 mod C; folded j + 1): an
     // event record between two kernels costs the stream ~6 us of idle time (measured 5.9 us per
@@ -611,6 +722,17 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
       PB_TRY(wait_event(ctx, k->ring[(fold ? j + 1 : j) % R], "KSP convergence poll"));
       if (k->h_done[j + 1]) k->stopped = true;
     }
+  }
+  if (k->sr) {
+    // the residual-sum stage of the batch's last iteration (folded runs), then the state back
+    // into slot 0 for the next batch and the other entry points
+    if (fold && n > 0)
+      PB_TRY(cg_sr_finalize(ctx, k->sr_nparts, k->d_st + (n & 1), k->d_hist, k->h_done_dev,
+                            k->host_iter - 1));
+    if (n & 1)
+      PB_HIP(hipMemcpyAsync(k->d_st, k->d_st + 1, sizeof(CgState), hipMemcpyDeviceToDevice,
+                            ctx->stream));
+    return PB_OK;
   }
   if (fold && n > 0)
     PB_TRY(cg_fold_tail(ctx, k->fold_nparts_b, k->d_st, k->d_hist, k->h_done_dev,

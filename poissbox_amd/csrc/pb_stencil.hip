@@ -150,9 +150,10 @@ using PassA = PassAT<true>;
 // PST (PB_CG_PSTORE_B): the field is p re-formed from (r, p_old) by CombineLoad, stored to p_out;
 // r is read from op[0] (= r) and written to r_out (another buffer: neighbouring waves still read
 // r through the z-queue, an in-place update would race with them).
-template <int XU, bool PST = false>
+// SUMS = false: the single-reduction iteration's pass P (the residual sums move to pass S)
+template <int XU, bool PST = false, bool SUMS = true>
 struct PassB {
-  static constexpr int NS = 4, NE = XU == 1 ? 3 : (XU == 2 ? 2 : (XU == 3 ? 5 : 1));
+  static constexpr int NS = SUMS ? 4 : 0, NE = XU == 1 ? 3 : (XU == 2 ? 2 : (XU == 3 ? 5 : 1));
   static constexpr bool RAW = false;  // put() takes the Laplacian, not the 7 values
   // one workgroup per CU (z-chunks of half the slab at 512^3): 8-10 % faster than 3 per CU
   static constexpr int WGCU = PST ? PB_PSTB_WGCU : 1;
@@ -194,13 +195,16 @@ struct PassB {
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       rv[e] = op[0][e] + (-alpha) * w[e];
-      const double s = dinv * rv[e];
-      const double t = s - mu;
-      acc[0] += t;
-      acc[1] += t * t;
-      acc[2] += t * rv[e];
-      acc[3] += rv[e];
+      if constexpr (SUMS) {
+        const double s = dinv * rv[e];
+        const double t = s - mu;
+        acc[0] += t;
+        acc[1] += t * t;
+        acc[2] += t * rv[e];
+        acc[3] += rv[e];
+      }
     }
+    (void)acc;
     if constexpr (PST) {
       store_row<V>(r_out, idx, rv, nt);
       store_row<V>(p_out, idx, c, nt);
@@ -232,6 +236,55 @@ struct PassB {
   }
 };
 
+// Single-reduction CG pass S (PETSc KSPSolve_CG_SingleReduction: z = B r, S = A z, then z'z,
+// z'r and z'S in one reduction): the field is t = dinv r' - mu_old, formed on load (ghost planes
+// of a split grid hold raw r' and are transformed too); the engine's Laplacian is s = A t. Sums
+// t, t^2, t.r', r' (norm, beta and the mean as pass B's) and t.s (delta = z'A z: z = t - const
+// and A annihilates constants, so t'A t is z'A z up to rounding). Read-only: 8 B/DoF.
+struct ZLoad {
+  static constexpr int NR = 1;
+  static constexpr bool GHOST_RAW = true;
+  const double* __restrict__ r;
+  const CgState* st;
+  double dinv = 1.0, shift = 0.0;
+  __device__ __forceinline__ void prepare() { prepare_from(*st); }
+  template <class S>
+  __device__ __forceinline__ void prepare_from(const S& s) {
+    dinv = s.dinv;
+    shift = -s.mu;
+  }
+  __device__ __forceinline__ const double* src(int) const { return r; }
+  __device__ __forceinline__ double value(const double* raw) const {
+    double z = dinv * raw[0];
+    return z + shift;
+  }
+};
+template <bool TALLV>
+struct SrSumsT {
+  static constexpr int NS = 5, NE = 1;
+  static constexpr bool RAW = false, TALL = TALLV;
+  static constexpr int WGCU = 1;
+  static constexpr bool CAP = true, WIDE8 = true;
+  static constexpr bool PREFETCH = true;
+  // operand 0 (r') is the centre plane's raw queue value
+  static constexpr int qop(int a) { return a == 0 ? 0 : -1; }
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ const double* src(int) const { return nullptr; }
+  template <int V>
+  __device__ __forceinline__ void put(RowIx, const double (&c)[V], const double (&w)[V],
+                                      double (&op)[1][V], double* acc, int) const {
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const double t = c[e], rv = op[0][e];
+      acc[0] += t;
+      acc[1] += t * t;
+      acc[2] += t * rv;
+      acc[3] += rv;
+      acc[4] += t * w[e];
+    }
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 // Finalize folded into the next pass's prologue (one rank, Jacobi CG): EVERY WAVE reduces the
 // previous pass's partials in the finalize kernel's fixed order (lane-strided sums, xor
@@ -242,7 +295,9 @@ struct PassB {
 // boundaries) from every iteration.
 // ---------------------------------------------------------------------------------------------
 struct Fold {
-  int stage = 0;                  // 0: no fold; 1: stage 1 (pass B); 2: stage 2 (pass A)
+  // 0: no fold; 1: stage 1 (pass B); 2: stage 2 (pass A); single-reduction pass P: 3: the
+  // residual-sum stage of the previous iteration, then the top of this one; 4: the top only
+  int stage = 0;
   int nparts = 0, width = 1;      // partials of the previous pass
   const double* parts = nullptr;
   const CgState* in = nullptr;    // state slot read
@@ -906,6 +961,7 @@ __device__ __forceinline__ bool finite(double v) { return v == v && v - v == 0.0
 // passes: one workgroup per CU); beyond it, a 256-thread tree (a lone wave took 29 us over the
 // 2048 partials of the elementwise kernels of the preconditioned CG)
 static constexpr int kFoldMaxParts = 1024;
+static constexpr int kMaxSums = 5;  // partial sums per block (single-reduction pass S: 5)
 // fixed-order reduction of nparts x width partials by ONE wave: lane l sums blocks l, l+64, ...
 // in order, then an xor butterfly (every lane ends with the same bits). Used by the finalize
 // kernel (wave 0) and by every wave of a folded pass prologue, so both paths round alike.
@@ -913,7 +969,7 @@ __device__ __forceinline__ void wave_reduce_parts(const double* __restrict__ par
                                                   int width, double* S) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < kMaxSums; ++s) {
     double v = 0.0;
     if (s < width)
       for (int b = lane; b < nparts; b += 64) v += parts[(int64_t)b * width + s];
@@ -998,6 +1054,25 @@ __device__ __forceinline__ void cg_stage1(CgState& st, double dpi) {
   }
 }
 
+// iterations i % D < D-1 leave alpha_i p_i pending in x; the last of each D applied them all
+// (PassB<XU>)
+__device__ __forceinline__ void cg_pend(CgState& st) {
+  const int64_t i = st.it;
+  const int D = st.defer_x;
+  const int m = D > 0 ? (int)(i % D) : 0;
+  if (D > 0 && m < D - 1) {
+    // (value selects, no computed index: st may be a register copy)
+    st.pa[0] = m == 0 ? st.alpha : st.pa[0];
+    st.pa[1] = m == 1 ? st.alpha : st.pa[1];
+    st.pa[2] = m == 2 ? st.alpha : st.pa[2];
+    st.pend_iter = i - m;
+    st.pend_count = m + 1;
+  } else {
+    st.pend_iter = -1;
+    st.pend_count = 0;
+  }
+}
+
 // stage 2 (after pass B / the PC apply): residual sums -> norm, convergence tests, next beta
 __device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* hist, int* h_done,
                                           int64_t host_iter) {
@@ -1012,21 +1087,8 @@ __device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* 
       zr = S[2] - delta * S[3];
     }
     const double dp = sqrt(zz > 0.0 ? zz : 0.0);
-    // iterations i % D < D-1 leave alpha_i p_i pending in x; the last of each D applied them all
-    // (PassB<XU>)
-    const int D = st.defer_x;
-    const int m = D > 0 ? (int)(i % D) : 0;
-    if (D > 0 && m < D - 1) {
-      // (value selects, no computed index: st may be a register copy)
-      st.pa[0] = m == 0 ? st.alpha : st.pa[0];
-      st.pa[1] = m == 1 ? st.alpha : st.pa[1];
-      st.pa[2] = m == 2 ? st.alpha : st.pa[2];
-      st.pend_iter = i - m;
-      st.pend_count = m + 1;
-    } else {
-      st.pend_iter = -1;
-      st.pend_count = 0;
-    }
+    // (single reduction: alpha_i was booked by cg_sr_top, before pass P applied it)
+    if (!st.sr) cg_pend(st);
     st.dp = dp;
     st.its = i + 1;
     if (i + 1 < st.nhist) {
@@ -1045,6 +1107,7 @@ __device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* 
     } else {
       st.beta = zr;
       st.mu = mu;
+      st.delta = S[4];  // (single reduction: z'A z, read by the next cg_sr_top)
       st.it = i + 1;
       if (!finite(zr)) {
         st.reason = PB_KSP_DIVERGED_NANORINF;
@@ -1068,19 +1131,31 @@ __device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* 
   if (h_done) h_done[host_iter + 1] = st.done;
 }
 
+// Top of a single-reduction iteration (PETSc KSPSolve_CG_SingleReduction, real scalars): the
+// beta checks ran with the residual-sum stage (cg_stage0 / cg_stage2, as in KSPSolve_CG); here
+// p'w = delta (i = 0: p = z, w = A z) or delta - beta^2 dpiold / betaold^2, then stage 1's
+// INDEFINITE_MAT / NaN exits and alpha, and alpha_i's deferred-x bookkeeping (pass P applies it)
+__device__ __forceinline__ void cg_sr_top(CgState& st) {
+  if (st.done) return;
+  const double dpi = st.it == 0 ? st.delta
+                                : st.delta - st.beta * st.beta * st.dpi / (st.betaold * st.betaold);
+  cg_stage1(st, dpi);
+  if (!st.done) cg_pend(st);
+}
+
 // Finalize: deterministic fixed-order reduction of the per-block partials, then the PETSc CG
 // scalar logic (KSPSolve_CG + KSPConvergedDefault) on the device. mode bit 1 = reduce partials
 // into sums[], bit 2 = update the state from sums[] (split around the RCCL allreduce).
-// stage 0 = after init, 1 = after pass A (p.w), 2 = after pass B (residual sums).
+// stage 0 = after init, 1 = after pass A (p.w), 2 = after pass B (residual sums), 3 = delta only.
 __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restrict__ parts,
                                                           int nparts, int width, double* sums,
                                                           int mode, int stage, CgState* st,
                                                           double* hist, int* h_done,
                                                           int64_t host_iter) {
-  double S[4];
+  double S[kMaxSums];
   if ((mode & 1) && nparts > kFoldMaxParts) {
     // many partials (elementwise / multigrid kernels): 256-thread fixed-order tree
-    __shared__ double red[256][4];
+    __shared__ double red[256][kMaxSums];
     for (int s = 0; s < width; ++s) {
       double v = 0.0;
       for (int b = threadIdx.x; b < nparts; b += 256) v += parts[(int64_t)b * width + s];
@@ -1102,10 +1177,11 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
       for (int s = 0; s < width; ++s) sums[s] = S[s];
   }
   if (!(mode & 2) || threadIdx.x != 0) return;
-  for (int s = 0; s < 4; ++s) S[s] = s < width ? sums[s] : 0.0;
+  for (int s = 0; s < kMaxSums; ++s) S[s] = s < width ? sums[s] : 0.0;
   if (stage == 0) cg_stage0(*st, S, hist, h_done);
   else if (stage == 1) cg_stage1(*st, S[0]);
-  else cg_stage2(*st, S, hist, h_done, host_iter);
+  else if (stage == 2) cg_stage2(*st, S, hist, h_done, host_iter);
+  else st->delta = S[4];  // 3: the single-reduction setup's delta = z0'A z0
 }
 
 // field-wise copy (an aggregate copy becomes a memcpy that pins the register copy in scratch)
@@ -1119,16 +1195,25 @@ __device__ __forceinline__ void cg_copy(CgState& d, const CgState& s) {
   d.reason = s.reason, d.done = s.done, d.pc = s.pc, d.nullspace = s.nullspace;
   d.defer_x = s.defer_x;
   d.bbp = s.bbp;
+  d.delta = s.delta, d.sr = s.sr;
 }
-static_assert(sizeof(CgState) == 232, "cg_copy lists every CgState field");
+static_assert(sizeof(CgState) == 248, "cg_copy lists every CgState field");
 
 __device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st) {
-  double S[4];
+  double S[kMaxSums];
   cg_copy(st, *f.in);
-  wave_reduce_parts(f.parts, f.nparts, f.width, S);  // (garbage if done: the stages ignore it)
+  // (garbage if done: the stages ignore it)
+  if (f.stage != 4) wave_reduce_parts(f.parts, f.nparts, f.width, S);
   const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-  if (f.stage == 1) cg_stage1(st, S[0]);
-  else cg_stage2(st, S, lead ? f.hist : nullptr, lead ? f.h_done : nullptr, f.host_iter);
+  if (f.stage == 1) {
+    cg_stage1(st, S[0]);
+  } else if (f.stage == 2) {
+    cg_stage2(st, S, lead ? f.hist : nullptr, lead ? f.h_done : nullptr, f.host_iter);
+  } else {
+    if (f.stage == 3)
+      cg_stage2(st, S, lead ? f.hist : nullptr, lead ? f.h_done : nullptr, f.host_iter);
+    cg_sr_top(st);
+  }
   if (lead) cg_copy(*f.out, st);
 }
 
@@ -1318,6 +1403,75 @@ int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_d
   PB_HIP(hipGetLastError());
   PB_HIP(hipMemcpyAsync(st2, st2 + 1, sizeof(CgState), hipMemcpyDeviceToDevice, ctx->stream));
   return PB_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Single-reduction CG (-ksp_cg_single_reduction): pass P (p, r' and the deferred x update; no
+// sums) and pass S (t = dinv r' - mu, s = A t, five sums). 32 + 8 B/DoF per iteration (+ the x
+// update's 32 every fourth), one reduction -- against 16 + 32 and two for the KSPSolve_CG passes.
+// ---------------------------------------------------------------------------------------------
+template <int XU>
+static int sr_pass_p_one(pb_grid* g, const Star& s, const double* r, const double* const* p_prev,
+                         double* p_new, double* x, double* r_out, const StencilPlanes& gp,
+                         const Fold& f, int mode) {
+  PassB<XU, true, false> ep{x, nullptr, p_prev[0], XU == 3 ? p_prev[1] : nullptr,
+                            XU == 3 ? p_prev[2] : nullptr, nullptr, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  ep.r_out = r_out;
+  ep.p_out = p_new;
+  CombineLoad ld{r, p_prev[0], nullptr, 0.0, 0.0, 0.0};
+  ld.after1 = 1;  // b = beta / betaold as the prologue's top found it (bbp)
+  return launch_any(g, s, ld, gp, ep, nullptr, mode, 0, nullptr, 1, 0, f);
+}
+
+int launch_cg_sr_pass_p(pb_grid* g, const Star& s, const double* r, const double* const* p_prev,
+                        double* p_new, double* x, double* r_out, const StencilPlanes& gp,
+                        const SrFold& sf, int mode, int64_t host_iter, int defer) {
+  Fold f;
+  f.stage = sf.fold_sums ? 3 : 4;
+  f.nparts = sf.nparts_s;
+  f.width = 5;
+  f.parts = g->ctx->d_partials;
+  f.in = sf.in;
+  f.out = sf.out;
+  f.hist = sf.hist;
+  f.h_done = sf.h_done;
+  f.host_iter = host_iter - 1;  // the residual-sum stage of the previous iteration
+  if (defer == 4 && host_iter % 4 == 3) {
+    ScopedTimer tm(g->ctx, timer_name(mode, "cg_sr_p_x4", "cg_sr_p_x4_interior", "cg_sr_p_x4_boundary"));
+    return sr_pass_p_one<3>(g, s, r, p_prev, p_new, x, r_out, gp, f, mode);
+  }
+  if (defer == 4) {
+    ScopedTimer tm(g->ctx, timer_name(mode, "cg_sr_p", "cg_sr_p_interior", "cg_sr_p_boundary"));
+    return sr_pass_p_one<0>(g, s, r, p_prev, p_new, x, r_out, gp, f, mode);
+  }
+  if (defer == 2 && host_iter % 2 == 1) {
+    ScopedTimer tm(g->ctx, timer_name(mode, "cg_sr_p_x2", "cg_sr_p_x2_interior", "cg_sr_p_x2_boundary"));
+    return sr_pass_p_one<1>(g, s, r, p_prev, p_new, x, r_out, gp, f, mode);
+  }
+  if (defer == 2) {
+    ScopedTimer tm(g->ctx, timer_name(mode, "cg_sr_p", "cg_sr_p_interior", "cg_sr_p_boundary"));
+    return sr_pass_p_one<0>(g, s, r, p_prev, p_new, x, r_out, gp, f, mode);
+  }
+  ScopedTimer tm(g->ctx, timer_name(mode, "cg_sr_p_x1", "cg_sr_p_x1_interior", "cg_sr_p_x1_boundary"));
+  return sr_pass_p_one<2>(g, s, r, p_prev, p_new, x, r_out, gp, f, mode);
+}
+
+int launch_cg_sr_pass_s(pb_grid* g, const Star& s, const double* r, const StencilPlanes& gp,
+                        const CgState* st, int mode, int part_off, int* nblocks) {
+  ScopedTimer tm(g->ctx, timer_name(mode, "cg_sr_s", "cg_sr_s_interior", "cg_sr_s_boundary"));
+  // (marches upwards after pass P marched downwards: it starts on the planes P wrote last)
+  const int shape = tune("sr_s_shape", 0);
+  const int wg = shape == 1 ? 2 : (shape == 2 ? 3 : (shape == 4 ? 2 : (shape == 5 ? 3 : 0)));
+  if (shape >= 3)
+    return launch_any(g, s, ZLoad{r, st}, gp, SrSumsT<true>{}, &st->done, mode, part_off,
+                      nblocks, 0, wg);
+  return launch_any(g, s, ZLoad{r, st}, gp, SrSumsT<false>{}, &st->done, mode, part_off, nblocks,
+                    0, wg);
+}
+
+int cg_sr_finalize(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done,
+                   int64_t host_iter, bool stage_delta0) {
+  return cg_reduce_update(ctx, stage_delta0 ? 3 : 2, nparts, 5, st, hist, h_done, host_iter);
 }
 
 // x += alpha * p (the pending half of the deferred solution update)

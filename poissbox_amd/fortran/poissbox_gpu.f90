@@ -55,6 +55,7 @@ module poissbox_gpu
      integer(c_int) :: ksp_type, pc_type, nullspace, monitor, converged_reason, check_every
      integer(c_int) :: mg_levels, mg_coarse_its
      real(c_double) :: sor_omega
+     integer(c_int) :: cg_single_reduction
   end type pb_ksp_opts
 
   type, bind(C), public :: pb_ksp_result

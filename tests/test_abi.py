@@ -65,6 +65,17 @@ def test_options_parse_petsc_names():
     assert (d.rtol, d.atol, d.dtol, d.max_it, d.pc_type) == (1e-5, 1e-50, 1e5, 10000, pb.PC_JACOBI)
     with pytest.raises(pb.PbError):
         pb.ksp_options(["-ksp_type", "gmres"])
+    assert d.cg_single_reduction == 0
+
+
+def test_options_parse_single_reduction():
+    """-ksp_cg_single_reduction (PetscOptionsBool: bare flag = true, or an explicit value)."""
+    assert pb.ksp_options(["-ksp_cg_single_reduction"]).cg_single_reduction == 1
+    o = pb.ksp_options(["-ksp_cg_single_reduction", "-ksp_rtol", "1e-9"])
+    assert o.cg_single_reduction == 1 and o.rtol == 1e-9
+    for v, want in (("true", 1), ("1", 1), ("yes", 1), ("false", 0), ("0", 0), ("no", 0)):
+        o = pb.ksp_options(["-ksp_cg_single_reduction", v, "-ksp_max_it", "5"])
+        assert o.cg_single_reduction == want and o.max_it == 5
 
 
 def test_tuning_table_round_trip():

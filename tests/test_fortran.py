@@ -134,3 +134,29 @@ def test_fortran_demo_dead_peer_is_an_error():
     for p in procs:
         o, e = p.communicate(timeout=120)
         assert p.returncode != 0, o + e
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks,args,oracle_kw", [
+    # -pc_type mg over the shm transport (no all-to-all: the coarse levels stay decomposed,
+    # ADVICE r04 -- before, every PC apply failed with PB_ERR_COMM)
+    (4, ["-pc_type", "mg"], {"pc": "mg", "nranks": 4}),
+    # -ksp_cg_single_reduction through the reference's options path (KSPSetFromOptions)
+    (3, ["-ksp_cg_single_reduction"], {"single_reduction": 1}),
+])
+def test_fortran_demo_shm_options(nranks, args, oracle_kw):
+    from oracle import oracle as O
+    if not os.path.exists(DEMO):
+        subprocess.run(["make", "-s", "-C", FDIR], check=True)
+    outs = _launch(nranks, ["-n", "64", "-ksp_rtol", "1e-8", "-ksp_converged_reason"] + args)
+    for rc, o, e in outs:
+        assert rc == 0, o + e
+    txt = "".join(o for _, o, _ in outs)
+    n3 = (64, 64, 64)
+    h = (1 / 64,) * 3
+    b = O.stencil(O.fill_random(64 ** 3, 20231015), n3, h)
+    _, reason, its, _ = O.cg_solve(b, n3, h, rtol=1e-8, **oracle_kw)
+    m = re.findall(r"converged due to CONVERGED_RTOL iterations (\d+)", txt)
+    assert reason == 2 and m and all(int(v) == its for v in m), txt[-2000:]
+    res = float(re.search(r"Solution residual \(L2 norm\):\s+(\S+)", txt).group(1))
+    assert res < 1e-4 * np.linalg.norm(b)

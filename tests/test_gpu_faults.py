@@ -72,11 +72,14 @@ def test_long_local_work_is_not_a_comm_timeout(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_stalled_peer_times_out(monkeypatch, tune):
+@pytest.mark.parametrize("forced", [True, False])
+def test_stalled_peer_times_out(monkeypatch, tune, forced):
     """A communication that starts and never finishes -- the test hook comm_stall_test_ms puts a
     kernel that waits for a peer's data (a host-mapped flag) inside the allreduce's
     communication scope -- fails the wait with PB_ERR_COMM after PB_COMM_TIMEOUT_MS (200 ms), the
-    failure releases the waiting kernel, and the failed context refuses further collectives."""
+    failure releases the waiting kernel, and the failed context refuses further collectives.
+    forced = False: the stall rides in a group without a progress mark of its own (marks only
+    every 1000th group) -- the wait marks the unmarked groups before it polls."""
     import time
     monkeypatch.setenv("PB_COMM_TIMEOUT_MS", "200")
     loop = lambda lo, hi: (hi.copy(), lo.copy())  # noqa: E731 - loop-back halo
@@ -86,7 +89,9 @@ def test_stalled_peer_times_out(monkeypatch, tune):
         x = pb.Vec(da)
         x.set_random(1)
         assert x.norm() > 0                        # the hook off: a normal allreduce
-        tune.set("comm_stall_test_ms", 20000)      # (the kernel ends by itself after 20 s)
+        if not forced:
+            tune.set("comm_mark_every", 1000)
+        tune.set("comm_stall_test_ms", 20000 if forced else -20000)  # (ends by itself after 20 s)
         t0 = time.monotonic()
         with pytest.raises(PbError) as e:
             x.norm()

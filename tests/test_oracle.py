@@ -217,6 +217,41 @@ def test_cg_restatement_converges():
         assert np.linalg.norm(err) / np.linalg.norm(xt) < 1.0
 
 
+@pytest.mark.parametrize("n3,rtol", [((32, 32, 32), 1e-10), ((64, 64, 64), 1e-10),
+                                     ((48, 40, 36), 1e-10), ((32, 32, 32), 1e-5)])
+def test_cg_single_reduction_restatement(n3, rtol):
+    """PETSc KSPSolve_CG_SingleReduction restated (form 1: w and p'w by recurrence) reproduces
+    the KSPSolve_CG restatement's reason, iteration count and history (1e-11; they are equal in
+    exact arithmetic), and form 2 (w = A p recomputed, the GPU passes' arithmetic) stays within
+    the same bar of form 1."""
+    N = int(np.prod(n3))
+    h = tuple(1.0 / m for m in n3)
+    b = O.stencil(O.fill_random(N, 1234), n3, h)
+    out = {sr: O.cg_solve(b, n3, h, rtol=rtol, single_reduction=sr) for sr in (0, 1, 2)}
+    (x0, r0, i0, h0), (x1, r1, i1, h1), (x2, r2, i2, h2) = out[0], out[1], out[2]
+    assert r0 == r1 == r2 == 2 and i0 == i1 == i2
+    assert np.max(np.abs(h1 - h0) / h0) < 1e-11
+    assert np.max(np.abs(h2 - h1) / h1) < 1e-11
+    assert np.max(np.abs(x1 - x0)) < 1e-12 * np.max(np.abs(x0))
+    assert np.max(np.abs(x2 - x1)) < 1e-12 * np.max(np.abs(x1))
+
+
+def test_cg_single_reduction_breakdowns():
+    """Single reduction at the edges KSPSolve_CG_SingleReduction handles: max_it (DIVERGED_ITS,
+    its = max_it), zero rhs (CONVERGED_ATOL at iteration 0), an indefinite operator sign flip
+    is out of reach of the 7-point operator -- the first two against KSPSolve_CG's restatement."""
+    n3 = (16, 16, 16)
+    h = (1 / 16,) * 3
+    b = O.stencil(O.fill_random(4096, 7), n3, h)
+    for max_it in (1, 2, 5):
+        _, r0, i0, h0 = O.cg_solve(b, n3, h, rtol=0.0, max_it=max_it)
+        _, r1, i1, h1 = O.cg_solve(b, n3, h, rtol=0.0, max_it=max_it, single_reduction=1)
+        assert (r0, i0) == (r1, i1) == (-3, max_it) and len(h0) == len(h1) == max_it + 1
+        assert np.max(np.abs(h1 - h0) / h0) < 1e-12
+    x, r, i, hz = O.cg_solve(np.zeros(4096), n3, h, single_reduction=1)
+    assert (r, i, len(hz)) == (3, 0, 1) and not np.any(x)
+
+
 def test_fill_random_distribution():
     x = O.fill_random(1 << 16, 20231015)
     assert x.min() >= -1.0 and x.max() <= 1.0 and abs(x.mean()) < 0.01
