@@ -39,6 +39,28 @@ PASS_BYTES = {
     1: {"a": 16, "b_even": 32, "b_x": {0: 48, 2: 48, 4: 64}},
 }
 MATVEC_BYTES = 16            # y = A x: read x, write y
+# single-reduction CG (-ksp_cg_single_reduction, pb_solver.cpp enqueue_sr_iteration): pass P reads
+# r, p_old and writes p, r' (32; + x read / write and p_{i-2}, p_{i-3} every 4th iteration: 64);
+# pass S reads r' (8): 32 + 8 + 32/4 = 48 B/DoF per iteration at D = 4
+SR_BYTES = {"p": 32, "p_x4": 64, "s": 8}
+SR_ITER_BYTES = SR_BYTES["p"] + SR_BYTES["s"] + (SR_BYTES["p_x4"] - SR_BYTES["p"]) / 4
+
+
+def memory_clock():
+    """The memory clock level in use per card (sysfs pp_dpm_mclk, the level marked '*'), read
+    without starting a program (no rocm-smi: under rocprofv3 a child would re-exec), or None."""
+    import glob
+    import re
+    res = {}
+    for f in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_mclk")):
+        try:
+            for line in open(f):
+                if "*" in line:
+                    m = re.search(r"(\d+)\s*Mhz", line, re.I)
+                    res[f.split("/")[4]] = int(m.group(1)) if m else line.strip()
+        except Exception:
+            pass
+    return res or None
 
 
 def pstore_mode(setting=None):
@@ -55,6 +77,67 @@ def cg_iter_bytes(defer, pstore=1):
         return pb_["a"] + pb_["b_x"][0]
     return pb_["a"] + ((defer - 1) * pb_["b_even"] + pb_["b_x"][defer]) / defer
 SEED = 20231015
+
+
+def nloc_even(n):
+    return n - (n % 2)
+
+
+def sustained_median_ms(samples):
+    return float(np.median(samples)) if len(samples) else None
+
+
+def run_sr_variant(args, pb, ctx, A, P, b, da, dist, world):
+    """The single-reduction iteration (-ksp_cg_single_reduction: 2 passes, one reduction, 48 B/DoF)
+    on the same system, same protocol as the headline (W untimed, K timed between barriers, max
+    over ranks), then 16 iterations with every pass timed. A stated variant line: the headline
+    stays PETSc's default KSPSolve_CG."""
+    x = pb.Vec(da)
+    opts = pb.ksp_options(["-ksp_type", "cg", "-pc_type", "jacobi", "-ksp_cg_single_reduction"],
+                          rtol=0.0, atol=0.0, dtol=1e300, max_it=args.warmup + args.steps + 32,
+                          check_every=8)
+    ksp = pb.KSP(A, P, opts)
+    ksp.begin(b, x)
+    ksp.iterate(args.warmup)
+    ctx.barrier()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ksp.iterate(args.steps)
+    ctx.sync()
+    elapsed = time.perf_counter() - t0
+    ctx.barrier()
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    ksp.iterate(16)
+    ctx.sync()
+    passes = {}
+    nloc = da.nlocal
+    for nm, key in (("cg_sr_p", "p"), ("cg_sr_p_x4", "p_x4"), ("cg_sr_s", "s")):
+        ms, cnt = ctx.timing(nm)
+        if cnt:
+            t_ = ms / cnt / 1e3
+            gb = SR_BYTES[key] * nloc / t_ / 1e9
+            passes[nm] = {"avg_ms": t_ * 1e3, "GBps": gb, "frac": gb / HBM_PEAK_GBS,
+                          "bytes_per_dof": SR_BYTES[key]}
+    ctx.set_timing(False)
+    reason, its, hist = ksp.end()
+    ksp.destroy()
+    x.destroy()
+    N = int(np.prod(da.n))
+    per_step = elapsed / args.steps
+    return {"ksp": "-ksp_type cg -pc_type jacobi -ksp_cg_single_reduction (PETSc "
+                   "KSPSolve_CG_SingleReduction: z'z, z'r, z'Az in one reduction)",
+            "ms_per_step": per_step * 1e3, "iter_per_s": 1.0 / per_step,
+            "value": (N * args.steps / elapsed) if N else None, "unit": "DoF-updates/s",
+            "bytes_per_dof": SR_ITER_BYTES,
+            "achieved_GBps": SR_ITER_BYTES * nloc / per_step / 1e9 if nloc else None,
+            "passes": passes, "its": its, "rnorm_last": float(hist[-1])}
 
 
 def global_grid(ngpus, base=512):
@@ -761,6 +844,13 @@ def main():
     ctx.sync()
     mv_s = ctx.timing_samples("stencil")
     ctx.set_timing(False)
+    # HBM calibration in this same process: a flat copy of the matvec's
+    # bytes, so a slow-mode box shows up as a slow copy too
+    try:
+        cp_best, cp_med = ctx.copy_probe(n=nloc_even(da.nlocal), reps=10)
+    except Exception:
+        cp_best = cp_med = None
+    sr_var = run_sr_variant(args, pb, ctx, A, P, b, da, dist, world)
 
     nloc = da.nlocal
     N = n[0] * n[1] * n[2]
@@ -815,7 +905,16 @@ def main():
                          "achieved": gbs(roof_bytes, t_roof), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs(roof_bytes, t_roof) / HBM_PEAK_GBS,
                          "traffic": None, "bytes_per_dof": roof_bytes,
-                         "avg_launch_ms": t_roof * 1e3},
+                         "avg_launch_ms": t_roof * 1e3,
+                         # the north-star kernel (standalone 7-point matvec, 16 B/DoF) and this
+                         # process's flat-copy calibration of the same bytes, in the roofline
+                         # object (the driver keeps it)
+                         "matvec_ms": t_mv * 1e3,
+                         "matvec_frac": gbs(MATVEC_BYTES, t_mv) / HBM_PEAK_GBS,
+                         "matvec_sustained_median_ms": sustained_median_ms(mv_s),
+                         "copy_probe_GBps": cp_best, "copy_probe_median_GBps": cp_med,
+                         "copy_probe_frac": (cp_best / HBM_PEAK_GBS) if cp_best else None,
+                         "mclk_MHz": memory_clock()},
             "kernels": {
                 "cg_pass_a": {"avg_ms": t_a * 1e3, "GBps": gbs(PB["a"], t_a),
                               "frac": gbs(PB["a"], t_a) / HBM_PEAK_GBS, "bytes_per_dof": PB["a"]},
@@ -831,6 +930,7 @@ def main():
                                  "bytes_per_dof": MATVEC_BYTES},
             },
             "matvec_star7_sustained": sustained_row(mv_s, nloc, gbs),
+            "variants": {"cg_single_reduction": sr_var},
             "cg_x_update_every": defer,
             "launcher": os.environ.get("PB_BENCH_LAUNCHER",
                                        "torch.distributed.run" if dist else "none"),

@@ -128,6 +128,11 @@ int pb_ctx_get_timing(pb_ctx* ctx, const char* name, double* total_ms, int64_t* 
 int pb_ctx_get_timing_samples(pb_ctx* ctx, const char* name, float* ms, int64_t cap,
                               int64_t* count);
 int pb_ctx_reset_timing(pb_ctx* ctx);
+/* HBM calibration of this process's device (no reference counterpart; bench.py reports it beside
+ * the matvec's rate): a flat fp64 copy of n doubles -- 16-B loads, non-temporal 16-B stores, the
+ * standalone matvec's access mix without its stencil -- `reps` timed launches after two warm-ups;
+ * GB/s counted as 16 B per element. Allocates and frees its own 2 x n doubles. */
+int pb_ctx_copy_probe(pb_ctx* ctx, int64_t n, int reps, double* best_gbps, double* median_gbps);
 
 /* ---- tuning (kernel selection and launch shapes; no reference counterpart) ----
  * Process-wide table of the launchers' parameters (INTEGRATION.md lists the names: z-march

@@ -204,6 +204,12 @@ class Context:
                    out.ctypes.data_as(C.POINTER(C.c_float)), cnt.value, C.byref(cnt))
         return out
 
+    def copy_probe(self, n=1 << 27, reps=10):
+        """HBM calibration: (best, median) GB/s of a flat fp64 copy of n doubles."""
+        best, med = C.c_double(), C.c_double()
+        L.call("pb_ctx_copy_probe", self.h, int(n), int(reps), C.byref(best), C.byref(med))
+        return best.value, med.value
+
     def reset_timing(self):
         L.call("pb_ctx_reset_timing", self.h)
 

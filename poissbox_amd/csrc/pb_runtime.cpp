@@ -838,6 +838,18 @@ int pb_ctx_reset_timing(pb_ctx* ctx) {
   return PB_OK;
 }
 
+int pb_ctx_copy_probe(pb_ctx* ctx, int64_t n, int reps, double* best_gbps, double* median_gbps) {
+  PB_CHECK_ARG(ctx && n >= 2 && reps >= 1 && best_gbps && median_gbps, "bad copy probe args");
+  PB_HIP(hipSetDevice(ctx->device));
+  std::vector<float> ms;
+  PB_TRY(copy_probe(ctx, n, reps, ms));
+  std::sort(ms.begin(), ms.end());
+  const double bytes = 16.0 * (double)(n / 2 * 2);
+  *best_gbps = bytes / (ms.front() * 1e-3) / 1e9;
+  *median_gbps = bytes / (ms[ms.size() / 2] * 1e-3) / 1e9;
+  return PB_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Grid
 // ---------------------------------------------------------------------------------------------

@@ -3,6 +3,9 @@
 // and the synthetic-input generator. Grid-stride, 16-byte accesses, fixed-order
 // block reductions so every sum is deterministic run to run.
 #include "pb_internal.hpp"
+#include "pb_device.hpp"
+
+#include <algorithm>
 
 namespace pb {
 
@@ -123,6 +126,61 @@ int vec_reduce(pb_ctx* ctx, int kind, const double* x, const double* y, int64_t 
   PB_SYNC(ctx, "vector reduction");
   *out = ctx->h_scalars[0];
   return PB_OK;
+}
+
+// HBM calibration (pb_ctx_copy_probe): flat fp64 copy, 16-B loads and non-temporal 16-B stores,
+// grid-stride over 4 .. 32 workgroups per CU (the fastest grid counts) -- the access mix of the standalone matvec without its
+// stencil, so bench.py can put the matvec's rate beside what this process's device streams
+__global__ __launch_bounds__(256) void copy_probe_kernel(const dv2* __restrict__ x,
+                                                         dv2* __restrict__ y, int64_t n2) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256)
+    __builtin_nontemporal_store(x[i], y + i);
+}
+
+int copy_probe(pb_ctx* ctx, int64_t n, int reps, std::vector<float>& ms) {
+  const int64_t n2 = n / 2;
+  dv2 *x = nullptr, *y = nullptr;
+  if (hipMalloc(&x, n2 * sizeof(dv2)) != hipSuccess)
+    return set_error(PB_ERR_ALLOC, "copy probe: out of device memory");
+  if (hipMalloc(&y, n2 * sizeof(dv2)) != hipSuccess) {
+    (void)hipFree(x);
+    return set_error(PB_ERR_ALLOC, "copy probe: out of device memory");
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = PB_OK;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
+      hipMemsetAsync(x, 0, n2 * sizeof(dv2), ctx->stream) != hipSuccess) {
+    rc = set_error(PB_ERR_HIP, "copy probe: setup failed");
+  }
+  // grids of 4 .. 32 workgroups per CU; the samples of the fastest (by median) are returned
+  float best_med = 1e30f;
+  for (int per_cu = 4; rc == PB_OK && per_cu <= 32; per_cu *= 2) {
+    const int nb = ctx->num_cus * per_cu;
+    std::vector<float> cur;
+    for (int i = -2; rc == PB_OK && i < reps; ++i) {  // two untimed warm-up launches
+      float t = 0.0f;
+      if (hipEventRecord(e0, ctx->stream) != hipSuccess) rc = set_error(PB_ERR_HIP, "copy probe");
+      hipLaunchKernelGGL(copy_probe_kernel, dim3(nb), dim3(256), 0, ctx->stream, x, y, n2);
+      if (rc == PB_OK && (hipEventRecord(e1, ctx->stream) != hipSuccess ||
+                          hipEventSynchronize(e1) != hipSuccess ||
+                          hipEventElapsedTime(&t, e0, e1) != hipSuccess))
+        rc = set_error(PB_ERR_HIP, "copy probe: launch failed");
+      if (rc == PB_OK && i >= 0) cur.push_back(t);
+    }
+    if (rc != PB_OK) break;
+    std::vector<float> srt = cur;
+    std::sort(srt.begin(), srt.end());
+    if (srt[srt.size() / 2] < best_med) {
+      best_med = srt[srt.size() / 2];
+      ms = cur;
+    }
+  }
+  (void)hipStreamSynchronize(ctx->stream);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipFree(x);
+  (void)hipFree(y);
+  return rc;
 }
 
 // Test hook for the bounded waits (tuning "comm_stall_test_ms"): one wave polls a host-mapped

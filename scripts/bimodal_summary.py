@@ -1,5 +1,5 @@
-"""Summarise scripts/gpu_bimodal.sh: per profiled process, the x-update pass's (PassB<3, true>)
-and the even pass B's (PassB<0, true>) mean duration and mean L2 counters per launch.
+"""Summarise scripts/gpu_bimodal.sh: per profiled process, the x-update pass's (PassB<3, true, true>)
+and the even pass B's (PassB<0, true, true>) mean duration and mean L2 counters per launch.
 usage: python scripts/bimodal_summary.py gpurun_out/bimodal"""
 import csv
 import glob
@@ -9,7 +9,7 @@ import re
 import sys
 from collections import defaultdict
 
-PAT = {"x4": r"PassB<3, true>", "even": r"PassB<0, true>", "pass_a": r"PassAT<false>"}
+PAT = {"x4": r"PassB<3, true, true>", "even": r"PassB<0, true, true>", "pass_a": r"PassAT<false>"}
 
 
 def main(d):

@@ -21,16 +21,20 @@ ROLES = {
     "": {
         "matvec_star7": r"star7_kernel<.*PlainLoad, pb::StoreY>",
         "cg_pass_a": r"star7_kernel<.*CombineLoad, pb::PassAT<true>",
-        "cg_pass_b_even": r"star7_kernel<.*PassB<0, false>",
-        "cg_pass_b_odd": r"star7_kernel<.*PassB<1, false>",
-        "cg_pass_b_x4": r"star7_kernel<.*PassB<3, false>",
+        "cg_pass_b_even": r"star7_kernel<.*PassB<0, false, true>",
+        "cg_pass_b_odd": r"star7_kernel<.*PassB<1, false, true>",
+        "cg_pass_b_x4": r"star7_kernel<.*PassB<3, false, true>",
     },
     "/pstore_b": {
         "matvec_star7": r"star7_kernel<.*PlainLoad, pb::StoreY>",
         "cg_pass_a": r"star7_kernel<.*CombineLoad, pb::PassAT<false>",
-        "cg_pass_b_even": r"star7_kernel<.*PassB<0, true>",
-        "cg_pass_b_odd": r"star7_kernel<.*PassB<1, true>",
-        "cg_pass_b_x4": r"star7_kernel<.*PassB<3, true>",
+        "cg_pass_b_even": r"star7_kernel<.*PassB<0, true, true>",
+        "cg_pass_b_odd": r"star7_kernel<.*PassB<1, true, true>",
+        "cg_pass_b_x4": r"star7_kernel<.*PassB<3, true, true>",
+        # single-reduction iteration (bench.py's variant line)
+        "cg_sr_p": r"star7_kernel<.*PassB<0, true, false>",
+        "cg_sr_p_x4": r"star7_kernel<.*PassB<3, true, false>",
+        "cg_sr_s": r"star7_kernel<.*ZLoad, pb::SrSumsT",
     },
 }
 
