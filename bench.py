@@ -26,18 +26,11 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X spec (MI355X_MICROARCH.md "Chip-level parameters")
 PASS_B_X_NAME = {0: "cg_pass_b", 2: "cg_pass_b_odd", 4: "cg_pass_b_x4"}
-# Algorithmic bytes per DoF of each CG pass, by where p is stored (tuning parameter cg_pstore_b,
-# library default 1, pb_solver.cpp):
-#  pstore 0: pass A reads r, p_old, writes p (24); pass B reads p (stencil), r, writes r (24);
-#            the x update every D-th iteration (cg_defer_x = D, default 4) adds x read/write
-#            and p_{i-1} .. p_{i-D+1}
-#  pstore 1: pass A reads r, p_old (16, p.Ap only); pass B re-forms p from r, p_old, writes p and
-#            r into the other residual buffer (32); the x update adds x read/write and
-#            p_{i-2} .. p_{i-D+1} (p_{i-1} = p_old is already in the z-queue)
-PASS_BYTES = {
-    0: {"a": 24, "b_even": 24, "b_x": {0: 40, 2: 48, 4: 64}},
-    1: {"a": 16, "b_even": 32, "b_x": {0: 48, 2: 48, 4: 64}},
-}
+# Algorithmic bytes per DoF of each CG pass (Jacobi / none on the fused operator, pb_solver.cpp):
+# pass A reads r, p_old (16, p.Ap only); pass B re-forms p from r, p_old, writes p and r into the
+# other residual buffer (32); the x update every D-th iteration (cg_defer_x = D, default 4) adds x
+# read / write and p_{i-2} .. p_{i-D+1} (p_{i-1} = p_old is already in the z-queue)
+PASS_BYTES = {1: {"a": 16, "b_even": 32, "b_x": {0: 48, 2: 48, 4: 64}}}
 MATVEC_BYTES = 16            # y = A x: read x, write y
 # single-reduction CG (-ksp_cg_single_reduction, pb_solver.cpp enqueue_sr_iteration): pass P reads
 # r, p_old and writes p, r' (32; + x read / write and p_{i-2}, p_{i-3} every 4th iteration: 64);
@@ -61,11 +54,6 @@ def memory_clock():
         except Exception:
             pass
     return res or None
-
-
-def pstore_mode(setting=None):
-    """The library's p-store placement from the cg_pstore_b tuning setting (None: default 1)."""
-    return 0 if setting == 0 else 1
 
 
 def cg_iter_bytes(defer, pstore=1):
@@ -779,7 +767,7 @@ def main():
     # around every launch add ~2 % of gaps to the measured step; around every pass A ~0.7 %).
     # The roofline kernel is the one with the largest share of the step: pass A when it stores p
     # (cg_pstore_b = 0), otherwise pass B without the x update (3 of 4 iterations at D = 4)
-    pstore = pstore_mode(pb.tune_get("cg_pstore_b"))
+    pstore = 1  # pass B stores p
     roof = "cg_pass_b_even" if (pstore and defer == 4) else "cg_pass_a"
     ctx.set_timing(True, only=roof, every=4)
     ctx.reset_timing()

@@ -493,8 +493,8 @@ int pb_pcr_alpha_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_st
   PB_CHECK_ARG(ctx && d, "bad pcr args");
   PB_CHECK_ARG(n >= 3 && n <= 4096 && nbatch >= 1, "pcr: 3 <= n <= 4096");
   ScopedTimer tm(ctx, "pcr");
-  const int lines_ok = tune("pcr_lines", 1);
-  if (lines_ok) {  // register-resident factorised solve with cross-lane scans (n = 64*C)
+  // register line solves where the extent allows; pcr_lines = 0 keeps the PCR kernel (tests)
+  if (tune("pcr_lines", 1)) {  // register-resident factorised solve with cross-lane scans (n = 64*C)
     const int rc = lines_solve_batched(ctx, n, nbatch, line_stride, elem_stride, alpha, d);
     if (rc != PB_ERR_UNSUPPORTED) return rc;
   }

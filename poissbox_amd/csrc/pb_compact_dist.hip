@@ -70,7 +70,7 @@ static void launch_slab_transpose(pb_grid* g, const YSlabPlan& p, double* zs, in
   pb_ctx* ctx = g->ctx;
   const int64_t ny = g->n[1];
   const int P = ctx->nranks;
-  if (g->n[0] % 2 == 0 && tune("slab_rows", 1)) {
+  if (g->n[0] % 2 == 0) {
     const int64_t rows = g->nzl * ny;
     const int hp = (int)(g->n[0] / 2), rpb = hp < 256 ? 256 / hp : 1;
     const int nb = (int)std::min<int64_t>((rows + rpb - 1) / rpb, (int64_t)ctx->num_cus * 16);
@@ -184,7 +184,7 @@ int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double
   const int64_t dy[3] = {g->n[0], p.ny_me, g->n[2]};
   PB_TRY(compact_pass_z(g->ctx, dy, h, fy, uy, vy));
   if (blocked) *blocked = false;
-  if (plan_out && blocked && yslab_blocked(p) && tune("compact_fuse_transpose", 1)) {
+  if (plan_out && blocked && yslab_blocked(p)) {
     // received straight into u, v (nlocal doubles each) in the all-to-all layout
     PB_TRY(alltoallv_device(g->ctx, uy, p.yc.data(), u, p.zc.data()));
     PB_TRY(alltoallv_device(g->ctx, vy, p.yc.data(), v, p.zc.data()));

@@ -49,8 +49,8 @@ struct LinePass {
   int ninner, ntiles_inner, nouter, TL, P;
   int ablate;  // tuning only (PB_LINES_ABLATE=1): copy lines through, no solves (the build flag
                // -DPB_LINES_ABLATE_TRAFFIC=1 drops the tiled passes' global loads / stores instead)
-  int remap;   // XCD-aware tile order (PB_LINES_REMAP, default off: Z pass 0.74-0.78 vs 0.715-0.72 ms
-               // at 512^3, profiles/r02/ab_remap_compact.jsonl)
+  int remap;   // XCD-aware tile order: off (Z pass 0.74-0.78 vs 0.715-0.72 ms with it at 512^3,
+               // profiles/r02/ab_remap_compact.jsonl)
   LineOp J, L;
   const int* skip;  // pb_ctx::op_skip (exit at entry once set)
   // CG fusions (CgFuse): Z pass forming p from in0 = z and in1 = p_old (CGP kernels), X pass
@@ -723,7 +723,6 @@ bool compact_cg_fusable(const pb_grid* g) {
   return !grid_split(g) && !g->ctx->split && tune("compact_lines", 1) &&
          compact_lines_supported(g->n[0]) && compact_lines_supported(g->n[1]) &&
          compact_lines_supported(g->n[2]) && g->n[2] <= 512 && g->n[0] % 2 == 0 &&
-         !tune("lines_cfg", 0) && tune("lines_xdirect", 1) &&
          tune("cg_fuse", 1);
 }
 
@@ -768,38 +767,9 @@ static int launch_lines_k(pb_ctx* ctx, LinePass& p, int64_t nouter) {
 // Launch shapes (measured at 512^3, profiles/r01/tune_compact*.jsonl): strided passes use 16-line
 // tiles (128-B row segments, two blocks per CU), the contiguous X pass 8-line tiles; the batched
 // interleaved solve (PASS 3: little compute per tile to hide the next tile's loads under) 32-line
-// tiles with two tiles' inputs in flight. C > 8 keeps 8-line tiles for LDS. PB_LINES_CFG = 1..10
-// selects an alternative shape (tuning, C = 4 and 8).
+// tiles with two tiles' inputs in flight. C > 8 keeps 8-line tiles for LDS.
 template <int C, int LAYOUT, int PASS>
 static int launch_lines_c(pb_ctx* ctx, LinePass& p, int64_t nouter) {
-  const int cfg = tune("lines_cfg", 0);
-  if constexpr ((C == 4 || C == 8) && PASS != 4) {  // (A/B configs: not for the blocked Y pass)
-    switch (cfg) {
-      case 1: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 1>>(ctx, p, nouter);
-      case 2: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 8, 1>>(ctx, p, nouter);
-      case 3: return launch_lines_k<C, LAYOUT, PASS, LineCfg<8, 8, 1>>(ctx, p, nouter);
-      case 4: return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 0>>(ctx, p, nouter);
-      case 5: return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 1>>(ctx, p, nouter);
-      case 6: return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 0>>(ctx, p, nouter);
-      case 7:
-        if constexpr (PASS == 0 || PASS == 3)
-          return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 16, 2>>(ctx, p, nouter);
-        break;
-      case 8:
-        if constexpr (PASS == 0 || PASS == 3)
-          return launch_lines_k<C, LAYOUT, PASS, LineCfg<8, 8, 2>>(ctx, p, nouter);
-        break;
-      case 9:
-        if constexpr (PASS == 0 || PASS == 3)
-          return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 2>>(ctx, p, nouter);
-        break;
-      case 10:
-        if constexpr (PASS == 0 || PASS == 3)
-          return launch_lines_k<C, LAYOUT, PASS, LineCfg<16, 8, 2>>(ctx, p, nouter);
-        break;
-      default: break;
-    }
-  }
   if constexpr (LAYOUT == 0 && C <= 8 && PASS == 3)  // batched solve: 0.62 -> 0.48 ms at 512
     return launch_lines_k<C, LAYOUT, PASS, LineCfg<32, 16, 2>>(ctx, p, nouter);
   else if constexpr (LAYOUT == 0 && C <= 8)
@@ -833,7 +803,7 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
   ScopedTimer tm(ctx, names[axis]);
   LinePass p{};
   p.skip = ctx->op_skip;
-  p.remap = tune("lines_remap", 0);
+  p.remap = 0;
   const int ablate = PB_ABLATE_LINES;
   p.ablate = ablate;
   p.in0 = in0;
@@ -849,7 +819,7 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
     p.ninner = (int)nx;
     CgFuse* cf = ctx->cg_fuse;
     if (cf && cf->z && C <= 8 && nx % 2 == 0 && ((uintptr_t)cf->z & 15) == 0 &&
-        ((uintptr_t)out0 & 15) == 0 && !tune("lines_cfg", 0)) {
+        ((uintptr_t)out0 & 15) == 0) {
       // CG's p formed by the Z pass from z and p_old (CgFuse); in0 is not read
       p.in0 = cf->z;
       p.in1 = cf->p_old;
@@ -891,20 +861,17 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
   p.lo = nx * ny;
   p.es = 1;
   p.ninner = (int)ny;
-  const int xdirect = tune("lines_xdirect", 1);
-  if (xdirect) {
-    switch (C) {
-      case 1: return launch_x_direct<1>(ctx, p, ny * nz);
-      case 2: return launch_x_direct<2>(ctx, p, ny * nz);
-      case 3: return launch_x_direct<3>(ctx, p, ny * nz);
-      case 4: return launch_x_direct<4>(ctx, p, ny * nz);
-      case 6: return launch_x_direct<6>(ctx, p, ny * nz);
-      case 8: return launch_x_direct<8>(ctx, p, ny * nz);
-      case 12: return launch_x_direct<12>(ctx, p, ny * nz);
-      case 16: return launch_x_direct<16>(ctx, p, ny * nz);
-    }
+  switch (C) {
+    case 1: return launch_x_direct<1>(ctx, p, ny * nz);
+    case 2: return launch_x_direct<2>(ctx, p, ny * nz);
+    case 3: return launch_x_direct<3>(ctx, p, ny * nz);
+    case 4: return launch_x_direct<4>(ctx, p, ny * nz);
+    case 6: return launch_x_direct<6>(ctx, p, ny * nz);
+    case 8: return launch_x_direct<8>(ctx, p, ny * nz);
+    case 12: return launch_x_direct<12>(ctx, p, ny * nz);
+    case 16: return launch_x_direct<16>(ctx, p, ny * nz);
   }
-  return launch_lines<1, 2>(ctx, p, n, nz);
+  return set_error(PB_ERR_UNSUPPORTED, "compact lines: X extent %lld", (long long)nx);
 }
 
 // Batched periodic (alpha, 1, alpha) solve, in place, n = 64*C points per line: contiguous
@@ -917,7 +884,7 @@ int lines_solve_batched(pb_ctx* ctx, int64_t n, int64_t nbatch, int64_t line_str
   const int C = (int)(n / 64);
   LinePass p{};
   p.skip = ctx->op_skip;
-  p.remap = tune("lines_remap", 0);
+  p.remap = 0;
   p.in0 = d;
   p.out0 = d;
   p.J = make_solve_op(alpha, C);

@@ -61,19 +61,15 @@ struct DhtPass {
   const double* tab;  // [Lx | Jx | Ly | Jy | Lz | Jz] (SCALE only)
   int nx, ny, j0;     // global x / y sizes, global y of the box's row 0 (SCALE only)
   double scale, thr;  // 1 / (nx ny nz) and the null-mode threshold (SCALE only)
-  int remap;          // XCD-aware tile order (PB_FFT_REMAP, default on): consecutive tiles share an
-                      // XCD; Z pass 1.35-1.36 vs 1.375-1.378 ms at 512^3 (ab_remap_fft.jsonl)
-  int order;          // strided passes: 0 = consecutive tiles are x-adjacent (same outer row),
-                      // 1 = consecutive tiles walk the outer rows (PB_FFT_ZORDER / _YORDER)
+  int remap;          // XCD-aware tile order (on): consecutive tiles share an XCD; Z pass
+                      // 1.35-1.36 vs 1.375-1.378 ms without at 512^3 (ab_remap_fft.jsonl)
   // CG's residual sums taken by the last pass (X inverse) as it writes z: t = z - mu, over the
   // tile, against r = sr -> parts[block * 4 + (t, t^2, t r, r)] (cg_pc_sums_kernel's sums)
   const double* sr;
   double* parts;
   const CgState* st;
   int nparts_out;     // (host) partial blocks written
-  int stagger, ncu;   // PB_FFT_STAGGER=s: the second resident round of blocks (blockIdx in
-                      // [ncu, 2 ncu)) sleeps s x 8128 cycles first, so co-resident blocks run out of
-                      // phase (one loads while the other transforms) -- A/B knob
+  int ncu;
   // CG's x / r update on the first X pass (register-edge kernel): the line input is
   // r = ru_in + (-alpha) ru_w, also stored to ru_out; ru_x = ru_x + alpha ru_p (ru_first: alpha p)
   const double* ru_in;
@@ -465,17 +461,15 @@ constexpr int tile_lines() { return N == 1024 ? 16 : (N > 512 ? 8 : 16); }
 // LAYOUT 0: the tile's lines are adjacent (li = 1), elements strided (rows of TL doubles);
 // LAYOUT 1: lines contiguous (es = 1), each wave loads / stores its own two lines (no block
 // barrier around the transforms). MODE 0: one DHT; MODE 1: DHT, 1/(N lambda), DHT.
-// One tile per block, except with PF (the LDS-tile X pass on <= 512 points, or PFS): persistent
+// One tile per block, except with PF (the LDS-tile X pass on <= 512 points): persistent
 // blocks walk the tiles and fetch the next tile's input into registers while the current one is
 // transformed and stored (+32 VGPRs at n = 512; occupancy stays LDS-bound at two blocks per CU).
-template <int N, int TL_, int LAYOUT, int MODE, bool SUMS, bool PFS>
+template <int N, int TL_, int LAYOUT, int MODE, bool SUMS>
 __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(DhtPass p,
                                                                              const int* skip) {
   using T = DhtTile<N, TL_>;
   constexpr int TL = T::TL, NT = T::NT, LP = T::LP;
   if (skip && *skip) return;  // CG's device convergence flag (uniform)
-  if (p.stagger && (int)blockIdx.x >= p.ncu && (int)blockIdx.x < 2 * p.ncu)
-    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l0 = 2 * wave;
@@ -492,13 +486,8 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
   // tile t: lines [inner0, inner0 + nl) of row `outer`
   const int ntiles = p.ntiles_inner * p.nouter;
   auto tile_of = [&](int t, int64_t& outer, int& inner0, int& nl, int64_t& base) {
-    if (p.order) {
-      outer = t % p.nouter;
-      inner0 = (t / p.nouter) * TL;
-    } else {
-      outer = t / p.ntiles_inner;
-      inner0 = (t % p.ntiles_inner) * TL;
-    }
+    outer = t / p.ntiles_inner;  // consecutive tiles are x-adjacent (same outer row)
+    inner0 = (t % p.ntiles_inner) * TL;
     nl = min(TL, p.ninner - inner0);  // even: every extent is
     base = outer * p.lo + (int64_t)inner0 * p.li;
   };
@@ -542,7 +531,7 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
   // PF (persistent blocks, next tile prefetched into registers): the contiguous X pass at <= 512
   // points (512^3: 0.448 -> 0.398 ms). The strided passes run one tile per block and rely on the
   // second resident block for overlap (prefetching there measured slower: Z 0.707 -> 0.808 ms)
-  constexpr bool PF = (LAYOUT == 1 || PFS) && N <= 512;
+  constexpr bool PF = LAYOUT == 1 && N <= 512;
   dv2 pre[PF ? NR : 1];
   // Every tile load is unconditional, from a valid address (pairs past the tile re-read the
   // tile's first pair; put ignores them): a load under a runtime `if` made the compiler wait for
@@ -877,15 +866,15 @@ int launch_dht_reg_x(pb_ctx* ctx, DhtPass& p, const int* skip) {
   return PB_OK;
 }
 
-// TL lines per tile, PFS: persistent blocks + register prefetch on a strided pass
-template <int N, int TL, int LAYOUT, int MODE, bool PFS>
+// TL lines per tile
+template <int N, int TL, int LAYOUT, int MODE>
 int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
   using T = DhtTile<N, TL>;
   p.ntiles_inner = (p.ninner + T::TL - 1) / T::TL;
   const int64_t ntiles = (int64_t)p.ntiles_inner * p.nouter;
   constexpr bool SUMS = LAYOUT == 1 && MODE == 0;
-  auto kern = dht_lines_kernel<N, TL, LAYOUT, MODE, false, PFS>;
-  auto kern_s = dht_lines_kernel<N, TL, LAYOUT, MODE, SUMS, PFS>;
+  auto kern = dht_lines_kernel<N, TL, LAYOUT, MODE, false>;
+  auto kern_s = dht_lines_kernel<N, TL, LAYOUT, MODE, SUMS>;
   static int occ = 0;
   if (!occ) {
     PB_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -895,11 +884,9 @@ int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
     PB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern_s, T::NT, T::LDS));
     if (occ < 1) occ = 1;
   }
-  // persistent passes: one resident round of blocks (PB_FFT_BLOCKS_PER_CU overrides, tuning);
-  // the others one tile per block
-  const int bpc = tune("fft_blocks_per_cu", 0);
-  int64_t nblocks = (int64_t)(bpc > 0 ? bpc : occ) * ctx->num_cus;
-  const bool persist = N <= 512 && (LAYOUT == 1 || PFS);
+  // persistent passes: one resident round of blocks; the others one tile per block
+  int64_t nblocks = (int64_t)occ * ctx->num_cus;
+  const bool persist = N <= 512 && LAYOUT == 1;
   if (!persist || nblocks > ntiles) nblocks = ntiles;
   if (p.parts) {
     if (!SUMS) return set_error(PB_ERR_STATE, "fft pc: residual sums on the X pass only");
@@ -916,44 +903,16 @@ int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
 
 // Launch shapes (512^3, profiles/r03/fft_ab*.jsonl, lines_ab.jsonl): the strided passes stage
 // 16-line tiles (128-B row pieces), one tile per block -- with unconditional tile loads that
-// beats persistent blocks with register prefetch (Y 0.389 vs 0.452 ms, Z 0.646 vs 0.651;
-// PB_FFT_PF_STRIDED=1 selects those); PB_FFT_TL_Z = 32 (512-point lines): 32-line Z tiles, 256-B
-// pieces, one block per CU (measured no faster).
-static bool reg_x_on() {
-  const int reg = tune("fft_reg", 1);
-  return reg != 0;
-}
-
+// beats persistent blocks with register prefetch (Y 0.389 vs 0.452 ms, Z 0.646 vs 0.651);
+// 32-line Z tiles (256-B pieces, one block per CU) measured no faster. The contiguous X passes run
+// the register-edge kernel (launch_dht_reg_x) where it has a plan.
 template <int N, int LAYOUT, int MODE>
 int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
   if (p.ninner % 2)
     return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines (even counts only)", p.ninner);
-  if constexpr (RegPlan<N>::OK && LAYOUT == 1) {
-    // PB_FFT_REG=0: the X passes on the LDS-tile kernel
-    if (reg_x_on()) return launch_dht_reg_x<N>(ctx, p, skip);
-  }
+  if constexpr (RegPlan<N>::OK && LAYOUT == 1) return launch_dht_reg_x<N>(ctx, p, skip);
   if (p.ru_st) return set_error(PB_ERR_STATE, "fft pc: r update on the register-edge X pass only");
-  constexpr int TL = tile_lines<N>();
-  if constexpr (LAYOUT == 1) {
-    return launch_dht_k<N, TL, 1, MODE, false>(ctx, p, skip);
-  } else {
-    const int pfs = tune("fft_pf_strided", 0);
-    if constexpr (N == 512 && MODE == 1) {
-      const int tlz = tune("fft_tl_z", 16);
-      if (tlz == 32)
-        return pfs ? launch_dht_k<N, 32, 0, 1, true>(ctx, p, skip)
-                   : launch_dht_k<N, 32, 0, 1, false>(ctx, p, skip);
-    }
-    if constexpr (N <= 512)
-      if (pfs) return launch_dht_k<N, TL, 0, MODE, true>(ctx, p, skip);
-    if constexpr (N > 512) {
-      // PB_FFT_TL_LONG=8 / 16: the tile width on 768 / 1024-point lines (A/B)
-      const int tll = tune("fft_tl_long", 0);
-      if (tll == 16 && TL != 16) return launch_dht_k<N, 16, 0, MODE, false>(ctx, p, skip);
-      if (tll == 8 && TL != 8) return launch_dht_k<N, 8, 0, MODE, false>(ctx, p, skip);
-    }
-    return launch_dht_k<N, TL, 0, MODE, false>(ctx, p, skip);
-  }
+  return launch_dht_k<N, tile_lines<N>(), LAYOUT, MODE>(ctx, p, skip);
 }
 
 // the line lengths with a compiled transform: 2^a (32..1024), 3 * 2^a (48..768), 5 * 2^a (40..640)
@@ -1126,9 +1085,8 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   static const char* names[3] = {"pc_fft_x", "pc_fft_y", "pc_fft_z"};
   ScopedTimer tm(ctx, names[axis]);
   DhtPass p{};
-  p.remap = tune("fft_remap", 1);
+  p.remap = 1;
   p.ablate = PB_ABLATE_FFT;
-  p.stagger = tune("fft_stagger", 0);
   p.ncu = ctx->num_cus;
   p.in = in;
   p.out = out;
@@ -1166,7 +1124,6 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
     p.es = nx;
     p.ninner = (int)nx;
     p.nouter = (int)nz;
-    p.order = tune("fft_yorder", 0);
     if (blk) {  // row (kl, j) of the z-slab lives at block j / nyl, row kl * nyl + j % nyl
       const int64_t nyl = blk->nyl[0];
       int sh = 0;
@@ -1190,7 +1147,6 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
   p.es = pl_in ? pl_in : nx * ny;  // in place: pl_out == pl_in
   p.ninner = (int)nx;
   p.nouter = (int)ny;
-  p.order = tune("fft_zorder", 0);
   p.tab = f->tab;
   p.nx = (int)f->g->n[0];
   p.ny = (int)f->g->n[1];
@@ -1201,7 +1157,7 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
 }
 
 bool fftpc_fuses_r_update(const FftPc* f) {
-  return reg_x_on() && (f->g->n[0] == 512 || f->g->n[0] == 1024) && f->g->n[1] % 2 == 0;
+  return (f->g->n[0] == 512 || f->g->n[0] == 1024) && f->g->n[1] % 2 == 0;
 }
 
 int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgState* sums_st,
@@ -1230,7 +1186,7 @@ int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgS
     double* fy = f->ybuf;
     PB_TRY(yslab_begin(g, fy + yslab_len(g), &yp));
     const int64_t by[3] = {g->n[0], yp.ny_me, g->n[2]};
-    if (yslab_blocked(yp) && tune("fft_fuse_transpose", 1)) {
+    if (yslab_blocked(yp)) {
       // the Y passes write / read the all-to-all buffer in its blocked layout: no pack / unpack
       // pass (two field copies per apply)
       PB_TRY(dht_axis(ctx, f, b, 1, z, yp.stage, skip, 0, nullptr, nullptr, nullptr, nullptr, 0,
@@ -1248,9 +1204,8 @@ int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgS
       PB_TRY(dht_axis(ctx, f, b, 1, z, z, skip));
     }
   }
-  // with sums_st: the residual sums of CG (PB_FFT_SUMS, default on) are taken by the last pass
-  const int fused = tune("fft_sums", 1);
-  if (sums_st && nparts && fused) return dht_axis(ctx, f, b, 0, z, z, skip, 0, r, sums_st, nparts);
+  // with sums_st: the residual sums of CG are taken by the last pass
+  if (sums_st && nparts) return dht_axis(ctx, f, b, 0, z, z, skip, 0, r, sums_st, nparts);
   return dht_axis(ctx, f, b, 0, z, z, skip);
 }
 

@@ -353,6 +353,7 @@ int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_d
 struct SrFold {
   int fold_sums = 0;
   int nparts_s = 0;
+  const double* parts = nullptr;  // the partials fold_sums reduces (5 wide)
   const CgState* in = nullptr;
   CgState* out = nullptr;
   double* hist = nullptr;
@@ -363,10 +364,16 @@ int launch_cg_sr_pass_p(pb_grid* g, const Star& s, const double* r, const double
                         const SrFold& f, int mode, int64_t host_iter, int defer);
 int launch_cg_sr_pass_s(pb_grid* g, const Star& s, const double* r, const StencilPlanes& gp,
                         const CgState* st, int mode, int part_off, int* nblocks);
-// after pass S (unfolded): reduce its partials (+ allreduce on split grids) and run the
+// after pass S (unfolded): reduce its partials `parts` (+ allreduce on split grids) and run the
 // residual-sum stage on st in place (stage_delta0: the setup's delta = z0'A z0 only)
-int cg_sr_finalize(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done,
-                   int64_t host_iter, bool stage_delta0 = false);
+int cg_sr_finalize(pb_ctx* ctx, const double* parts, int nparts, CgState* st, double* hist,
+                   int* h_done, int64_t host_iter, bool stage_delta0 = false);
+// The same iteration as ONE pass (pb_cg_sr.hip; one rank, even nx, tuning cg_sr_fused): p, r',
+// and all five sums; the prologue as pass P's (sf), partials into parts_out (*nblocks blocks)
+bool cg_sr1_supported(const pb_grid* g);
+int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_old,
+                  double* p_new, double* r_out, const SrFold& sf, const double* parts_in,
+                  double* parts_out, int64_t host_iter, int* nblocks);
 
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----
 int64_t compact_fast_work_len(const pb_grid* g);

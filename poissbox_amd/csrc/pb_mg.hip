@@ -61,11 +61,10 @@ struct Mg {
   // the z-marching stencil engine (PB_MG_ENGINE_MIN_PLANE; smaller levels: per-pair kernels,
   // whose short z-chunks would not amortise the engine's prologue)
   int64_t engine_min_plane = 256 * 256;
-  // prolongation (PB_MG_PROLONG_CELL): 0 one thread per fine pair, 1 one thread per coarse cell,
-  // 2 one thread per coarse column marching in z (levels of >= restrict_z_min_cols columns)
-  int prolong_cell = 2;
-  int restrict_z = 1;    // restriction marching in z per coarse column (PB_MG_RESTRICT_Z) on
-  int64_t restrict_z_min_cols = 4096;  // coarse levels of >= this many columns
+  // restriction and prolongation: one thread per coarse column marching in z on coarse levels of
+  // >= restrict_z_min_cols columns, one thread per coarse cell (prolongation) / point
+  // (restriction) below
+  int64_t restrict_z_min_cols = 4096;
   bool tail_attr = false;  // mg_tail_kernel's dynamic-LDS limit raised
   // Decomposed grids (r04): the coarse levels [La, L) are gathered onto every rank once per
   // V-cycle (one all-to-all of level La's right-hand side) and run there as the one-launch tail
@@ -340,45 +339,7 @@ __global__ __launch_bounds__(256) void mg_restrict_z_kernel(MgGeo F, const doubl
   }
 }
 
-// x_f += P x_c for both points of the pair (trilinear, cell-centred: near parent 3/4, far 1/4)
-__device__ __forceinline__ void mg_prolong_body(MgGeo F, double* __restrict__ xf, MgGeo Cg, const double* __restrict__ xc, const double* __restrict__ lo, const double* __restrict__ hi, int64_t t0, int64_t ts) {
-  const int64_t npairs = F.nlocal >> 1;
-  for (int64_t q = t0; q < npairs;
-       q += ts) {
-    const PairPos P = pair_pos(F, q);
-    const int I = P.i0 >> 1, J = P.j >> 1, K = P.k >> 1;
-    const int fI0 = wrapm(I - 1, Cg.nx), fI1 = wrapm(I + 1, Cg.nx);
-    const int fJ = wrapm((P.j & 1) ? J + 1 : J - 1, Cg.ny);
-    const int fK = (P.k & 1) ? K + 1 : K - 1;
-    const double* pn = xc + (int64_t)K * Cg.plane;
-    const double* pf = fK < 0 ? lo : (fK >= Cg.nzl ? hi : xc + (int64_t)fK * Cg.plane);
-    const int64_t rn = (int64_t)J * Cg.nx, rf = (int64_t)fJ * Cg.nx;
-    // point i0 (even): far parent I-1; point i0+1 (odd): far parent I+1
-    const double vn0 = 0.75 * (0.75 * pn[rn + I] + 0.25 * pn[rn + fI0]) +
-                       0.25 * (0.75 * pn[rf + I] + 0.25 * pn[rf + fI0]);
-    const double vf0 = 0.75 * (0.75 * pf[rn + I] + 0.25 * pf[rn + fI0]) +
-                       0.25 * (0.75 * pf[rf + I] + 0.25 * pf[rf + fI0]);
-    const double vn1 = 0.75 * (0.75 * pn[rn + I] + 0.25 * pn[rn + fI1]) +
-                       0.25 * (0.75 * pn[rf + I] + 0.25 * pn[rf + fI1]);
-    const double vf1 = 0.75 * (0.75 * pf[rn + I] + 0.25 * pf[rn + fI1]) +
-                       0.25 * (0.75 * pf[rf + I] + 0.25 * pf[rf + fI1]);
-    dv2 o = *(const dv2*)(xf + P.idx);
-    o.x = o.x + (0.75 * vn0 + 0.25 * vf0);
-    o.y = o.y + (0.75 * vn1 + 0.25 * vf1);
-    *(dv2*)(xf + P.idx) = o;
-  }
-}
-__global__ __launch_bounds__(256) void mg_prolong_kernel(MgGeo F, double* __restrict__ xf, MgGeo Cg,
-                                                         const double* __restrict__ xc,
-                                                         const double* __restrict__ lo,
-                                                         const double* __restrict__ hi,
-                                                         const int* skip) {
-  if (skip && *skip) return;
-  mg_prolong_body(F, xf, Cg, xc, lo, hi, (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
-                  (int64_t)gridDim.x * blockDim.x);
-}
-
-// The same prolongation, one thread per coarse cell: its 2 x 2 x 2 fine children from the
+// x_f += P x_c (trilinear, cell-centred: near parent 3/4, far 1/4), one thread per coarse cell: its 2 x 2 x 2 fine children from the
 // 3 x 3 x 3 coarse neighbourhood (each child by the formula above, same operation order), so a
 // fine row pair is read and written with 16-byte accesses and each coarse value is fetched
 // ~27/8 times per fine point instead of 6.
@@ -529,7 +490,6 @@ struct TailArgs {
   TailLevel lv[kTailMax];
   int nl;           // levels in the tail; lv[nl-1] is the coarsest
   int coarse_its;
-  int prolong_cell;
   double omega;
   int lds;          // 1: every tail array lives in LDS (lv[0].b copied in, lv[0].x copied out)
 };
@@ -589,10 +549,7 @@ __global__ __launch_bounds__(512) void mg_tail_kernel(TailArgs A, const int* ski
     const TailLevel& Cl = A.lv[t + 1];
     double* xf = X(t);
     const double* xc = X(t + 1);
-    if (A.prolong_cell)
-      mg_prolong_cell_body(F.G, xf, Cl.G, xc, wrap_lo(Cl.G, xc), xc, t0, ts);
-    else
-      mg_prolong_body(F.G, xf, Cl.G, xc, wrap_lo(Cl.G, xc), xc, t0, ts);
+    mg_prolong_cell_body(F.G, xf, Cl.G, xc, wrap_lo(Cl.G, xc), xc, t0, ts);
     __syncthreads();
     smooth(t, 1, 0);
     smooth(t, 0, 0);
@@ -607,8 +564,8 @@ __global__ __launch_bounds__(512) void mg_tail_kernel(TailArgs A, const int* ski
 // chunks of coarse planes for the z-marching transfer kernels: ~16 resident waves per CU, at
 // least 4 coarse planes per chunk
 static int transfer_chunk(pb_ctx* ctx, int64_t cols, int64_t nzl, int64_t* nchunk_out) {
-  const int64_t tpc = tune("mg_transfer_tpc", 1024);  // threads per CU
-  const int64_t minz = tune("mg_transfer_minz", 4);   // coarse planes per chunk, at least
+  const int64_t tpc = 1024;  // threads per CU
+  const int64_t minz = 4;    // coarse planes per chunk, at least
   int64_t nchunk = ((int64_t)ctx->num_cus * tpc + cols - 1) / cols;
   nchunk = std::max<int64_t>(1, std::min<int64_t>(nchunk, nzl / minz));
   const int kc = (int)((nzl + nchunk - 1) / nchunk);
@@ -723,7 +680,7 @@ static int mg_agglomerate_setup(Mg* mg) {
   mg->La = 0;
   if (!ctx->split || L < 2 || !tune("mg_agglomerate", 1)) return PB_OK;
   if (!ctx->comm && !ctx->h_alltoallv) return PB_OK;
-  const int64_t tail_max = tune("mg_agglomerate_max", tune("mg_tail_max", 8192));
+  const int64_t tail_max = tune("mg_tail_max", 8192);
   int La = L;
   for (int l = L - 1; l >= 1; --l) {
     const MgLevel& v = mg->lv[l];
@@ -788,8 +745,7 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
   // levels that take the fused post-smoothing (PB_MG_POST_FUSED, one rank): an xs array each
   // (N ranks: the unrolled fused passes with deep ghost planes, r04; mg_split_fused = 0 keeps
   // the decomposed V-cycle on the per-pass kernels)
-  const bool split_ok = !ctx->split || tune("mg_split_fused", 1) != 0;
-  const bool want_post = split_ok && tune("mg_post_fused", 1) != 0;
+  const bool want_post = !ctx->split || tune("mg_split_fused", 1) != 0;
   const int64_t post_min_plane = tune("mg_engine_min_plane", mg_engine_min_plane_default(ctx));
   auto takes_post = [&](const MgLevel& lv, int l) {
     return want_post && l < L - 1 && lv.g->plane >= post_min_plane && sor_sweep2_supported(lv.g);
@@ -849,14 +805,11 @@ int mg_create(pb_grid* g, const double deltas[3], int pc_type, int levels_req, i
 // array (mg_create), the fused pre-smoothing applies, and so does the marching prolongation
 static bool post_fused(const Mg* mg, int l) {
   const MgLevel& F = mg->lv[l];
-  if (!F.xs || l + 1 >= (int)mg->lv.size() || F.g->plane < mg->engine_min_plane ||
-      !tune("mg_presmooth_fused", 1) || !tune("mg_post_fused", 1) ||
-      mg->prolong_cell != 2)
-    return false;
+  if (!F.xs || l + 1 >= (int)mg->lv.size() || F.g->plane < mg->engine_min_plane) return false;
   const MgLevel& C = mg->lv[l + 1];
   // N ranks: the unrolled kernel with deep ghosts (even slab origin, >= 2 planes per slab)
-  if (mg->ctx->split && (!tune("mg_split_fused", 1) || tune("postx", 3) < 3 || F.g->k0 % 2 ||
-                         F.g->nzl < 2 || C.g->nzl < 2))
+  if (mg->ctx->split && (!tune("mg_split_fused", 1) || F.g->k0 % 2 || F.g->nzl < 2 ||
+                         C.g->nzl < 2))
     return false;
   return C.g->n[0] * C.g->n[1] >= mg->restrict_z_min_cols;
 }
@@ -867,8 +820,6 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
   ScopedTimer tm(mg->ctx, "mg_apply");
   mg->skip = skip;
   mg->engine_min_plane = tune("mg_engine_min_plane", mg_engine_min_plane_default(mg->ctx));
-  mg->prolong_cell = tune("mg_prolong_cell", 2);
-  mg->restrict_z = tune("mg_restrict_z", 1);
   mg->restrict_z_min_cols = tune("mg_restrict_z_min_cols", 4096);
   const int L = (int)mg->lv.size();
   mg->lv[0].b = const_cast<double*>(r);
@@ -877,7 +828,7 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
   // the coarse tail in one launch (one rank): levels Lt .. L-1 of <= PB_MG_TAIL_MAX points
   int Lt = L;
   if (mg->La > 0) Lt = mg->La;  // decomposed grid: the agglomerated levels run as the tail
-  else if (!ctx->split && tune("mg_tail", 1)) {
+  else if (!ctx->split) {
     const int64_t tail_max = tune("mg_tail_max", 8192);
     Lt = L - 1;
     while (Lt > 1 && mg->lv[Lt - 1].g->nlocal <= tail_max) --Lt;
@@ -888,12 +839,11 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     MgLevel& F = mg->lv[l];
     MgLevel& Cl = mg->lv[l + 1];
     // large level: zero-start red + black half-sweeps and the residual in one pass
-    const bool fused = F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g) &&
-                       tune("mg_presmooth_fused", 1);
+    const bool fused = F.g->plane >= mg->engine_min_plane && sor_sweep2_supported(F.g);
     // one rank: the restriction too (the residual is never stored)
-    const bool fused_r = fused && F.g->nzl % 2 == 0 && tune("mg_presmooth_restrict", 1) &&
+    const bool fused_r = fused && F.g->nzl % 2 == 0 &&
                          (!ctx->split || (tune("mg_split_fused", 1) && F.g->nzl >= 3 &&
-                                          F.g->k0 % 2 == 0 && tune("prrx", 2) == 2));
+                                          F.g->k0 % 2 == 0));
     if (fused_r) {
       ScopedTimer t1(ctx, l == 0 ? "mg_fine_smooth_first" : "mg_coarse_levels");
       PB_TRY(launch_presmooth_restrict(F.g, F.s, Cl.g, F.b, post_fused(mg, l) ? F.xs : F.x, Cl.b,
@@ -926,7 +876,7 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     PB_TRY(ghosts(F, F.res, &lo, &hi));
     const MgGeo CG = Cl.geo();
     const int64_t cols = (int64_t)CG.nx * CG.ny;
-    if (mg->restrict_z && cols >= mg->restrict_z_min_cols) {
+    if (cols >= mg->restrict_z_min_cols) {
       int64_t nchunk = 1;
       const int kc = transfer_chunk(ctx, cols, CG.nzl, &nchunk);
       hipLaunchKernelGGL(mg_restrict_z_kernel, dim3(mg_blocks(ctx, cols * nchunk)), dim3(256), 0,
@@ -952,7 +902,6 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     TailArgs A{};
     A.nl = L - Lt;
     A.coarse_its = mg->coarse_its;
-    A.prolong_cell = mg->prolong_cell;
     A.omega = mg->omega;
     int64_t off = 0;
     for (int t = 0; t < A.nl; ++t) {
@@ -967,7 +916,7 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     }
     // the tail in LDS when it fits (512^3: 109 KB of the 160 KB per CU)
     const size_t lds = (size_t)off * sizeof(double);
-    A.lds = tune("mg_tail_lds", 1) && lds <= kTailLdsMax;
+    A.lds = lds <= kTailLdsMax;
     if (A.lds && !mg->tail_attr) {
       PB_HIP(hipFuncSetAttribute((const void*)mg_tail_kernel,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTailLdsMax));
@@ -1006,7 +955,7 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     const MgGeo G = F.geo(), CG = Cl.geo();
     const int64_t cols = (int64_t)CG.nx * CG.ny;
     bool fused = false;
-    if (mg->prolong_cell == 2 && cols >= mg->restrict_z_min_cols) {
+    if (cols >= mg->restrict_z_min_cols) {
       int64_t nchunk = 1;
       const int kc = transfer_chunk(ctx, cols, CG.nzl, &nchunk);
       // fused post-smoothing: prolongate into the residual scratch, then both half-sweeps in one
@@ -1015,12 +964,10 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
       hipLaunchKernelGGL(mg_prolong_z_kernel, dim3(mg_blocks(ctx, cols * nchunk)), dim3(256), 0,
                          ctx->stream, G, (const double*)F.x, fused ? F.res : F.x, CG, kc, xc, lo,
                          hi, mg->skip);
-    } else if (mg->prolong_cell)
+    } else {
       hipLaunchKernelGGL(mg_prolong_cell_kernel, dim3(mg_blocks(ctx, CG.nlocal)), dim3(256), 0,
                          ctx->stream, G, F.x, CG, xc, lo, hi, mg->skip);
-    else
-      hipLaunchKernelGGL(mg_prolong_kernel, dim3(mg_blocks(ctx, G.nlocal / 2)), dim3(256), 0,
-                         ctx->stream, G, F.x, CG, xc, lo, hi, mg->skip);
+    }
     PB_HIP(hipGetLastError());
     if (fused) {
       PB_TRY(launch_sor_sweep2(F.g, F.s, F.res, F.b, F.x, mg->omega, 1, mg->skip,

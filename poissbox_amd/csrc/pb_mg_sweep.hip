@@ -51,17 +51,13 @@ struct Sweep2Geo {
   const double* bg_hi;
 };
 
-// M = 0: SOR sweep (first colour c1, then the other) of xin -> xout.
-// M = 1: pre-smoothing from x = 0 plus residual: S1 = the zero-start red + black half-sweeps
-//        (red = w D^-1 b, black from those -- Red0Load + SorHalf's arithmetic; xin = b, c1 = 1),
-//        xout = S1 and res = b - A S1 (the residual kernel's summation order).
-template <bool SUMS, int M, bool SPLIT>
+// SOR sweep (first colour c1, then the other) of xin -> xout.
+template <bool SUMS, bool SPLIT>
 __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, double cx, double cy,
                                                                double cz, double cc, double omega,
                                                                int c1, const double* __restrict__ xin,
                                                                const double* __restrict__ b,
                                                                double* __restrict__ xout,
-                                                               double* __restrict__ res,
                                                                const CgState* st, double* parts,
                                                                const int* skip) {
   if (skip && *skip) return;
@@ -140,24 +136,6 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
         for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
       }
     };
-    // M = 1: b values of plane kk -> the x of the zero-start red half-sweep (red: w D^-1 b,
-    // black: still 0)
-    auto xform = [&](double (&v)[kRW][2], int kk) {
-      if constexpr (M == 1) {
-        const int kp = kpar(kk);
-#pragma unroll
-        for (int r = 0; r < kRW; ++r) {
-          // one red point per pair, at a wave-uniform element: one division per pair
-          const bool red1 = ((par_row[r] + kp) & 1) != 0;  // the red point is element 1
-          const double t = ((red1 ? v[r][1] : v[r][0]) - 0.0) * icc;
-          const double red = (1.0 - omega) * 0.0 + omega * t;
-          v[r][0] = red1 ? 0.0 : red;
-          v[r][1] = red1 ? red : 0.0;
-        }
-      }
-      (void)v;
-      (void)kk;
-    };
     // first half-sweep at plane kk (rows 1 .. kRW-2): x planes xm (kk-1), xc (kk), xp (kk+1)
     auto half1 = [&](const double (&xm)[kRW][2], const double (&xc)[kRW][2],
                      const double (&xp)[kRW][2], const double (&bb)[kRW][2], int kk,
@@ -197,13 +175,9 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
       ldx(xq[0], kb - 1);
       ldx(xq[1], kb);
       ldb(bb, kb - 1);
-      xform(xa, kb - 2);
-      xform(xq[0], kb - 1);
-      xform(xq[1], kb);
       half1(xa, xq[0], xq[1], bb, kb - 1, s1[0]);
       ldx(xq[2], kb + 1);
       ldb(bq[0], kb);
-      xform(xq[2], kb + 1);
       half1(xq[0], xq[1], xq[2], bq[0], kb, s1[1]);
       // shift x queue to (kb, kb+1, kb+2)
 #pragma unroll
@@ -215,7 +189,6 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
         }
       ldx(xq[2], kb + 2);
       ldb(bq[1], kb + 1);
-      xform(xq[2], kb + 2);
     }
     for (int k = kb; k < ke; ++k) {
       const bool more = k + 1 < ke;
@@ -229,29 +202,6 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
       const int64_t base = pl(k);
 #pragma unroll
       for (int r = 2; r < 2 + kTY2; ++r) {
-        if constexpr (M == 1) {  // x = S1; res = b - A S1 (z-, y-, x-, c, x+, y+, z+)
-          const double lo = dpp_from_lower(s1[1][r][1]);
-          const double hi = dpp_from_upper(s1[1][r][0]);
-          double rv[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double xl = e == 0 ? lo : s1[1][r][0];
-            const double xr = e == 1 ? hi : s1[1][r][1];
-            double a = cz * s1[0][r][e];
-            a = a + cy * s1[1][r - 1][e];
-            a = a + cx * xl;
-            a = a + cc * s1[1][r][e];
-            a = a + cx * xr;
-            a = a + cy * s1[1][r + 1][e];
-            a = a + cz * s1[2][r][e];
-            rv[e] = bq[0][r][e] - a;
-          }
-          if (out_ok && j0 + r - 2 < ny) {
-            store_row<2>(xout, rix(base + ro[r]), s1[1][r], g.nt);
-            store_row<2>(res, rix(base + ro[r]), rv, g.nt);
-          }
-          continue;
-        }
         const bool a1 = ((par_row[r] + kp) & 1) == c1;  // second-colour point is element 1
         const double lo = dpp_from_lower(s1[1][r][1]);
         const double hi = dpp_from_upper(s1[1][r][0]);
@@ -302,7 +252,6 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
           bq[0][r][e] = bq[1][r][e];
           bq[1][r][e] = bn[r][e];
         }
-      xform(xq[2], k + 3);
     }
   }
   if constexpr (SUMS) block_partials<4>(acc, parts);
@@ -313,7 +262,7 @@ __global__ __launch_bounds__(kThreads) void sor_sweep2_kernel(Sweep2Geo g, doubl
 // after the zero-start red half-sweep every pair holds ONE non-zero (its red point, w b / c), and
 // the black half-sweep reads only red values -- so the x queue keeps one double per pair (the red
 // value) instead of two, and b is loaded once per plane (the red values are formed from the raw
-// rows that also serve as the b operand). Same per-point operations as sor_sweep2_kernel M = 1
+// rows that also serve as the b operand). Same per-point operations as the zero-start sweeps
 // (Red0Load + SorHalf, then ResidEpi's order): bit-identical. 42 fewer VGPRs -> two waves per SIMD
 // instead of one.
 // ---------------------------------------------------------------------------------------------
@@ -501,453 +450,20 @@ __global__ __launch_bounds__(kThreads) void presmooth_resid_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Pre-smoothing from x = 0, residual AND restriction in one pass (one rank; the unrolled form also
-// on N ranks with three-deep ghosts of b, r04): the residual is
-// never stored -- each wave owns the two fine rows 2J, 2J+1 of one coarse row J and forms the
-// residual on the four rows 2J-1 .. 2J+2 that the restriction reads (so S1 on six rows, red values
-// on eight), then the restriction's x and y sums per fine plane and its z sum over the four planes
-// 2K-1 .. 2K+2 as the planes pass. Per fine point: read b, write x (+ 1/8 of a coarse b) --
-// 17 B/DoF instead of the pre-smoothing pass's 24 plus the restriction's 9. Arithmetic: the slim
-// pre-smoothing kernel's (red, black, residual) and mg_restrict_z_kernel's (restrict_xy, then the
-// z sum in the same order), so results are bit-identical.
-// ---------------------------------------------------------------------------------------------
-static constexpr int kTYR = 2;         // own fine rows per wave (one coarse row)
-static constexpr int kRR = kTYR + 6;   // b rows held: j0-3 .. j0+4 (red values on all of them)
-
-#ifndef PB_PRR_WPE
-#define PB_PRR_WPE 2  // waves per SIMD the register allocation aims for (A/B builds)
-#endif
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PB_PRR_WPE))) void
-presmooth_restrict_kernel(Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz,
-                          double cc, double omega, const double* __restrict__ b,
-                          double* __restrict__ xout, double* __restrict__ bc, const int* skip) {
-  if (skip && *skip) return;
-  const double icc = 1.0 / cc;  // SOR: multiply by the inverted diagonal
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int bid = xcd_block(g.remap);
-  const int seg = bid % g.nseg;
-  bid /= g.nseg;
-  const int tile = bid % g.ntile;
-  const int chunk = bid / g.ntile;
-  const int j0 = (tile * kWaves + wid) * kTYR;  // even: fine rows 2J, 2J+1
-  const int kb = chunk * g.kc;                  // even (kc even)
-  const int ke = min(kb + g.kc, g.nzl);
-  const int nx = g.nx, ny = g.ny, nz = g.nzl;
-  int ip = seg * kSegOut + 2 * (lane - kSegLead);
-  if (ip < 0) ip += nx;
-  if (ip >= nx) ip -= nx;
-  const int o = seg * kSegOut + 2 * (lane - kSegLead);
-  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
-  if (!(j0 < ny && kb < nz)) return;
-  int64_t ro[kRR];
-  int par_row[kRR];
-#pragma unroll
-  for (int r = 0; r < kRR; ++r) {
-    int j = j0 - 3 + r;
-    if (j < 0) j += ny;
-    if (j >= ny) j -= ny;
-    ro[r] = (int64_t)j * nx;
-    par_row[r] = (ip + j) & 1;
-  }
-  const unsigned boff = (unsigned)ip * 8u;
-  auto rix = [&](int64_t row) { return RowIx{row, boff}; };
-  auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
-  auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
-  auto ldraw = [&](double (&dst)[kRR][2], int kk) {
-    const int64_t base = (int64_t)wrapk(kk) * g.plane;
-#pragma unroll
-    for (int r = 0; r < kRR; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
-  };
-  // raw b rows -> the red value of each pair (presmooth_resid_kernel's redv)
-  auto redv = [&](const double (&v)[kRR][2], int kk, double (&red)[kRR]) {
-    const int kp = kpar(kk);
-#pragma unroll
-    for (int r = 0; r < kRR; ++r) {
-      const double bv = pick(((par_row[r] + kp) & 1) != 0, v[r]);  // red point is element 1
-      const double t = (bv - 0.0) * icc;
-      red[r] = (1.0 - omega) * 0.0 + omega * t;
-    }
-  };
-  // black half-sweep at plane kk, rows 1 .. kRR-2 (presmooth_resid_kernel's half1)
-  auto black = [&](const double (&rm)[kRR], const double (&rc)[kRR], const double (&rp)[kRR],
-                   const double (&bb)[kRR][2], int kk, double (&out)[kRR][2]) {
-    const int kp = kpar(kk);
-#pragma unroll
-    for (int r = 1; r < kRR - 1; ++r) {
-      const bool a1 = ((par_row[r] + kp) & 1) != 1;  // the black point is element 1
-      const double lo = dpp_from_lower(rc[r]);
-      const double hi = dpp_from_upper(rc[r]);
-      const double xl = a1 ? rc[r] : lo;
-      const double xr = a1 ? hi : rc[r];
-      double nb = cz * rm[r];
-      nb = nb + cy * rc[r - 1];
-      nb = nb + cx * xl;
-      nb = nb + cx * xr;
-      nb = nb + cy * rc[r + 1];
-      nb = nb + cz * rp[r];
-      const double t = (pick(a1, bb[r]) - nb) * icc;
-      const double v = (1.0 - omega) * 0.0 + omega * t;
-      out[r][0] = a1 ? rc[r] : v;
-      out[r][1] = a1 ? v : rc[r];
-    }
-  };
-  const int J = j0 >> 1;
-  const int I = o >> 1;
-  // queues at iteration k: red values of planes k, k+1; S1 of planes k-1 (rows 2..5) and k
-  // (rows 1..6); b of planes k (rows 2..5) and k+1 (rows 1..6); the z sums of coarse planes K
-  // (A) and K-1 (B) for the fine plane k in 2K-1 .. 2K
-  double rq0[kRR], rq1[kRR], rq2[kRR];  // red values, planes k, k+1, k+2
-  double s1m[kRR][2], s1c[kRR][2];
-  double bq0[kRR][2], bq1[kRR][2], bq2[kRR][2];  // b, planes k, k+1, k+2
-  double accA = 0.0, accB = 0.0;
-  {
-    double raw[kRR][2];
-    ldraw(raw, kb - 3);
-    redv(raw, kb - 3, rq0);
-    ldraw(bq1, kb - 2);
-    redv(bq1, kb - 2, rq1);
-    ldraw(bq2, kb - 1);
-    redv(bq2, kb - 1, rq2);
-  }
-#pragma unroll
-  for (int r = 0; r < kRR; ++r)
-#pragma unroll
-    for (int e = 0; e < 2; ++e) s1m[r][e] = s1c[r][e] = bq0[r][e] = 0.0;
-  // planes kb-3, kb-2: S1 warm-up; kb-1 and ke: residual for the restriction only
-#pragma unroll 1
-  for (int k = kb - 3; k <= ke; ++k) {
-    double raw[kRR][2], s1p[kRR][2];
-    ldraw(raw, k + 3);  // in flight during this plane's sweeps (consumed at the rotation)
-    black(rq0, rq1, rq2, bq1, k + 1, s1p);  // S1 at plane k+1
-    if (k >= kb - 1) {
-      // x = S1 on the own rows; res = b - A S1 on rows 2..5 (z-, y-, x-, c, x+, y+, z+)
-      double rv[kRR][2];
-#pragma unroll
-      for (int r = 2; r < kRR - 2; ++r) {
-        const double lo = dpp_from_lower(s1c[r][1]);
-        const double hi = dpp_from_upper(s1c[r][0]);
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const double xl = e == 0 ? lo : s1c[r][0];
-          const double xr = e == 1 ? hi : s1c[r][1];
-          double a = cz * s1m[r][e];
-          a = a + cy * s1c[r - 1][e];
-          a = a + cx * xl;
-          a = a + cc * s1c[r][e];
-          a = a + cx * xr;
-          a = a + cy * s1c[r + 1][e];
-          a = a + cz * s1p[r][e];
-          rv[r][e] = bq0[r][e] - a;
-        }
-      }
-      if (k >= kb && k < ke && out_ok) {
-        const int64_t base = (int64_t)k * g.plane;
-#pragma unroll
-        for (int r = 3; r < 3 + kTYR; ++r) store_row<2>(xout, rix(base + ro[r]), s1c[r], g.nt);
-      }
-      // restriction: x then y sums of fine rows 2J-1 .. 2J+2 (restrict_xy's order)
-      const double w[4] = {0.125, 0.375, 0.375, 0.125};
-      double sy = 0.0;
-#pragma unroll
-      for (int bb = 0; bb < 4; ++bb) {
-        const int r = 2 + bb;
-        const double lo = dpp_from_lower(rv[r][1]);
-        const double hi = dpp_from_upper(rv[r][0]);
-        double sx = w[0] * lo;
-        sx = sx + w[1] * rv[r][0];
-        sx = sx + w[2] * rv[r][1];
-        sx = sx + w[3] * hi;
-        sy = sy + w[bb] * sx;
-      }
-      if (k & 1) {  // k = 2K-1: third term of K-1, first of K
-        accB = accB + 0.375 * sy;
-        accA = 0.0;
-        accA = accA + 0.125 * sy;
-      } else {      // k = 2K: last term of K-1 (complete), second of K
-        accB = accB + 0.125 * sy;
-        if (k >= kb + 2 && out_ok)
-          bc[(int64_t)((k >> 1) - 1) * cplane + (int64_t)J * ncx + I] = accB;
-        accA = accA + 0.375 * sy;
-        accB = accA;
-      }
-    }
-    // rotate: red (k+1, k+2, k+3), S1 (k, k+1), b (k+1, k+2, k+3)
-    double rn[kRR];
-    redv(raw, k + 3, rn);
-#pragma unroll
-    for (int r = 0; r < kRR; ++r) {
-      rq0[r] = rq1[r];
-      rq1[r] = rq2[r];
-      rq2[r] = rn[r];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        s1m[r][e] = s1c[r][e];
-        s1c[r][e] = s1p[r][e];
-        bq0[r][e] = bq1[r][e];
-        bq1[r][e] = bq2[r][e];
-        bq2[r][e] = raw[r][e];
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// The same pre-smoothing + residual + restriction pass with rows shared between the waves of a
-// block (r03). presmooth_restrict_kernel's waves load eight b rows for their two own rows and form
-// red values on eight rows, black values on six and the residual on four. Here a block of NW
-// waves stacks NW x TY rows (TY / 2 coarse rows per wave) and each wave forms red, black and
-// residual values on its own rows only; the values one row out come from the neighbouring waves
-// through LDS (red values, the smoothed pairs, and the residual's x sums), one block barrier per
-// plane. Red values of plane k+3 and the smoothed pairs of plane k+1 are published one iteration
-// before their use; the residual's x sums of plane k too -- the restriction of plane k runs one
-// iteration late. Each step loses a row at the block's ends (red -> black -> residual -> y sum),
-// so a block stores its fine rows 4 .. NW TY - 5 and blocks advance by NW TY - 8 rows. Same
-// operations on the same operands as presmooth_restrict_kernel: bit-identical.
-// ---------------------------------------------------------------------------------------------
-template <int NW, int TY>
-__global__ __launch_bounds__(64 * NW) void presmooth_restrict_xch_kernel(
-    Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
-    double omega, const double* __restrict__ b, double* __restrict__ xout,
-    double* __restrict__ bc, const int* skip) {
-  static_assert(TY % 2 == 0 && TY >= 2, "whole coarse rows per wave");
-  constexpr int RB = NW * TY;  // block rows
-  constexpr int SB = RB - 8;   // stored rows per block
-  constexpr int NCR = TY / 2;  // coarse rows per wave
-  // per plane parity, per wave: red values of own rows 0 / TY-1 (plane k+3), smoothed pairs of
-  // rows 0 / TY-1 (plane k+1: e0, e1 each), residual x sums of rows 0 / TY-1 (plane k)
-  __shared__ double xch[2][8][NW][64];
-  if (skip && *skip) return;
-  const double icc = 1.0 / cc;
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int bid = xcd_block(g.remap);
-  const int seg = bid % g.nseg;
-  bid /= g.nseg;
-  const int tile = bid % g.ntile;
-  const int chunk = bid / g.ntile;
-  const int kb = chunk * g.kc;  // even (kc even)
-  const int ke = min(kb + g.kc, g.nzl);
-  const int nx = g.nx, ny = g.ny, nz = g.nzl;
-  if (kb >= nz) return;  // block-uniform
-  const int g0 = tile * SB - 4;  // fine row of block row 0 (even)
-  const int br0 = wid * TY;
-  const int j0 = g0 + br0;       // even: fine rows 2 J0 .. of coarse rows J0 ..
-  auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
-  int ip = seg * kSegOut + 2 * (lane - kSegLead);
-  if (ip < 0) ip += nx;
-  if (ip >= nx) ip -= nx;
-  const int o = seg * kSegOut + 2 * (lane - kSegLead);
-  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
-  int64_t ro[TY];
-  int par_row[TY];
-  unsigned row_ok = 0;  // own rows this wave stores (x; coarse row c when rows 2c, 2c+1 are)
-#pragma unroll
-  for (int r = 0; r < TY; ++r) {
-    const int j = wrap(j0 + r, ny);
-    ro[r] = (int64_t)j * nx;
-    par_row[r] = (ip + j) & 1;
-    const int brow = br0 + r;
-    if (brow >= 4 && brow < RB - 4 && g0 + brow < ny) row_ok |= 1u << r;
-  }
-  const unsigned boff = (unsigned)ip * 8u;
-  auto rix = [&](int64_t row) { return RowIx{row, boff}; };
-  // planes up to a few steps past the chunk (the last step's spare planes): any distance
-  auto wrapk = [&](int kk) { kk %= nz; return kk < 0 ? kk + nz : kk; };
-  auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
-  auto ldraw = [&](double (&dst)[TY][2], int kk) {
-    const int64_t base = (int64_t)wrapk(kk) * g.plane;
-#pragma unroll
-    for (int r = 0; r < TY; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
-  };
-  auto redv = [&](const double (&v)[TY][2], int kk, double (&red)[TY]) {
-    const int kp = kpar(kk);
-#pragma unroll
-    for (int r = 0; r < TY; ++r) {
-      const double bv = pick(((par_row[r] + kp) & 1) != 0, v[r]);  // red point is element 1
-      const double t = (bv - 0.0) * icc;
-      red[r] = (1.0 - omega) * 0.0 + omega * t;
-    }
-  };
-  // black half-sweep at plane kk on the own rows; rh: red values of rows -1 / TY of plane kk
-  auto black = [&](const double (&rm)[TY], const double (&rc)[TY], const double (&rp)[TY],
-                   const double (&rh)[2], const double (&bb)[TY][2], int kk,
-                   double (&out)[TY][2]) {
-    const int kp = kpar(kk);
-#pragma unroll
-    for (int r = 0; r < TY; ++r) {
-      const bool a1 = ((par_row[r] + kp) & 1) != 1;  // the black point is element 1
-      const double lo = dpp_from_lower(rc[r]);
-      const double hi = dpp_from_upper(rc[r]);
-      const double xl = a1 ? rc[r] : lo;
-      const double xr = a1 ? hi : rc[r];
-      double nb = cz * rm[r];
-      nb = nb + cy * (r == 0 ? rh[0] : rc[r == 0 ? 0 : r - 1]);
-      nb = nb + cx * xl;
-      nb = nb + cx * xr;
-      nb = nb + cy * (r == TY - 1 ? rh[1] : rc[r == TY - 1 ? r : r + 1]);
-      nb = nb + cz * rp[r];
-      const double t = (pick(a1, bb[r]) - nb) * icc;
-      const double v = (1.0 - omega) * 0.0 + omega * t;
-      out[r][0] = a1 ? rc[r] : v;
-      out[r][1] = a1 ? v : rc[r];
-    }
-  };
-  const int wm = wid > 0 ? wid - 1 : wid, wp = wid < NW - 1 ? wid + 1 : wid;
-  const int J0 = j0 >> 1;
-  const int I = o >> 1;
-  const double w[4] = {0.125, 0.375, 0.375, 0.125};
-  // queues at iteration k: red values of planes k, k+1, k+2 (and rows -1 / TY of plane k+1);
-  // smoothed pairs of planes k-1, k; b of planes k, k+1, k+2; the residual x sums of plane k-1
-  double rq0[TY], rq1[TY], rq2[TY], rh1[2];
-  double s1m[TY][2], s1c[TY][2];
-  double bq0[TY][2], bq1[TY][2], bq2[TY][2];
-  double sxp[TY];
-  double accA[NCR], accB[NCR];
-  {
-    double raw[TY][2];
-    ldraw(raw, kb - 3);
-    redv(raw, kb - 3, rq0);
-    ldraw(bq1, kb - 2);
-    redv(bq1, kb - 2, rq1);
-    ldraw(bq2, kb - 1);
-    redv(bq2, kb - 1, rq2);
-    // rows -1 / TY of plane kb-2 now; those of plane kb-1 as if iteration kb-4 had formed them
-    xch[(kb - 3) & 1][0][wid][lane] = rq1[0];
-    xch[(kb - 3) & 1][1][wid][lane] = rq1[TY - 1];
-    __syncthreads();
-    rh1[0] = xch[(kb - 3) & 1][1][wm][lane];
-    rh1[1] = xch[(kb - 3) & 1][0][wp][lane];
-    xch[(kb - 4) & 1][0][wid][lane] = rq2[0];
-    xch[(kb - 4) & 1][1][wid][lane] = rq2[TY - 1];
-  }
-#pragma unroll
-  for (int r = 0; r < TY; ++r) {
-    sxp[r] = 0.0;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) s1m[r][e] = s1c[r][e] = bq0[r][e] = 0.0;
-  }
-#pragma unroll
-  for (int c = 0; c < NCR; ++c) accA[c] = accB[c] = 0.0;
-  // planes kb-3, kb-2: black warm-up; residual on kb-1 .. ke; restriction of plane k-1
-#pragma unroll 1
-  for (int k = kb - 3; k <= ke + 1; ++k) {
-    double raw[TY][2], s1p[TY][2], rh2[2], sh[2][2], sxh[2];
-    ldraw(raw, k + 3);  // in flight during this plane's work (consumed at the rotation)
-    __syncthreads();
-    {
-      const int rp = (k - 1) & 1;
-      rh2[0] = xch[rp][1][wm][lane];  // red, plane k+2
-      rh2[1] = xch[rp][0][wp][lane];
-      sh[0][0] = xch[rp][4][wm][lane];  // smoothed pairs, plane k: row -1
-      sh[0][1] = xch[rp][5][wm][lane];
-      sh[1][0] = xch[rp][2][wp][lane];  // row TY
-      sh[1][1] = xch[rp][3][wp][lane];
-      sxh[0] = xch[rp][7][wm][lane];  // residual x sums, plane k-1
-      sxh[1] = xch[rp][6][wp][lane];
-    }
-    const int cur = k & 1;
-    black(rq0, rq1, rq2, rh1, bq1, k + 1, s1p);  // smoothed pairs of plane k+1
-    xch[cur][2][wid][lane] = s1p[0][0];
-    xch[cur][3][wid][lane] = s1p[0][1];
-    xch[cur][4][wid][lane] = s1p[TY - 1][0];
-    xch[cur][5][wid][lane] = s1p[TY - 1][1];
-    double sxc[TY];
-    if (k >= kb - 1 && k <= ke) {
-      // x = S1 on the own rows; res = b - A S1 (z-, y-, x-, c, x+, y+, z+), then its x sums
-#pragma unroll
-      for (int r = 0; r < TY; ++r) {
-        const double lo = dpp_from_lower(s1c[r][1]);
-        const double hi = dpp_from_upper(s1c[r][0]);
-        double rv[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const double xl = e == 0 ? lo : s1c[r][0];
-          const double xr = e == 1 ? hi : s1c[r][1];
-          const double ym = r == 0 ? sh[0][e] : s1c[r == 0 ? 0 : r - 1][e];
-          const double yp = r == TY - 1 ? sh[1][e] : s1c[r == TY - 1 ? r : r + 1][e];
-          double a = cz * s1m[r][e];
-          a = a + cy * ym;
-          a = a + cx * xl;
-          a = a + cc * s1c[r][e];
-          a = a + cx * xr;
-          a = a + cy * yp;
-          a = a + cz * s1p[r][e];
-          rv[e] = bq0[r][e] - a;
-        }
-        const double rlo = dpp_from_lower(rv[1]);
-        const double rhi = dpp_from_upper(rv[0]);
-        double sx = w[0] * rlo;
-        sx = sx + w[1] * rv[0];
-        sx = sx + w[2] * rv[1];
-        sx = sx + w[3] * rhi;
-        sxc[r] = sx;
-      }
-      if (k >= kb && k < ke && out_ok) {
-        const int64_t base = (int64_t)k * g.plane;
-#pragma unroll
-        for (int r = 0; r < TY; ++r)
-          if (row_ok >> r & 1u) store_row<2>(xout, rix(base + ro[r]), s1c[r], g.nt);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < TY; ++r) sxc[r] = 0.0;
-    }
-    xch[cur][6][wid][lane] = sxc[0];
-    xch[cur][7][wid][lane] = sxc[TY - 1];
-    const int kr = k - 1;  // restriction of plane k-1: y sums of fine rows 2J-1 .. 2J+2
-    if (kr >= kb - 1) {
-#pragma unroll
-      for (int c = 0; c < NCR; ++c) {
-        double sy = 0.0;
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
-          const int r = 2 * c - 1 + bb;
-          const double sxv = r < 0 ? sxh[0] : (r >= TY ? sxh[1] : sxp[r < 0 ? 0 : (r >= TY ? 0 : r)]);
-          sy = sy + w[bb] * sxv;
-        }
-        if (kr & 1) {  // kr = 2K-1: third term of K-1, first of K
-          accB[c] = accB[c] + 0.375 * sy;
-          accA[c] = 0.0;
-          accA[c] = accA[c] + 0.125 * sy;
-        } else {       // kr = 2K: last term of K-1 (complete), second of K
-          accB[c] = accB[c] + 0.125 * sy;
-          if (kr >= kb + 2 && out_ok && (row_ok >> (2 * c) & 1u))
-            bc[(int64_t)((kr >> 1) - 1) * cplane + (int64_t)wrap(J0 + c, ny >> 1) * ncx + I] =
-                accB[c];
-          accA[c] = accA[c] + 0.375 * sy;
-          accB[c] = accA[c];
-        }
-      }
-    }
-    // rotate: red (k+1, k+2, k+3), smoothed pairs (k, k+1), b (k+1, k+2, k+3), x sums (k)
-    double rn[TY];
-    redv(raw, k + 3, rn);
-    xch[cur][0][wid][lane] = rn[0];
-    xch[cur][1][wid][lane] = rn[TY - 1];
-    rh1[0] = rh2[0];
-    rh1[1] = rh2[1];
-#pragma unroll
-    for (int r = 0; r < TY; ++r) {
-      rq0[r] = rq1[r];
-      rq1[r] = rq2[r];
-      rq2[r] = rn[r];
-      sxp[r] = sxc[r];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        s1m[r][e] = s1c[r][e];
-        s1c[r][e] = s1p[r][e];
-        bq0[r][e] = bq1[r][e];
-        bq1[r][e] = bq2[r][e];
-        bq2[r][e] = raw[r][e];
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// presmooth_restrict_xch_kernel with the plane loop unrolled by four (r03). Its queues (red values,
-// smoothed pairs, b rows, x sums, halo values) become rings of four or two register slots whose
-// roles rotate with the unrolled copy, so no value is copied from one iteration to the next, and
-// each copy knows its plane's parity: with an even slab origin k0 (one rank: 0; N ranks: the MG
+// Pre-smoothing from x = 0, residual AND restriction in one pass (one rank, or N ranks with
+// three-deep ghosts of b): the residual is never stored. Per fine point: read b, write x (+ 1/8 of
+// a coarse b) -- 17 B/DoF instead of the pre-smoothing pass's 24 plus the restriction's 9.
+// Arithmetic: the slim pre-smoothing kernel's (red, black, residual) and mg_restrict_z_kernel's
+// (restrict_xy, then the z sum in the same order), so results are bit-identical.
+// Rows shared between the waves of a block (r03): a block of NW waves stacks NW x TY rows (TY / 2
+// coarse rows per wave) and each wave forms red, black and residual values on its own rows only;
+// the values one row out come from the neighbouring waves through LDS (red values, the smoothed
+// pairs, and the residual's x sums), one block barrier per plane. Each step loses a row at the
+// block's ends (red -> black -> residual -> y sum), so a block stores its fine rows 4 .. NW TY - 5
+// and blocks advance by NW TY - 8 rows. The plane loop is unrolled by four: the queues (red
+// values, smoothed pairs, b rows, x sums, halo values) are rings of four or two register slots
+// whose roles rotate with the unrolled copy, so no value is copied from one iteration to the
+// next, and each copy knows its plane's parity: with an even slab origin k0 (one rank: 0; N ranks: the MG
 // plan keeps every level's slab origins even) and even extents, pair origins and
 // row origins, the colour of every element is known at compile time, so the colour choices are
 // register choices instead of selects and each half-sweep needs one DPP shift per row, not two.
@@ -1005,7 +521,7 @@ __device__ __forceinline__ void presmooth_restrict_u4_range(
     for (int r = 0; r < TY; ++r) load_row<2>(src, rix(ro[r]), dst[r]);
   };
   // element holding the red point of own row r on a plane of parity P (pair origin i even, row
-  // origin j0 even, k0 even): presmooth_restrict_kernel's ((i + j) & 1) + kpar != 0
+  // origin j0 even, k0 even): ((i + j) & 1) + kpar != 0
   auto red_e = [](int r, int P) { return (r + P) & 1; };
 
   auto redv = [&](auto Pc, const double (&v)[TY][2], double (&red)[TY]) {
@@ -1217,7 +733,9 @@ __global__ __launch_bounds__(64 * NW) void presmooth_restrict_u4_kernel(
     Sweep2Geo g, int ncx, int64_t cplane, double cx, double cy, double cz, double cc,
     double omega, const double* __restrict__ b, double* __restrict__ xout,
     double* __restrict__ bc, const int* skip) {
-  __shared__ double xch[2][8][NW][64];  // as presmooth_restrict_xch_kernel's
+  // per plane parity, per wave: red values of own rows 0 / TY-1 (plane k+3), smoothed pairs of
+  // rows 0 / TY-1 (plane k+1: e0, e1 each), residual x sums of rows 0 / TY-1 (plane k)
+  __shared__ double xch[2][8][NW][64];
   if (skip && *skip) return;
   int bid = xcd_block(g.remap);
   if (g.wsplit > 0) {  // ranges start on even planes (W, nzl even)
@@ -1259,549 +777,12 @@ struct PostGeo {
   const double* cgh;
 };
 
-#ifndef PB_POST_WPE
-#define PB_POST_WPE 2  // waves per SIMD the register allocation aims for (A/B builds)
-#endif
-template <bool SUMS>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PB_POST_WPE))) void post_sweep_kernel(
-    Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
-    const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
-    double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
-  if (skip && *skip) return;
-  const double icc = 1.0 / cc;  // SOR: multiply by the inverted diagonal
-  constexpr int c1 = 1;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  const double mu = SUMS ? st->mu : 0.0;
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int bid = xcd_block(g.remap);
-  const int seg = bid % g.nseg;
-  bid /= g.nseg;
-  const int tile = bid % g.ntile;
-  const int chunk = bid / g.ntile;
-  const int j0 = (tile * kWaves + wid) * kTY2;
-  const int kb = chunk * g.kc;
-  const int ke = min(kb + g.kc, g.nzl);
-  const int nx = g.nx, ny = g.ny, nz = g.nzl;
-  int ip = seg * kSegOut + 2 * (lane - kSegLead);
-  if (ip < 0) ip += nx;
-  if (ip >= nx) ip -= nx;
-  const int o = seg * kSegOut + 2 * (lane - kSegLead);
-  const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
-  if (j0 < ny && kb < nz) {
-    int64_t ro[kRW];
-    int par_row[kRW];
-#pragma unroll
-    for (int r = 0; r < kRW; ++r) {
-      int j = j0 - 2 + r;
-      if (j < 0) j += ny;
-      if (j >= ny) j -= ny;
-      ro[r] = (int64_t)j * nx;
-      par_row[r] = (ip + j) & 1;
-    }
-    const unsigned boff = (unsigned)ip * 8u;
-    auto rix = [&](int64_t row) { return RowIx{row, boff}; };
-    auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
-    auto pl = [&](int kk) -> int64_t { return (int64_t)wrapk(kk) * g.plane; };
-    auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
-    // coarse rows Jb .. Jb+5 cover the 7 fine rows j0-2 .. j0+4 and their far rows
-    const int p0 = j0 & 1;
-    const int Jb = ((j0 - 2) >> 1) - 1;
-    int64_t crow[6];
-#pragma unroll
-    for (int t = 0; t < 6; ++t) {
-      int J = Jb + t;
-      if (J < 0) J += cgeo.ncy;
-      if (J >= cgeo.ncy) J -= cgeo.ncy;
-      crow[t] = (int64_t)J * cgeo.ncx;
-    }
-    const unsigned cboff = (unsigned)(ip >> 1) * 8u;  // coarse column I = ip / 2
-    // fine plane kk: raw x_s rows and the coarse rows of its near / far coarse planes
-    auto ldx = [&](double (&dst)[kRW][2], double (&cv)[2][6], int kk) {
-      const int64_t base = pl(kk);
-#pragma unroll
-      for (int r = 0; r < kRW; ++r) load_row<2>(xs, rix(base + ro[r]), dst[r]);
-      const int kw = wrapk(kk);
-      const int K = kw >> 1;
-      int fK = (kw & 1) ? K + 1 : K - 1;
-      if (fK < 0) fK += cgeo.ncz;
-      if (fK >= cgeo.ncz) fK -= cgeo.ncz;
-      const double* cn = xc + (int64_t)K * cgeo.cplane;
-      const double* cf = xc + (int64_t)fK * cgeo.cplane;
-#pragma unroll
-      for (int t = 0; t < 6; ++t) {
-        cv[0][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cn + crow[t]) + cboff);
-        cv[1][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cf + crow[t]) + cboff);
-      }
-    };
-    // x_s + P x_c (mg_prolong_z_kernel's operation order); P0 = j0 parity (wave-uniform). The
-    // x-interpolated coarse values are formed once per coarse row and plane (each serves two or
-    // three fine rows): the same operations on the same operands, so the same results
-    auto prolong_p = [&](auto P0c, double (&v)[kRW][2], const double (&cv)[2][6]) {
-      constexpr int P0 = decltype(P0c)::value;
-      // element 0: far column I-1; element 1: I+1
-      double xi[2][6][2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-          const double c = cv[q][t];
-          xi[q][t][0] = 0.75 * c + 0.25 * dpp_from_lower(c);
-          xi[q][t][1] = 0.75 * c + 0.25 * dpp_from_upper(c);
-        }
-#pragma unroll
-      for (int r = 0; r < kRW; ++r) {
-        // fine row j0-2+r: coarse row J at index tJ, far row (J-1 even / J+1 odd) at tf
-        const int odd = (P0 + r) & 1;
-        const int tJ = 1 + ((P0 + r) >> 1);
-        const int tf = odd ? tJ + 1 : tJ - 1;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const double vn = 0.75 * xi[0][tJ][e] + 0.25 * xi[0][tf][e];
-          const double vf = 0.75 * xi[1][tJ][e] + 0.25 * xi[1][tf][e];
-          v[r][e] = v[r][e] + (0.75 * vn + 0.25 * vf);
-        }
-      }
-    };
-    auto prolong = [&](double (&v)[kRW][2], const double (&cv)[2][6]) {
-      if (p0) prolong_p(std::integral_constant<int, 1>{}, v, cv);
-      else prolong_p(std::integral_constant<int, 0>{}, v, cv);
-    };
-    auto ldb = [&](double (&dst)[kRW][2], int kk) {
-      const int64_t base = pl(kk);
-#pragma unroll
-      for (int r = 1; r < kRW - 1; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
-    };
-    // element of the c1 point in row r of plane kk (the c2 point is the other one)
-    auto ec1 = [&](int kk, int r) -> bool { return ((par_row[r] + kpar(kk)) & 1) != c1; };
-    // first half-sweep (colour c1) at plane kk, rows 1 .. kRW-2 -> the c1 value of each pair.
-    // zmv: plane kk-1's values at those points (its c2 points); xcn, xp: planes kk, kk+1 (full)
-    auto half1 = [&](const double (&zmv)[kRW], const double (&xcn)[kRW][2],
-                     const double (&xp)[kRW][2], const double (&bb)[kRW][2], int kk,
-                     double (&out)[kRW]) {
-#pragma unroll
-      for (int r = 1; r < kRW - 1; ++r) {
-        const bool a1 = ec1(kk, r);  // c1 point is element 1
-        const double lo = dpp_from_lower(xcn[r][1]);
-        const double hi = dpp_from_upper(xcn[r][0]);
-        const double xl = a1 ? xcn[r][0] : lo;
-        const double xr = a1 ? hi : xcn[r][1];
-        const double zm = zmv[r];
-        const double ym = pick(a1, xcn[r - 1]);
-        const double yp = pick(a1, xcn[r + 1]);
-        const double zp = pick(a1, xp[r]);
-        const double bv = pick(a1, bb[r]);
-        const double xo = pick(a1, xcn[r]);
-        double nb = cz * zm;
-        nb = nb + cy * ym;
-        nb = nb + cx * xl;
-        nb = nb + cx * xr;
-        nb = nb + cy * yp;
-        nb = nb + cz * zp;
-        const double t = (bv - nb) * icc;
-        out[r] = (1.0 - omega) * xo + omega * t;
-      }
-    };
-    // the c2 values of a full plane (rows 1 .. kRW-2)
-    auto c2of = [&](const double (&v)[kRW][2], int kk, double (&out)[kRW]) {
-#pragma unroll
-      for (int r = 1; r < kRW - 1; ++r) out[r] = pick(!ec1(kk, r), v[r]);
-    };
-    auto c1of = [&](const double (&v)[kRW][2], int kk, double (&out)[kRW]) {
-#pragma unroll
-      for (int r = 1; r < kRW - 1; ++r) out[r] = pick(ec1(kk, r), v[r]);
-    };
-    // second half-sweep at plane kk, own rows 2 .. 2+TY2-1: the c2 points from the c1 values
-    // around them (sor_sweep2_kernel's, M = 0). sm, sc, sp: c1 values at planes kk-1, kk, kk+1;
-    // xo, bo: the plane's c2 input values and right-hand side (bc1: b at its c1 points, sums only)
-    auto half2 = [&](int kk, const double (&sm)[kRW], const double (&sc)[kRW],
-                     const double (&sp)[kRW], const double (&xo)[kRW], const double (&bo)[kRW],
-                     const double (&bc1)[SUMS ? kRW : 1]) {
-      const int64_t base = pl(kk);
-#pragma unroll
-      for (int r = 2; r < 2 + kTY2; ++r) {
-        const bool a1 = !ec1(kk, r);  // second-colour point is element 1
-        const double cself = sc[r];
-        const double lo = dpp_from_lower(cself);
-        const double hi = dpp_from_upper(cself);
-        const double xl = a1 ? cself : lo;
-        const double xr = a1 ? hi : cself;
-        double nb = cz * sm[r];
-        nb = nb + cy * sc[r - 1];
-        nb = nb + cx * xl;
-        nb = nb + cx * xr;
-        nb = nb + cy * sc[r + 1];
-        nb = nb + cz * sp[r];
-        const double t = (bo[r] - nb) * icc;
-        const double v = (1.0 - omega) * xo[r] + omega * t;
-        double ov[2];
-        ov[0] = a1 ? cself : v;
-        ov[1] = a1 ? v : cself;
-        if (out_ok && j0 + r - 2 < ny) {
-          store_row<2>(xout, rix(base + ro[r]), ov, g.nt);
-          if constexpr (SUMS) {
-            double rv2[2];
-            rv2[0] = a1 ? bc1[r] : bo[r];
-            rv2[1] = a1 ? bo[r] : bc1[r];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const double t2 = ov[e] - mu;
-              acc[0] += t2;
-              acc[1] += t2 * t2;
-              acc[2] += t2 * rv2[e];
-              acc[3] += rv2[e];
-            }
-          }
-        }
-      }
-    };
-    // Iteration k issues plane k+2's loads, runs the second half at plane k-1 while they are in
-    // flight, then prolongates plane k+2 and runs the first half at plane k+1. The queues keep
-    // only the c2 values of planes k-1 and k (x: the second half's old value, and the first half's
-    // z-neighbour; b: the second half's right-hand side). The loop starts two planes early
-    // (kb-2, kb-1: first halves only) so the queues fill without a separate prologue; the second
-    // half at plane ke-1 follows the loop.
-    double xm[kRW], x0[kRW];  // x input, c2 points: planes k-1, k
-    double xq1[kRW][2];       // x input, plane k+1
-    double s1[4][kRW];        // c1 values after the first half: planes k-2 .. k+1
-    double bm[kRW], b0[kRW];  // b at c2 points: planes k-1, k
-    double bm1[SUMS ? kRW : 1], b01[SUMS ? kRW : 1];  // and (sums only) at the c1 points
-    {
-      double cv[2][6];
-      ldx(xq1, cv, kb - 2);
-      prolong(xq1, cv);
-      c2of(xq1, kb - 2, x0);
-      ldx(xq1, cv, kb - 1);
-      prolong(xq1, cv);
-    }
-#pragma unroll
-    for (int r = 0; r < kRW; ++r) {
-      xm[r] = bm[r] = b0[r] = 0.0;
-      s1[0][r] = s1[1][r] = s1[2][r] = 0.0;
-      if constexpr (SUMS) bm1[r] = b01[r] = 0.0;
-    }
-#pragma unroll 1
-    for (int k = kb - 2; k < ke; ++k) {
-      double xq2[kRW][2], bq1[kRW][2], cv[2][6];
-      ldx(xq2, cv, k + 2);
-      ldb(bq1, k + 1);
-      if (k > kb) half2(k - 1, s1[0], s1[1], s1[2], xm, bm, bm1);
-      prolong(xq2, cv);
-      half1(x0, xq1, xq2, bq1, k + 1, s1[3]);  // c1 values at plane k+1
-      // rotate: planes k-1 <- k <- k+1 (c2 values), k+1 <- k+2
-#pragma unroll
-      for (int r = 0; r < kRW; ++r) {
-        xm[r] = x0[r];
-        bm[r] = b0[r];
-        if constexpr (SUMS) bm1[r] = b01[r];
-        s1[0][r] = s1[1][r];
-        s1[1][r] = s1[2][r];
-        s1[2][r] = s1[3][r];
-      }
-      c2of(xq1, k + 1, x0);
-      c2of(bq1, k + 1, b0);
-      if constexpr (SUMS) c1of(bq1, k + 1, b01);
-#pragma unroll
-      for (int r = 0; r < kRW; ++r)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) xq1[r][e] = xq2[r][e];
-    }
-    half2(ke - 1, s1[0], s1[1], s1[2], xm, bm, bm1);
-  }
-  if constexpr (SUMS) block_partials<4>(acc, parts);
-}
-
 // ---------------------------------------------------------------------------------------------
-// The same post-smoothing with rows shared between the waves of a block (r03). post_sweep_kernel's
-// waves each load TY2 + 4 rows of x_s (and TY2 + 2 of b, 12 coarse rows) for their TY2 own rows --
-// 2.3x the rows they store -- because the two half-sweeps need input two rows out, and they
-// recompute the first half on the TY2 + 2 middle rows. Here a block of NW waves stacks NW x TY
-// rows and each wave loads and sweeps only its own rows: the input (prolongated) rows and the
-// first-half values one row out come from the neighbouring waves through LDS, with one block
-// barrier per plane (written one iteration ahead of their use, double-buffered by plane parity).
-// The block's two outer rows at each end are halo (their inputs end at the block), so blocks
-// advance by NW TY - 4 rows. Same operations on the same operands as post_sweep_kernel (the
-// prolongation's per-coarse-row x stage, the half-sweeps' operand order): bit-identical.
-// ---------------------------------------------------------------------------------------------
-template <bool SUMS, int NW, int TY>
-__global__ __launch_bounds__(64 * NW) void post_sweep_xch_kernel(
-    Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
-    const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
-    double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
-  static_assert(TY % 2 == 0 && TY >= 2, "own rows start on an even fine row (prolongation parity)");
-  constexpr int RB = NW * TY;     // block rows
-  constexpr int SB = RB - 4;      // stored rows per block
-  constexpr int NC = TY / 2 + 2;  // coarse rows under a wave's own rows (near and far)
-  // per plane parity: prolongated input, own row 0 (e0, e1) and row TY-1 (e0, e1); first-half
-  // (c1) values of own rows 0 and TY-1
-  __shared__ double xch[2][6][NW][64];
-  if (skip && *skip) return;
-  const double icc = 1.0 / cc;
-  constexpr int c1 = 1;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  const double mu = SUMS ? st->mu : 0.0;
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int bid = xcd_block(g.remap);
-  const int seg = bid % g.nseg;
-  bid /= g.nseg;
-  const int tile = bid % g.ntile;
-  const int chunk = bid / g.ntile;
-  const int nx = g.nx, ny = g.ny, nz = g.nzl;
-  const int kb = chunk * g.kc;
-  const int ke = min(kb + g.kc, nz);
-  if (kb < nz) {  // block-uniform: every wave takes part in the barriers
-    const int g0 = tile * SB - 2;   // fine row of block row 0 (even)
-    const int br0 = wid * TY;       // block row of own row 0
-    const int j0 = g0 + br0;        // even, may lie outside [0, ny): rows wrap periodically
-    auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
-    int ip = seg * kSegOut + 2 * (lane - kSegLead);
-    if (ip < 0) ip += nx;
-    if (ip >= nx) ip -= nx;
-    const int o = seg * kSegOut + 2 * (lane - kSegLead);
-    const bool out_ok = lane >= kSegLead && lane < kSegLead + kSegOut / 2 && o < nx;
-    int64_t ro[TY];
-    int par_row[TY + 2];  // rows -1 .. TY
-    unsigned row_ok = 0;  // own rows this wave stores (wave-uniform bit mask)
-#pragma unroll
-    for (int r = -1; r <= TY; ++r) {
-      const int j = wrap(j0 + r, ny);
-      par_row[r + 1] = (ip + j) & 1;
-      if (r >= 0 && r < TY) {
-        ro[r] = (int64_t)j * nx;
-        const int brow = br0 + r;
-        if (brow >= 2 && brow < RB - 2 && g0 + brow < ny) row_ok |= 1u << r;
-      }
-    }
-    const unsigned boff = (unsigned)ip * 8u;
-    auto rix = [&](int64_t row) { return RowIx{row, boff}; };
-    auto wrapk = [&](int kk) { return kk < 0 ? kk + nz : (kk >= nz ? kk - nz : kk); };
-    auto pl = [&](int kk) -> int64_t { return (int64_t)wrapk(kk) * g.plane; };
-    auto kpar = [&](int kk) -> int { return (g.k0 + wrapk(kk)) & 1; };
-    int64_t crow[NC];  // coarse rows J0-1 .. J0+TY/2 (J0 = j0 / 2)
-#pragma unroll
-    for (int t = 0; t < NC; ++t) crow[t] = (int64_t)wrap((j0 >> 1) - 1 + t, cgeo.ncy) * cgeo.ncx;
-    const unsigned cboff = (unsigned)(ip >> 1) * 8u;
-    auto ldx = [&](double (&dst)[TY][2], double (&cv)[2][NC], int kk) {
-      const int64_t base = pl(kk);
-#pragma unroll
-      for (int r = 0; r < TY; ++r) load_row<2>(xs, rix(base + ro[r]), dst[r]);
-      const int kw = wrapk(kk);
-      const int K = kw >> 1;
-      int fK = (kw & 1) ? K + 1 : K - 1;
-      if (fK < 0) fK += cgeo.ncz;
-      if (fK >= cgeo.ncz) fK -= cgeo.ncz;
-      const double* cn = xc + (int64_t)K * cgeo.cplane;
-      const double* cf = xc + (int64_t)fK * cgeo.cplane;
-#pragma unroll
-      for (int t = 0; t < NC; ++t) {
-        cv[0][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cn + crow[t]) + cboff);
-        cv[1][t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cf + crow[t]) + cboff);
-      }
-    };
-    // x_s + P x_c on the own rows (post_sweep_kernel's prolong_p with an even first row)
-    auto prolong = [&](double (&v)[TY][2], const double (&cv)[2][NC]) {
-      double xi[2][NC][2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int t = 0; t < NC; ++t) {
-          const double c = cv[q][t];
-          xi[q][t][0] = 0.75 * c + 0.25 * dpp_from_lower(c);
-          xi[q][t][1] = 0.75 * c + 0.25 * dpp_from_upper(c);
-        }
-#pragma unroll
-      for (int r = 0; r < TY; ++r) {
-        const int tJ = 1 + (r >> 1);
-        const int tf = (r & 1) ? tJ + 1 : tJ - 1;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const double vn = 0.75 * xi[0][tJ][e] + 0.25 * xi[0][tf][e];
-          const double vf = 0.75 * xi[1][tJ][e] + 0.25 * xi[1][tf][e];
-          v[r][e] = v[r][e] + (0.75 * vn + 0.25 * vf);
-        }
-      }
-    };
-    auto ldb = [&](double (&dst)[TY][2], int kk) {
-      const int64_t base = pl(kk);
-#pragma unroll
-      for (int r = 0; r < TY; ++r) load_row<2>(b, rix(base + ro[r]), dst[r]);
-    };
-    auto ec1 = [&](int kk, int r) -> bool { return ((par_row[r + 1] + kpar(kk)) & 1) != c1; };
-    // first half-sweep at plane kk on the own rows; xcn holds rows -1 .. TY of plane kk
-    auto half1 = [&](const double (&zmv)[TY], const double (&xcn)[TY + 2][2],
-                     const double (&xp)[TY][2], const double (&bb)[TY][2], int kk,
-                     double (&out)[TY]) {
-#pragma unroll
-      for (int r = 0; r < TY; ++r) {
-        const bool a1 = ec1(kk, r);
-        const double lo = dpp_from_lower(xcn[r + 1][1]);
-        const double hi = dpp_from_upper(xcn[r + 1][0]);
-        const double xl = a1 ? xcn[r + 1][0] : lo;
-        const double xr = a1 ? hi : xcn[r + 1][1];
-        const double zm = zmv[r];
-        const double ym = pick(a1, xcn[r]);
-        const double yp = pick(a1, xcn[r + 2]);
-        const double zp = pick(a1, xp[r]);
-        const double bv = pick(a1, bb[r]);
-        const double xo = pick(a1, xcn[r + 1]);
-        double nb = cz * zm;
-        nb = nb + cy * ym;
-        nb = nb + cx * xl;
-        nb = nb + cx * xr;
-        nb = nb + cy * yp;
-        nb = nb + cz * zp;
-        const double t = (bv - nb) * icc;
-        out[r] = (1.0 - omega) * xo + omega * t;
-      }
-    };
-    auto c2of = [&](const double (&v)[TY][2], int kk, double (&out)[TY]) {
-#pragma unroll
-      for (int r = 0; r < TY; ++r) out[r] = pick(!ec1(kk, r), v[r]);
-    };
-    auto c1of = [&](const double (&v)[TY][2], int kk, double (&out)[TY]) {
-#pragma unroll
-      for (int r = 0; r < TY; ++r) out[r] = pick(ec1(kk, r), v[r]);
-    };
-    // second half-sweep at plane kk on the own rows; sh: c1 values of rows -1 and TY
-    auto half2 = [&](int kk, const double (&sm)[TY], const double (&sc)[TY],
-                     const double (&sp)[TY], const double (&sh)[2], const double (&xo)[TY],
-                     const double (&bo)[TY], const double (&bc1)[SUMS ? TY : 1]) {
-      const int64_t base = pl(kk);
-#pragma unroll
-      for (int r = 0; r < TY; ++r) {
-        const bool a1 = !ec1(kk, r);
-        const double cself = sc[r];
-        const double lo = dpp_from_lower(cself);
-        const double hi = dpp_from_upper(cself);
-        const double xl = a1 ? cself : lo;
-        const double xr = a1 ? hi : cself;
-        double nb = cz * sm[r];
-        nb = nb + cy * (r == 0 ? sh[0] : sc[r == 0 ? 0 : r - 1]);
-        nb = nb + cx * xl;
-        nb = nb + cx * xr;
-        nb = nb + cy * (r == TY - 1 ? sh[1] : sc[r == TY - 1 ? r : r + 1]);
-        nb = nb + cz * sp[r];
-        const double t = (bo[r] - nb) * icc;
-        const double v = (1.0 - omega) * xo[r] + omega * t;
-        double ov[2];
-        ov[0] = a1 ? cself : v;
-        ov[1] = a1 ? v : cself;
-        if (out_ok && (row_ok >> r & 1u)) {
-          store_row<2>(xout, rix(base + ro[r]), ov, g.nt);
-          if constexpr (SUMS) {
-            double rv2[2];
-            rv2[0] = a1 ? bc1[r] : bo[r];
-            rv2[1] = a1 ? bo[r] : bc1[r];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const double t2 = ov[e] - mu;
-              acc[0] += t2;
-              acc[1] += t2 * t2;
-              acc[2] += t2 * rv2[e];
-              acc[3] += rv2[e];
-            }
-          }
-        }
-      }
-    };
-    const int wm = wid > 0 ? wid - 1 : wid, wp = wid < NW - 1 ? wid + 1 : wid;
-    auto put_x = [&](int par, const double (&v)[TY][2]) {
-      xch[par][0][wid][lane] = v[0][0];
-      xch[par][1][wid][lane] = v[0][1];
-      xch[par][2][wid][lane] = v[TY - 1][0];
-      xch[par][3][wid][lane] = v[TY - 1][1];
-    };
-    // Iteration k: loads of plane k+2 (x_s, coarse) and k+1 (b) go out, the barrier publishes
-    // what iteration k-1 wrote (the input rows -1 / TY of plane k+1, the c1 values of rows -1 / TY
-    // of plane k), then the second half at plane k-1, the prolongation of plane k+2 and the first
-    // half at plane k+1 (post_sweep_kernel's order).
-    double xq1[TY + 2][2];  // input, plane k+1, rows -1 .. TY
-    double xm[TY], x0[TY];  // input c2 values, planes k-1, k
-    double s1[4][TY];       // c1 values after the first half, planes k-2 .. k+1
-    double shp[2], shc[2];  // c1 values of rows -1 / TY: planes k-1, k
-    double bm[TY], b0[TY];
-    double bm1[SUMS ? TY : 1], b01[SUMS ? TY : 1];
-    {
-      double xa[TY][2], cv[2][NC];
-      ldx(xa, cv, kb - 2);
-      prolong(xa, cv);
-      c2of(xa, kb - 2, x0);
-      ldx(xa, cv, kb - 1);
-      prolong(xa, cv);
-      put_x((kb - 3) & 1, xa);
-#pragma unroll
-      for (int r = 0; r < TY; ++r) {
-        xq1[r + 1][0] = xa[r][0];
-        xq1[r + 1][1] = xa[r][1];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < TY; ++r) {
-      xm[r] = bm[r] = b0[r] = 0.0;
-      s1[0][r] = s1[1][r] = s1[2][r] = 0.0;
-      if constexpr (SUMS) bm1[r] = b01[r] = 0.0;
-    }
-    shp[0] = shp[1] = 0.0;
-    // loads of one iteration: x_s and coarse values of plane k+2, b of plane k+1
-    struct Ld {
-      double x[TY][2], cv[2][NC], b[TY][2];
-    };
-    auto step = [&](int k, Ld& cur) {
-      ldx(cur.x, cur.cv, k + 2);
-      ldb(cur.b, k + 1);
-      __syncthreads();
-      {
-        const int rp = (k - 1) & 1;
-        xq1[0][0] = xch[rp][2][wm][lane];
-        xq1[0][1] = xch[rp][3][wm][lane];
-        xq1[TY + 1][0] = xch[rp][0][wp][lane];
-        xq1[TY + 1][1] = xch[rp][1][wp][lane];
-        shc[0] = xch[rp][5][wm][lane];
-        shc[1] = xch[rp][4][wp][lane];
-      }
-      if (k > kb) half2(k - 1, s1[0], s1[1], s1[2], shp, xm, bm, bm1);
-      prolong(cur.x, cur.cv);
-      put_x(k & 1, cur.x);
-      half1(x0, xq1, cur.x, cur.b, k + 1, s1[3]);
-      xch[k & 1][4][wid][lane] = s1[3][0];
-      xch[k & 1][5][wid][lane] = s1[3][TY - 1];
-#pragma unroll
-      for (int r = 0; r < TY; ++r) {
-        xm[r] = x0[r];
-        bm[r] = b0[r];
-        if constexpr (SUMS) bm1[r] = b01[r];
-        s1[0][r] = s1[1][r];
-        s1[1][r] = s1[2][r];
-        s1[2][r] = s1[3][r];
-      }
-      shp[0] = shc[0];
-      shp[1] = shc[1];
-      {
-        double own[TY][2];
-#pragma unroll
-        for (int r = 0; r < TY; ++r) {
-          own[r][0] = xq1[r + 1][0];
-          own[r][1] = xq1[r + 1][1];
-        }
-        c2of(own, k + 1, x0);
-      }
-      c2of(cur.b, k + 1, b0);
-      if constexpr (SUMS) c1of(cur.b, k + 1, b01);
-#pragma unroll
-      for (int r = 0; r < TY; ++r)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) xq1[r + 1][e] = cur.x[r][e];
-    };
-    Ld A;
-#pragma unroll 1
-    for (int k = kb - 2; k < ke; ++k) step(k, A);
-    half2(ke - 1, s1[0], s1[1], s1[2], shp, xm, bm, bm1);
-  }
-  if constexpr (SUMS) block_partials<4>(acc, parts);
-}
-
-// ---------------------------------------------------------------------------------------------
-// post_sweep_xch_kernel with the plane loop unrolled by four (r03), as
-// presmooth_restrict_u4_kernel: the queues (input planes with their halo rows, first-half values,
+// The post-smoothing pass (r03): rows shared between the waves of a block through LDS as in
+// presmooth_restrict_u4_kernel -- a wave loads its own input rows only, the rows one out (the
+// prolongated input and the first-half values) come from the neighbouring waves, published one
+// plane before use, one barrier per plane; a block stores rows 2 .. NW TY - 3 -- and the plane
+// loop unrolled by four: the queues (input planes with their halo rows, first-half values,
 // c2 inputs and right-hand sides, halo first-half values) are rings of four or two register slots
 // whose roles rotate with the unrolled copy, and each copy knows its plane's parity (even k0,
 // even extents and origins), so the colour choices are register choices and each half-sweep
@@ -1881,9 +862,9 @@ __device__ __forceinline__ void post_sweep_u4_range(
       for (int t = 0; t < NC; ++t)
         cv[t] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(cp + crow[t]) + cboff);
     };
-    // one coarse plane interpolated in x, then in y onto each own row (post_sweep_kernel's
-    // prolong_p: the same operations, formed once per coarse plane instead of once per fine plane
-    // that reads it -- each serves the two fine planes it is near to and the two it is far from)
+    // one coarse plane interpolated in x, then in y onto each own row (mg_prolong_z_kernel's
+    // operations, formed once per coarse plane instead of once per fine plane that reads it --
+    // each serves the two fine planes it is near to and the two it is far from)
     auto yinterp = [&](const double (&cv)[NC], double (&Y)[TY][2]) {
       double xi[NC][2];
 #pragma unroll
@@ -1915,8 +896,8 @@ __device__ __forceinline__ void post_sweep_u4_range(
 #pragma unroll
       for (int r = 0; r < TY; ++r) load_row<2>(src, rix(ro[r]), dst[r]);
     };
-    // element of the c1 (first-half) point of own row r on a plane of parity P: post_sweep_kernel's
-    // ec1 with ((i + j) & 1) = r & 1 and c1 = 1
+    // element of the c1 (first-half) point of own row r on a plane of parity P (((i + j) & 1) =
+    // r & 1, c1 = 1)
     auto e1 = [](int r, int P) { return ((r + P) & 1) ^ 1; };
     auto half1 = [&](auto Pc, const double (&zmv)[TY], const double (&xcn)[TY + 2][2],
                      const double (&xp)[TY + 2][2], const double (&bb)[TY][2],
@@ -2081,7 +1062,9 @@ __global__ __launch_bounds__(64 * NW) void post_sweep_u4_kernel(
     Sweep2Geo g, PostGeo cgeo, double cx, double cy, double cz, double cc, double omega,
     const double* __restrict__ xs, const double* __restrict__ xc, const double* __restrict__ b,
     double* __restrict__ xout, const CgState* st, double* parts, const int* skip) {
-  __shared__ double xch[2][6][NW][64];  // as post_sweep_xch_kernel's
+  // per plane parity, per wave: the prolongated input of own rows 0 / TY-1 (e0, e1 each), the
+  // first-half values of rows 0 / TY-1
+  __shared__ double xch[2][6][NW][64];
   if (skip && *skip) return;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const double mu = SUMS ? st->mu : 0.0;
@@ -2145,12 +1128,12 @@ static int64_t sweep2_geo(pb_grid* g, Sweep2Geo& geo) {
   geo.nseg = (geo.nx + kSegOut - 1) / kSegOut;
   geo.ntile = (geo.ny + kWaves * kTY2 - 1) / (kWaves * kTY2);
   geo.k0 = (int)g->k0;
-  geo.remap = tune("xcd_remap", 1);
-  geo.nt = tune("stencil_nt", 1);
+  geo.remap = 1;
+  geo.nt = 1;
   const int columns = geo.nseg * geo.ntile;
   // chunks: ~PB_SWEEP2_WGCU (16) workgroups per CU (many rounds: the loop is latency-bound),
   // at least 16 planes per chunk
-  const int target = tune("sweep2_wgcu", 16) * g->ctx->num_cus;
+  const int target = 16 * g->ctx->num_cus;
   int nchunk = std::max(1, (target + columns - 1) / columns);
   nchunk = std::min(nchunk, std::max(1, geo.nzl / 16));
   geo.kc = (geo.nzl + nchunk - 1) / nchunk;
@@ -2169,16 +1152,16 @@ int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double
     if (nblocks * 4 > g->ctx->partials_cap)
       return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
                        (long long)nblocks);
-    auto kern = geo.split ? sor_sweep2_kernel<true, 0, true> : sor_sweep2_kernel<true, 0, false>;
+    auto kern = geo.split ? sor_sweep2_kernel<true, true> : sor_sweep2_kernel<true, false>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
-                       (double*)nullptr, sums_st, g->ctx->d_partials, skip);
+                       sums_st, g->ctx->d_partials, skip);
     if (nparts) *nparts = (int)nblocks;
   } else {
-    auto kern = geo.split ? sor_sweep2_kernel<false, 0, true> : sor_sweep2_kernel<false, 0, false>;
+    auto kern = geo.split ? sor_sweep2_kernel<false, true> : sor_sweep2_kernel<false, false>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
                        g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, c1, xin, b, xout,
-                       (double*)nullptr, (const CgState*)nullptr, (double*)nullptr, skip);
+                       (const CgState*)nullptr, (double*)nullptr, skip);
   }
   PB_HIP(hipGetLastError());
   return PB_OK;
@@ -2204,8 +1187,6 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
                       const int* skip, const CgState* sums_st, int* nparts) {
   ScopedTimer tm(g->ctx, "mg_post_sweep");
   const bool split = g->ctx->split;
-  if (split && tune("postx", 3) < 3)
-    return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing on N ranks: unrolled kernels only");
   if (xs == xout) return set_error(PB_ERR_ARG, "fused post-smoothing must run out of place");
   if (cg->n[0] * 2 != g->n[0] || cg->n[1] * 2 != g->n[1] || cg->nzl * 2 != g->nzl)
     return set_error(PB_ERR_ARG, "fused post-smoothing: coarse grid is not half the fine one");
@@ -2232,60 +1213,34 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     cgeo.split = 1;
     cgeo.cgh = gc->ghost2;
   }
-  // rows shared through LDS: 1, 2 = post_sweep_xch_kernel with 8 waves x 4 / x 2 rows; 3, 4 = the
-  // same with the plane loop unrolled by four (post_sweep_u4_kernel; compile-time colours: even k0,
-  // chunk starts at multiples of 4); 0 = the per-wave kernel below
-  const int xv = tune("postx", 3);
-  if (xv >= 1 && xv <= 4) {
-    const int nw = 8, ty = (xv & 1) ? 4 : 2;
-    geo.ntile = (geo.ny + nw * ty - 5) / (nw * ty - 4);
-    const int columns = geo.nseg * geo.ntile;
-    // z-chunks: every chunk re-reads two planes and runs up to five spare ones, so chunks stay
-    // >= 64 planes where the grid has 512 (measured: 0.733 -> 0.700 ms at 512^3 against 16) and
-    // >= nz / 8 on shallower grids, which need the workgroups
-    const int target = tune("postx_wgcu", 8) * g->ctx->num_cus;
-    int nchunk = std::max(1, (target + columns - 1) / columns);
-    const int minz = std::min(tune("postx_minz", 64), std::max(16, geo.nzl / 8));
-    nchunk = std::min(nchunk, std::max(1, geo.nzl / minz));
-    geo.kc = (geo.nzl + nchunk - 1) / nchunk;
-    geo.kc = (geo.kc + 3) & ~3;  // chunk starts at multiples of 4 (the unrolled kernels' parities)
-    geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
-    nblocks = (int64_t)columns * geo.nchunk;
-    if (xv >= 3 && g->k0 % 2 != 0)  // (the unrolled kernels' compile-time colours)
-      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: odd slab origin");
-    if (split && xv < 3)
-      return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing on N ranks: unrolled kernels only");
-    if (xv >= 3) nblocks = balanced_split(g, geo, tune("postx_split", 0), 4, nblocks);
-    if (sums_st && nblocks * 4 > g->ctx->partials_cap)
-      return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
-                       (long long)nblocks);
-    decltype(&post_sweep_u4_kernel<true, 8, 4>) kern;
-    if (sums_st)
-      kern = xv == 1 ? post_sweep_xch_kernel<true, 8, 4> : xv == 2 ? post_sweep_xch_kernel<true, 8, 2>
-           : xv == 3 ? post_sweep_u4_kernel<true, 8, 4> : post_sweep_u4_kernel<true, 8, 2>;
-    else
-      kern = xv == 1 ? post_sweep_xch_kernel<false, 8, 4> : xv == 2 ? post_sweep_xch_kernel<false, 8, 2>
-           : xv == 3 ? post_sweep_u4_kernel<false, 8, 4> : post_sweep_u4_kernel<false, 8, 2>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo, cgeo,
-                       s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout, sums_st,
-                       sums_st ? g->ctx->d_partials : (double*)nullptr, skip);
-    if (sums_st && nparts) *nparts = (int)nblocks;
-    PB_HIP(hipGetLastError());
-    return PB_OK;
-  }
-  if (sums_st) {
-    if (nblocks * 4 > g->ctx->partials_cap)
-      return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
-                       (long long)nblocks);
-    hipLaunchKernelGGL(post_sweep_kernel<true>, dim3((unsigned)nblocks), dim3(kThreads), 0,
-                       g->ctx->stream, geo, cgeo, s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout,
-                       sums_st, g->ctx->d_partials, skip);
-    if (nparts) *nparts = (int)nblocks;
-  } else {
-    hipLaunchKernelGGL(post_sweep_kernel<false>, dim3((unsigned)nblocks), dim3(kThreads), 0,
-                       g->ctx->stream, geo, cgeo, s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout,
-                       (const CgState*)nullptr, (double*)nullptr, skip);
-  }
+  // 8 waves x 4 rows (unrolled: compile-time colours need an even k0, chunks start at multiples
+  // of 4)
+  constexpr int nw = 8, ty = 4;
+  geo.ntile = (geo.ny + nw * ty - 5) / (nw * ty - 4);
+  const int columns = geo.nseg * geo.ntile;
+  // z-chunks: every chunk re-reads two planes and runs up to five spare ones, so chunks stay
+  // >= 64 planes where the grid has 512 (measured: 0.733 -> 0.700 ms at 512^3 against 16) and
+  // >= nz / 8 on shallower grids, which need the workgroups (~8 per CU)
+  const int target = 8 * g->ctx->num_cus;
+  int nchunk = std::max(1, (target + columns - 1) / columns);
+  const int minz = std::min(64, std::max(16, geo.nzl / 8));
+  nchunk = std::min(nchunk, std::max(1, geo.nzl / minz));
+  geo.kc = (geo.nzl + nchunk - 1) / nchunk;
+  geo.kc = (geo.kc + 3) & ~3;
+  geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
+  nblocks = (int64_t)columns * geo.nchunk;
+  if (g->k0 % 2 != 0)
+    return set_error(PB_ERR_UNSUPPORTED, "fused post-smoothing: odd slab origin");
+  // (mg_u4_split: the balanced work split, tests only -- slower here at any count, r04)
+  nblocks = balanced_split(g, geo, std::max(0, tune("mg_u4_split", 0)), 4, nblocks);
+  if (sums_st && nblocks * 4 > g->ctx->partials_cap)
+    return set_error(PB_ERR_UNSUPPORTED, "fused sweep of %lld blocks exceeds partials capacity",
+                     (long long)nblocks);
+  auto kern = sums_st ? post_sweep_u4_kernel<true, nw, ty> : post_sweep_u4_kernel<false, nw, ty>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo, cgeo,
+                     s.cx, s.cy, s.cz, s.cc, omega, xs, xc, b, xout, sums_st,
+                     sums_st ? g->ctx->d_partials : (double*)nullptr, skip);
+  if (sums_st && nparts) *nparts = (int)nblocks;
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
@@ -2294,8 +1249,8 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
                               double* xout, double* bc, double omega, const int* skip) {
   ScopedTimer tm(g->ctx, "mg_presmooth_restrict");
   const bool split = g->ctx->split;
-  if (split && (tune("prrx", 2) != 2 || g->nzl < 3))
-    return set_error(PB_ERR_UNSUPPORTED, "fused restriction on N ranks: unrolled kernel, >= 3 planes");
+  if (split && g->nzl < 3)
+    return set_error(PB_ERR_UNSUPPORTED, "fused restriction on N ranks: >= 3 planes per slab");
   if (b == xout) return set_error(PB_ERR_ARG, "fused pre-smoothing must run out of place");
   if (!sor_sweep2_supported(g) || g->nzl % 2)
     return set_error(PB_ERR_UNSUPPORTED, "fused restriction: grid not supported");
@@ -2312,60 +1267,37 @@ int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, cons
     geo.split = 1;
     geo.xg = g->ghost2;
   }
-  // rows shared through LDS: 1 = presmooth_restrict_xch_kernel, 2 = the same with the plane loop
-  // unrolled by four (presmooth_restrict_u4_kernel; compile-time colours: even k0, even chunk
-  // starts), both 8 waves x 4 rows; 0 = the per-wave kernel below
-  const int xv = tune("prrx", 2);
-  if (xv == 1 || xv == 2) {
-    constexpr int nw = 8, ty = 4;
-    geo.ntile = (geo.ny + nw * ty - 9) / (nw * ty - 8);
-    const int columns = geo.nseg * geo.ntile;
-    // z-chunks: each chunk forms red, black and residual values on five planes outside it, and
-    // the passes are latency-bound at two waves per SIMD, so (measured at 512^3, one box) few long
-    // chunks at most one workgroup per CU win (2 chunks of 256 planes, 220 workgroups: 0.503 ms)
-    // over many (10 of 52, 1100 workgroups: 0.566 ms) -- while a count just above one per CU
-    // leaves some CUs two workgroups (3 chunks of 172, 330 workgroups: 0.685 vs 0.609 on another
-    // box). So: at most one workgroup per CU when that keeps chunks of >= PB_PRRX_LONGZ planes,
-    // else ~4 per CU (256^3 and smaller grids)
-    int nchunk = std::max(1, g->ctx->num_cus / columns);
-    if (geo.nzl / nchunk < tune("prrx_longz", 128))
-      nchunk = std::max(1, (tune("prrx_wgcu", 4) * g->ctx->num_cus + columns - 1) / columns);
-    nchunk = std::min(nchunk, std::max(1, geo.nzl / tune("prrx_minz", 16)));
-    geo.kc = (geo.nzl + nchunk - 1) / nchunk;
-    geo.kc += geo.kc & 1;
-    geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
-    int64_t nblocks = (int64_t)columns * geo.nchunk;
-    if (g->k0 % 2 != 0)  // (the unrolled kernel's compile-time colours)
-      return set_error(PB_ERR_UNSUPPORTED, "fused restriction: odd slab origin");
-    // balanced split (prrx_split workgroups per CU; default: 1 where the chunks above need more
-    // than one round of workgroups -- this pass runs one per CU (254 VGPRs): 512^3's 256^3 level,
-    // 528 workgroups, 0.405 -> 0.382 ms for the coarse levels; on the 512^3 level itself, 220
-    // workgroups in one round, the split was slower, 0.506 -> 0.521 ms, r04/mg/split_ab.jsonl)
-    if (xv == 2) {
-      const int ps = tune("prrx_split", -1);
-      nblocks = balanced_split(g, geo, ps >= 0 ? ps : (nblocks > g->ctx->num_cus ? 1 : 0), 2,
-                               nblocks);
-    }
-    auto kern = xv == 1 ? presmooth_restrict_xch_kernel<nw, ty> : presmooth_restrict_u4_kernel<nw, ty>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(64 * nw), 0, g->ctx->stream, geo,
-                       (int)cg->n[0], cg->plane, s.cx, s.cy, s.cz, s.cc, omega, b, xout, bc, skip);
-    PB_HIP(hipGetLastError());
-    return PB_OK;
-  }
-  geo.ntile = (geo.ny + kWaves * kTYR - 1) / (kWaves * kTYR);
-  // chunks of an even number of planes (the restriction pairs them); each chunk also forms S1 on
-  // three planes and the residual on two planes outside it, so chunks stay long
+  // 8 waves x 4 rows, the plane loop unrolled by four (compile-time colours: even k0, even
+  // chunk starts)
+  constexpr int nw = 8, ty = 4;
+  geo.ntile = (geo.ny + nw * ty - 9) / (nw * ty - 8);
   const int columns = geo.nseg * geo.ntile;
-  const int target = tune("prr_wgcu", 4) * g->ctx->num_cus;
-  int nchunk = std::max(1, (target + columns - 1) / columns);
-  nchunk = std::min(nchunk, std::max(1, geo.nzl / tune("prr_minz", 32)));
+  // z-chunks: each chunk forms red, black and residual values on five planes outside it, and
+  // the pass is latency-bound at two waves per SIMD, so (measured at 512^3, one box) few long
+  // chunks at most one workgroup per CU win (2 chunks of 256 planes, 220 workgroups: 0.503 ms)
+  // over many (10 of 52, 1100 workgroups: 0.566 ms) -- while a count just above one per CU
+  // leaves some CUs two workgroups (3 chunks of 172, 330 workgroups: 0.685 vs 0.609 on another
+  // box). So: at most one workgroup per CU when that keeps chunks of >= 128 planes, else ~4 per
+  // CU (256^3 and smaller grids), chunks of >= 16 planes
+  int nchunk = std::max(1, g->ctx->num_cus / columns);
+  if (geo.nzl / nchunk < 128) nchunk = std::max(1, (4 * g->ctx->num_cus + columns - 1) / columns);
+  nchunk = std::min(nchunk, std::max(1, geo.nzl / 16));
   geo.kc = (geo.nzl + nchunk - 1) / nchunk;
   geo.kc += geo.kc & 1;
   geo.nchunk = (geo.nzl + geo.kc - 1) / geo.kc;
-  const int64_t nblocks = (int64_t)columns * geo.nchunk;
-  hipLaunchKernelGGL(presmooth_restrict_kernel, dim3((unsigned)nblocks), dim3(kThreads), 0,
-                     g->ctx->stream, geo, (int)cg->n[0], cg->plane, s.cx, s.cy, s.cz, s.cc, omega,
-                     b, xout, bc, skip);
+  int64_t nblocks = (int64_t)columns * geo.nchunk;
+  if (g->k0 % 2 != 0)
+    return set_error(PB_ERR_UNSUPPORTED, "fused restriction: odd slab origin");
+  // balanced split (one workgroup per CU where the chunks above need more than one round of
+  // workgroups -- this pass runs one per CU (254 VGPRs): 512^3's 256^3 level, 528 workgroups,
+  // 0.405 -> 0.382 ms for the coarse levels; on the 512^3 level itself, 220 workgroups in one
+  // round, the split was slower, 0.506 -> 0.521 ms, r04/mg/split_ab.jsonl)
+  const int ps = tune("mg_u4_split", -1);
+  nblocks = balanced_split(g, geo, ps >= 0 ? ps : (nblocks > g->ctx->num_cus ? 1 : 0), 2,
+                           nblocks);
+  hipLaunchKernelGGL((presmooth_restrict_u4_kernel<nw, ty>), dim3((unsigned)nblocks),
+                     dim3(64 * nw), 0, g->ctx->stream, geo, (int)cg->n[0], cg->plane, s.cx, s.cy,
+                     s.cz, s.cc, omega, b, xout, bc, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
@@ -2378,16 +1310,9 @@ int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double
   Sweep2Geo geo;
   const int64_t nblocks = sweep2_geo(g, geo);
   PB_TRY(sweep2_ghosts(g, b, b, geo));
-  if (tune("mg_presmooth_slim", 1)) {  // one double per pair in the x queue
-    auto kern = geo.split ? presmooth_resid_kernel<true> : presmooth_resid_kernel<false>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0, g->ctx->stream, geo,
-                       s.cx, s.cy, s.cz, s.cc, omega, b, x, res, skip);
-  } else {
-    auto kern = geo.split ? sor_sweep2_kernel<false, 1, true> : sor_sweep2_kernel<false, 1, false>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0,
-                       g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, omega, 1, b, b, x, res,
-                       (const CgState*)nullptr, (double*)nullptr, skip);
-  }
+  auto kern = geo.split ? presmooth_resid_kernel<true> : presmooth_resid_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nblocks), dim3(kThreads), 0, g->ctx->stream, geo,
+                     s.cx, s.cy, s.cz, s.cc, omega, b, x, res, skip);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }

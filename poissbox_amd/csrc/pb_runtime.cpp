@@ -32,17 +32,10 @@ std::unordered_map<std::string, int> g_tune;
 // every name a kernel launcher consults; the defaults live at the call sites (the measured
 // choices), the table only holds values a caller set
 const char* const kTuneNames[] = {
-    "cg_defer_x", "cg_fold", "cg_fuse", "cg_pstore_b", "compact_fuse_transpose", "compact_lines", "fft_blocks_per_cu", "fft_fuse_transpose",
-    "fft_pf_strided", "fft_poll", "fft_reg", "fft_remap", "fft_rupd", "fft_stagger", "fft_sums",
-    "fft_tl_long", "fft_tl_z", "fft_yorder", "fft_zorder", "fft_zpad", "fft_zpad_min_plane",
-    "comm_mark_every", "comm_stall_test_ms", "force_comm", "ksp_event_all", "ksp_lazy0", "lines_cfg", "lines_remap", "lines_xdirect",
-    "mg_agglomerate", "mg_agglomerate_max", "mg_engine_min_plane", "mg_post_fused", "mg_presmooth_fused", "mg_presmooth_restrict",
-    "mg_presmooth_slim", "mg_prolong_cell", "mg_restrict_z", "mg_restrict_z_min_cols",
-    "mg_split_fused", "mg_sweep2", "mg_tail", "mg_tail_lds", "mg_tail_max", "mg_transfer_minz", "mg_transfer_tpc", "passa_nt",
-    "pcr_lines", "postx", "postx_minz", "postx_split", "postx_wgcu", "prr_minz", "prr_wgcu", "prrx",
-    "prrx_longz", "prrx_minz", "prrx_split", "prrx_wgcu", "slab_rows", "sor_omega_any", "sr_s_shape", "stencil_blocks", "stencil_kcmin", "stencil_nt",
-    "stencil_tall", "stencil_tall_min_plane", "stencil_ty", "sweep2_wgcu", "tall_wgcu",
-    "xcd_remap", "zalt"};
+    "cg_defer_x", "cg_fold", "cg_fuse", "cg_sr_fused", "cg_sr_shape", "comm_mark_every",
+    "comm_stall_test_ms", "compact_lines", "fft_rupd", "fft_zpad", "fft_zpad_min_plane",
+    "force_comm", "ksp_lazy0", "mg_agglomerate", "mg_engine_min_plane", "mg_restrict_z_min_cols",
+    "mg_split_fused", "mg_sweep2", "mg_tail_max", "mg_u4_split", "pcr_lines", "sor_omega_any"};
 bool tune_known(const char* name) {
   for (const char* n : kTuneNames)
     if (strcmp(n, name) == 0) return true;

@@ -29,7 +29,7 @@ struct pb_ksp {
   pb_op* P = nullptr;
   pb_ksp_opts opts;
   double* r = nullptr;
-  // PB_CG_PSTORE_B (Jacobi, fused operator): pass B forms and stores p and writes the residual to
+  // Jacobi / none on the fused operator: pass B forms and stores p and writes the residual to
   // the other buffer -- iteration i reads rbuf(i), writes rbuf(i + 1)
   double* r2 = nullptr;
   bool pst = false;
@@ -67,7 +67,8 @@ struct pb_ksp {
   int sr_nparts = 0;
 };
 
-static int sr_pass_s(pb_ksp* k, const double* r, const CgState* st, int* nparts);
+static int sr_pass_s(pb_ksp* k, const double* r, const CgState* st, int* nparts, int64_t n);
+static const double* sr_region(const pb_ctx* ctx, int64_t n);
 
 extern "C" {
 
@@ -298,7 +299,7 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
   if ((k->opts.pc_type == PB_PC_SOR || k->opts.pc_type == PB_PC_MG) && k->opts.check_every > 2)
     k->opts.check_every = 2;
   if (k->opts.pc_type == PB_PC_FFT)
-    k->opts.check_every = std::min(k->opts.check_every, std::max(1, tune("fft_poll", 1)));
+    k->opts.check_every = 1;
   const int pc = k->opts.pc_type;
   if (pc != PB_PC_NONE && pc != PB_PC_JACOBI && pc != PB_PC_SOR && pc != PB_PC_MG &&
       pc != PB_PC_FFT)
@@ -393,8 +394,8 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
   st.defer_x = k->defer_x;
   // p stored by pass B (default): pass A read-only, 56 instead of 58 B/DoF per iteration and
   // the passes closer to their patterns' rates -- 1.29 vs 1.36 ms/iteration at 512^3 on one box
-  // (profiles/r02/ab_pst_defer_512.jsonl); PB_CG_PSTORE_B=0 stores p in pass A
-  k->pst = tune("cg_pstore_b", 1) != 0 && fused_kind(k->A->kind) && !k->stored_z();
+  // (profiles/r02/ab_pst_defer_512.jsonl); with a stored-z PC pass A stores p (the r01 split)
+  k->pst = fused_kind(k->A->kind) && !k->stored_z();
   // single reduction: the fused operator with Jacobi / no PC (pass P forms p from r on load);
   // elsewhere the KSPSolve_CG iteration runs (equal in exact arithmetic; pb_ksp_opts)
   k->sr = k->opts.cg_single_reduction != 0 && fused_kind(k->A->kind) && !k->stored_z();
@@ -434,8 +435,9 @@ int pb_ksp_begin(pb_ksp* k, const pb_vec* b, pb_vec* x) {
     if (k->sr) {
       // KSPSolve_CG_SingleReduction's setup: S = A z, delta = z'S (pass S over r0 = b)
       int np = 0;
-      PB_TRY(sr_pass_s(k, k->r, k->d_st, &np));
-      PB_TRY(cg_sr_finalize(ctx, np, k->d_st, k->d_hist, k->h_done_dev, -1, true));
+      PB_TRY(sr_pass_s(k, k->r, k->d_st, &np, 0));
+      PB_TRY(cg_sr_finalize(ctx, sr_region(ctx, 0), np, k->d_st, k->d_hist, k->h_done_dev, -1,
+                            true));
     }
   }
   PB_SYNC(ctx, "pb_ksp_begin");
@@ -528,29 +530,40 @@ static int enqueue_pc_iteration(pb_ksp* k) {
 
 // pass S over r (t = dinv r - mu of state st): split grids exchange r's boundary planes (raw;
 // the loader transforms ghosts too) under the interior planes
-static int sr_pass_s(pb_ksp* k, const double* r, const CgState* st, int* nparts) {
+// the single-reduction iteration's two partial-sum regions (5 wide): iteration n of a batch
+// writes region n & 1 and its folded prologue reduces region (n - 1) & 1, so a launch never
+// overwrites the partials its own blocks may still be reading (part_off in 5-wide blocks)
+static int64_t sr_region_off(const pb_ctx* ctx, int64_t n) {
+  return (n & 1) * (ctx->partials_cap / 10);
+}
+static const double* sr_region(const pb_ctx* ctx, int64_t n) {
+  return ctx->d_partials + sr_region_off(ctx, n) * 5;
+}
+
+static int sr_pass_s(pb_ksp* k, const double* r, const CgState* st, int* nparts, int64_t n) {
   pb_grid* g = k->A->grid;
   pb_ctx* ctx = g->ctx;
   Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};
   StencilPlanes gp;
+  const int off = (int)sr_region_off(ctx, n);
   if (!ctx->split) {
     gp.ghost_lo = gp.ghost_hi = nullptr;
     gp.wrap = true;
-    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, 0, nparts);
+    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, off, nparts);
   }
   gp.ghost_lo = g->ghost_lo;
   gp.ghost_hi = g->ghost_hi;
   const double* hi = r + (g->nzl - 1) * g->plane;
   if (g->nzl < 3) {
     PB_TRY(halo_exchange(g, r, hi));
-    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, 0, nparts);
+    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, off, nparts);
   }
   int nb1 = 0, nb2 = 0;
   ScopedTimer tm(ctx, "cg_sr_s");
   PB_TRY(halo_begin(g, r, hi));
-  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_INTERIOR, 0, &nb1));
+  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_INTERIOR, off, &nb1));
   PB_TRY(halo_end(g));
-  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_BOUNDARY, nb1, &nb2));
+  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_BOUNDARY, off + nb1, &nb2));
   *nparts = nb1 + nb2;
   return PB_OK;
 }
@@ -573,11 +586,21 @@ static int enqueue_sr_iteration(pb_ksp* k, bool fold, int64_t n) {
   SrFold f;
   f.fold_sums = fold && n > 0;
   f.nparts_s = k->sr_nparts;
+  f.parts = sr_region(ctx, n - 1);
   f.in = st_in;
   f.out = st_out;
   f.hist = k->d_hist;
   f.h_done = k->h_done_dev;
   StencilPlanes gp;
+  // one pass per iteration where it applies: one rank, x update not due (depth-4 deferral)
+  if (cg_sr1_supported(g) && k->defer_x == 4 && i % 4 != 3) {
+    PB_TRY(launch_cg_sr1(g, s, r, p_prev[0], p_new, r_out, f, f.parts,
+                         const_cast<double*>(sr_region(ctx, n)), i, &k->sr_nparts));
+    if (!fold)
+      PB_TRY(cg_sr_finalize(ctx, sr_region(ctx, n), k->sr_nparts, st_out, k->d_hist,
+                            k->h_done_dev, i));
+    return PB_OK;
+  }
   if (!ctx->split) {
     gp.ghost_lo = gp.ghost_hi = nullptr;
     gp.wrap = true;
@@ -602,8 +625,10 @@ static int enqueue_sr_iteration(pb_ksp* k, bool fold, int64_t n) {
                                  i, k->defer_x));
     }
   }
-  PB_TRY(sr_pass_s(k, r_out, st_out, &k->sr_nparts));
-  if (!fold) PB_TRY(cg_sr_finalize(ctx, k->sr_nparts, st_out, k->d_hist, k->h_done_dev, i));
+  PB_TRY(sr_pass_s(k, r_out, st_out, &k->sr_nparts, n));
+  if (!fold)
+    PB_TRY(cg_sr_finalize(ctx, sr_region(ctx, n), k->sr_nparts, st_out, k->d_hist,
+                          k->h_done_dev, i));
   return PB_OK;
 }
 
@@ -624,7 +649,7 @@ static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
   // Jacobi: pass A builds z = dinv*r - mu on the fly; SOR / MG: z is stored (dinv = 1)
   double* r = k->rbuf(i);
   const double* zsrc = k->stored_z() ? k->z : r;
-  // PB_CG_PSTORE_B: pass A read-only, pass B stores p and the residual into the other buffer
+  // Jacobi / none: pass A read-only, pass B stores p and the residual into the other buffer
   PStore ps;
   if (k->pst) {
     ps.zsrc = zsrc;
@@ -712,8 +737,7 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
     // only the iterations the poll below waits for get an event (j = 0 mod C; folded j + 1): an
     // event record between two kernels costs the stream ~6 us of idle time (measured 5.9 us per
     // iteration with one record per iteration; profiles/r02/cg_gaps_*.txt)
-    const bool every = tune("ksp_event_all", 0) != 0;  // (A/B: one per iteration)
-    if (every || hi % C == (fold ? 1 : 0) % C)
+    if (hi % C == (fold ? 1 : 0) % C)
       PB_HIP(hipEventRecord(k->ring[hi % R], ctx->stream));
     // lagged, rank-consistent poll: decide on the flag of iteration hi + 1 - C only (folded:
     // that flag is written by the next iteration's pass A, so wait for that iteration's event)
@@ -727,8 +751,8 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
     // the residual-sum stage of the batch's last iteration (folded runs), then the state back
     // into slot 0 for the next batch and the other entry points
     if (fold && n > 0)
-      PB_TRY(cg_sr_finalize(ctx, k->sr_nparts, k->d_st + (n & 1), k->d_hist, k->h_done_dev,
-                            k->host_iter - 1));
+      PB_TRY(cg_sr_finalize(ctx, sr_region(ctx, n - 1), k->sr_nparts, k->d_st + (n & 1),
+                            k->d_hist, k->h_done_dev, k->host_iter - 1));
     if (n & 1)
       PB_HIP(hipMemcpyAsync(k->d_st, k->d_st + 1, sizeof(CgState), hipMemcpyDeviceToDevice,
                             ctx->stream));

@@ -23,7 +23,7 @@
 //     ghost copy is made on one rank.
 // Summation order per point matches the reference dot product with its zero terms dropped:
 // z-, y-, x-, centre, x+, y+, z+ (built with -ffp-contract=off => bit-identical to the oracle).
-#include "pb_device.hpp"
+#include "pb_cg_device.hpp"
 
 namespace pb {
 
@@ -116,15 +116,15 @@ struct PassAT {
   static constexpr int WGCU = STORE ? 3 : 1;        // (4-row tiles; 1 with 8 rows)
   static constexpr bool CAP = !STORE, WIDE8 = !STORE;
   static constexpr bool PREFETCH = true;
+  // (p stores non-temporal like every engine output: cached stores, which pass B could re-read
+  // from the Infinity Cache, measured within noise, profiles/r01/ab_passa_nt.txt)
   double* __restrict__ p_new;
-  int nt_p;  // non-temporal p stores (PB_PASSA_NT, default on; cached stores, which pass B could
-             // re-read from the Infinity Cache, measured within noise: profiles/r01/ab_passa_nt.txt)
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ const double* src(int) const { return nullptr; }
   template <int V>
   __device__ __forceinline__ void put(RowIx idx, const double (&c)[V], const double (&w)[V],
                                       double (&)[1][V], double* acc, int nt) const {
-    if constexpr (STORE) store_row<V>(p_new, idx, c, nt && nt_p);
+    if constexpr (STORE) store_row<V>(p_new, idx, c, nt);
 #pragma unroll
     for (int e = 0; e < V; ++e) acc[0] += w[e] * c[e];
   }
@@ -259,10 +259,9 @@ struct ZLoad {
     return z + shift;
   }
 };
-template <bool TALLV>
-struct SrSumsT {
+struct SrSums {
   static constexpr int NS = 5, NE = 1;
-  static constexpr bool RAW = false, TALL = TALLV;
+  static constexpr bool RAW = false;
   static constexpr int WGCU = 1;
   static constexpr bool CAP = true, WIDE8 = true;
   static constexpr bool PREFETCH = true;
@@ -285,28 +284,6 @@ struct SrSumsT {
   }
 };
 
-// ---------------------------------------------------------------------------------------------
-// Finalize folded into the next pass's prologue (one rank, Jacobi CG): EVERY WAVE reduces the
-// previous pass's partials in the finalize kernel's fixed order (lane-strided sums, xor
-// butterfly: bit-identical in every lane) and runs the PETSc scalar step (stage 1 before pass B,
-// stage 2 of the previous iteration before pass A) on a register copy of the state -- no LDS, no
-// barrier; lane 0 of block 0 stores the result into the OTHER state slot, so the slot this launch
-// reads is never written while it runs. Removes the two finalize launches (and their kernel
-// boundaries) from every iteration.
-// ---------------------------------------------------------------------------------------------
-struct Fold {
-  // 0: no fold; 1: stage 1 (pass B); 2: stage 2 (pass A); single-reduction pass P: 3: the
-  // residual-sum stage of the previous iteration, then the top of this one; 4: the top only
-  int stage = 0;
-  int nparts = 0, width = 1;      // partials of the previous pass
-  const double* parts = nullptr;
-  const CgState* in = nullptr;    // state slot read
-  CgState* out = nullptr;         // state slot written (block 0)
-  double* hist = nullptr;         // stage 2: history / host-mapped done flags, as finalize's
-  int* h_done = nullptr;
-  int64_t host_iter = 0;          // stage 2: the iteration whose stage 2 this is
-};
-__device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st);
 
 // Epi::qop(a) (optional): operand a is raw z-queue array qop(a) of the centre plane (-1: loaded)
 template <class E, class = void>
@@ -613,7 +590,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 // exchange of a multi-rank step overlap the interior.
 static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   Geo geo;
-  geo.rev = tune("zalt", 1) ? rev : 0;
+  geo.rev = rev;
   geo.k0 = (int)g->k0;
   geo.wrap = 0;
   geo.nx = (int)g->n[0];
@@ -621,8 +598,8 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   geo.nzl = (int)g->nzl;
   geo.plane = g->plane;
   geo.ty = TY;
-  geo.remap = tune("xcd_remap", 1);
-  geo.nt = tune("stencil_nt", 1);
+  geo.remap = 1;  // XCD-aware block remap
+  geo.nt = 1;     // non-temporal output stores
   geo.nsegx = (geo.nx + 64 * V - 1) / (64 * V);
   geo.ntile = (geo.ny + kWaves * TY - 1) / (kWaves * TY);
   if (mode == PLANES_BOUNDARY) {
@@ -640,13 +617,13 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   // wgcu (the epilogue's WGCU) workgroups per CU: long z-chunks, few chunk-boundary re-reads.
   // Measured at 512^3: 3 per CU for the matvec and pass A (768 blocks beat 512 even where the
   // registers allow only 2 resident), 1 per CU for pass B
-  int target = tune("stencil_blocks", wgcu * g->ctx->num_cus);
+  int target = wgcu * g->ctx->num_cus;
   int nchunk = (target + columns - 1) / columns;
-  // z-chunks shorter than PB_STENCIL_KCMIN (64) planes re-read too many boundary planes (2 per
+  // z-chunks shorter than 64 planes re-read too many boundary planes (2 per
   // chunk): use fewer, longer chunks, but keep at least one workgroup per CU (256^3: 8 chunks of
   // 32 planes instead of 24 of 11, measured 8-15 % faster)
-  const int kcmin = tune("stencil_kcmin", 64);
-  if (!tune_is_set("stencil_blocks") && kcmin > 0 && nk / nchunk < kcmin) {
+  const int kcmin = 64;
+  if (nk / nchunk < kcmin) {
     const int floor_cu = (g->ctx->num_cus + columns - 1) / columns;
     nchunk = std::max(nk / kcmin, floor_cu);
   }
@@ -659,8 +636,6 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
 }
 
 static int pick_ty(int ny) {
-  int forced = tune("stencil_ty", 0);
-  if ((forced == 1 || forced == 2 || forced == 4) && ny % forced == 0) return forced;
   if (ny % 4 == 0) return 4;
   if (ny % 2 == 0) return 2;
   return 1;
@@ -742,17 +717,13 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
   if constexpr (Wide8Of<Epi>::v) {
     const int64_t cols4 = ((g->n[0] + 127) / 128) * ((g->n[1] + kWaves * 4 - 1) / (kWaves * 4));
     const int w = wgcu > 0 ? wgcu : Epi::WGCU;
-    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && !tune_is_set("stencil_ty") &&
-        cols4 > (int64_t)w * g->ctx->num_cus)
+    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && cols4 > (int64_t)w * g->ctx->num_cus)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
   }
   if constexpr (TallOf<Epi>::v) {
-    const int tall = tune("stencil_tall", 1);  // read per launch (A/B tuning)
-    const int64_t tall_min = tune("stencil_tall_min_plane", 512 * 512);
-    if (vec2 && ty == 4 && tall && !tune_is_set("stencil_ty") && g->n[1] % 8 == 0 &&
-        g->plane >= tall_min)
+    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && g->plane >= 512 * 512)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev,
-                            wgcu > 0 ? wgcu : tune("tall_wgcu", 1), fold);
+                            wgcu > 0 ? wgcu : 1, fold);
   }
   if (vec2) {
     switch (ty) {
@@ -951,197 +922,6 @@ __global__ __launch_bounds__(256) void cg_boundary_kernel(const double* __restri
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// CG scalar logic (PETSc KSPSolve_CG + KSPConvergedDefault), shared by the finalize kernel and
-// the folded pass prologues
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool finite(double v) { return v == v && v - v == 0.0; }
-
-// partial counts up to which the finalize kernel reduces with one wave in this order (the CG
-// passes: one workgroup per CU); beyond it, a 256-thread tree (a lone wave took 29 us over the
-// 2048 partials of the elementwise kernels of the preconditioned CG)
-static constexpr int kFoldMaxParts = 1024;
-static constexpr int kMaxSums = 5;  // partial sums per block (single-reduction pass S: 5)
-// fixed-order reduction of nparts x width partials by ONE wave: lane l sums blocks l, l+64, ...
-// in order, then an xor butterfly (every lane ends with the same bits). Used by the finalize
-// kernel (wave 0) and by every wave of a folded pass prologue, so both paths round alike.
-__device__ __forceinline__ void wave_reduce_parts(const double* __restrict__ parts, int nparts,
-                                                  int width, double* S) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int s = 0; s < kMaxSums; ++s) {
-    double v = 0.0;
-    if (s < width)
-      for (int b = lane; b < nparts; b += 64) v += parts[(int64_t)b * width + s];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    S[s] = v;
-  }
-}
-
-// stage 0 (after init / the first PC apply): S = (sum t, sum t^2, sum t.r, sum r)
-__device__ __forceinline__ void cg_stage0(CgState& st, const double* S, double* hist,
-                                          int* h_done) {
-  const double N = st.ntot;
-  double mu = 0.0, zz = S[1], zr = S[2];
-  if (st.nullspace) {
-    const double delta = S[0] / N;
-    mu = delta;
-    zz = S[1] - N * delta * delta;
-    zr = S[2] - delta * S[3];
-  }
-  const double dp = sqrt(zz > 0.0 ? zz : 0.0);
-  st.mu = mu;
-  st.dp = dp;
-  st.rnorm0 = dp;
-  st.it = 0;
-  st.its = 0;
-  st.dpi = 0.0;
-  st.alpha = 0.0;
-  st.alpha_prev = 0.0;
-  st.pend_iter = -1;
-  st.pend_count = 0;
-  st.reason = 0;
-  st.done = 0;
-  if (st.nhist > 0 && hist) hist[0] = dp;
-  st.nlog = st.nhist > 0 ? 1 : 0;
-  if (!finite(dp)) {
-    st.reason = PB_KSP_DIVERGED_NANORINF;
-    st.done = 1;
-  } else {
-    st.ttol = fmax(st.rtol * dp, st.atol);
-    if (dp <= st.ttol) {
-      st.reason = dp < st.atol ? PB_KSP_CONVERGED_ATOL : PB_KSP_CONVERGED_RTOL;
-      st.done = 1;
-    } else {
-      st.beta = zr;
-      if (!finite(zr)) {
-        st.reason = PB_KSP_DIVERGED_NANORINF;
-        st.done = 1;
-      } else if (zr == 0.0) {
-        st.its = 1;
-        st.reason = PB_KSP_CONVERGED_ATOL;
-        st.done = 1;
-      } else if (st.max_it <= 0) {
-        st.reason = PB_KSP_DIVERGED_ITS;
-        st.done = 1;
-      }
-    }
-  }
-  if (h_done) h_done[0] = st.done;
-}
-
-// stage 1 (after pass A): dpi = p.w -> alpha, or an INDEFINITE_MAT / NaN exit
-__device__ __forceinline__ void cg_stage1(CgState& st, double dpi) {
-  if (st.done) return;
-  const int64_t i = st.it;
-  const double sp = (double)((dpi > 0) - (dpi < 0)), so = (double)((st.dpi > 0) - (st.dpi < 0));
-  if (!finite(dpi)) {
-    st.its = i + 1;
-    st.reason = PB_KSP_DIVERGED_NANORINF;
-    st.done = 1;
-  } else if (dpi == 0.0 || (i > 0 && sp * so < 0.0)) {
-    st.its = i + 1;
-    st.reason = PB_KSP_DIVERGED_INDEFINITE_MAT;
-    st.done = 1;
-  } else {
-    st.dpiold = st.dpi;
-    st.dpi = dpi;
-    st.bbp = i == 0 ? 0.0 : st.beta / st.betaold;  // CombineLoad's bb of this pass A
-    st.betaold = st.beta;
-    st.alpha_prev = st.alpha;
-    st.alpha = st.beta / dpi;
-  }
-}
-
-// iterations i % D < D-1 leave alpha_i p_i pending in x; the last of each D applied them all
-// (PassB<XU>)
-__device__ __forceinline__ void cg_pend(CgState& st) {
-  const int64_t i = st.it;
-  const int D = st.defer_x;
-  const int m = D > 0 ? (int)(i % D) : 0;
-  if (D > 0 && m < D - 1) {
-    // (value selects, no computed index: st may be a register copy)
-    st.pa[0] = m == 0 ? st.alpha : st.pa[0];
-    st.pa[1] = m == 1 ? st.alpha : st.pa[1];
-    st.pa[2] = m == 2 ? st.alpha : st.pa[2];
-    st.pend_iter = i - m;
-    st.pend_count = m + 1;
-  } else {
-    st.pend_iter = -1;
-    st.pend_count = 0;
-  }
-}
-
-// stage 2 (after pass B / the PC apply): residual sums -> norm, convergence tests, next beta
-__device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* hist, int* h_done,
-                                          int64_t host_iter) {
-  if (!st.done) {
-    const double N = st.ntot;
-    const int64_t i = st.it;
-    double mu = st.mu, zz = S[1], zr = S[2];
-    if (st.nullspace) {
-      const double delta = S[0] / N;
-      mu = st.mu + delta;
-      zz = S[1] - N * delta * delta;
-      zr = S[2] - delta * S[3];
-    }
-    const double dp = sqrt(zz > 0.0 ? zz : 0.0);
-    // (single reduction: alpha_i was booked by cg_sr_top, before pass P applied it)
-    if (!st.sr) cg_pend(st);
-    st.dp = dp;
-    st.its = i + 1;
-    if (i + 1 < st.nhist) {
-      if (hist) hist[i + 1] = dp;
-      st.nlog = i + 2;
-    }
-    if (!finite(dp)) {
-      st.reason = PB_KSP_DIVERGED_NANORINF;
-      st.done = 1;
-    } else if (dp <= st.ttol) {
-      st.reason = dp < st.atol ? PB_KSP_CONVERGED_ATOL : PB_KSP_CONVERGED_RTOL;
-      st.done = 1;
-    } else if (dp >= st.dtol * st.rnorm0) {
-      st.reason = PB_KSP_DIVERGED_DTOL;
-      st.done = 1;
-    } else {
-      st.beta = zr;
-      st.mu = mu;
-      st.delta = S[4];  // (single reduction: z'A z, read by the next cg_sr_top)
-      st.it = i + 1;
-      if (!finite(zr)) {
-        st.reason = PB_KSP_DIVERGED_NANORINF;
-        st.done = 1;
-      } else if (st.it >= st.max_it) {
-        st.reason = PB_KSP_DIVERGED_ITS;
-        st.done = 1;
-      } else if (zr == 0.0) {
-        st.its = st.it + 1;
-        st.reason = PB_KSP_CONVERGED_ATOL;
-        st.done = 1;
-      } else if (zr * st.betaold < 0.0) {
-        // PETSc KSPSolve_CG, top of iteration i+1 (real scalars): beta*betaold < 0 -> the
-        // preconditioner is indefinite (betaold = the beta iteration i used, stage 1)
-        st.its = st.it + 1;
-        st.reason = PB_KSP_DIVERGED_INDEFINITE_PC;
-        st.done = 1;
-      }
-    }
-  }
-  if (h_done) h_done[host_iter + 1] = st.done;
-}
-
-// Top of a single-reduction iteration (PETSc KSPSolve_CG_SingleReduction, real scalars): the
-// beta checks ran with the residual-sum stage (cg_stage0 / cg_stage2, as in KSPSolve_CG); here
-// p'w = delta (i = 0: p = z, w = A z) or delta - beta^2 dpiold / betaold^2, then stage 1's
-// INDEFINITE_MAT / NaN exits and alpha, and alpha_i's deferred-x bookkeeping (pass P applies it)
-__device__ __forceinline__ void cg_sr_top(CgState& st) {
-  if (st.done) return;
-  const double dpi = st.it == 0 ? st.delta
-                                : st.delta - st.beta * st.beta * st.dpi / (st.betaold * st.betaold);
-  cg_stage1(st, dpi);
-  if (!st.done) cg_pend(st);
-}
 
 // Finalize: deterministic fixed-order reduction of the per-block partials, then the PETSc CG
 // scalar logic (KSPSolve_CG + KSPConvergedDefault) on the device. mode bit 1 = reduce partials
@@ -1184,53 +964,23 @@ __global__ __launch_bounds__(256) void cg_finalize_kernel(const double* __restri
   else st->delta = S[4];  // 3: the single-reduction setup's delta = z0'A z0
 }
 
-// field-wise copy (an aggregate copy becomes a memcpy that pins the register copy in scratch)
-__device__ __forceinline__ void cg_copy(CgState& d, const CgState& s) {
-  d.beta = s.beta, d.betaold = s.betaold, d.dpi = s.dpi, d.dpiold = s.dpiold;
-  d.alpha = s.alpha, d.alpha_prev = s.alpha_prev, d.mu = s.mu, d.dp = s.dp, d.ttol = s.ttol;
-  d.rnorm0 = s.rnorm0, d.pa[0] = s.pa[0], d.pa[1] = s.pa[1], d.pa[2] = s.pa[2];
-  d.rtol = s.rtol, d.atol = s.atol, d.dtol = s.dtol, d.dinv = s.dinv, d.ntot = s.ntot;
-  d.it = s.it, d.its = s.its, d.max_it = s.max_it, d.nhist = s.nhist, d.pend_iter = s.pend_iter;
-  d.pend_count = s.pend_count, d.nlog = s.nlog;
-  d.reason = s.reason, d.done = s.done, d.pc = s.pc, d.nullspace = s.nullspace;
-  d.defer_x = s.defer_x;
-  d.bbp = s.bbp;
-  d.delta = s.delta, d.sr = s.sr;
-}
-static_assert(sizeof(CgState) == 248, "cg_copy lists every CgState field");
-
-__device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st) {
-  double S[kMaxSums];
-  cg_copy(st, *f.in);
-  // (garbage if done: the stages ignore it)
-  if (f.stage != 4) wave_reduce_parts(f.parts, f.nparts, f.width, S);
-  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-  if (f.stage == 1) {
-    cg_stage1(st, S[0]);
-  } else if (f.stage == 2) {
-    cg_stage2(st, S, lead ? f.hist : nullptr, lead ? f.h_done : nullptr, f.host_iter);
-  } else {
-    if (f.stage == 3)
-      cg_stage2(st, S, lead ? f.hist : nullptr, lead ? f.h_done : nullptr, f.host_iter);
-    cg_sr_top(st);
-  }
-  if (lead) cg_copy(*f.out, st);
-}
 
 static int cg_reduce_update(pb_ctx* ctx, int stage, int nparts, int width, CgState* st,
-                            double* hist, int* h_done, int64_t host_iter) {
+                            double* hist, int* h_done, int64_t host_iter,
+                            const double* parts = nullptr) {
   double* sums = ctx->d_scalars;
+  if (!parts) parts = ctx->d_partials;
   if (!ctx->split) {
-    hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+    hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, parts,
                        nparts, width, sums, 3, stage, st, hist, h_done, host_iter);
     PB_HIP(hipGetLastError());
     return PB_OK;
   }
-  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, parts,
                      nparts, width, sums, 1, stage, st, hist, h_done, host_iter);
   PB_HIP(hipGetLastError());
   PB_TRY(allreduce_device(ctx, sums, width));
-  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, ctx->d_partials,
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, parts,
                      nparts, width, sums, 2, stage, st, hist, h_done, host_iter);
   PB_HIP(hipGetLastError());
   return PB_OK;
@@ -1270,11 +1020,10 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
                      int* nblocks, bool store) {
   ScopedTimer tm(g->ctx,
                  timer_name(mode, "cg_pass_a", "cg_pass_a_interior", "cg_pass_a_boundary"));
-  const int nt_p = tune("passa_nt", 1);  // read per launch (A/B tuning)
   const CombineLoad ld{r, p_old, st, 0.0, 0.0, 0.0};
   if (!store)
-    return launch_any(g, s, ld, gp, PassAT<false>{p_new, nt_p}, &st->done, mode, part_off, nblocks);
-  return launch_any(g, s, ld, gp, PassA{p_new, nt_p}, &st->done, mode, part_off, nblocks);
+    return launch_any(g, s, ld, gp, PassAT<false>{p_new}, &st->done, mode, part_off, nblocks);
+  return launch_any(g, s, ld, gp, PassA{p_new}, &st->done, mode, part_off, nblocks);
 }
 
 // Folded iteration (one rank, Jacobi): partial sums of pass A at block 0, of pass B at
@@ -1297,12 +1046,11 @@ int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const do
   f.hist = hist;
   f.h_done = h_done;
   f.host_iter = host_iter - 1;  // stage 2 of the previous iteration
-  const int nt_p = tune("passa_nt", 1);
   const CombineLoad ld{r, p_old, nullptr, 0.0, 0.0, 0.0};
   if (!store)
-    return launch_any(g, s, ld, gp, PassAT<false>{p_new, nt_p}, nullptr, PLANES_ALL, 0, nblocks, 0,
+    return launch_any(g, s, ld, gp, PassAT<false>{p_new}, nullptr, PLANES_ALL, 0, nblocks, 0,
                       0, f);
-  return launch_any(g, s, ld, gp, PassA{p_new, nt_p}, nullptr, PLANES_ALL, 0, nblocks, 0, 0, f);
+  return launch_any(g, s, ld, gp, PassA{p_new}, nullptr, PLANES_ALL, 0, nblocks, 0, 0, f);
 }
 
 int cg_finalize_init(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done) {
@@ -1430,7 +1178,7 @@ int launch_cg_sr_pass_p(pb_grid* g, const Star& s, const double* r, const double
   f.stage = sf.fold_sums ? 3 : 4;
   f.nparts = sf.nparts_s;
   f.width = 5;
-  f.parts = g->ctx->d_partials;
+  f.parts = sf.parts ? sf.parts : g->ctx->d_partials;
   f.in = sf.in;
   f.out = sf.out;
   f.hist = sf.hist;
@@ -1460,18 +1208,15 @@ int launch_cg_sr_pass_s(pb_grid* g, const Star& s, const double* r, const Stenci
                         const CgState* st, int mode, int part_off, int* nblocks) {
   ScopedTimer tm(g->ctx, timer_name(mode, "cg_sr_s", "cg_sr_s_interior", "cg_sr_s_boundary"));
   // (marches upwards after pass P marched downwards: it starts on the planes P wrote last)
-  const int shape = tune("sr_s_shape", 0);
-  const int wg = shape == 1 ? 2 : (shape == 2 ? 3 : (shape == 4 ? 2 : (shape == 5 ? 3 : 0)));
-  if (shape >= 3)
-    return launch_any(g, s, ZLoad{r, st}, gp, SrSumsT<true>{}, &st->done, mode, part_off,
-                      nblocks, 0, wg);
-  return launch_any(g, s, ZLoad{r, st}, gp, SrSumsT<false>{}, &st->done, mode, part_off, nblocks,
-                    0, wg);
+  // 4-row tiles, two workgroups per CU (a single read-only stream: 0.218-0.221 ms at 512^3 against
+  // 0.247 with one per CU, 0.223-0.228 with three, 0.224 with 8-row tiles; gpurun_out sr2/sr3)
+  return launch_any(g, s, ZLoad{r, st}, gp, SrSums{}, &st->done, mode, part_off, nblocks, 0, 2);
 }
 
-int cg_sr_finalize(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done,
-                   int64_t host_iter, bool stage_delta0) {
-  return cg_reduce_update(ctx, stage_delta0 ? 3 : 2, nparts, 5, st, hist, h_done, host_iter);
+int cg_sr_finalize(pb_ctx* ctx, const double* parts, int nparts, CgState* st, double* hist,
+                   int* h_done, int64_t host_iter, bool stage_delta0) {
+  return cg_reduce_update(ctx, stage_delta0 ? 3 : 2, nparts, 5, st, hist, h_done, host_iter,
+                          parts);
 }
 
 // x += alpha * p (the pending half of the deferred solution update)

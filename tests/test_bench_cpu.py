@@ -15,15 +15,6 @@ def test_cg_iter_bytes():
     assert bench.cg_iter_bytes(4) == 56
     assert bench.cg_iter_bytes(2) == 56
     assert bench.cg_iter_bytes(0) == 64
-    # p stored by pass A (PB_CG_PSTORE_B=0): 24 + (3 * 24 + 64) / 4
-    assert bench.cg_iter_bytes(4, 0) == 58
-    assert bench.cg_iter_bytes(0, 0) == 64
-
-
-def test_pstore_mode_setting():
-    assert bench.pstore_mode() == 1          # cg_pstore_b unset: the library default
-    assert bench.pstore_mode(1) == 1
-    assert bench.pstore_mode(0) == 0
 
 
 def test_host_info_fields():

@@ -298,48 +298,6 @@ def test_cg_folded_finalize_bit_identical(ctx, case, tune):
     check_history(h1, ho)
 
 
-@pytest.mark.parametrize("n3", [(64, 32, 16), (512, 512, 8)])
-@pytest.mark.parametrize("fold", ["1", "0"])
-@pytest.mark.parametrize("defer", ["4", "2", "0"])
-def test_cg_pass_b_pstore_bit_identical(ctx, n3, fold, defer, tune):
-    """PB_CG_PSTORE_B=1: pass A only takes p.Ap, pass B re-forms p from (r, p_old), stores it and
-    writes the residual into a second buffer. Same arithmetic per value, so reason, iteration count,
-    history and x are bit-identical to the default split (p stored by pass A), with and without
-    the folded finalize and at every x-update deferral depth. On planes of >= 512^2 points the
-    storing pass A runs 8-row tiles and the read-only one 4-row tiles with one workgroup per CU:
-    other blocks, so p.Ap is summed in another order -- there the two runs agree to rounding
-    (history 1e-12) instead of bit for bit. Checked against the oracle as well."""
-    N = int(np.prod(n3))
-    h = tuple(1.0 / m for m in n3)
-    b = O.stencil(O.fill_random(N, SEED), n3, h)
-    opts = ["-ksp_rtol", "1e-9", "-ksp_max_it", "60"]
-    tune.setenv("PB_CG_FOLD", fold)
-    tune.setenv("PB_CG_DEFER_X", defer)
-    out = {}
-    for pst in ("1", "0"):
-        tune.setenv("PB_CG_PSTORE_B", pst)
-        da = pb.DA(ctx, n3)
-        P, A, x, bv = pb.initialise_linear_system(da, h)
-        bv.set_values(b)
-        k = pb.KSP(A, P, pb.ksp_options(opts))
-        k.begin(bv, x)
-        k.iterate(5)   # odd split: the residual buffers swap parity across calls
-        k.iterate(1000)
-        reason, its, hist = k.end()
-        k.destroy()
-        out[pst] = (reason, its, np.asarray(hist), x.get_values())
-    (r1, i1, h1, x1), (r0, i0, h0, x0) = out["1"], out["0"]
-    assert (r1, i1) == (r0, i0)
-    if n3[0] * n3[1] < 512 * 512:
-        assert np.array_equal(h1, h0) and np.array_equal(x1, x0)
-    else:
-        assert np.max(np.abs(h1 - h0) / h0) < 1e-12
-        check_x(x1, x0, bar=1e-12)
-    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-9, max_it=60)
-    assert (r1, i1) == (ro, itso)
-    check_history(h1, ho)
-
-
 def test_cg_zero_rhs_converges_immediately(ctx):
     n3 = (8, 8, 8)
     da = pb.DA(ctx, n3)
@@ -728,30 +686,16 @@ def test_cg_with_compact_operator(ctx):
 # restatement of the same V-cycle (bit-exact PC apply), CG histories within HIST_RTOL
 # ---------------------------------------------------------------------------------------------
 # kernel selections of the V-cycle (all bit-identical): default thresholds (small test grids run
-# the per-pair kernels), and every level forced onto the stencil-engine SOR/residual kernels and
-# the z-marching restriction / prolongation; the per-coarse-cell and per-fine-pair prolongations
+# the per-pair kernels), every level forced onto the stencil-engine SOR / residual kernels and the
+# z-marching restriction / prolongation, and every level on the per-pair / per-cell kernels
 MG_KERNELS = {"default": {},
               "engine": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
-              "cell": {"PB_MG_PROLONG_CELL": "1", "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
-              "legacy": {"PB_MG_ENGINE_MIN_PLANE": "1000000000", "PB_MG_RESTRICT_Z": "0",
-                         "PB_MG_PROLONG_CELL": "0"},
-              "unfused": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_SWEEP2": "0",
-                          "PB_MG_PRESMOOTH_FUSED": "0"},
-              # per-level launches for the coarse tail, and the pre-r02 pre-smoothing kernel
-              "notail": {"PB_MG_TAIL": "0", "PB_MG_PRESMOOTH_SLIM": "0"},
+              "legacy": {"PB_MG_ENGINE_MIN_PLANE": "1000000000",
+                         "PB_MG_RESTRICT_Z_MIN_COLS": "1000000000"},
+              # half-sweeps and residual as separate engine passes (no fused sweeps)
+              "unfused": {"PB_MG_ENGINE_MIN_PLANE": "0", "PB_MG_SWEEP2": "0"},
               # a longer one-launch tail (every level up to 32^3)
               "bigtail": {"PB_MG_TAIL_MAX": "40000"},
-              # prolongation and post-smoothing as two launches (the pre-r02 up-leg)
-              "nopost": {"PB_MG_POST_FUSED": "0", "PB_MG_ENGINE_MIN_PLANE": "0",
-                         "PB_MG_RESTRICT_Z_MIN_COLS": "0"},
-              # residual stored and restricted by its own pass (the pre-r02 down-leg)
-              "norestrict": {"PB_MG_PRESMOOTH_RESTRICT": "0", "PB_MG_ENGINE_MIN_PLANE": "0"},
-              # short chunks: more z-chunk seams in the fused restriction
-              "prrchunks": {"PB_PRR_WGCU": "64", "PB_PRR_MINZ": "2",
-                            "PB_PRRX_WGCU": "64", "PB_PRRX_MINZ": "2",
-                            "PB_MG_ENGINE_MIN_PLANE": "0"},
-              # the per-wave fused sweeps (before rows were shared through LDS, r03)
-              "perwave": {"PB_PRRX": "0", "PB_POSTX": "0", "PB_MG_ENGINE_MIN_PLANE": "0"},
               # decomposed grids: coarse levels with halo exchanges instead of gathered onto
               # every rank (the pre-r04 N > 1 path)
               "noagg": {"PB_MG_AGGLOMERATE": "0"},
@@ -828,8 +772,7 @@ def test_cg_sor_mg_matches_oracle(ctx, kern, pc, n, tune):
         assert its <= 16  # h-independent V-cycle preconditioning
 
 
-@pytest.mark.parametrize("kern", ["default", "engine", "legacy", "unfused", "nopost",
-                                  "norestrict"])
+@pytest.mark.parametrize("kern", ["default", "engine", "legacy", "unfused"])
 def test_cg_mg_fused_post_smoothing(ctx, kern, tune):
     """x extent >= 128: the V-cycle's post-smoothing runs as ONE fused two-colour pass (out of
     place, with CG's residual sums on level 0); history / solution within the CG bar, PC apply
@@ -858,20 +801,18 @@ def test_cg_mg_fused_post_smoothing(ctx, kern, tune):
     k.destroy()
 
 
-# fused post-smoothing kernels: rows shared between the waves of a block through LDS
-# (PB_POSTX 1, 2 = 8 waves x 4 / x 2 rows; 3, 4 the same with the plane loop unrolled by four) and
-# the per-wave kernel (0); y extents that are no multiple of a block's stored rows (28 / 12), one
-# smaller than a block (8 rows: the block's rows wrap several times), four planes (the unrolled
-# kernels' spare planes wrap around the grid more than once), plane counts that are no multiple
-# of the unrolled loop's four (6, 12), and the full-size test's 256^2 planes
+# the fused pre-smoothing + residual + restriction and prolongation + post-smoothing passes (rows
+# shared between the waves of a block through LDS, plane loop unrolled by four) on every level: y
+# extents that are no multiple of a block's stored rows (24 / 28), one smaller than a block (8
+# rows: the block's rows wrap several times), four planes (the unrolled kernels' spare planes
+# wrap around the grid more than once), plane counts that are no multiple of the unrolled loop's
+# four (6, 12), and the full-size test's 256^2 planes
 POSTX_SHAPES = [(256, 256, 32), (128, 40, 16), (256, 8, 8), (128, 96, 24), (256, 16, 4),
                 (128, 24, 6), (256, 16, 12)]
 
 
-@pytest.mark.parametrize("postx", ["0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("n3", POSTX_SHAPES)
-def test_mg_post_sweep_variants_bit_exact(ctx, postx, n3, tune):
-    tune.setenv("PB_POSTX", postx)
+def test_mg_fused_passes_bit_exact(ctx, n3, tune):
     tune.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
     tune.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
     N = int(np.prod(n3))
@@ -888,44 +829,13 @@ def test_mg_post_sweep_variants_bit_exact(ctx, postx, n3, tune):
     k.destroy()
 
 
-@pytest.mark.parametrize("prrx", ["0", "1", "2"])
-@pytest.mark.parametrize("chunks", [False, True])
-@pytest.mark.parametrize("n3", POSTX_SHAPES)
-def test_mg_presmooth_restrict_variants_bit_exact(ctx, prrx, chunks, n3, tune):
-    """Fused pre-smoothing + residual + restriction: rows shared through LDS (PB_PRRX 1 = 8
-    waves x 4 rows, 2 = the same with the plane loop unrolled by four) and the per-wave kernel
-    (0); short z chunks put chunk seams inside the restriction's plane pairs' neighbourhood."""
-    tune.setenv("PB_PRRX", prrx)
-    tune.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
-    tune.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
-    if chunks:
-        for k_ in ("PB_PRR_WGCU", "PB_PRRX_WGCU"):
-            tune.setenv(k_, "64")
-        for k_ in ("PB_PRR_MINZ", "PB_PRRX_MINZ"):
-            tune.setenv(k_, "2")
-    N = int(np.prod(n3))
-    h = tuple(1.0 / m for m in n3)
-    r = O.fill_random(N, 6)
-    ref = O.mg_apply(r, n3, h, pc="mg")
-    da = pb.DA(ctx, n3)
-    P, A, _, _ = pb.initialise_linear_system(da, h)
-    k = pb.KSP(A, P, pb.ksp_options(["-pc_type", "mg"]))
-    rv, zv = pb.Vec(da), pb.Vec(da)
-    rv.set_values(r)
-    k.pc_apply(rv, zv)
-    assert np.array_equal(zv.get_values(), ref)
-    k.destroy()
-
-
 @pytest.mark.parametrize("split", [1, 2, 7, 64])
 @pytest.mark.parametrize("n3", POSTX_SHAPES)
 def test_mg_u4_balanced_split_bit_exact(ctx, split, n3, tune):
-    """The unrolled fused passes with the balanced work split (prrx_split / postx_split =
-    workgroups per CU): the columns' planes cut into equal pieces, so one workgroup may run the
+    """The unrolled fused passes with the balanced work split (mg_u4_split = workgroups per CU): the columns' planes cut into equal pieces, so one workgroup may run the
     end of one column and the start of the next, or several columns (64 per CU: pieces of 2 or 4
     planes, shorter than the passes' warm-up) -- PC apply bit-identical to the oracle."""
-    tune.set("prrx_split", split)
-    tune.set("postx_split", split)
+    tune.set("mg_u4_split", split)
     tune.set("mg_engine_min_plane", 0)
     tune.set("mg_restrict_z_min_cols", 0)
     N = int(np.prod(n3))
@@ -942,15 +852,12 @@ def test_mg_u4_balanced_split_bit_exact(ctx, split, n3, tune):
     k.destroy()
 
 
-@pytest.mark.parametrize("postx,split", [("1", 0), ("2", 0), ("3", 0), ("4", 0), ("3", 1),
-                                         ("3", 7)])
-def test_cg_mg_post_sweep_xch_sums(ctx, postx, split, tune):
+@pytest.mark.parametrize("split", [0, 1, 7])
+def test_cg_mg_post_sweep_xch_sums(ctx, split, tune):
     """The LDS-shared post-smoothing also takes CG's residual sums on level 0 (a partial per
     block; split > 0: a partial per balanced-split workgroup, whatever ranges it ran): CG + MG
     history / solution within the CG bar."""
-    tune.setenv("PB_POSTX", postx)
-    tune.set("postx_split", split)
-    tune.set("prrx_split", split)
+    tune.set("mg_u4_split", split)
     tune.setenv("PB_MG_ENGINE_MIN_PLANE", "0")
     tune.setenv("PB_MG_RESTRICT_Z_MIN_COLS", "0")
     n3 = (128, 96, 24)
