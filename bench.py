@@ -65,6 +65,7 @@ def cg_iter_bytes(defer, pstore=1):
         return pb_["a"] + pb_["b_x"][0]
     return pb_["a"] + ((defer - 1) * pb_["b_even"] + pb_["b_x"][defer]) / defer
 SEED = 20231015
+SECONDARY_TIMEOUT_STATUS = 3  # exit status when the secondary workloads' watchdog fires
 
 
 def nloc_even(n):
@@ -506,7 +507,8 @@ def run_secondary(args, pb, ctx, rank, world, dist, comm_transport, comm_nranks,
     (compact-fft, 512^3 strong-scaled) and star7-mg -- so every N of a scaling run records them
     beside the headline, under "secondary". A watchdog bounds them (PB_BENCH_SECONDARY_TIMEOUT_S,
     default 240 s): if they do not finish, rank 0 prints the headline line with the error and the
-    process exits, so a secondary can never cost the headline measurement."""
+    process exits with status SECONDARY_TIMEOUT_STATUS (3), so a secondary can never cost the
+    headline measurement and a launcher still sees the failure."""
     import threading
     limit = float(os.environ.get("PB_BENCH_SECONDARY_TIMEOUT_S", "240"))
     done = threading.Event()
@@ -518,9 +520,9 @@ def run_secondary(args, pb, ctx, rank, world, dist, comm_transport, comm_nranks,
             o = dict(holder["out"])
             o.setdefault("secondary", {})["error"] = f"timed out after {limit:.0f} s"
             os.write(json_fd, (json.dumps(o) + "\n").encode())
-        print(f"bench: secondary workloads timed out after {limit:.0f} s; exiting", file=sys.stderr,
-              flush=True)
-        os._exit(0)
+        print(f"bench: secondary workloads timed out after {limit:.0f} s; exiting with status "
+              f"{SECONDARY_TIMEOUT_STATUS}", file=sys.stderr, flush=True)
+        os._exit(SECONDARY_TIMEOUT_STATUS)  # (not 0; the headline line is out)
 
     timer = threading.Timer(limit, fire)
     timer.daemon = True

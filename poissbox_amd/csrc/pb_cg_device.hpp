@@ -208,18 +208,7 @@ __device__ __forceinline__ void cg_sr_top(CgState& st) {
 // reads is never written while it runs. Removes the two finalize launches (and their kernel
 // boundaries) from every iteration.
 // ---------------------------------------------------------------------------------------------
-struct Fold {
-  // 0: no fold; 1: stage 1 (pass B); 2: stage 2 (pass A); single-reduction pass P: 3: the
-  // residual-sum stage of the previous iteration, then the top of this one; 4: the top only
-  int stage = 0;
-  int nparts = 0, width = 1;      // partials of the previous pass
-  const double* parts = nullptr;
-  const CgState* in = nullptr;    // state slot read
-  CgState* out = nullptr;         // state slot written (block 0)
-  double* hist = nullptr;         // stage 2: history / host-mapped done flags, as finalize's
-  int* h_done = nullptr;
-  int64_t host_iter = 0;          // stage 2: the iteration whose stage 2 this is
-};
+// (struct Fold: pb_internal.hpp)
 
 // field-wise copy (an aggregate copy becomes a memcpy that pins the register copy in scratch)
 __device__ __forceinline__ void cg_copy(CgState& d, const CgState& s) {

@@ -41,13 +41,22 @@ struct SrGeo {
   int remap, nt;
 };
 
-template <int NW, int TY>
+// the deferred solution update on the iterations that carry it (depth 4, i % 4 = 3), PassB<3>'s
+// arithmetic: x += a3 p_{i-3} + a2 p_{i-2} + a1 p_{i-1} + alpha p_i, as p_i is formed
+struct SrX {
+  double* x;
+  const double* pm2;  // p_{i-2}
+  const double* pm3;  // p_{i-3}
+};
+
+template <int NW, int TY, bool XU>
 __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, double cz,
                                           double cc, const double* __restrict__ r,
                                           const double* __restrict__ p_old,
                                           double* __restrict__ p_new, double* __restrict__ r_out,
                                           double dinv, double shift, double bb, double alpha,
-                                          int seg, int tile, int kb, int ke,
+                                          const SrX& xu, const double (&xa)[3], int seg,
+                                          int tile, int kb, int ke,
                                           dv2 (&xch)[2][4][NW][64], double (&acc)[5]) {
   constexpr int RB = NW * TY;
   constexpr int SB = RB - 4;
@@ -108,6 +117,13 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
     // planes k+4 in flight for two steps (plane k+3's loads are already on their way)
     ld(r, k + 4, R[Q]);
     ld(p_old, k + 4, PO[Q]);
+    // x-update operands of plane k+2 (consumed at the end of this step)
+    double XX[XU ? TY : 1][2], M2[XU ? TY : 1][2], M3[XU ? TY : 1][2];
+    if constexpr (XU) {
+      ld(xu.x, k + 2, XX);
+      ld(xu.pm2, k + 2, M2);
+      ld(xu.pm3, k + 2, M3);
+    }
     // p(k+2) = (dinv r - mu) + b p_old (CombineLoad::f)
 #pragma unroll
     for (int q = 0; q < TY; ++q)
@@ -195,6 +211,24 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
         }
       }
     }
+    if constexpr (XU) {  // x(k+2) += a3 p_{i-3} + a2 p_{i-2} + a1 p_{i-1} + alpha p_i
+      if (in2) {
+        const int64_t base = pl(k + 2);
+#pragma unroll
+        for (int q = 0; q < TY; ++q) {
+          double xv[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            double u = xa[0] * M3[q][e];
+            u = u + xa[1] * M2[q][e];
+            u = u + xa[2] * PO[(Q + 2) & 3][q][e];
+            u = u + alpha * pk2[q][e];
+            xv[e] = XX[q][e] + u;
+          }
+          if (row_ok >> q & 1u) store_row<2>(xu.x, rix(base + ro[q]), xv, g.nt);
+        }
+      }
+    }
   };
   // steps kb-4 .. ke-1 (padded to whole four-step rounds: the spare steps store and sum nothing)
 #pragma unroll 1
@@ -206,24 +240,25 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
   }
 }
 
-template <int NW, int TY>
+template <int NW, int TY, bool XU>
 __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, double cy, double cz,
                                                          double cc, const double* __restrict__ r,
                                                          const double* __restrict__ p_old,
                                                          double* __restrict__ p_new,
-                                                         double* __restrict__ r_out,
+                                                         double* __restrict__ r_out, SrX xu,
                                                          double* parts, Fold fold) {
   __shared__ dv2 xch[2][4][NW][64];
   CgState st;
   fold_prologue(fold, st);  // every wave: the previous residual-sum stage + this iteration's top
   if (st.done) return;      // (uniform: every wave computed the same state)
   const double dinv = st.dinv, shift = -st.mu, bb = st.bbp, alpha = st.alpha;
+  const double xa[3] = {st.pa[0], st.pa[1], st.pa[2]};  // pending alphas of i-3, i-2, i-1
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   const int bid = xcd_block(g.remap);
   const int ncol = g.nseg * g.ntile, W = g.W, T = g.nzl / W;
   auto run = [&](int col, int kb, int ke) {
-    sr1_range<NW, TY>(g, cx, cy, cz, cc, r, p_old, p_new, r_out, dinv, shift, bb, alpha,
-                      col % g.nseg, col / g.nseg, kb, ke, xch, acc);
+    sr1_range<NW, TY, XU>(g, cx, cy, cz, cc, r, p_old, p_new, r_out, dinv, shift, bb, alpha, xu,
+                          xa, col % g.nseg, col / g.nseg, kb, ke, xch, acc);
   };
   if (bid < T * ncol) {  // bands of W planes of every column
     const int kb = (bid / ncol) * W;
@@ -253,8 +288,9 @@ bool cg_sr1_supported(const pb_grid* g) {
 
 template <int NW, int TY>
 static int launch_sr1_t(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                        double* p_new, double* r_out, const SrFold& sf, const double* parts_in,
-                        double* parts_out, int64_t host_iter, int* nblocks) {
+                        double* p_new, double* r_out, const SrX* xu, const SrFold& sf,
+                        const double* parts_in, double* parts_out, int64_t host_iter,
+                        int* nblocks) {
   pb_ctx* ctx = g->ctx;
   SrGeo geo;
   geo.nx = (int)g->n[0];
@@ -281,30 +317,35 @@ static int launch_sr1_t(pb_grid* g, const Star& s, const double* r, const double
   f.hist = sf.hist;
   f.h_done = sf.h_done;
   f.host_iter = host_iter - 1;
-  hipLaunchKernelGGL((cg_sr1_kernel<NW, TY>), dim3((unsigned)nb), dim3(64 * NW), 0,
-                     ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out, parts_out,
-                     f);
+  if (xu)
+    hipLaunchKernelGGL((cg_sr1_kernel<NW, TY, true>), dim3((unsigned)nb), dim3(64 * NW), 0,
+                       ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out, *xu,
+                       parts_out, f);
+  else
+    hipLaunchKernelGGL((cg_sr1_kernel<NW, TY, false>), dim3((unsigned)nb), dim3(64 * NW), 0,
+                       ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out,
+                       SrX{nullptr, nullptr, nullptr}, parts_out, f);
   PB_HIP(hipGetLastError());
   *nblocks = (int)nb;
   return PB_OK;
 }
 
 int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                  double* p_new, double* r_out, const SrFold& sf, const double* parts_in,
-                  double* parts_out, int64_t host_iter, int* nblocks) {
-  ScopedTimer tm(g->ctx, "cg_sr1");
+                  double* p_new, double* r_out, double* x, const double* p_m2, const double* p_m3,
+                  const SrFold& sf, const double* parts_in, double* parts_out, int64_t host_iter,
+                  int* nblocks) {
+  ScopedTimer tm(g->ctx, x ? "cg_sr1_x4" : "cg_sr1");
+  const SrX xv{x, p_m2, p_m3};
+  const SrX* xu = x ? &xv : nullptr;
   switch (tune("cg_sr_shape", 0)) {
     case 1:  // 12 waves of 2 rows: three waves per SIMD
-      return launch_sr1_t<12, 2>(g, s, r, p_old, p_new, r_out, sf, parts_in, parts_out,
-                                 host_iter, nblocks);
-    case 2:
-      return launch_sr1_t<16, 2>(g, s, r, p_old, p_new, r_out, sf, parts_in, parts_out,
+      return launch_sr1_t<12, 2>(g, s, r, p_old, p_new, r_out, xu, sf, parts_in, parts_out,
                                  host_iter, nblocks);
     case 3:
-      return launch_sr1_t<8, 3>(g, s, r, p_old, p_new, r_out, sf, parts_in, parts_out,
+      return launch_sr1_t<8, 3>(g, s, r, p_old, p_new, r_out, xu, sf, parts_in, parts_out,
                                 host_iter, nblocks);
     default:  // 8 waves of 2 rows: two waves per SIMD
-      return launch_sr1_t<8, 2>(g, s, r, p_old, p_new, r_out, sf, parts_in, parts_out,
+      return launch_sr1_t<8, 2>(g, s, r, p_old, p_new, r_out, xu, sf, parts_in, parts_out,
                                 host_iter, nblocks);
   }
 }

@@ -280,9 +280,12 @@ int launch_sor_sweep2(pb_grid* g, const Star& s, const double* xin, const double
 // pre-smoothing from zero + residual + restriction to the coarse b in one pass (one rank)
 int launch_presmooth_restrict(pb_grid* g, const Star& s, const pb_grid* cg, const double* b,
                               double* xout, double* bc, double omega, const int* skip);
+// xc_full (decomposed grids, agglomerated coarse level): the whole coarse correction on this
+// rank -- its ghost planes are read in place instead of exchanged
 int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double* xs,
                       const double* xc, const double* b, double* xout, double omega,
-                      const int* skip, const CgState* sums_st = nullptr, int* nparts = nullptr);
+                      const int* skip, const CgState* sums_st = nullptr, int* nparts = nullptr,
+                      const double* xc_full = nullptr);
 int launch_presmooth_residual(pb_grid* g, const Star& s, const double* b, double* x, double* res,
                               double omega, const int* skip);
 int launch_mg_residual(pb_grid* g, const Star& s, const double* x, const double* b,
@@ -308,7 +311,28 @@ struct CgState {
 };
 int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p, CgState* st,
                    double dinv, double* hist, int* h_done);
+struct Fold {
+  // 0: no fold; 1: stage 1 (pass B); 2: stage 2 (pass A); single-reduction pass P: 3: the
+  // residual-sum stage of the previous iteration, then the top of this one; 4: the top only
+  int stage = 0;
+  int nparts = 0, width = 1;      // partials of the previous pass
+  const double* parts = nullptr;
+  const CgState* in = nullptr;    // state slot read
+  CgState* out = nullptr;         // state slot written (block 0)
+  double* hist = nullptr;         // stage 2: history / host-mapped done flags, as finalize's
+  int* h_done = nullptr;
+  int64_t host_iter = 0;          // stage 2: the iteration whose stage 2 this is
+};
+// fold.stage = 2: the previous iteration's stage 2 in the prologue (split grids, folded iteration)
+int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st,
+                       const Fold& fold);
 int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st);
+// split grids, folded iteration: a pass's partials reduced and allreduced into ctx->d_scalars
+int cg_reduce_allreduce(pb_ctx* ctx, int nparts, int width, bool b_region);
+int cg_reduce_allreduce(pb_ctx* ctx, const double* parts, int nparts, int width);
+// stage 2 on st in place from the sums cg_reduce_allreduce left in ctx->d_scalars
+int cg_stage2_from_sums(pb_ctx* ctx, int width, CgState* st, double* hist, int* h_done,
+                        int64_t host_iter);
 // store = false: pass A only takes p.Ap; pass B forms and stores p (PB_CG_PSTORE_B, PStore)
 int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
                      double* p_new, const StencilPlanes& gp, CgState* st, int mode, int part_off,
@@ -337,7 +361,8 @@ int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const do
 int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
                             const double* const* p_prev, double* x, double* r,
                             const StencilPlanes& gp, CgState* st2, int nparts_a, int64_t host_iter,
-                            int defer, int* nparts_b, const PStore& ps = PStore{});
+                            int defer, int* nparts_b, const PStore& ps = PStore{},
+                            const double* parts_a = nullptr);
 int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_done,
                  int64_t host_iter);
 // Single-reduction CG (PETSc KSPSolve_CG_SingleReduction, -ksp_cg_single_reduction), two engine
@@ -371,9 +396,12 @@ int cg_sr_finalize(pb_ctx* ctx, const double* parts, int nparts, CgState* st, do
 // The same iteration as ONE pass (pb_cg_sr.hip; one rank, even nx, tuning cg_sr_fused): p, r',
 // and all five sums; the prologue as pass P's (sf), partials into parts_out (*nblocks blocks)
 bool cg_sr1_supported(const pb_grid* g);
+// x != nullptr: the iteration also carries the depth-4 deferred x update (p_m2, p_m3 = p_{i-2},
+// p_{i-3}; p_{i-1} is p_old)
 int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                  double* p_new, double* r_out, const SrFold& sf, const double* parts_in,
-                  double* parts_out, int64_t host_iter, int* nblocks);
+                  double* p_new, double* r_out, double* x, const double* p_m2, const double* p_m3,
+                  const SrFold& sf, const double* parts_in, double* parts_out, int64_t host_iter,
+                  int* nblocks);
 
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----
 int64_t compact_fast_work_len(const pb_grid* g);

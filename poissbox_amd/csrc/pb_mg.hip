@@ -937,9 +937,11 @@ int mg_apply(Mg* mg, const double* r, double* z, const int* skip, const CgState*
     if (post_fused(mg, l)) {
       // prolongation + correction + both post-smoothing half-sweeps in one pass, xs -> x
       // (agglomerated coarse level: this rank's planes of the full coarse correction)
-      const double* xcp = agg && l + 1 == mg->La ? mg->ax[0] + Cl.g->k0 * Cl.g->plane : Cl.x;
+      const bool from_agg = agg && l + 1 == mg->La;
+      const double* xcp = from_agg ? mg->ax[0] + Cl.g->k0 * Cl.g->plane : Cl.x;
       PB_TRY(launch_post_sweep(F.g, F.s, Cl.g, F.xs, xcp, F.b, F.x, mg->omega, mg->skip,
-                               l == 0 ? sums_st : nullptr, l == 0 ? nparts : nullptr));
+                               l == 0 ? sums_st : nullptr, l == 0 ? nparts : nullptr,
+                               from_agg ? mg->ax[0] : nullptr));
       continue;
     }
     const double *lo, *hi;

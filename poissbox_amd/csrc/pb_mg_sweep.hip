@@ -772,9 +772,10 @@ struct PostGeo {
   int ncx, ncy, ncz;   // coarse extents (one rank: the whole coarse grid; N ranks: the slab)
   int64_t cplane;
   // N ranks (post_sweep_u4_kernel): the coarse correction's planes -2, -1, ncz, ncz+1 (in that
-  // order) in cgh; the fine x_s ghosts (-2, -1, nz, nz+1) in Sweep2Geo::xg, b's in bg_lo / bg_hi
+  // order) at cgh[0..3]; the fine x_s ghosts (-2, -1, nz, nz+1) in Sweep2Geo::xg, b's in bg_lo /
+  // bg_hi
   int split;
-  const double* cgh;
+  const double* cgh[4];
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -856,7 +857,7 @@ __device__ __forceinline__ void post_sweep_u4_range(
         cp = xc + (int64_t)K * cgeo.cplane;
       } else {
         const int gi = K < 0 ? max(K + 2, 0) : 2 + min(K - cgeo.ncz, 1);
-        cp = cgeo.cgh + (int64_t)gi * cgeo.cplane;
+        cp = cgeo.cgh[gi];
       }
 #pragma unroll
       for (int t = 0; t < NC; ++t)
@@ -1184,7 +1185,8 @@ static int64_t balanced_split(const pb_grid* g, Sweep2Geo& geo, int per_cu, int 
 
 int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double* xs,
                       const double* xc, const double* b, double* xout, double omega,
-                      const int* skip, const CgState* sums_st, int* nparts) {
+                      const int* skip, const CgState* sums_st, int* nparts,
+                      const double* xc_full) {
   ScopedTimer tm(g->ctx, "mg_post_sweep");
   const bool split = g->ctx->split;
   if (xs == xout) return set_error(PB_ERR_ARG, "fused post-smoothing must run out of place");
@@ -1194,7 +1196,8 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
   int64_t nblocks = sweep2_geo(g, geo);
   geo.split = 0;
   geo.xg = geo.bg_lo = geo.bg_hi = nullptr;
-  PostGeo cgeo{(int)cg->n[0], (int)cg->n[1], (int)cg->nzl, cg->plane, 0, nullptr};
+  PostGeo cgeo{(int)cg->n[0], (int)cg->n[1], (int)cg->nzl, cg->plane, 0,
+                {nullptr, nullptr, nullptr, nullptr}};
   if (split) {  // x_s two deep, b one deep, the coarse correction two deep
     pb_grid* gc = const_cast<pb_grid*>(cg);
     if (g->nzl < 2 || gc->nzl < 2)
@@ -1204,14 +1207,24 @@ int launch_post_sweep(pb_grid* g, const Star& s, const pb_grid* cg, const double
     PB_TRY(halo_exchange_n(g, xs, xs + (g->nzl - 2) * g->plane, 2, g->ghost2,
                            g->ghost2 + 2 * g->plane));
     PB_TRY(halo_exchange(g, b, b + (g->nzl - 1) * g->plane));
-    PB_TRY(halo_exchange_n(gc, xc, xc + (gc->nzl - 2) * gc->plane, 2, gc->ghost2,
-                           gc->ghost2 + 2 * gc->plane));
     geo.split = 1;
     geo.xg = g->ghost2;
     geo.bg_lo = g->ghost_lo;
     geo.bg_hi = g->ghost_hi;
     cgeo.split = 1;
-    cgeo.cgh = gc->ghost2;
+    if (xc_full) {
+      // the agglomerated coarse level: every rank holds the whole coarse correction, so its
+      // planes -2, -1, nzl, nzl+1 are read in place (no coarse halo exchange)
+      const int64_t nzc = gc->n[2];
+      for (int i = 0; i < 4; ++i) {
+        const int64_t kk = i < 2 ? gc->k0 - 2 + i : gc->k0 + gc->nzl + (i - 2);
+        cgeo.cgh[i] = xc_full + ((kk % nzc + nzc) % nzc) * gc->plane;
+      }
+    } else {
+      PB_TRY(halo_exchange_n(gc, xc, xc + (gc->nzl - 2) * gc->plane, 2, gc->ghost2,
+                             gc->ghost2 + 2 * gc->plane));
+      for (int i = 0; i < 4; ++i) cgeo.cgh[i] = gc->ghost2 + (int64_t)i * gc->plane;
+    }
   }
   // 8 waves x 4 rows (unrolled: compile-time colours need an even k0, chunks start at multiples
   // of 4)

@@ -3,6 +3,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdlib>
@@ -27,8 +28,6 @@ void field_free(void* p) {
 
 // ---- tuning table (pb_tune_set; pb_internal.hpp tune()) ----
 namespace {
-std::mutex g_tune_mu;
-std::unordered_map<std::string, int> g_tune;
 // every name a kernel launcher consults; the defaults live at the call sites (the measured
 // choices), the table only holds values a caller set
 const char* const kTuneNames[] = {
@@ -36,23 +35,30 @@ const char* const kTuneNames[] = {
     "comm_stall_test_ms", "compact_lines", "fft_rupd", "fft_zpad", "fft_zpad_min_plane",
     "force_comm", "ksp_lazy0", "mg_agglomerate", "mg_engine_min_plane", "mg_restrict_z_min_cols",
     "mg_split_fused", "mg_sweep2", "mg_tail_max", "mg_u4_split", "pcr_lines", "sor_omega_any"};
-bool tune_known(const char* name) {
-  for (const char* n : kTuneNames)
-    if (strcmp(n, name) == 0) return true;
-  return false;
+constexpr int kNumTune = (int)(sizeof(kTuneNames) / sizeof(kTuneNames[0]));
+// lock-free table (tune() runs several times per CG iteration / V-cycle): a value and
+// a set flag per name, and a count of set names so the common case (nothing set) is one load.
+// Like every table update, pb_tune_set is not meant to race with running calls.
+std::atomic<int> g_tune_val[kNumTune];
+std::atomic<int> g_tune_set[kNumTune];
+std::atomic<int> g_tune_nset{0};
+int tune_index(const char* name) {
+  for (int i = 0; i < kNumTune; ++i)
+    if (strcmp(kTuneNames[i], name) == 0) return i;
+  return -1;
 }
 }  // namespace
 
 int tune(const char* name, int dflt) {
-  std::lock_guard<std::mutex> lk(g_tune_mu);
-  if (g_tune.empty()) return dflt;
-  auto it = g_tune.find(name);
-  return it == g_tune.end() ? dflt : it->second;
+  if (g_tune_nset.load(std::memory_order_acquire) == 0) return dflt;
+  const int i = tune_index(name);
+  if (i < 0 || !g_tune_set[i].load(std::memory_order_acquire)) return dflt;
+  return g_tune_val[i].load(std::memory_order_relaxed);
 }
 
 bool tune_is_set(const char* name) {
-  std::lock_guard<std::mutex> lk(g_tune_mu);
-  return g_tune.count(name) != 0;
+  const int i = tune_index(name);
+  return i >= 0 && g_tune_set[i].load(std::memory_order_acquire) != 0;
 }
 
 static thread_local char g_err[1024] = "";
@@ -754,25 +760,27 @@ int pb_ctx_destroy(pb_ctx* ctx) {
 
 int pb_tune_set(const char* name, int value) {
   PB_CHECK_ARG(name, "tuning name is NULL");
-  if (!tune_known(name)) return set_error(PB_ERR_ARG, "unknown tuning parameter '%s'", name);
-  std::lock_guard<std::mutex> lk(g_tune_mu);
-  g_tune[name] = value;
+  const int i = tune_index(name);
+  if (i < 0) return set_error(PB_ERR_ARG, "unknown tuning parameter '%s'", name);
+  g_tune_val[i].store(value, std::memory_order_relaxed);
+  if (g_tune_set[i].exchange(1, std::memory_order_acq_rel) == 0)
+    g_tune_nset.fetch_add(1, std::memory_order_acq_rel);
   return PB_OK;
 }
 
 int pb_tune_get(const char* name, int* value, int* is_set) {
   PB_CHECK_ARG(name && value, "bad tuning args");
-  if (!tune_known(name)) return set_error(PB_ERR_ARG, "unknown tuning parameter '%s'", name);
-  std::lock_guard<std::mutex> lk(g_tune_mu);
-  auto it = g_tune.find(name);
-  if (is_set) *is_set = it != g_tune.end();
-  if (it != g_tune.end()) *value = it->second;
+  const int i = tune_index(name);
+  if (i < 0) return set_error(PB_ERR_ARG, "unknown tuning parameter '%s'", name);
+  const bool set = g_tune_set[i].load(std::memory_order_acquire) != 0;
+  if (is_set) *is_set = set;
+  if (set) *value = g_tune_val[i].load(std::memory_order_relaxed);
   return PB_OK;
 }
 
 int pb_tune_reset(void) {
-  std::lock_guard<std::mutex> lk(g_tune_mu);
-  g_tune.clear();
+  for (int i = 0; i < kNumTune; ++i) g_tune_set[i].store(0, std::memory_order_release);
+  g_tune_nset.store(0, std::memory_order_release);
   return PB_OK;
 }
 

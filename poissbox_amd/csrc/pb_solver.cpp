@@ -581,10 +581,13 @@ static int enqueue_sr_iteration(pb_ksp* k, bool fold, int64_t n) {
   double* p_new = k->pb[(i + 1) % ns];
   double* r = k->rbuf(i);
   double* r_out = k->rbuf(i + 1);
-  CgState* st_in = k->d_st + (n & 1);
-  CgState* st_out = k->d_st + ((n + 1) & 1);
+  // one rank: the state alternates between the slots by the batch index's parity; split grids:
+  // slot 0 holds the state after the residual-sum stage (written by the boundary-plane kernel's
+  // folded prologue, or copied there unfolded), slot 1 after the top of the iteration (pass P)
+  CgState* st_in = ctx->split ? k->d_st : k->d_st + (n & 1);
+  CgState* st_out = ctx->split ? k->d_st + 1 : k->d_st + ((n + 1) & 1);
   SrFold f;
-  f.fold_sums = fold && n > 0;
+  f.fold_sums = fold && n > 0 && !ctx->split;
   f.nparts_s = k->sr_nparts;
   f.parts = sr_region(ctx, n - 1);
   f.in = st_in;
@@ -592,10 +595,13 @@ static int enqueue_sr_iteration(pb_ksp* k, bool fold, int64_t n) {
   f.hist = k->d_hist;
   f.h_done = k->h_done_dev;
   StencilPlanes gp;
-  // one pass per iteration where it applies: one rank, x update not due (depth-4 deferral)
-  if (cg_sr1_supported(g) && k->defer_x == 4 && i % 4 != 3) {
-    PB_TRY(launch_cg_sr1(g, s, r, p_prev[0], p_new, r_out, f, f.parts,
-                         const_cast<double*>(sr_region(ctx, n)), i, &k->sr_nparts));
+  // one pass per iteration where it applies: one rank, depth-4 x deferral (every 4th iteration
+  // the pass also updates x)
+  if (cg_sr1_supported(g) && k->defer_x == 4) {
+    const bool xu = i % 4 == 3;
+    PB_TRY(launch_cg_sr1(g, s, r, p_prev[0], p_new, r_out, xu ? k->x->d : nullptr, p_prev[1],
+                         p_prev[2], f, f.parts, const_cast<double*>(sr_region(ctx, n)), i,
+                         &k->sr_nparts));
     if (!fold)
       PB_TRY(cg_sr_finalize(ctx, sr_region(ctx, n), k->sr_nparts, st_out, k->d_hist,
                             k->h_done_dev, i));
@@ -607,10 +613,24 @@ static int enqueue_sr_iteration(pb_ksp* k, bool fold, int64_t n) {
     PB_TRY(launch_cg_sr_pass_p(g, s, r, p_prev, p_new, k->x->d, r_out, gp, f, PLANES_ALL, i,
                                k->defer_x));
   } else {
-    // p's boundary planes (b from the completed state in st_in) -> halo, under the interior
+    // p's boundary planes -> halo, under the interior planes. Folded: the boundary-plane kernel
+    // first runs the previous iteration's residual-sum stage from pass S's allreduced sums (a
+    // one-block partial, slot 1 -> slot 0); pass P then runs the top (slot 0 -> slot 1)
+    Fold fb;
+    if (fold && n > 0) {
+      fb.stage = 2;
+      fb.nparts = 1;
+      fb.width = 5;
+      fb.parts = ctx->d_scalars;
+      fb.in = k->d_st + 1;
+      fb.out = k->d_st;
+      fb.hist = k->d_hist;
+      fb.h_done = k->h_done_dev;
+      fb.host_iter = i - 1;
+    }
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
-    PB_TRY(launch_cg_boundary(g, r, p_prev[0], st_in));
+    PB_TRY(launch_cg_boundary(g, r, p_prev[0], st_in, fb));
     if (g->nzl < 3) {
       PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
       PB_TRY(launch_cg_sr_pass_p(g, s, r, p_prev, p_new, k->x->d, r_out, gp, f, PLANES_ALL, i,
@@ -626,9 +646,13 @@ static int enqueue_sr_iteration(pb_ksp* k, bool fold, int64_t n) {
     }
   }
   PB_TRY(sr_pass_s(k, r_out, st_out, &k->sr_nparts, n));
+  if (fold && ctx->split) return cg_reduce_allreduce(ctx, sr_region(ctx, n), k->sr_nparts, 5);
   if (!fold)
     PB_TRY(cg_sr_finalize(ctx, sr_region(ctx, n), k->sr_nparts, st_out, k->d_hist,
                           k->h_done_dev, i));
+  if (!fold && ctx->split)  // the next boundary-plane kernel reads slot 0
+    PB_HIP(hipMemcpyAsync(k->d_st, st_out, sizeof(CgState), hipMemcpyDeviceToDevice,
+                          ctx->stream));
   return PB_OK;
 }
 
@@ -658,7 +682,8 @@ static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
   const bool store_a = !k->pst;
   StencilPlanes gp;
   int nparts = 0;
-  if (fold) {
+  const bool fold_split = fold && ctx->split;
+  if (fold && !ctx->split) {
     gp.ghost_lo = gp.ghost_hi = nullptr;
     gp.wrap = true;
     if (fold_a)
@@ -669,6 +694,45 @@ static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
                               store_a));
     return launch_cg_pass_b_folded(g, s, p_new, p_prev, k->x->d, r, gp, k->d_st, nparts, i,
                                    k->defer_x, &k->fold_nparts_b, ps);
+  }
+  if (fold_split) {
+    // split grids, folded (r05): the boundary-plane kernel runs the previous iteration's stage 2
+    // from pass B's allreduced sums (a one-block partial), pass B stage 1 from pass A's; only the
+    // reductions before each allreduce stay separate launches (bit-identical to unfolded)
+    Fold fb;
+    if (fold_a) {
+      fb.stage = 2;
+      fb.nparts = 1;
+      fb.width = 4;
+      fb.parts = ctx->d_scalars;
+      fb.in = k->d_st + 1;
+      fb.out = k->d_st;
+      fb.hist = k->d_hist;
+      fb.h_done = k->h_done_dev;
+      fb.host_iter = i - 1;
+    }
+    PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st, fb));
+    gp.ghost_lo = g->ghost_lo;
+    gp.ghost_hi = g->ghost_hi;
+    if (g->nzl < 3) {
+      PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
+      PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts,
+                              store_a));
+    } else {
+      int nb1 = 0, nb2 = 0;
+      ScopedTimer tm(ctx, "cg_pass_a");
+      PB_TRY(halo_begin(g, g->bnd_lo, g->bnd_hi));
+      PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1,
+                              store_a));
+      PB_TRY(halo_end(g));
+      PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1, &nb2,
+                              store_a));
+      nparts = nb1 + nb2;
+    }
+    PB_TRY(cg_reduce_allreduce(ctx, nparts, 1, false));
+    PB_TRY(launch_cg_pass_b_folded(g, s, p_new, p_prev, k->x->d, r, gp, k->d_st, 1, i,
+                                   k->defer_x, &k->fold_nparts_b, ps, ctx->d_scalars));
+    return cg_reduce_allreduce(ctx, k->fold_nparts_b, 4, true);
   }
   if (!ctx->split) {
     // periodic wrap read in place: pass A combines r, p_old of the wrap planes itself and pass B
@@ -727,8 +791,7 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
   PB_TRY(ensure_done_cap(k, k->host_iter + iters + 2));
   // one rank, Jacobi, fused operator: the finalize steps ride in the passes' prologues
   // (PB_CG_FOLD=0 keeps the separate finalize launches)
-  const bool fold = C >= 2 && !ctx->split && fused_kind(k->A->kind) && !k->stored_z() &&
-                    tune("cg_fold", 1) != 0;
+  const bool fold = C >= 2 && fused_kind(k->A->kind) && !k->stored_z() && tune("cg_fold", 1) != 0;
   int64_t n = 0;
   for (; n < iters && !k->stopped; ++n) {
     if (k->sr) PB_TRY(enqueue_sr_iteration(k, fold, n));
@@ -750,6 +813,15 @@ int pb_ksp_iterate(pb_ksp* k, int64_t iters) {
   if (k->sr) {
     // the residual-sum stage of the batch's last iteration (folded runs), then the state back
     // into slot 0 for the next batch and the other entry points
+    if (ctx->split) {  // (unfolded: the state is in slot 0 already)
+      if (fold && n > 0) {
+        PB_TRY(cg_stage2_from_sums(ctx, 5, k->d_st + 1, k->d_hist, k->h_done_dev,
+                                   k->host_iter - 1));
+        PB_HIP(hipMemcpyAsync(k->d_st, k->d_st + 1, sizeof(CgState), hipMemcpyDeviceToDevice,
+                              ctx->stream));
+      }
+      return PB_OK;
+    }
     if (fold && n > 0)
       PB_TRY(cg_sr_finalize(ctx, sr_region(ctx, n - 1), k->sr_nparts, k->d_st + (n & 1),
                             k->d_hist, k->h_done_dev, k->host_iter - 1));

@@ -906,15 +906,22 @@ __global__ __launch_bounds__(256) void cg_init_kernel(const double* __restrict__
 }
 
 // boundary planes of p_new (for the halo exchange / periodic self-wrap)
+// fold.stage = 2 (split grids): every wave first runs the previous iteration's stage 2 from the
+// allreduced sums (a one-block partial) and the lead lane stores the state (fold.out)
 __global__ __launch_bounds__(256) void cg_boundary_kernel(const double* __restrict__ r,
                                                           const double* __restrict__ p,
                                                           int64_t plane, int64_t last_off,
                                                           double* __restrict__ lo,
                                                           double* __restrict__ hi,
-                                                          const CgState* st) {
+                                                          const CgState* st, Fold fold) {
+  CgState sst;
+  if (fold.stage) {
+    fold_prologue(fold, sst);
+    st = &sst;
+  }
   if (st->done) return;
-  CombineLoad c{r, p, st, 0.0, 0.0, 0.0};
-  c.prepare();
+  CombineLoad c{r, p, nullptr, 0.0, 0.0, 0.0};
+  c.prepare_from(*st);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < plane;
        i += (int64_t)gridDim.x * blockDim.x) {
     lo[i] = c.one(i);
@@ -1005,14 +1012,19 @@ int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p,
   return cg_reduce_update(ctx, 0, nb, 4, st, hist, h_done, -1);
 }
 
-int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st) {
+int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st,
+                       const Fold& fold) {
   pb_ctx* ctx = g->ctx;
   ScopedTimer tm(ctx, "cg_boundary");
   const int nb = elementwise_blocks(ctx, g->plane);
   hipLaunchKernelGGL(cg_boundary_kernel, dim3(nb), dim3(256), 0, ctx->stream, r, p_old, g->plane,
-                     (g->nzl - 1) * g->plane, g->bnd_lo, g->bnd_hi, (const CgState*)st);
+                     (g->nzl - 1) * g->plane, g->bnd_lo, g->bnd_hi, (const CgState*)st, fold);
   PB_HIP(hipGetLastError());
   return PB_OK;
+}
+
+int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st) {
+  return launch_cg_boundary(g, r, p_old, st, Fold{});
 }
 
 int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p_old,
@@ -1051,6 +1063,32 @@ int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const do
     return launch_any(g, s, ld, gp, PassAT<false>{p_new}, nullptr, PLANES_ALL, 0, nblocks, 0,
                       0, f);
   return launch_any(g, s, ld, gp, PassA{p_new}, nullptr, PLANES_ALL, 0, nblocks, 0, 0, f);
+}
+
+// split grids, folded iteration: reduce a pass's partials and allreduce them into d_scalars, where
+// the next kernel's prologue reads them as a one-block partial (pass A's -> pass B; pass B's ->
+// the next boundary-plane kernel); b_region: pass B's partials (fold_parts_b_off)
+int cg_reduce_allreduce(pb_ctx* ctx, int nparts, int width, bool b_region) {
+  return cg_reduce_allreduce(ctx, ctx->d_partials + (b_region ? fold_parts_b_off(ctx) * 4 : 0),
+                             nparts, width);
+}
+
+int cg_reduce_allreduce(pb_ctx* ctx, const double* parts, int nparts, int width) {
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream, parts, nparts, width,
+                     ctx->d_scalars, 1, 0, (CgState*)nullptr, (double*)nullptr, (int*)nullptr,
+                     (int64_t)0);
+  PB_HIP(hipGetLastError());
+  return allreduce_device(ctx, ctx->d_scalars, width);
+}
+
+// the residual-sum stage (2) on st in place from sums already allreduced into d_scalars
+int cg_stage2_from_sums(pb_ctx* ctx, int width, CgState* st, double* hist, int* h_done,
+                        int64_t host_iter) {
+  hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream,
+                     (const double*)nullptr, 0, width, ctx->d_scalars, 2, 2, st, hist, h_done,
+                     host_iter);
+  PB_HIP(hipGetLastError());
+  return PB_OK;
 }
 
 int cg_finalize_init(pb_ctx* ctx, int nparts, CgState* st, double* hist, int* h_done) {
@@ -1130,12 +1168,12 @@ int launch_cg_pass_b(pb_grid* g, const Star& s, const double* p, const double* c
 int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
                             const double* const* p_prev, double* x, double* r,
                             const StencilPlanes& gp, CgState* st2, int nparts_a, int64_t host_iter,
-                            int defer, int* nparts_b, const PStore& ps) {
+                            int defer, int* nparts_b, const PStore& ps, const double* parts_a) {
   Fold f;
   f.stage = 1;
   f.nparts = nparts_a;
   f.width = 1;
-  f.parts = g->ctx->d_partials;
+  f.parts = parts_a ? parts_a : g->ctx->d_partials;
   f.in = st2;
   f.out = st2 + 1;
   return pass_b_launch(g, s, p, p_prev, x, r, gp, nullptr, host_iter, defer, f, ps, nparts_b);
@@ -1145,9 +1183,10 @@ int launch_cg_pass_b_folded(pb_grid* g, const Star& s, const double* p,
 // then st2[0] = st2[1], so the unfolded entry points find the complete state in slot 0
 int cg_fold_tail(pb_ctx* ctx, int nparts_b, CgState* st2, double* hist, int* h_done,
                  int64_t host_iter) {
+  // split grids: pass B's sums are already reduced and allreduced into d_scalars (mode 2 only)
   hipLaunchKernelGGL(cg_finalize_kernel, dim3(1), dim3(256), 0, ctx->stream,
-                     ctx->d_partials + fold_parts_b_off(ctx) * 4, nparts_b, 4, ctx->d_scalars, 3,
-                     2, st2 + 1, hist, h_done, host_iter);
+                     ctx->d_partials + fold_parts_b_off(ctx) * 4, nparts_b, 4, ctx->d_scalars,
+                     ctx->split ? 2 : 3, 2, st2 + 1, hist, h_done, host_iter);
   PB_HIP(hipGetLastError());
   PB_HIP(hipMemcpyAsync(st2, st2 + 1, sizeof(CgState), hipMemcpyDeviceToDevice, ctx->stream));
   return PB_OK;

@@ -1551,3 +1551,41 @@ def test_split_apply_timers_cover_whole_applies(tune):
     assert a_cnt == ai[1] == bi[1] >= 6
     assert a_ms >= ai[0] + bi[0] - 1e-6  # the apply spans both launches
     ctx.set_timing(False)
+
+
+@pytest.mark.parametrize("sr", [False, True])
+@pytest.mark.parametrize("nranks,n", [(2, (16, 16, 12)), (3, (32, 16, 12)), (2, (32, 16, 4))])
+def test_multirank_cg_folded_bit_identical(nranks, n, sr):
+    """Split grids, Jacobi CG (and -ksp_cg_single_reduction): the state stages folded into the
+    next kernel's prologue, the allreduced sums read as a one-block partial (check_every >= 2,
+    r05) against the separate finalize launches (check_every 1) -- reason, its, history and x
+    bit-identical on every rank, begin / iterate(3) / iterate(rest) included (state slots across
+    calls); and the oracle's history."""
+    N = int(np.prod(n))
+    h = tuple(1.0 / m for m in n)
+    b = O.stencil(O.fill_random(N, SEED), n, h)
+    xo, ro, itso, ho = O.cg_solve(b, n, h, rtol=1e-9, single_reduction=int(sr))
+    argv = ["-ksp_rtol", "1e-9"] + (["-ksp_cg_single_reduction"] if sr else [])
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        out = {}
+        for check in (8, 1):
+            P, A, x, bv = pb.initialise_linear_system(da, h)
+            bv.set_values(b.reshape(n[2], -1)[k0:k0 + nk])
+            k = pb.KSP(A, P, pb.ksp_options(argv, check_every=check))
+            k.begin(bv, x)
+            k.iterate(3)
+            k.iterate(100000)
+            reason, its, hist = k.end()
+            k.destroy()
+            out[check] = (reason, its, np.asarray(hist), x.get_values())
+        return out, k0, nk
+
+    for out, k0, nk in run_ranks(nranks, body):
+        (r8, i8, h8, x8), (r1, i1, h1, x1) = out[8], out[1]
+        assert (r8, i8) == (r1, i1) == (ro, itso)
+        assert np.array_equal(h8, h1) and np.array_equal(x8, x1)
+        check_history(h8, ho)
+        check_x(x8, xo.reshape(n[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
