@@ -12,6 +12,13 @@ namespace pb {
 // the folded pass prologues
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool finite(double v) { return v == v && v - v == 0.0; }
+// timing-only ablation builds (wrong results): every exit but the iteration limit is ignored
+template <class S>
+__device__ __forceinline__ void ablate_keep_going(S& st) {
+#ifdef PB_ABLATE_NO_EXITS
+  if (st.reason != PB_KSP_DIVERGED_ITS) st.reason = 0, st.done = 0;
+#endif
+}
 
 // partial counts up to which the finalize kernel reduces with one wave in this order (the CG
 // passes: one workgroup per CU); beyond it, a 256-thread tree (a lone wave took 29 us over the
@@ -108,6 +115,7 @@ __device__ __forceinline__ void cg_stage1(CgState& st, double dpi) {
     st.alpha_prev = st.alpha;
     st.alpha = st.beta / dpi;
   }
+  ablate_keep_going(st);
 }
 
 // iterations i % D < D-1 leave alpha_i p_i pending in x; the last of each D applied them all
@@ -184,6 +192,7 @@ __device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* 
       }
     }
   }
+  ablate_keep_going(st);
   if (h_done) h_done[host_iter + 1] = st.done;
 }
 

@@ -8,67 +8,142 @@
 //            w(k+1) = A p   -> r'(k+1) = r - alpha w     (stored), t(k+1) = dinv r' - mu
 //            s(k)   = A t   -> sums t, t^2, t.r', r' (plane k+1) and t.s (plane k)
 // so per point it reads r, p_old and writes p, r': 32 B/DoF, the single-reduction floor without
-// the x update (the iterations that carry the deferred x update run the two passes).
+// the x update (the iterations that carry the deferred x update run the two passes: pass P's
+// x-update form streams at the copy rate, a fused form would not fit the register budget).
 //
-// The stencils at a wave's tile edges need p and t one point outside it. Rows: a block stacks NW
-// waves of TY rows, each wave forms every stage on its own rows only, and the values one row
-// out come from the neighbouring waves through LDS (published one step before use, double
-// buffered by step parity, one block barrier per step); each stage loses a row at the block's
-// ends, so blocks store rows 2 .. NW TY - 3 and advance by NW TY - 4 rows. Columns: a wave spans
-// 64 pairs but owns lanes 4..59 (112 points), so every x-neighbour is a DPP lane shift. Work is
-// split evenly over one workgroup per CU (bands of W planes of every column, then the last band's
-// column-planes cut into pieces of W), each z-range warming up four planes below its start.
+// The stencils at a wave's tile edges need p two points and t one point outside it.
+// Rows: a block stacks NW waves of TY rows, each wave forms every stage on its own rows only, and
+// the values one row out come from the neighbouring waves through LDS (published one step before
+// use, double buffered by step parity, one block barrier per step); each stage loses a row at the
+// block's ends, so blocks store rows 2 .. NW TY - 3 and advance by NW TY - 4 rows.
+// Columns: a wave owns 128 points (64 lanes x one 16-B pair: whole 128-B lines, segments that
+// tile a 512-point row exactly). The two points either side of each row are a "halo pair", all
+// of a wave's halo pairs in ONE more register set: lane q holds row q's left pair (x0 - 2,
+// x0 - 1), lane 64 - TY + q row q's right pair (x0 + 128, x0 + 129). The halo's inner point gets
+// p, w, r', t like any other point: its x-neighbours are its outer point and the segment's edge
+// value (read from lane 0 / 63), its y-neighbours the next lanes (DPP; across waves through LDS),
+// its z-neighbours the same register of the next planes. Lane 0's left and lane 63's right
+// neighbours are then read from the halo lanes; every other x-neighbour is a DPP lane shift.
+// Work is split evenly over one workgroup per CU (bands of W planes of every column, then the
+// last band's column-planes cut into pieces of W), each z-range warming up four planes below its
+// start.
 //
 // Per-point arithmetic is pass P's and pass S's (CombineLoad, PassB<., true, false>, ZLoad,
 // SrSums: reference summation order, no FMA contraction), so p, r' and every summand are
 // bit-identical to the two-pass iteration; only the blocks the sums are taken over differ.
 #include <type_traits>
+#include <utility>
 
 #include "pb_cg_device.hpp"
 
 namespace pb {
 
-// outputs per wave segment: lanes 4 .. 59 (pairs), 896 B = seven whole 128-B lines, so no line
-// is written by two waves (segments of 124 points -- lanes 1 .. 62 -- wrote partial lines at both
-// ends and ran 1.07-1.16 ms at 512^3 against the 112-point segments' same segment count)
-static constexpr int kSrSegOut = 112, kSrLead = 4;
+static constexpr int kSrSeg = 128;  // points per wave segment
 
 struct SrGeo {
   int nx, ny, nzl;
   int64_t plane;
-  int nseg, ntile;  // x segments of kSrSegOut points, y tiles of NW TY - 4 rows
+  int nseg, ntile;  // x segments of kSrSeg points, y tiles of NW TY - 4 rows
   int W;            // planes of work per workgroup
-  int remap, nt;
+  int remap;
 };
 
-// the deferred solution update on the iterations that carry it (depth 4, i % 4 = 3), PassB<3>'s
-// arithmetic: x += a3 p_{i-3} + a2 p_{i-2} + a1 p_{i-1} + alpha p_i, as p_i is formed
-struct SrX {
-  double* x;
-  const double* pm2;  // p_{i-2}
-  const double* pm3;  // p_{i-3}
+template <int... Qs, class F>
+__device__ __forceinline__ void unroll_steps(std::integer_sequence<int, Qs...>, F&& f) {
+  (f(std::integral_constant<int, Qs>{}), ...);
+}
+
+// one 7-point sum in the reference order (z-, y-, x-, c, x+, y+, z+)
+__device__ __forceinline__ double star7_sum(double cx, double cy, double cz, double cc,
+                                            double zm, double ym, double xm, double c, double xp,
+                                            double yp, double zp) {
+  double w = cz * zm;
+  w = w + cy * ym;
+  w = w + cx * xm;
+  w = w + cc * c;
+  w = w + cx * xp;
+  w = w + cy * yp;
+  w = w + cz * zp;
+  return w;
+}
+
+// DPP moves of a double: row shifts by N lanes within 16-lane rows (N = 0: the value itself)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <int N>
+__device__ __forceinline__ double dpp_row_shl(double v) {  // lane l <- lane l + N
+  if constexpr (N == 0) return v;
+  else return dpp_d<0x100 + N>(v);
+}
+template <int N>
+__device__ __forceinline__ double dpp_row_shr(double v) {  // lane l <- lane l - N
+  if constexpr (N == 0) return v;
+  else return dpp_d<0x110 + N>(v);
+}
+// wave shifts by one lane that keep `old` where the source lane is outside the wave (lane 0 for
+// shr, lane 63 for shl)
+template <int CTRL>
+__device__ __forceinline__ double dpp_keep(double old, double v) {
+  const long long b = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, old);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_shr1_keep(double old, double v) {  // lane l <- lane l-1
+  return dpp_keep<0x138>(old, v);
+}
+__device__ __forceinline__ double dpp_shl1_keep(double old, double v) {  // lane l <- lane l+1
+  return dpp_keep<0x130>(old, v);
+}
+
+static constexpr unsigned kOob = 0x80000000u;  // a store offset past every plane: dropped
+
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_pair(__amdgpu_buffer_rsrc_t rs, unsigned off,
+                                           const double (&v)[2]) {
+  const dv2 d{v[0], v[1]};
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, d), rs, (int)off, 0, 0);
+}
+
+template <int NW, int TY>
+struct SrLds {
+  dv2 xch[2][4][NW][64];  // [step parity][p row 0, p row TY-1, t row 0, t row TY-1][wave][lane]
+  double xh[2][NW][64];   // [step parity][wave][lane]: the halo lanes' p
 };
 
-template <int NW, int TY, bool XU>
+template <int NW, int TY>
 __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, double cz,
                                           double cc, const double* __restrict__ r,
                                           const double* __restrict__ p_old,
                                           double* __restrict__ p_new, double* __restrict__ r_out,
                                           double dinv, double shift, double bb, double alpha,
-                                          const SrX& xu, const double (&xa)[3], int seg,
-                                          int tile, int kb, int ke,
-                                          dv2 (&xch)[2][4][NW][64], double (&acc)[5]) {
+                                          int seg, int tile, int kb, int ke, SrLds<NW, TY>& L,
+                                          double (&acc)[5]) {
   constexpr int RB = NW * TY;
   constexpr int SB = RB - 4;
+  // register ring slots: plane loads D = U - 2 steps ahead of the step that forms p from them.
+  // U = 3 (one step ahead) fits the 256-register budget; at U = 4 the x-halo registers spill
+  // (two-step prefetch measured within noise before the halo lanes: 0.86-0.93 vs 0.87-0.90 ms)
+  constexpr int U = 3;
+  constexpr int D = U - 2;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nx = g.nx, ny = g.ny, nz = g.nzl;
   const int g0 = tile * SB - 2;  // global row of block row 0
   const int br0 = wid * TY;
   const int j0 = g0 + br0;
   auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
-  const int o = seg * kSrSegOut + 2 * (lane - kSrLead);  // this lane's pair (output index)
-  const int ip = wrap(o, nx);  // (nx even: a pair never straddles the wrap)
-  const bool out_ok = lane >= kSrLead && lane < kSrLead + kSrSegOut / 2 && o < nx;
+  const int x0 = seg * kSrSeg;
+  const int o = x0 + 2 * lane;  // this lane's pair
+  const int ip = wrap(o, nx);   // (nx even: a pair never straddles the wrap)
+  const bool out_ok = o < nx;
+  const bool left = lane < 32;  // halo pair: left (x0 - 2, x0 - 1) or right (x0 + 128, x0 + 129)
+  const int qh = left ? lane % TY : (lane - (64 - TY)) % TY;  // the halo lane's row (other lanes: any)
+  const int ih = wrap(left ? x0 - 2 : x0 + kSrSeg, nx);
   int64_t ro[TY];
   unsigned row_ok = 0;
 #pragma unroll
@@ -78,82 +153,153 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
     if (out_ok && brow >= 2 && brow < RB - 2 && g0 + brow < ny) row_ok |= 1u << q;
   }
   const unsigned boff = (unsigned)ip * 8u;
-  auto rix = [&](int64_t row) { return RowIx{row, boff}; };
   auto pl = [&](int kk) -> int64_t { return (int64_t)wrap(kk, nz) * g.plane; };
+  // stores: buffer stores through a descriptor of the plane (out-of-range offsets are dropped by
+  // the range check), so that no store sits under a branch -- control flow in the step made the
+  // compiler's wait counts drain the two-plane prefetch
+  unsigned roff[TY];
+#pragma unroll
+  for (int q = 0; q < TY; ++q) roff[q] = (unsigned)(ro[q] * 8) + boff;
+  const int pbytes = (int)(g.plane * 8);
+  auto plane_rsrc = [&](double* base, int kk) {
+    // (inputs readfirstlane'd: a descriptor the compiler cannot prove uniform is waterfall'd)
+    const uint64_t a = (uint64_t)(base + pl(kk));
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a),
+                   hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    void* pa = (void*)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(pa, (short)0, __builtin_amdgcn_readfirstlane(pbytes),
+                                             0x00020000);
+  };
+  unsigned hoff = 0;  // the halo lane's byte offset in a plane
+#pragma unroll
+  for (int q = 0; q < TY; ++q)
+    if (qh == q) hoff = (unsigned)((ro[q] + ih) * 8);
+  // LDS lanes of the halo rows TY-1 (read by row 0) and 0 (read by row TY-1), same side
+  const int hl_lo = left ? TY - 1 : 63, hl_hi = left ? 0 : 64 - TY;
   const int wm = wid > 0 ? wid - 1 : wid, wp = wid < NW - 1 ? wid + 1 : wid;
+  // halo pair: inner point (next to the segment) and outer point
+  auto inner = [&](const double (&v)[2]) { return left ? v[1] : v[0]; };  // next to the segment
+  auto outer = [&](const double (&v)[2]) { return left ? v[0] : v[1]; };
 
-  // rings of four register slots whose roles rotate with the unrolled step (no copies):
-  double P[4][TY][2];   // p of planes k, k+1, k+2 at slots Q, Q+1, Q+2
-  double R[4][TY][2];   // r of planes k+1 .. k+3 at slots Q+1 .. Q+3; slot Q receives plane k+4
-  double T[4][TY][2];   // t of planes k-1, k, k+1 at slots Q, Q+1, Q+2
-  double PO[4][TY][2];  // p_old of planes k+2, k+3 at slots Q+2, Q+3; slot Q receives k+4
+  // rings of U register slots whose roles rotate with the unrolled step (no copies); *H = the
+  // halo lanes' pairs
+  double P[U][TY][2], PH[U][2];    // p of planes k, k+1, k+2 at slots Q, Q+1, Q+2
+  double R[U][TY][2], RH[U][2];    // r of planes k+1 .. k+1+D; slot Q receives plane k+2+D
+  double T[U][TY][2], TH[U];       // t of planes k-1, k, k+1 (halo: inner point only)
+  double PO[U][TY][2], POH[U][2];  // p_old of planes k+2 .. k+1+D; slot Q receives k+2+D
 #pragma unroll
-  for (int s = 0; s < 4; ++s)
+  for (int s = 0; s < U; ++s) {
+    TH[s] = 0.0;
 #pragma unroll
-    for (int q = 0; q < TY; ++q)
+    for (int e = 0; e < 2; ++e) {
+      PH[s][e] = RH[s][e] = POH[s][e] = 0.0;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) P[s][q][e] = R[s][q][e] = T[s][q][e] = PO[s][q][e] = 0.0;
-  auto ld = [&](const double* src, int kk, double (&dst)[TY][2]) {
+      for (int q = 0; q < TY; ++q) P[s][q][e] = R[s][q][e] = T[s][q][e] = PO[s][q][e] = 0.0;
+    }
+  }
+  auto ld = [&](const double* src, int kk, double (&dst)[TY][2], double (&dsth)[2]) {
     const int64_t base = pl(kk);
 #pragma unroll
-    for (int q = 0; q < TY; ++q) load_row<2>(src, rix(base + ro[q]), dst[q]);
+    for (int q = 0; q < TY; ++q) load_row<2>(src, RowIx{base + ro[q], boff}, dst[q]);
+    load_row<2>(src, RowIx{base, hoff}, dsth);
   };
-  // the first step (k = kb - 4, Q = 0) forms p(kb - 2); plane kb - 1 is in flight
-  ld(r, kb - 2, R[2]);
-  ld(p_old, kb - 2, PO[2]);
-  ld(r, kb - 1, R[3]);
-  ld(p_old, kb - 1, PO[3]);
+  // Cross-lane moves are DPP only (row shifts within a 16-lane row, wave shifts by one) and every
+  // choice a per-lane select: a readlane under a per-lane condition becomes a branch, and any
+  // control flow in the step drains the prefetch (the compiler's wait counts merge at joins).
+  // the segment's edge value of row q (lane 0's first / lane 63's second point) in the halo lanes
+  auto edge = [&](const double (&v)[TY][2]) {
+    double e = 0.0;
+    unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const double a = dpp_row_shr<q>(v[q][0]);            // lane q <- lane 0
+      const double b = dpp_row_shl<TY - 1 - q>(v[q][1]);   // lane 64 - TY + q <- lane 63
+      e = qh == q ? (left ? a : b) : e;
+    });
+    return e;
+  };
+  // x-neighbours of row q's pairs: lane 0's left and lane 63's right come from the halo lanes
+  // (wave shifts keep the old value where the source lane is outside the wave)
+  auto x_lo = [&](const double (&pair)[2], double hv, auto qc) {
+    constexpr int q = decltype(qc)::value;
+    return dpp_shr1_keep(dpp_row_shl<q>(hv), pair[1]);  // lane 0 <- halo lane q
+  };
+  auto x_hi = [&](const double (&pair)[2], double hv, auto qc) {
+    constexpr int q = decltype(qc)::value;
+    return dpp_shl1_keep(dpp_row_shr<TY - 1 - q>(hv), pair[0]);  // lane 63 <- 64 - TY + q
+  };
+  // the first step (k = kb - 4, Q = 0) forms p(kb - 2); planes kb - 1 .. kb - 3 + D are in flight
+#pragma unroll
+  for (int m = 0; m < D; ++m) {
+    ld(r, kb - 2 + m, R[(2 + m) % U], RH[(2 + m) % U]);
+    ld(p_old, kb - 2 + m, PO[(2 + m) % U], POH[(2 + m) % U]);
+  }
 
   auto body = [&](auto Qc, int k) {
     constexpr int Q = decltype(Qc)::value;
+    constexpr int Q1 = (Q + 1) % U, Q2 = (Q + 2) % U;
     double (&pk)[TY][2] = P[Q];
-    double (&pk1)[TY][2] = P[(Q + 1) & 3];
-    double (&pk2)[TY][2] = P[(Q + 2) & 3];
-    double (&rk1)[TY][2] = R[(Q + 1) & 3];
-    double (&rk2)[TY][2] = R[(Q + 2) & 3];
+    double (&pk1)[TY][2] = P[Q1];
+    double (&pk2)[TY][2] = P[Q2];
+    double (&hk)[2] = PH[Q];
+    double (&hk1)[2] = PH[Q1];
+    double (&hk2)[2] = PH[Q2];
     double (&tkm)[TY][2] = T[Q];
-    double (&tk)[TY][2] = T[(Q + 1) & 3];
-    double (&tk1)[TY][2] = T[(Q + 2) & 3];
-    // planes k+4 in flight for two steps (plane k+3's loads are already on their way)
-    ld(r, k + 4, R[Q]);
-    ld(p_old, k + 4, PO[Q]);
-    // x-update operands of plane k+2 (consumed at the end of this step)
-    double XX[XU ? TY : 1][2], M2[XU ? TY : 1][2], M3[XU ? TY : 1][2];
-    if constexpr (XU) {
-      ld(xu.x, k + 2, XX);
-      ld(xu.pm2, k + 2, M2);
-      ld(xu.pm3, k + 2, M3);
-    }
-    // p(k+2) = (dinv r - mu) + b p_old (CombineLoad::f)
+    double (&tk)[TY][2] = T[Q1];
+    double (&tk1)[TY][2] = T[Q2];
+    // planes k+2+D in flight for D steps
+    ld(r, k + 2 + D, R[Q], RH[Q]);
+    ld(p_old, k + 2 + D, PO[Q], POH[Q]);
+    // p(k+2) = (dinv r - mu) + b p_old (CombineLoad::f), halo pair included
 #pragma unroll
     for (int q = 0; q < TY; ++q)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        double z = dinv * rk2[q][e];
+        double z = dinv * R[Q2][q][e];
         z = z + shift;
-        pk2[q][e] = z + bb * PO[(Q + 2) & 3][q][e];
+        pk2[q][e] = z + bb * PO[Q2][q][e];
       }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      double zh = dinv * RH[Q2][e];
+      zh = zh + shift;
+      hk2[e] = zh + bb * POH[Q2][e];
+    }
     __syncthreads();
     // rows -1 / TY of p(k+1) and t(k): published by the neighbouring waves at step k-1
     const int rp = (k + 1) & 1, cur = k & 1;
-    const dv2 phl = xch[rp][1][wm][lane], phh = xch[rp][0][wp][lane];
-    const dv2 thl = xch[rp][3][wm][lane], thh = xch[rp][2][wp][lane];
-    xch[cur][0][wid][lane] = dv2{pk2[0][0], pk2[0][1]};
-    xch[cur][1][wid][lane] = dv2{pk2[TY - 1][0], pk2[TY - 1][1]};
+    const dv2 phl = L.xch[rp][1][wm][lane], phh = L.xch[rp][0][wp][lane];
+    const dv2 thl = L.xch[rp][3][wm][lane], thh = L.xch[rp][2][wp][lane];
+    const double hhl = L.xh[rp][wm][hl_lo], hhh = L.xh[rp][wp][hl_hi];
+    L.xch[cur][0][wid][lane] = dv2{pk2[0][0], pk2[0][1]};
+    L.xch[cur][1][wid][lane] = dv2{pk2[TY - 1][0], pk2[TY - 1][1]};
+    L.xh[cur][wid][lane] = inner(hk2);
     const bool in2 = k + 2 >= kb && k + 2 < ke, in1 = k + 1 >= kb && k + 1 < ke,
                in0 = k >= kb && k < ke;
-    if (in2) {
-      const int64_t base = pl(k + 2);
+    {
+      const auto rs = plane_rsrc(p_new, k + 2);
 #pragma unroll
       for (int q = 0; q < TY; ++q)
-        if (row_ok >> q & 1u) store_row<2>(p_new, rix(base + ro[q]), pk2[q], g.nt);
+        store_pair(rs, in2 && (row_ok >> q & 1u) ? roff[q] : kOob, pk2[q]);
     }
-    // w(k+1) = A p (z-, y-, x-, c, x+, y+, z+), r' = r - alpha w, t = dinv r' - mu
-    const int64_t base1 = pl(k + 1);
-#pragma unroll
-    for (int q = 0; q < TY; ++q) {
-      const double lo = dpp_from_lower(pk1[q][1]);
-      const double hi = dpp_from_upper(pk1[q][0]);
+    // w(k+1) = A p, r' = r - alpha w, t = dinv r' - mu: the halo lanes' inner points first
+    const double hc = inner(hk1);
+    {
+      const double eg = edge(pk1);
+      const double xm = left ? outer(hk1) : eg;
+      const double xp = left ? eg : outer(hk1);
+      const double dl = dpp_from_lower(hc), du = dpp_from_upper(hc);
+      const double ym = qh == 0 ? hhl : dl;
+      const double yp = qh == TY - 1 ? hhh : du;
+      const double w = star7_sum(cx, cy, cz, cc, inner(hk), ym, xm, hc, xp, yp, inner(hk2));
+      const double rv = inner(RH[Q1]) + (-alpha) * w;
+      const double z = dinv * rv;
+      TH[Q2] = z + shift;
+    }
+    const auto rs1 = plane_rsrc(r_out, k + 1);
+    unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const double lo = x_lo(pk1[q], hc, qc);
+      const double hi = x_hi(pk1[q], hc, qc);
       double rv[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -161,104 +307,68 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
         const double xp = e == 1 ? hi : pk1[q][1];
         const double ym = q == 0 ? phl[e] : pk1[q == 0 ? 0 : q - 1][e];
         const double yp = q == TY - 1 ? phh[e] : pk1[q == TY - 1 ? q : q + 1][e];
-        double w = cz * pk[q][e];
-        w = w + cy * ym;
-        w = w + cx * xm;
-        w = w + cc * pk1[q][e];
-        w = w + cx * xp;
-        w = w + cy * yp;
-        w = w + cz * pk2[q][e];
-        rv[e] = rk1[q][e] + (-alpha) * w;
+        const double w = star7_sum(cx, cy, cz, cc, pk[q][e], ym, xm, pk1[q][e], xp, yp, pk2[q][e]);
+        rv[e] = R[Q1][q][e] + (-alpha) * w;
         double z = dinv * rv[e];
         tk1[q][e] = z + shift;
       }
-      if (in1 && (row_ok >> q & 1u)) {
-        store_row<2>(r_out, rix(base1 + ro[q]), rv, g.nt);
+      const bool ok = in1 && (row_ok >> q & 1u);
+      store_pair(rs1, ok ? roff[q] : kOob, rv);
+      // summands times 1 or 0 (exact; no branch): a zero of either sign leaves a sum unchanged
+      const double m = ok ? 1.0 : 0.0;
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const double t = tk1[q][e];
-          acc[0] += t;
-          acc[1] += t * t;
-          acc[2] += t * rv[e];
-          acc[3] += rv[e];
-        }
+      for (int e = 0; e < 2; ++e) {
+        const double t = tk1[q][e];
+        acc[0] += t * m;
+        acc[1] += (t * t) * m;
+        acc[2] += (t * rv[e]) * m;
+        acc[3] += rv[e] * m;
       }
-    }
-    xch[cur][2][wid][lane] = dv2{tk1[0][0], tk1[0][1]};
-    xch[cur][3][wid][lane] = dv2{tk1[TY - 1][0], tk1[TY - 1][1]};
+    });
+    L.xch[cur][2][wid][lane] = dv2{tk1[0][0], tk1[0][1]};
+    L.xch[cur][3][wid][lane] = dv2{tk1[TY - 1][0], tk1[TY - 1][1]};
     // s(k) = A t, delta sum t.s
-    if (in0) {
+    unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const double lo = x_lo(tk[q], TH[Q1], qc);
+      const double hi = x_hi(tk[q], TH[Q1], qc);
+      const double m = in0 && (row_ok >> q & 1u) ? 1.0 : 0.0;
 #pragma unroll
-      for (int q = 0; q < TY; ++q) {
-        const double lo = dpp_from_lower(tk[q][1]);
-        const double hi = dpp_from_upper(tk[q][0]);
-        if (row_ok >> q & 1u) {
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const double xm = e == 0 ? lo : tk[q][0];
-            const double xp = e == 1 ? hi : tk[q][1];
-            const double ym = q == 0 ? thl[e] : tk[q == 0 ? 0 : q - 1][e];
-            const double yp = q == TY - 1 ? thh[e] : tk[q == TY - 1 ? q : q + 1][e];
-            double sv = cz * tkm[q][e];
-            sv = sv + cy * ym;
-            sv = sv + cx * xm;
-            sv = sv + cc * tk[q][e];
-            sv = sv + cx * xp;
-            sv = sv + cy * yp;
-            sv = sv + cz * tk1[q][e];
-            acc[4] += tk[q][e] * sv;
-          }
-        }
+      for (int e = 0; e < 2; ++e) {
+        const double xm = e == 0 ? lo : tk[q][0];
+        const double xp = e == 1 ? hi : tk[q][1];
+        const double ym = q == 0 ? thl[e] : tk[q == 0 ? 0 : q - 1][e];
+        const double yp = q == TY - 1 ? thh[e] : tk[q == TY - 1 ? q : q + 1][e];
+        const double sv = star7_sum(cx, cy, cz, cc, tkm[q][e], ym, xm, tk[q][e], xp, yp, tk1[q][e]);
+        acc[4] += (tk[q][e] * sv) * m;
       }
-    }
-    if constexpr (XU) {  // x(k+2) += a3 p_{i-3} + a2 p_{i-2} + a1 p_{i-1} + alpha p_i
-      if (in2) {
-        const int64_t base = pl(k + 2);
-#pragma unroll
-        for (int q = 0; q < TY; ++q) {
-          double xv[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            double u = xa[0] * M3[q][e];
-            u = u + xa[1] * M2[q][e];
-            u = u + xa[2] * PO[(Q + 2) & 3][q][e];
-            u = u + alpha * pk2[q][e];
-            xv[e] = XX[q][e] + u;
-          }
-          if (row_ok >> q & 1u) store_row<2>(xu.x, rix(base + ro[q]), xv, g.nt);
-        }
-      }
-    }
+    });
   };
-  // steps kb-4 .. ke-1 (padded to whole four-step rounds: the spare steps store and sum nothing)
+  // steps kb-4 .. ke-1 (padded to whole rounds of U steps: the spare steps store and sum nothing)
 #pragma unroll 1
-  for (int k = kb - 4; k < ke; k += 4) {
-    body(std::integral_constant<int, 0>{}, k);
-    body(std::integral_constant<int, 1>{}, k + 1);
-    body(std::integral_constant<int, 2>{}, k + 2);
-    body(std::integral_constant<int, 3>{}, k + 3);
-  }
+  for (int k = kb - 4; k < ke; k += U)
+    unroll_steps(std::make_integer_sequence<int, U>{},
+                 [&](auto Qc) { body(Qc, k + decltype(Qc)::value); });
 }
 
-template <int NW, int TY, bool XU>
+template <int NW, int TY>
 __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, double cy, double cz,
                                                          double cc, const double* __restrict__ r,
                                                          const double* __restrict__ p_old,
                                                          double* __restrict__ p_new,
-                                                         double* __restrict__ r_out, SrX xu,
+                                                         double* __restrict__ r_out,
                                                          double* parts, Fold fold) {
-  __shared__ dv2 xch[2][4][NW][64];
+  __shared__ SrLds<NW, TY> lds;
   CgState st;
   fold_prologue(fold, st);  // every wave: the previous residual-sum stage + this iteration's top
   if (st.done) return;      // (uniform: every wave computed the same state)
   const double dinv = st.dinv, shift = -st.mu, bb = st.bbp, alpha = st.alpha;
-  const double xa[3] = {st.pa[0], st.pa[1], st.pa[2]};  // pending alphas of i-3, i-2, i-1
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   const int bid = xcd_block(g.remap);
   const int ncol = g.nseg * g.ntile, W = g.W, T = g.nzl / W;
   auto run = [&](int col, int kb, int ke) {
-    sr1_range<NW, TY, XU>(g, cx, cy, cz, cc, r, p_old, p_new, r_out, dinv, shift, bb, alpha, xu,
-                          xa, col % g.nseg, col / g.nseg, kb, ke, xch, acc);
+    sr1_range<NW, TY>(g, cx, cy, cz, cc, r, p_old, p_new, r_out, dinv, shift, bb, alpha,
+                      col % g.nseg, col / g.nseg, kb, ke, lds, acc);
   };
   if (bid < T * ncol) {  // bands of W planes of every column
     const int kb = (bid / ncol) * W;
@@ -283,24 +393,25 @@ __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, dou
 
 
 bool cg_sr1_supported(const pb_grid* g) {
-  return !g->ctx->split && g->n[0] % 2 == 0 && tune("cg_sr_fused", 1) != 0;
+  // (plane byte offsets in 31 bits: buffer-store descriptors per plane)
+  return !g->ctx->split && g->n[0] % 2 == 0 && g->plane * 8 < ((int64_t)1 << 31) &&
+         tune("cg_sr_fused", 1) != 0;
 }
 
-template <int NW, int TY>
-static int launch_sr1_t(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                        double* p_new, double* r_out, const SrX* xu, const SrFold& sf,
-                        const double* parts_in, double* parts_out, int64_t host_iter,
-                        int* nblocks) {
+int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_old,
+                  double* p_new, double* r_out, const SrFold& sf, const double* parts_in,
+                  double* parts_out, int64_t host_iter, int* nblocks) {
+  constexpr int NW = 8, TY = 2;  // 8 waves of 2 rows: two waves per SIMD, one block per CU
   pb_ctx* ctx = g->ctx;
+  ScopedTimer tm(ctx, "cg_sr1");
   SrGeo geo;
   geo.nx = (int)g->n[0];
   geo.ny = (int)g->n[1];
   geo.nzl = (int)g->nzl;
   geo.plane = g->plane;
-  geo.nseg = (geo.nx + kSrSegOut - 1) / kSrSegOut;
+  geo.nseg = (geo.nx + kSrSeg - 1) / kSrSeg;
   geo.ntile = (geo.ny + NW * TY - 5) / (NW * TY - 4);
   geo.remap = 1;
-  geo.nt = 1;
   const int64_t work = (int64_t)geo.nseg * geo.ntile * geo.nzl;  // column-planes
   const int64_t want = (int64_t)(ctx->num_cus);
   geo.W = (int)std::max<int64_t>(1, (work + want - 1) / want);
@@ -317,37 +428,11 @@ static int launch_sr1_t(pb_grid* g, const Star& s, const double* r, const double
   f.hist = sf.hist;
   f.h_done = sf.h_done;
   f.host_iter = host_iter - 1;
-  if (xu)
-    hipLaunchKernelGGL((cg_sr1_kernel<NW, TY, true>), dim3((unsigned)nb), dim3(64 * NW), 0,
-                       ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out, *xu,
-                       parts_out, f);
-  else
-    hipLaunchKernelGGL((cg_sr1_kernel<NW, TY, false>), dim3((unsigned)nb), dim3(64 * NW), 0,
-                       ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out,
-                       SrX{nullptr, nullptr, nullptr}, parts_out, f);
+  hipLaunchKernelGGL((cg_sr1_kernel<NW, TY>), dim3((unsigned)nb), dim3(64 * NW), 0, ctx->stream,
+                     geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out, parts_out, f);
   PB_HIP(hipGetLastError());
   *nblocks = (int)nb;
   return PB_OK;
-}
-
-int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                  double* p_new, double* r_out, double* x, const double* p_m2, const double* p_m3,
-                  const SrFold& sf, const double* parts_in, double* parts_out, int64_t host_iter,
-                  int* nblocks) {
-  ScopedTimer tm(g->ctx, x ? "cg_sr1_x4" : "cg_sr1");
-  const SrX xv{x, p_m2, p_m3};
-  const SrX* xu = x ? &xv : nullptr;
-  switch (tune("cg_sr_shape", 0)) {
-    case 1:  // 12 waves of 2 rows: three waves per SIMD
-      return launch_sr1_t<12, 2>(g, s, r, p_old, p_new, r_out, xu, sf, parts_in, parts_out,
-                                 host_iter, nblocks);
-    case 3:
-      return launch_sr1_t<8, 3>(g, s, r, p_old, p_new, r_out, xu, sf, parts_in, parts_out,
-                                host_iter, nblocks);
-    default:  // 8 waves of 2 rows: two waves per SIMD
-      return launch_sr1_t<8, 2>(g, s, r, p_old, p_new, r_out, xu, sf, parts_in, parts_out,
-                                host_iter, nblocks);
-  }
 }
 
 }  // namespace pb

@@ -399,8 +399,7 @@ bool cg_sr1_supported(const pb_grid* g);
 // x != nullptr: the iteration also carries the depth-4 deferred x update (p_m2, p_m3 = p_{i-2},
 // p_{i-3}; p_{i-1} is p_old)
 int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                  double* p_new, double* r_out, double* x, const double* p_m2, const double* p_m3,
-                  const SrFold& sf, const double* parts_in, double* parts_out, int64_t host_iter,
+                  double* p_new, double* r_out, const SrFold& sf, const double* parts_in, double* parts_out, int64_t host_iter,
                   int* nblocks);
 
 // ---- compact fast path + generic CG (pb_compact_fast.hip) ----

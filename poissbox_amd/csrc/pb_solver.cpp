@@ -595,12 +595,10 @@ static int enqueue_sr_iteration(pb_ksp* k, bool fold, int64_t n) {
   f.hist = k->d_hist;
   f.h_done = k->h_done_dev;
   StencilPlanes gp;
-  // one pass per iteration where it applies: one rank, depth-4 x deferral (every 4th iteration
-  // the pass also updates x)
-  if (cg_sr1_supported(g) && k->defer_x == 4) {
-    const bool xu = i % 4 == 3;
-    PB_TRY(launch_cg_sr1(g, s, r, p_prev[0], p_new, r_out, xu ? k->x->d : nullptr, p_prev[1],
-                         p_prev[2], f, f.parts, const_cast<double*>(sr_region(ctx, n)), i,
+  // one pass per iteration where it applies: one rank, depth-4 x deferral; the iterations that
+  // carry the x update run the two passes (pass P's x-update form streams at the copy rate)
+  if (cg_sr1_supported(g) && k->defer_x == 4 && i % 4 != 3) {
+    PB_TRY(launch_cg_sr1(g, s, r, p_prev[0], p_new, r_out, f, f.parts, const_cast<double*>(sr_region(ctx, n)), i,
                          &k->sr_nparts));
     if (!fold)
       PB_TRY(cg_sr_finalize(ctx, sr_region(ctx, n), k->sr_nparts, st_out, k->d_hist,

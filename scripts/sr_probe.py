@@ -10,7 +10,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import poissbox_amd as pb  # noqa: E402
 
-PASSES = ("cg_pass_a", "cg_pass_b_even", "cg_pass_b_x4", "cg_sr_p", "cg_sr_p_x4", "cg_sr_s", "cg_sr1")
+PASSES = ("cg_pass_a", "cg_pass_b_even", "cg_pass_b_x4", "cg_sr_p", "cg_sr_p_x4", "cg_sr_s", "cg_sr1", "cg_sr1_x4")
 
 
 def run(ctx, n, sr, steps=100, warmup=12, diag=16):
@@ -56,7 +56,7 @@ def main():
     sizes = [int(a) for a in args if a.isdigit()] or [512, 256]
     ctx = pb.Context(0)
     for n in sizes:
-        for rep in range(3):
+        for rep in range(int(os.environ.get("SR_REPS", "3"))):
             for c in (combos or [None]):
                 for sr in ((1,) if combos else (0, 1)):
                     pb.tune_reset()
