@@ -314,7 +314,9 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       }
       const bool ok = in1 && (row_ok >> q & 1u);
       store_pair(rs1, ok ? roff[q] : kOob, rv);
-      // summands times 1 or 0 (exact; no branch): a zero of either sign leaves a sum unchanged
+      // summands times 1 or 0 (exact; no branch -- selects here became branches and spills):
+      // a zero of either sign leaves a sum unchanged. Masked rows hold finite values: real data,
+      // zero-initialised registers and the zeroed LDS exchange (a NaN there would survive x 0)
       const double m = ok ? 1.0 : 0.0;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -362,6 +364,13 @@ __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, dou
   CgState st;
   fold_prologue(fold, st);  // every wave: the previous residual-sum stage + this iteration's top
   if (st.done) return;      // (uniform: every wave computed the same state)
+  {  // zero the exchange: warm-up steps read it before any wave wrote it (stale LDS of earlier
+     // kernels, possibly NaN, which the masked sums' factor 0 would not cancel); the first step's
+     // barrier orders these stores before every read
+    double* z = reinterpret_cast<double*>(&lds);
+    constexpr int nd = (int)(sizeof(SrLds<NW, TY>) / sizeof(double));
+    for (int i = threadIdx.x; i < nd; i += 64 * NW) z[i] = 0.0;
+  }
   const double dinv = st.dinv, shift = -st.mu, bb = st.bbp, alpha = st.alpha;
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   const int bid = xcd_block(g.remap);

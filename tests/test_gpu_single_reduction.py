@@ -58,6 +58,27 @@ def test_single_reduction_matches_oracle(ctx, n3, rtol):
     check_x(xs, xo)
 
 
+def test_single_reduction_after_nan_in_lds(ctx):
+    """The one-pass kernel's warm-up steps read its LDS row exchange before any wave wrote it:
+    stale LDS of an earlier kernel (here the spectral PC's tiles, fed NaN) must not reach the
+    sums (a 16^3 solve once stopped at its 1, reason ATOL, after 380 other GPU tests)."""
+    n3 = (16, 16, 16)
+    h, b = _case(n3)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-5, single_reduction=1)
+    for _ in range(2):
+        m = (64, 64, 64)
+        da = pb.DA(ctx, m, (2 * np.pi,) * 3)
+        P = pb.Mat(da, pb.COMPACT, tuple(2 * np.pi / v for v in m))
+        k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
+        rv, zv = pb.Vec(da), pb.Vec(da)
+        rv.set_values(np.full(int(np.prod(m)), np.nan))
+        k.pc_apply(rv, zv)
+        k.destroy()
+        reason, its, hist, xs = _solve(ctx, n3, h, b, SR + ["-ksp_rtol", "1e-5"])
+        assert (reason, its) == (ro, itso)
+        check_history(hist, ho)
+
+
 @pytest.mark.parametrize("defer", ["0", "2", "4"])
 @pytest.mark.parametrize("max_it", [1, 2, 3, 4, 5, 8, 9, 11])
 def test_single_reduction_deferred_x_max_it(ctx, defer, max_it, tune):
@@ -178,6 +199,8 @@ def test_single_reduction_full_256(ctx):
 @pytest.mark.parametrize("nranks,n", [(2, (16, 16, 12)), (3, (16, 16, 12)), (3, (20, 16, 7)),
                                        # 1- and 2-plane slabs (no interior launch)
                                        (4, (16, 12, 6)),
+                                       # config 4's rank count (two-plane slabs)
+                                       (8, (16, 16, 16)),
                                        (2, (512, 512, 12))])
 def test_multirank_single_reduction(nranks, n):
     """N ranks (host transport, one GPU): p's boundary planes and r''s raw boundary planes are
