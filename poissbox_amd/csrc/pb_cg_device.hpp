@@ -249,7 +249,7 @@ __device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st) {
       cg_stage2(st, S, lead ? f.hist : nullptr, lead ? f.h_done : nullptr, f.host_iter);
     cg_sr_top(st);
   }
-  if (lead) cg_copy(*f.out, st);
+  if (lead && f.out) cg_copy(*f.out, st);  // (out null: the state in registers only)
 }
 
 }  // namespace pb

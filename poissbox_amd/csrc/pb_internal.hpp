@@ -10,6 +10,7 @@
 #include <deque>
 #include <map>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "poissbox_gpu.h"
@@ -77,6 +78,7 @@ struct pb_ctx {
   bool split = false;
   hipStream_t stream = nullptr;
   hipStream_t comm_stream = nullptr;  // RCCL halo exchange, overlapped with interior planes
+  hipStream_t engine_stream = nullptr;  // stencil-engine launches go here when set (EngineOn)
   hipEvent_t ev_ready = nullptr, ev_done = nullptr;
   ncclComm_t comm = nullptr;
   // bounded waits on split contexts (a dead or stalled peer must surface as PB_ERR_COMM, not a
@@ -188,6 +190,13 @@ void timers_collect(pb_ctx* ctx);
 
 bool timer_wanted(pb_ctx* ctx, const char* name);
 
+// stencil-engine launches of this scope go to stream s instead of the context stream
+struct EngineOn {
+  pb_ctx* ctx;
+  EngineOn(pb_ctx* c, hipStream_t s) : ctx(c) { ctx->engine_stream = s; }
+  ~EngineOn() { ctx->engine_stream = nullptr; }
+};
+
 struct ScopedTimer {
   pb_ctx* ctx;
   const char* name;
@@ -211,6 +220,10 @@ int halo_exchange(pb_grid* g, const double* lo, const double* hi);
 // Split form: begin (RCCL on the context's comm stream after an event on the compute stream;
 // host transport: synchronous), end (compute stream waits for the exchange).
 int halo_begin(pb_grid* g, const double* lo, const double* hi);
+// halo_begin with the boundary planes produced on the comm stream first (RCCL split grids): pre
+// enqueues their kernel on the given stream after the context stream's work so far
+int halo_begin_after(pb_grid* g, const double* lo, const double* hi,
+                     const std::function<int(hipStream_t)>& pre);
 // np-plane exchange into explicit buffers: send the np planes at `lo` (first owned) to rank-1
 // and at `hi` (last owned) to rank+1; rlo receives the np planes below the slab (from rank-1),
 // rhi the np planes above it (from rank+1). Stream ordered; one rank: periodic copies.
@@ -323,10 +336,15 @@ struct Fold {
   int* h_done = nullptr;
   int64_t host_iter = 0;          // stage 2: the iteration whose stage 2 this is
 };
-// fold.stage = 2: the previous iteration's stage 2 in the prologue (split grids, folded iteration)
+// fold.stage = 2: the previous iteration's stage 2 in the prologue (split grids, folded iteration;
+// fold.out = nullptr: the state stays in registers). stream = nullptr: the context stream.
 int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st,
-                       const Fold& fold);
+                       const Fold& fold, hipStream_t stream = nullptr);
 int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st);
+// pass A launch (mode: PLANES_*) whose prologue runs fold (stage 2, split grids)
+int launch_cg_pass_a_fold(pb_grid* g, const Star& s, const double* r, const double* p_old,
+                          double* p_new, const StencilPlanes& gp, const Fold& fold, int mode,
+                          int part_off, int* nblocks, bool store);
 // split grids, folded iteration: a pass's partials reduced and allreduced into ctx->d_scalars
 int cg_reduce_allreduce(pb_ctx* ctx, int nparts, int width, bool b_region);
 int cg_reduce_allreduce(pb_ctx* ctx, const double* parts, int nparts, int width);

@@ -385,6 +385,37 @@ int halo_begin(pb_grid* g, const double* lo, const double* hi) {
   return PB_OK;
 }
 
+int halo_begin_after(pb_grid* g, const double* lo, const double* hi,
+                     const std::function<int(hipStream_t)>& pre) {
+  pb_ctx* ctx = g->ctx;
+  PB_COMM_OK(ctx);
+  if (!ctx->split || !ctx->comm) {
+    PB_TRY(pre(ctx->stream));
+    return halo_exchange(g, lo, hi);
+  }
+  PB_HIP(hipEventRecord(ctx->ev_ready, ctx->stream));
+  PB_HIP(hipStreamWaitEvent(ctx->comm_stream, ctx->ev_ready, 0));
+  PB_TRY(pre(ctx->comm_stream));
+  const int64_t cnt = g->plane;
+  const int down = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
+  const int up = (ctx->rank + 1) % ctx->nranks;
+  hipEvent_t tev = nullptr;
+  const bool timed = ctx->timing && timer_wanted(ctx, "halo_comm");
+  if (timed) timer_begin(ctx, "halo_comm", &tev, ctx->comm_stream);
+  {
+    CommScope cs(ctx, ctx->comm_stream);
+    PB_NCCL(ncclGroupStart());
+    PB_NCCL(ncclSend(lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
+    PB_NCCL(ncclRecv(g->ghost_hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
+    PB_NCCL(ncclSend(hi, (size_t)cnt, ncclDouble, up, ctx->comm, ctx->comm_stream));
+    PB_NCCL(ncclRecv(g->ghost_lo, (size_t)cnt, ncclDouble, down, ctx->comm, ctx->comm_stream));
+    PB_NCCL(ncclGroupEnd());
+  }
+  if (timed) timer_end(ctx, "halo_comm", tev, ctx->comm_stream);
+  PB_HIP(hipEventRecord(ctx->ev_done, ctx->comm_stream));
+  return PB_OK;
+}
+
 int halo_end(pb_grid* g) {
   pb_ctx* ctx = g->ctx;
   if (!ctx->split || !ctx->comm) return PB_OK;

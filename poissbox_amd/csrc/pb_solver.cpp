@@ -694,9 +694,10 @@ static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
                                    k->defer_x, &k->fold_nparts_b, ps);
   }
   if (fold_split) {
-    // split grids, folded (r05): the boundary-plane kernel runs the previous iteration's stage 2
-    // from pass B's allreduced sums (a one-block partial), pass B stage 1 from pass A's; only the
-    // reductions before each allreduce stay separate launches (bit-identical to unfolded)
+    // split grids, folded (r05): the previous iteration's stage 2 runs in the prologues of the
+    // boundary-plane kernel and pass A (from pass B's allreduced sums, a one-block partial), stage
+    // 1 in pass B's (from pass A's); only the reductions before each allreduce stay separate
+    // launches (bit-identical to unfolded)
     Fold fb;
     if (fold_a) {
       fb.stage = 2;
@@ -709,23 +710,50 @@ static int enqueue_iteration(pb_ksp* k, bool fold, bool fold_a) {
       fb.h_done = k->h_done_dev;
       fb.host_iter = i - 1;
     }
-    PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st, fb));
     gp.ghost_lo = g->ghost_lo;
     gp.ghost_hi = g->ghost_hi;
-    if (g->nzl < 3) {
+    if (g->nzl >= 3) {
+      // the boundary-plane kernel runs on the comm stream ahead of the exchange, beside pass A's
+      // interior planes, from the stage-2 state in its registers; pass A's interior launch runs the
+      // same stage 2 in its prologue and writes the state (the boundary launch reads it)
+      Fold fbr = fb;
+      fbr.out = nullptr;
+      fbr.hist = nullptr;
+      fbr.h_done = nullptr;
+      int nb1 = 0, nb2 = 0;
+      ScopedTimer tm(ctx, "cg_pass_a");
+      PB_TRY(halo_begin_after(g, g->bnd_lo, g->bnd_hi, [&](hipStream_t sm) {
+        return launch_cg_boundary(g, zsrc, p_old, k->d_st, fbr, sm);
+      }));
+      if (fold_a)
+        PB_TRY(launch_cg_pass_a_fold(g, s, zsrc, p_old, p_new, gp, fb, PLANES_INTERIOR, 0, &nb1,
+                                     store_a));
+      else
+        PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1,
+                                store_a));
+      if (ctx->comm) {
+        // the two boundary planes on the comm stream right after the exchange (beside the
+        // interior planes), from the stage-2 state in registers as well
+        EngineOn eo(ctx, ctx->comm_stream);
+        if (fold_a)
+          PB_TRY(launch_cg_pass_a_fold(g, s, zsrc, p_old, p_new, gp, fbr, PLANES_BOUNDARY, nb1,
+                                       &nb2, store_a));
+        else
+          PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1,
+                                  &nb2, store_a));
+        PB_HIP(hipEventRecord(ctx->ev_done, ctx->comm_stream));
+        PB_TRY(halo_end(g));
+      } else {
+        PB_TRY(halo_end(g));
+        PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1,
+                                &nb2, store_a));
+      }
+      nparts = nb1 + nb2;
+    } else {
+      PB_TRY(launch_cg_boundary(g, zsrc, p_old, k->d_st, fb));
       PB_TRY(halo_exchange(g, g->bnd_lo, g->bnd_hi));
       PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_ALL, 0, &nparts,
                               store_a));
-    } else {
-      int nb1 = 0, nb2 = 0;
-      ScopedTimer tm(ctx, "cg_pass_a");
-      PB_TRY(halo_begin(g, g->bnd_lo, g->bnd_hi));
-      PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_INTERIOR, 0, &nb1,
-                              store_a));
-      PB_TRY(halo_end(g));
-      PB_TRY(launch_cg_pass_a(g, s, zsrc, p_old, p_new, gp, k->d_st, PLANES_BOUNDARY, nb1, &nb2,
-                              store_a));
-      nparts = nb1 + nb2;
     }
     PB_TRY(cg_reduce_allreduce(ctx, nparts, 1, false));
     PB_TRY(launch_cg_pass_b_folded(g, s, p_new, p_prev, k->x->d, r, gp, k->d_st, 1, i,

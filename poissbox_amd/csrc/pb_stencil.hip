@@ -674,7 +674,8 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
     if (nblocks > (int64_t)w * g->ctx->num_cus) lds = kLdsPerCu / (size_t)(w + 1) + 4096;
   }
   hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads),
-                     lds, g->ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
+                     lds, g->ctx->engine_stream ? g->ctx->engine_stream : g->ctx->stream, geo, s.cx,
+                     s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
                      g->ctx->d_partials + (int64_t)part_off * NS, skip, fold);
   PB_HIP(hipGetLastError());
   if (nb_out) *nb_out = (int)nblocks;
@@ -914,6 +915,24 @@ __global__ __launch_bounds__(256) void cg_boundary_kernel(const double* __restri
                                                           double* __restrict__ lo,
                                                           double* __restrict__ hi,
                                                           const CgState* st, Fold fold) {
+  // the first PER points of both planes are loaded before the state (prologue) is ready: the
+  // loads do not depend on it, so their latency hides the prologue's (r05: 23.7 -> 13.3 us with
+  // one block per CU alone, at 512^2)
+  constexpr int PER = 4;
+  const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double vr[2][PER], vp[2][PER];
+  auto fetch = [&](int64_t base) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int64_t i = min(base + q * gs, plane - 1);  // (clamped: valid address, unused)
+      vr[0][q] = r[i];
+      vp[0][q] = p[i];
+      vr[1][q] = r[last_off + i];
+      vp[1][q] = p[last_off + i];
+    }
+  };
+  fetch(i0);
   CgState sst;
   if (fold.stage) {
     fold_prologue(fold, sst);
@@ -922,10 +941,16 @@ __global__ __launch_bounds__(256) void cg_boundary_kernel(const double* __restri
   if (st->done) return;
   CombineLoad c{r, p, nullptr, 0.0, 0.0, 0.0};
   c.prepare_from(*st);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < plane;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    lo[i] = c.one(i);
-    hi[i] = c.one(last_off + i);
+  for (int64_t base = i0; base < plane; base += PER * gs) {
+    if (base != i0) fetch(base);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int64_t i = base + q * gs;
+      if (i < plane) {
+        lo[i] = c.f(vr[0][q], vp[0][q]);
+        hi[i] = c.f(vr[1][q], vp[1][q]);
+      }
+    }
   }
 }
 
@@ -1013,13 +1038,20 @@ int launch_cg_init(pb_grid* g, const double* b, double* x, double* r, double* p,
 }
 
 int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState* st,
-                       const Fold& fold) {
+                       const Fold& fold, hipStream_t stream) {
   pb_ctx* ctx = g->ctx;
-  ScopedTimer tm(ctx, "cg_boundary");
-  const int nb = elementwise_blocks(ctx, g->plane);
-  hipLaunchKernelGGL(cg_boundary_kernel, dim3(nb), dim3(256), 0, ctx->stream, r, p_old, g->plane,
+  hipStream_t sm = stream ? stream : ctx->stream;
+  hipEvent_t tev = nullptr;
+  const bool timed = ctx->timing && timer_wanted(ctx, "cg_boundary");
+  if (timed) timer_begin(ctx, "cg_boundary", &tev, sm);
+  // one block per CU at most, four points of each plane per thread (every wave of the folded
+  // form runs the stage-2 prologue first)
+  const int nb = (int)std::max<int64_t>(
+      1, std::min<int64_t>(ctx->num_cus, (g->plane + 256 * 4 - 1) / (256 * 4)));
+  hipLaunchKernelGGL(cg_boundary_kernel, dim3(nb), dim3(256), 0, sm, r, p_old, g->plane,
                      (g->nzl - 1) * g->plane, g->bnd_lo, g->bnd_hi, (const CgState*)st, fold);
   PB_HIP(hipGetLastError());
+  if (timed) timer_end(ctx, "cg_boundary", tev, sm);
   return PB_OK;
 }
 
@@ -1063,6 +1095,18 @@ int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const do
     return launch_any(g, s, ld, gp, PassAT<false>{p_new}, nullptr, PLANES_ALL, 0, nblocks, 0,
                       0, f);
   return launch_any(g, s, ld, gp, PassA{p_new}, nullptr, PLANES_ALL, 0, nblocks, 0, 0, f);
+}
+
+int launch_cg_pass_a_fold(pb_grid* g, const Star& s, const double* r, const double* p_old,
+                          double* p_new, const StencilPlanes& gp, const Fold& fold, int mode,
+                          int part_off, int* nblocks, bool store) {
+  ScopedTimer tm(g->ctx,
+                 timer_name(mode, "cg_pass_a", "cg_pass_a_interior", "cg_pass_a_boundary"));
+  const CombineLoad ld{r, p_old, nullptr, 0.0, 0.0, 0.0};
+  if (!store)
+    return launch_any(g, s, ld, gp, PassAT<false>{p_new}, nullptr, mode, part_off, nblocks, 0, 0,
+                      fold);
+  return launch_any(g, s, ld, gp, PassA{p_new}, nullptr, mode, part_off, nblocks, 0, 0, fold);
 }
 
 // split grids, folded iteration: reduce a pass's partials and allreduce them into d_scalars, where

@@ -1,7 +1,8 @@
 """Per-iteration time of the CG iterations on the decomposed code path (force_comm: a one-rank
 RCCL communicator -- boundary-plane kernel, halo exchange overlapped with the interior planes,
 allreduced sums folded into the next launch's prologue) against one rank, interleaved in one
-process, fixed iterations. usage: python scripts/probe_decomposed_cg.py [N ...] (default 512)
+process, fixed iterations. usage: [FC=0,1] [SR=0,1] [REPS=3] python scripts/probe_decomposed_cg.py
+[N ...] (default 512)
 One JSON line per (N, force_comm, variant, rep)."""
 import json
 import os
@@ -41,12 +42,12 @@ def main():
     sizes = [int(a) for a in sys.argv[1:]] or [512]
     for n in sizes:
         for rep in range(int(os.environ.get("REPS", "3"))):
-            for fc in (0, 1):
+            for fc in [int(v) for v in os.environ.get("FC", "0,1").split(",")]:
                 pb.tune_reset()
                 pb.tune_set("force_comm", fc)
                 ctx = pb.Context(0)
                 pb.tune_reset()
-                for sr in (0, 1):
+                for sr in [int(v) for v in os.environ.get("SR", "0,1").split(",")]:
                     ms, rl = run(ctx, n, sr)
                     print(json.dumps({"n": n, "force_comm": fc, "sr": sr, "rep": rep,
                                       "ms_per_it": round(ms, 4), "rnorm_last": rl}), flush=True)
