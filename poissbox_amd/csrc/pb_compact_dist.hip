@@ -20,7 +20,7 @@ namespace pb {
 __global__ __launch_bounds__(256) void slab_transpose_kernel(double* zs, double* buf, int nx,
                                                              int ny, int nzl, const int* jrank,
                                                              const int* j0, const int* nyl,
-                                                             int dir) {
+                                                             int dir, int me, double* self) {
   const int64_t n = (int64_t)nx * ny * nzl;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
        idx += (int64_t)gridDim.x * blockDim.x) {
@@ -31,10 +31,11 @@ __global__ __launch_bounds__(256) void slab_transpose_kernel(double* zs, double*
     const int j = (int)(row - (uint32_t)kl * (uint32_t)ny);
     const int r = jrank[j];
     const int64_t b = (int64_t)nzl * nx * j0[r] + ((int64_t)kl * nyl[r] + (j - j0[r])) * nx + i;
+    double* bb = self && r == me ? self : buf;  // the self block: straight to / from the y-slab
     if (dir == 0)
-      buf[b] = zs[idx];
+      bb[b] = zs[idx];
     else
-      zs[idx] = buf[b];
+      zs[idx] = bb[b];
   }
 }
 
@@ -44,7 +45,8 @@ __global__ __launch_bounds__(256) void slab_transpose_kernel(double* zs, double*
 // unpack: the per-element kernel moved ~3.4 TB/s).
 __global__ __launch_bounds__(256) void slab_rows_kernel(double* zs, double* buf, int nx, int ny,
                                                         int nzl, const int* jrank, const int* j0,
-                                                        const int* nyl, int dir) {
+                                                        const int* nyl, int dir, int me,
+                                                        double* self) {
   const int hp = nx >> 1;                              // pairs per row
   const int step = hp < 256 ? hp : 256;                // pair stride of a thread within its row
   const int rpb = hp < 256 ? 256 / hp : 1;             // rows per block step
@@ -57,17 +59,22 @@ __global__ __launch_bounds__(256) void slab_rows_kernel(double* zs, double* buf,
     const int r = jrank[j];
     const int64_t b = (int64_t)nzl * nx * j0[r] + ((int64_t)kl * nyl[r] + (j - j0[r])) * nx;
     const int64_t a = row * nx;
+    double* bb = self && r == me ? self : buf;  // the self block: straight to / from the y-slab
     for (int q = p0; q < hp; q += step) {
       if (dir == 0)
-        *reinterpret_cast<dv2*>(buf + b + 2 * q) = *reinterpret_cast<const dv2*>(zs + a + 2 * q);
+        *reinterpret_cast<dv2*>(bb + b + 2 * q) = *reinterpret_cast<const dv2*>(zs + a + 2 * q);
       else
-        *reinterpret_cast<dv2*>(zs + a + 2 * q) = *reinterpret_cast<const dv2*>(buf + b + 2 * q);
+        *reinterpret_cast<dv2*>(zs + a + 2 * q) = *reinterpret_cast<const dv2*>(bb + b + 2 * q);
     }
   }
 }
 
-static void launch_slab_transpose(pb_grid* g, const YSlabPlan& p, double* zs, int dir) {
+// ybuf: the y-slab buffer on the other side of the all-to-all (its self block is read / written
+// here directly when p.self_direct)
+static void launch_slab_transpose(pb_grid* g, const YSlabPlan& p, double* zs, int dir,
+                                  const double* ybuf) {
   pb_ctx* ctx = g->ctx;
+  double* self = p.self_direct ? const_cast<double*>(ybuf) + p.self_shift : nullptr;
   const int64_t ny = g->n[1];
   const int P = ctx->nranks;
   if (g->n[0] % 2 == 0) {
@@ -75,11 +82,13 @@ static void launch_slab_transpose(pb_grid* g, const YSlabPlan& p, double* zs, in
     const int hp = (int)(g->n[0] / 2), rpb = hp < 256 ? 256 / hp : 1;
     const int nb = (int)std::min<int64_t>((rows + rpb - 1) / rpb, (int64_t)ctx->num_cus * 16);
     hipLaunchKernelGGL(slab_rows_kernel, dim3(nb), dim3(256), 0, ctx->stream, zs, p.stage,
-                       (int)g->n[0], (int)ny, (int)g->nzl, p.tab, p.tab + ny, p.tab + ny + P, dir);
+                       (int)g->n[0], (int)ny, (int)g->nzl, p.tab, p.tab + ny, p.tab + ny + P, dir,
+                       p.me, self);
     return;
   }
   hipLaunchKernelGGL(slab_transpose_kernel, dim3(p.nb), dim3(256), 0, ctx->stream, zs, p.stage,
-                     (int)g->n[0], (int)ny, (int)g->nzl, p.tab, p.tab + ny, p.tab + ny + P, dir);
+                     (int)g->n[0], (int)ny, (int)g->nzl, p.tab, p.tab + ny, p.tab + ny + P, dir,
+                     p.me, self);
 }
 
 static void make_plan(const pb_grid* g, YSlabPlan* d) {
@@ -139,6 +148,16 @@ int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p) {
     p->yc[q] = p->nzl[q] * nx * p->ny_me;
   }
   p->nb = (int)std::min<int64_t>((g->nlocal + 255) / 256, (int64_t)ctx->num_cus * 16);
+  // the self block stays on the rank: RCCL contexts skip its copy (host staging moves whole
+  // buffers and keeps it)
+  p->me = ctx->rank;
+  p->self_direct = ctx->comm != nullptr && !tune("a2a_copy_self", 0);
+  int64_t zo = 0, yo = 0;
+  for (int q = 0; q < ctx->rank; ++q) {
+    zo += p->zc[q];
+    yo += p->yc[q];
+  }
+  p->self_shift = yo - zo;
   return PB_OK;
 }
 
@@ -154,17 +173,17 @@ int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy) {
   pb_ctx* ctx = g->ctx;
   {
     ScopedTimer tm(ctx, "slab_pack");
-    launch_slab_transpose(g, p, const_cast<double*>(f), 0);
+    launch_slab_transpose(g, p, const_cast<double*>(f), 0, fy);
     PB_HIP(hipGetLastError());
   }
-  return alltoallv_device(ctx, p.stage, p.zc.data(), fy, p.yc.data());
+  return alltoallv_device(ctx, p.stage, p.zc.data(), fy, p.yc.data(), p.self_direct);
 }
 
 int yslab_from(pb_grid* g, const YSlabPlan& p, const double* fy, double* f) {
   pb_ctx* ctx = g->ctx;
-  PB_TRY(alltoallv_device(ctx, fy, p.yc.data(), p.stage, p.zc.data()));
+  PB_TRY(alltoallv_device(ctx, fy, p.yc.data(), p.stage, p.zc.data(), p.self_direct));
   ScopedTimer tm(ctx, "slab_unpack");
-  launch_slab_transpose(g, p, f, 1);
+  launch_slab_transpose(g, p, f, 1, fy);
   PB_HIP(hipGetLastError());
   return PB_OK;
 }
@@ -186,9 +205,13 @@ int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double
   if (blocked) *blocked = false;
   if (plan_out && blocked && yslab_blocked(p)) {
     // received straight into u, v (nlocal doubles each) in the all-to-all layout
-    PB_TRY(alltoallv_device(g->ctx, uy, p.yc.data(), u, p.zc.data()));
-    PB_TRY(alltoallv_device(g->ctx, vy, p.yc.data(), v, p.zc.data()));
+    PB_TRY(alltoallv_device(g->ctx, uy, p.yc.data(), u, p.zc.data(), p.self_direct));
+    PB_TRY(alltoallv_device(g->ctx, vy, p.yc.data(), v, p.zc.data(), p.self_direct));
     *plan_out = p;
+    if (p.self_direct) {  // the Y pass reads the self block from uy, vy
+      plan_out->alt0 = uy + p.self_shift;
+      plan_out->alt1 = vy + p.self_shift;
+    }
     *blocked = true;
     return PB_OK;
   }

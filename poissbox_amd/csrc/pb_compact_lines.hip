@@ -64,6 +64,11 @@ struct LinePass {
   // outer stride lo_in, element e at (e >> esh_in) * ebs_in + (e & (2^esh_in - 1)) * es
   int64_t lo_in, ebs_in;
   int esh_in;
+  // the self block of a blocked input (YSlabPlan::self_direct): block alt_blk of in0 / in1 is read
+  // from alt0 / alt1 (the Z pass's y-slab outputs; the all-to-all did not copy it); -1: none
+  const double* alt0 = nullptr;
+  const double* alt1 = nullptr;
+  int alt_blk = -1;
 };
 
 static LineOp make_line_op(int kind, int C, double h) {
@@ -266,9 +271,12 @@ __device__ __forceinline__ void tile_fetch(const LinePass& p, const double* __re
     const bool ok = (T::NF % NT == 0 || f < T::NF) && l < nl;
     const int lc = ok ? l : 0, ec = ok ? e : 0;  // selects, not a branch around the load
     int64_t eo = (int64_t)ec * p.es;
-    if constexpr (BLK)
+    const double* s = src;
+    if constexpr (BLK) {
       eo = (int64_t)(ec >> p.esh_in) * p.ebs_in + (int64_t)(ec & ((1 << p.esh_in) - 1)) * p.es;
-    const double* a = src + b_in + lc * p.li + eo;
+      if ((ec >> p.esh_in) == p.alt_blk) s = src == p.in0 ? p.alt0 : p.alt1;  // (a select)
+    }
+    const double* a = s + b_in + lc * p.li + eo;
     if (V == 2) {
       const dv2 w = __builtin_nontemporal_load((const dv2*)a);
       t.v[r][0] = w.x;
@@ -852,6 +860,11 @@ int compact_lines_pass(pb_ctx* ctx, const int64_t dims[3], int axis, double h, c
       p.lo_in = nyl * nx;
       p.esh_in = sh;
       p.ebs_in = nz * nyl * nx;
+      if (blk_in->self_direct) {
+        p.alt_blk = blk_in->me;
+        p.alt0 = blk_in->alt0;
+        p.alt1 = blk_in->alt1;
+      }
       return launch_lines<0, 4>(ctx, p, n, nz);
     }
     return launch_lines<0, 1>(ctx, p, n, nz);

@@ -79,6 +79,11 @@ struct DhtPass {
   double* ru_x;
   int ru_first;
   const CgState* ru_st;
+  // the self block of a blocked Y pass (YSlabPlan::self_direct): element block alt_blk is read
+  // from in_alt / written to out_alt (the y-slab buffer; the all-to-all does not copy it); -1: none
+  const double* in_alt = nullptr;
+  double* out_alt = nullptr;
+  int alt_blk = -1;
   int ablate;         // timing experiments only (PB_FFT_ABLATE=1): no transforms (tile copy
                       // through LDS); builds with -DPB_FFT_ABLATE_TRAFFIC=1 drop the global loads
                       // and stores instead (transforms on stale LDS)
@@ -543,7 +548,9 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
     const bool ok = l < nl;
     const int lc = ok ? l : 0, ec = ok ? e : 0;  // selects, not a branch around the load
     if (PB_FFT_ABLATE_TRAFFIC) return dv2{0.0, 0.0};
-    return __builtin_nontemporal_load((const dv2*)(p.in + base + lc * p.li + eoff_in(ec)));
+    const double* src = p.in;
+    if (LAYOUT == 0 && p.esh_in && (ec >> p.esh_in) == p.alt_blk) src = p.in_alt;  // (a select)
+    return __builtin_nontemporal_load((const dv2*)(src + base + lc * p.li + eoff_in(ec)));
   };
   auto fetch = [&](int t) {
     int64_t outer, base;
@@ -643,7 +650,9 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
           if (v.x == 12345.678) p.out[a] = v.y;  // keeps the LDS reads (never true on real data)
           continue;
         }
-        __builtin_nontemporal_store(v, (dv2*)(p.out + a));
+        double* dst = p.out;
+        if (LAYOUT == 0 && p.esh_out && (e >> p.esh_out) == p.alt_blk) dst = p.out_alt;
+        __builtin_nontemporal_store(v, (dv2*)(dst + a));
         if constexpr (SUMS) {
           const dv2 rv = __builtin_nontemporal_load((const dv2*)(p.sr + a));
           const double t0 = v.x - mu, t1 = v.y - mu;
@@ -1137,6 +1146,11 @@ static int dht_axis(pb_ctx* ctx, const FftPc* f, const int64_t b[3], int axis, c
         p.esh_in = sh;
         p.ebs_in = nz * nyl * nx;
       }
+      if (blk->self_direct) {  // the self block goes straight to / comes from the y-slab
+        p.alt_blk = blk->me;
+        p.out_alt = blk->alt_out;
+        p.in_alt = blk->alt_out;
+      }
     }
     return launch_dht<0, 0>(ctx, ny, p, skip);
   }
@@ -1189,11 +1203,12 @@ int fftpc_apply(FftPc* f, const double* r, double* z, const int* skip, const CgS
     if (yslab_blocked(yp)) {
       // the Y passes write / read the all-to-all buffer in its blocked layout: no pack / unpack
       // pass (two field copies per apply)
+      yp.alt_out = fy + yp.self_shift;  // (used when yp.self_direct)
       PB_TRY(dht_axis(ctx, f, b, 1, z, yp.stage, skip, 0, nullptr, nullptr, nullptr, nullptr, 0,
                       0, &yp, 1));
-      PB_TRY(alltoallv_device(ctx, yp.stage, yp.zc.data(), fy, yp.yc.data()));
+      PB_TRY(alltoallv_device(ctx, yp.stage, yp.zc.data(), fy, yp.yc.data(), yp.self_direct));
       PB_TRY(dht_axis(ctx, f, by, 2, fy, fy, skip, (int)yp.j0[ctx->rank]));
-      PB_TRY(alltoallv_device(ctx, fy, yp.yc.data(), yp.stage, yp.zc.data()));
+      PB_TRY(alltoallv_device(ctx, fy, yp.yc.data(), yp.stage, yp.zc.data(), yp.self_direct));
       PB_TRY(dht_axis(ctx, f, b, 1, yp.stage, z, skip, 0, nullptr, nullptr, nullptr, nullptr, 0,
                       0, &yp, 2));
     } else {

@@ -481,6 +481,18 @@ struct YSlabPlan {
   double* stage = nullptr;
   int* tab = nullptr;
   int nb = 0;
+  // self block (r05): on RCCL contexts the block a rank keeps is never copied by the all-to-all;
+  // its producer writes it where the consumer reads it. A z-slab-layout offset o of the self
+  // block lives at ybuf + self_shift + o in a y-slab buffer (self_shift = the y-side block offset
+  // minus the z-side one)
+  bool self_direct = false;
+  int me = 0;
+  int64_t self_shift = 0;
+  // the y-slab buffers holding the self block of the blocked consumers' inputs / producer's
+  // output (set by the caller that owns them; + self_shift applied)
+  const double* alt0 = nullptr;
+  const double* alt1 = nullptr;
+  double* alt_out = nullptr;
 };
 int64_t yslab_len(const pb_grid* g);
 int64_t yslab_aux_len(const pb_grid* g);
@@ -491,8 +503,9 @@ int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy);
 bool yslab_blocked(const YSlabPlan& p);
 int yslab_from(pb_grid* g, const YSlabPlan& p, const double* fy, double* f);
 // all-to-all with per-peer counts; blocks are contiguous in rank order on both sides
+// skip_self: the rank's own block is already in place (YSlabPlan::self_direct), not copied
 int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,
-                     const int64_t* rcount);
+                     const int64_t* rcount, bool skip_self = false);
 // Config-5 iteration fusions (compact A with a stored-z preconditioner, one rank, register line
 // solves): the compact operator's Z pass forms p = (dinv z - mu) + beta/beta_old p_old from its
 // tile loads and stores p (cg_gen_p_kernel's arithmetic, bit-identical), and its X pass takes the

@@ -31,7 +31,7 @@ namespace {
 // every name a kernel launcher consults; the defaults live at the call sites (the measured
 // choices), the table only holds values a caller set
 const char* const kTuneNames[] = {
-    "cg_defer_x", "cg_fold", "cg_fuse", "cg_sr_fused", "comm_mark_every",
+    "a2a_copy_self", "cg_defer_x", "cg_fold", "cg_fuse", "cg_sr_fused", "comm_mark_every",
     "comm_stall_test_ms", "compact_lines", "fft_rupd", "fft_zpad", "fft_zpad_min_plane",
     "force_comm", "ksp_lazy0", "mg_agglomerate", "mg_engine_min_plane", "mg_restrict_z_min_cols",
     "mg_split_fused", "mg_sweep2", "mg_tail_max", "mg_u4_split", "pcr_lines", "sor_omega_any"};
@@ -424,7 +424,7 @@ int halo_end(pb_grid* g) {
 }
 
 int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, double* recv,
-                     const int64_t* rcount) {
+                     const int64_t* rcount, bool skip_self) {
   PB_COMM_OK(ctx);
   ScopedTimer tm(ctx, "alltoallv");
   const int P = ctx->nranks;
@@ -451,11 +451,13 @@ int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, dou
     }
     PB_NCCL(ncclGroupEnd());
     const int me = ctx->rank;
-    if (scount[me])
+    if (scount[me] && !skip_self)
       PB_HIP(hipMemcpyAsync(recv + ro[me], send + so[me], scount[me] * sizeof(double),
                             hipMemcpyDeviceToDevice, ctx->stream));
     return PB_OK;
   }
+  if (skip_self)  // (host staging moves whole buffers: the plan never elides there)
+    return set_error(PB_ERR_ARG, "all-to-all: self-block elision needs an RCCL context");
   if (!ctx->h_alltoallv)
     return set_error(PB_ERR_COMM, "host transport without an alltoallv callback");
   const size_t need = (size_t)(so[P] + ro[P]);

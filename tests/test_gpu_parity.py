@@ -1520,6 +1520,45 @@ def test_rccl_code_paths_one_rank_communicator(tune):
     ctx.destroy()
 
 
+@pytest.mark.parametrize("n3", [(64, 64, 64), (64, 40, 32)])
+def test_rccl_self_block_elision_bit_identical(tune, n3):
+    """force_comm (a one-rank RCCL communicator): the all-to-all transposes of the compact
+    operator and the spectral PC do not copy the rank's own block -- its producer writes it where
+    its consumer reads it (YSlabPlan::self_direct; 2^k rows: the blocked Y passes, 40 rows: the
+    pack / unpack kernels). Bit-identical to the copying form (tuning a2a_copy_self = 1) and to
+    the one-rank path."""
+    N = int(np.prod(n3))
+    hc = tuple(2 * np.pi / m for m in n3)
+    f = O.fill_random(N, 11)
+
+    def run(ctx):
+        da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+        xv, y = pb.Vec(da), pb.Vec(da)
+        xv.set_values(f)
+        pb.compact_lapl_fast(da, hc, xv, y)
+        P = pb.Mat(da, pb.COMPACT, hc)
+        k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
+        z = pb.Vec(da)
+        k.pc_apply(xv, z)
+        out = (y.get_values(), z.get_values())
+        k.destroy()
+        return out
+
+    res = {}
+    for name, fc, copy in (("one", 0, 0), ("elide", 1, 0), ("copy", 1, 1)):
+        tune.set("force_comm", fc)
+        ctx = pb.Context(0)
+        tune.set("force_comm", 0)
+        tune.set("a2a_copy_self", copy)
+        res[name] = run(ctx)
+        tune.set("a2a_copy_self", 0)
+        ctx.destroy()
+    for name in ("elide", "copy"):
+        for a, b in zip(res[name], res["one"]):
+            assert np.array_equal(a, b), name
+    assert np.isfinite(res["elide"][1]).all()
+
+
 def test_split_apply_timers_cover_whole_applies(tune):
     """On a decomposed grid a matvec / CG pass A is two launches (interior planes, then the
     boundary planes after the halo exchange). The "stencil" and "cg_pass_a" timers that bench.py
