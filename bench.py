@@ -363,6 +363,25 @@ def cpu_solve_baseline(workload, budget_s=None, m=128):
                       f"GPU box host"}
 
 
+def dominant_kernel(kern, s_per_solve):
+    """The phase with the largest time per solve among the timed kernels (the roofline kernel is
+    the one with fixed algorithmic bytes; for config 5 the PC's X passes take more time but carry
+    CG's x / r update and residual sums, so their bytes per launch vary)."""
+    best = None
+    for nm, row in kern.items():
+        if nm in ("pc_fft", "mg_apply", "alltoallv", "allreduce", "halo", "halo_comm"):
+            continue  # (wrappers of other phases, communication)
+        t = row["avg_ms"] * row["launches_per_solve"]
+        if best is None or t > best[1]:
+            best = (nm, t, row)
+    if best is None:
+        return None
+    nm, t, row = best
+    return {"name": nm, "ms_per_solve": t, "share_of_solve": t / (s_per_solve * 1e3),
+            "avg_launch_ms": row["avg_ms"], "launches_per_solve": row["launches_per_solve"],
+            "frac": row.get("frac")}
+
+
 def workload_grid(workload, scaling, world, base):
     return global_grid(world, base) if scaling == "weak" else (base,) * 3
 
@@ -477,7 +496,8 @@ def run_solve_workload(args, pb, ctx, workload, scaling, steps, warmup, rank, wo
             "roofline": {"bound": "hbm", "kernel": roof_desc, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None, "bytes_per_dof": roof_bytes,
-                         "avg_launch_ms": t_roof * 1e3, "launches_timed": cnt_roof},
+                         "avg_launch_ms": t_roof * 1e3, "launches_timed": cnt_roof,
+                         "dominant": dominant_kernel(kern, elapsed / max(steps, 1))},
             "kernels": kern,
             "launcher": os.environ.get("PB_BENCH_LAUNCHER",
                                        "torch.distributed.run" if dist else "none"),
