@@ -1486,6 +1486,15 @@ def test_rccl_code_paths_one_rank_communicator(tune):
         reason, its, hist = pb.solve(P, A, x, bv, ["-pc_type", pc, "-ksp_rtol", "1e-9"])
         assert (reason, its) == (ro, itso)
         check_history(hist, ho, bar=HIST_RTOL if pc == "jacobi" else HIST_RTOL_PC)
+    # single-reduction CG on the decomposed path (boundary-plane fold, one RCCL allreduce)
+    for check in (8, 1):
+        xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-9, single_reduction=1)
+        k = pb.KSP(A, P, pb.ksp_options(["-ksp_cg_single_reduction", "-ksp_rtol", "1e-9"],
+                                        check_every=check))
+        reason, its, hist = k.solve(bv, x)
+        k.destroy()
+        assert (reason, its) == (ro, itso)
+        check_history(np.asarray(hist), ho)
     hc = tuple(2 * np.pi / m for m in n3)
     ref = O.lapl(xt, n3, hc)
     pb.compact_lapl_fast(da, hc, xv, y)
