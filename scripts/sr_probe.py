@@ -10,7 +10,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import poissbox_amd as pb  # noqa: E402
 
-PASSES = ("cg_pass_a", "cg_pass_b_even", "cg_pass_b_x4", "cg_sr_p", "cg_sr_p_x4", "cg_sr_s", "cg_sr1", "cg_sr1_x4")
+PASSES = ("cg_pass_a", "cg_pass_b_even", "cg_pass_b_x4", "cg_sr_p", "cg_sr_p_x4", "cg_sr_s", "cg_sr1")
 
 
 def run(ctx, n, sr, steps=100, warmup=12, diag=16):
