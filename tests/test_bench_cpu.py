@@ -110,3 +110,20 @@ def test_solve_workload_dry_run_and_cpu_rows():
         cb = bench.cpu_solve_baseline(wl, budget_s=0.01, m=16)
         assert cb["reason"] == 2 and cb["value"] > 0 and cb["its_per_solve"] >= 1
         assert cb["kind"] == "port" and cb["cores"] >= 1
+
+
+def test_dominant_kernel_and_sr_bytes():
+    """The solve lines' dominant phase: largest time per solve among the timed kernels, wrappers
+    and communication left out; the single-reduction variant's bytes per iteration on one rank
+    (3 one-pass iterations of 32 B/DoF, one two-pass x-update iteration of 64 + 8)."""
+    kern = {"pc_fft": {"avg_ms": 2.6, "launches_per_solve": 2},
+            "pc_fft_x": {"avg_ms": 0.64, "launches_per_solve": 4},
+            "pc_fft_z": {"avg_ms": 0.51, "launches_per_solve": 2, "frac": 0.52},
+            "alltoallv": {"avg_ms": 5.0, "launches_per_solve": 7}}
+    d = bench.dominant_kernel(kern, 7.7e-3)
+    assert d["name"] == "pc_fft_x" and d["launches_per_solve"] == 4
+    assert abs(d["ms_per_solve"] - 2.56) < 1e-9 and abs(d["share_of_solve"] - 2.56 / 7.7) < 1e-9
+    assert bench.dominant_kernel({}, 1.0) is None
+    b = bench.SR_BYTES
+    assert (3 * b["sr1"] + b["p_x4"] + b["s"]) / 4 == 42
+    assert bench.SR_ITER_BYTES == 48
