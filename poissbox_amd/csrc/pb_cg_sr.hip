@@ -48,59 +48,6 @@ struct SrGeo {
   int remap;
 };
 
-template <int... Qs, class F>
-__device__ __forceinline__ void unroll_steps(std::integer_sequence<int, Qs...>, F&& f) {
-  (f(std::integral_constant<int, Qs>{}), ...);
-}
-
-// one 7-point sum in the reference order (z-, y-, x-, c, x+, y+, z+)
-__device__ __forceinline__ double star7_sum(double cx, double cy, double cz, double cc,
-                                            double zm, double ym, double xm, double c, double xp,
-                                            double yp, double zp) {
-  double w = cz * zm;
-  w = w + cy * ym;
-  w = w + cx * xm;
-  w = w + cc * c;
-  w = w + cx * xp;
-  w = w + cy * yp;
-  w = w + cz * zp;
-  return w;
-}
-
-// DPP moves of a double: row shifts by N lanes within 16-lane rows (N = 0: the value itself)
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-  const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, true);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, true);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-template <int N>
-__device__ __forceinline__ double dpp_row_shl(double v) {  // lane l <- lane l + N
-  if constexpr (N == 0) return v;
-  else return dpp_d<0x100 + N>(v);
-}
-template <int N>
-__device__ __forceinline__ double dpp_row_shr(double v) {  // lane l <- lane l - N
-  if constexpr (N == 0) return v;
-  else return dpp_d<0x110 + N>(v);
-}
-// wave shifts by one lane that keep `old` where the source lane is outside the wave (lane 0 for
-// shr, lane 63 for shl)
-template <int CTRL>
-__device__ __forceinline__ double dpp_keep(double old, double v) {
-  const long long b = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, old);
-  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double dpp_shr1_keep(double old, double v) {  // lane l <- lane l-1
-  return dpp_keep<0x138>(old, v);
-}
-__device__ __forceinline__ double dpp_shl1_keep(double old, double v) {  // lane l <- lane l+1
-  return dpp_keep<0x130>(old, v);
-}
-
 static constexpr unsigned kOob = 0x80000000u;  // a store offset past every plane: dropped
 
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
