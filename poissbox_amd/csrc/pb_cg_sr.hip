@@ -16,10 +16,11 @@
 // the values one row out come from the neighbouring waves through LDS (published one step before
 // use, double buffered by step parity, one block barrier per step); each stage loses a row at the
 // block's ends, so blocks store rows 2 .. NW TY - 3 and advance by NW TY - 4 rows.
-// Columns: a wave owns 128 points (64 lanes x one 16-B pair: whole 128-B lines, segments that
-// tile a 512-point row exactly). The two points either side of each row are a "halo pair", all
-// of a wave's halo pairs in ONE more register set: lane q holds row q's left pair (x0 - 2,
-// x0 - 1), lane 64 - TY + q row q's right pair (x0 + 128, x0 + 129). The halo's inner point gets
+// Columns: a wave owns 64 V points (V = 2, the default: 64 lanes x one 16-B pair, whole 128-B
+// lines, segments that tile a 512-point row exactly; V = 1 with 4-row waves, PB_SR_TY=4, measured
+// slower). The two points either side of each row are a "halo pair", all of a wave's halo pairs
+// in ONE more register set: lane q holds row q's left pair (x0 - 2, x0 - 1), lane 64 - TY + q row
+// q's right pair (x0 + 64 V, x0 + 64 V + 1). The halo's inner point gets
 // p, w, r', t like any other point: its x-neighbours are its outer point and the segment's edge
 // value (read from lane 0 / 63), its y-neighbours the next lanes (DPP; across waves through LDS),
 // its z-neighbours the same register of the next planes. Lane 0's left and lane 63's right
@@ -38,12 +39,10 @@
 
 namespace pb {
 
-static constexpr int kSrSeg = 128;  // points per wave segment
-
 struct SrGeo {
   int nx, ny, nzl;
   int64_t plane;
-  int nseg, ntile;  // x segments of kSrSeg points, y tiles of NW TY - 4 rows
+  int nseg, ntile;  // x segments of 64 V points, y tiles of NW TY - 4 rows
   int W;            // planes of work per workgroup
   int remap;
 };
@@ -51,28 +50,50 @@ struct SrGeo {
 static constexpr unsigned kOob = 0x80000000u;  // a store offset past every plane: dropped
 
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void store_pair(__amdgpu_buffer_rsrc_t rs, unsigned off,
-                                           const double (&v)[2]) {
-  const dv2 d{v[0], v[1]};
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, d), rs, (int)off, 0, 0);
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+// a lane's V points of a row (V = 2: one 16-B store, V = 1: 8 B)
+template <int V>
+__device__ __forceinline__ void store_pts(__amdgpu_buffer_rsrc_t rs, unsigned off,
+                                          const double (&v)[V]) {
+  if constexpr (V == 2) {
+    const dv2 d{v[0], v[1]};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, d), rs, (int)off, 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v[0]), rs, (int)off, 0, 0);
+  }
 }
 
-template <int NW, int TY>
+template <int V>
+using lane_pts = std::conditional_t<V == 2, dv2, double>;
+template <int V>
+__device__ __forceinline__ lane_pts<V> pack_pts(const double (&v)[V]) {
+  if constexpr (V == 2) return dv2{v[0], v[1]};
+  else return v[0];
+}
+template <int V>
+__device__ __forceinline__ double pt(const lane_pts<V>& x, int e) {
+  if constexpr (V == 2) return x[e];
+  else return x;
+}
+
+template <int NW, int TY, int V>
 struct SrLds {
-  dv2 xch[2][4][NW][64];  // [step parity][p row 0, p row TY-1, t row 0, t row TY-1][wave][lane]
-  double xh[2][NW][64];   // [step parity][wave][lane]: the halo lanes' p
+  // [step parity][p row 0, p row TY-1, t row 0, t row TY-1][wave][lane]
+  lane_pts<V> xch[2][4][NW][64];
+  double xh[2][NW][64];  // [step parity][wave][lane]: the halo lanes' p
 };
 
-template <int NW, int TY>
+template <int NW, int TY, int V>
 __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, double cz,
                                           double cc, const double* __restrict__ r,
                                           const double* __restrict__ p_old,
                                           double* __restrict__ p_new, double* __restrict__ r_out,
                                           double dinv, double shift, double bb, double alpha,
-                                          int seg, int tile, int kb, int ke, SrLds<NW, TY>& L,
+                                          int seg, int tile, int kb, int ke, SrLds<NW, TY, V>& L,
                                           double (&acc)[5]) {
   constexpr int RB = NW * TY;
   constexpr int SB = RB - 4;
+  constexpr int SEG = 64 * V;  // points per wave segment
   // register ring slots: plane loads D = U - 2 steps ahead of the step that forms p from them.
   // U = 3 (one step ahead) fits the 256-register budget; at U = 4 the x-halo registers spill
   // (two-step prefetch measured within noise before the halo lanes: 0.86-0.93 vs 0.87-0.90 ms)
@@ -84,13 +105,13 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
   const int br0 = wid * TY;
   const int j0 = g0 + br0;
   auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
-  const int x0 = seg * kSrSeg;
-  const int o = x0 + 2 * lane;  // this lane's pair
+  const int x0 = seg * SEG;
+  const int o = x0 + V * lane;  // this lane's points
   const int ip = wrap(o, nx);   // (nx even: a pair never straddles the wrap)
   const bool out_ok = o < nx;
-  const bool left = lane < 32;  // halo pair: left (x0 - 2, x0 - 1) or right (x0 + 128, x0 + 129)
+  const bool left = lane < 32;  // halo pair: left (x0 - 2, x0 - 1) or right (x0 + SEG, x0 + SEG + 1)
   const int qh = left ? lane % TY : (lane - (64 - TY)) % TY;  // the halo lane's row (other lanes: any)
-  const int ih = wrap(left ? x0 - 2 : x0 + kSrSeg, nx);
+  const int ih = wrap(left ? x0 - 2 : x0 + SEG, nx);
   int64_t ro[TY];
   unsigned row_ok = 0;
 #pragma unroll
@@ -130,49 +151,49 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
 
   // rings of U register slots whose roles rotate with the unrolled step (no copies); *H = the
   // halo lanes' pairs
-  double P[U][TY][2], PH[U][2];    // p of planes k, k+1, k+2 at slots Q, Q+1, Q+2
-  double R[U][TY][2], RH[U][2];    // r of planes k+1 .. k+1+D; slot Q receives plane k+2+D
-  double T[U][TY][2], TH[U];       // t of planes k-1, k, k+1 (halo: inner point only)
-  double PO[U][TY][2], POH[U][2];  // p_old of planes k+2 .. k+1+D; slot Q receives k+2+D
+  double P[U][TY][V], PH[U][2];    // p of planes k, k+1, k+2 at slots Q, Q+1, Q+2
+  double R[U][TY][V], RH[U][2];    // r of planes k+1 .. k+1+D; slot Q receives plane k+2+D
+  double T[U][TY][V], TH[U];       // t of planes k-1, k, k+1 (halo: inner point only)
+  double PO[U][TY][V], POH[U][2];  // p_old of planes k+2 .. k+1+D; slot Q receives k+2+D
 #pragma unroll
   for (int s = 0; s < U; ++s) {
     TH[s] = 0.0;
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      PH[s][e] = RH[s][e] = POH[s][e] = 0.0;
+    for (int e = 0; e < 2; ++e) PH[s][e] = RH[s][e] = POH[s][e] = 0.0;
+#pragma unroll
+    for (int e = 0; e < V; ++e)
 #pragma unroll
       for (int q = 0; q < TY; ++q) P[s][q][e] = R[s][q][e] = T[s][q][e] = PO[s][q][e] = 0.0;
-    }
   }
-  auto ld = [&](const double* src, int kk, double (&dst)[TY][2], double (&dsth)[2]) {
+  auto ld = [&](const double* src, int kk, double (&dst)[TY][V], double (&dsth)[2]) {
     const int64_t base = pl(kk);
 #pragma unroll
-    for (int q = 0; q < TY; ++q) load_row<2>(src, RowIx{base + ro[q], boff}, dst[q]);
+    for (int q = 0; q < TY; ++q) load_row<V>(src, RowIx{base + ro[q], boff}, dst[q]);
     load_row<2>(src, RowIx{base, hoff}, dsth);
   };
   // Cross-lane moves are DPP only (row shifts within a 16-lane row, wave shifts by one) and every
   // choice a per-lane select: a readlane under a per-lane condition becomes a branch, and any
   // control flow in the step drains the prefetch (the compiler's wait counts merge at joins).
   // the segment's edge value of row q (lane 0's first / lane 63's second point) in the halo lanes
-  auto edge = [&](const double (&v)[TY][2]) {
+  auto edge = [&](const double (&v)[TY][V]) {
     double e = 0.0;
     unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
       constexpr int q = decltype(qc)::value;
       const double a = dpp_row_shr<q>(v[q][0]);            // lane q <- lane 0
-      const double b = dpp_row_shl<TY - 1 - q>(v[q][1]);   // lane 64 - TY + q <- lane 63
+      const double b = dpp_row_shl<TY - 1 - q>(v[q][V - 1]);  // lane 64 - TY + q <- lane 63
       e = qh == q ? (left ? a : b) : e;
     });
     return e;
   };
   // x-neighbours of row q's pairs: lane 0's left and lane 63's right come from the halo lanes
   // (wave shifts keep the old value where the source lane is outside the wave)
-  auto x_lo = [&](const double (&pair)[2], double hv, auto qc) {
+  auto x_lo = [&](const double (&pts)[V], double hv, auto qc) {
     constexpr int q = decltype(qc)::value;
-    return dpp_shr1_keep(dpp_row_shl<q>(hv), pair[1]);  // lane 0 <- halo lane q
+    return dpp_shr1_keep(dpp_row_shl<q>(hv), pts[V - 1]);  // lane 0 <- halo lane q
   };
-  auto x_hi = [&](const double (&pair)[2], double hv, auto qc) {
+  auto x_hi = [&](const double (&pts)[V], double hv, auto qc) {
     constexpr int q = decltype(qc)::value;
-    return dpp_shl1_keep(dpp_row_shr<TY - 1 - q>(hv), pair[0]);  // lane 63 <- 64 - TY + q
+    return dpp_shl1_keep(dpp_row_shr<TY - 1 - q>(hv), pts[0]);  // lane 63 <- 64 - TY + q
   };
   // the first step (k = kb - 4, Q = 0) forms p(kb - 2); planes kb - 1 .. kb - 3 + D are in flight
 #pragma unroll
@@ -184,15 +205,15 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
   auto body = [&](auto Qc, int k) {
     constexpr int Q = decltype(Qc)::value;
     constexpr int Q1 = (Q + 1) % U, Q2 = (Q + 2) % U;
-    double (&pk)[TY][2] = P[Q];
-    double (&pk1)[TY][2] = P[Q1];
-    double (&pk2)[TY][2] = P[Q2];
+    double (&pk)[TY][V] = P[Q];
+    double (&pk1)[TY][V] = P[Q1];
+    double (&pk2)[TY][V] = P[Q2];
     double (&hk)[2] = PH[Q];
     double (&hk1)[2] = PH[Q1];
     double (&hk2)[2] = PH[Q2];
-    double (&tkm)[TY][2] = T[Q];
-    double (&tk)[TY][2] = T[Q1];
-    double (&tk1)[TY][2] = T[Q2];
+    double (&tkm)[TY][V] = T[Q];
+    double (&tk)[TY][V] = T[Q1];
+    double (&tk1)[TY][V] = T[Q2];
     // planes k+2+D in flight for D steps
     ld(r, k + 2 + D, R[Q], RH[Q]);
     ld(p_old, k + 2 + D, PO[Q], POH[Q]);
@@ -200,7 +221,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
 #pragma unroll
     for (int q = 0; q < TY; ++q)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
+      for (int e = 0; e < V; ++e) {
         double z = dinv * R[Q2][q][e];
         z = z + shift;
         pk2[q][e] = z + bb * PO[Q2][q][e];
@@ -214,11 +235,11 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
     __syncthreads();
     // rows -1 / TY of p(k+1) and t(k): published by the neighbouring waves at step k-1
     const int rp = (k + 1) & 1, cur = k & 1;
-    const dv2 phl = L.xch[rp][1][wm][lane], phh = L.xch[rp][0][wp][lane];
-    const dv2 thl = L.xch[rp][3][wm][lane], thh = L.xch[rp][2][wp][lane];
+    const lane_pts<V> phl = L.xch[rp][1][wm][lane], phh = L.xch[rp][0][wp][lane];
+    const lane_pts<V> thl = L.xch[rp][3][wm][lane], thh = L.xch[rp][2][wp][lane];
     const double hhl = L.xh[rp][wm][hl_lo], hhh = L.xh[rp][wp][hl_hi];
-    L.xch[cur][0][wid][lane] = dv2{pk2[0][0], pk2[0][1]};
-    L.xch[cur][1][wid][lane] = dv2{pk2[TY - 1][0], pk2[TY - 1][1]};
+    L.xch[cur][0][wid][lane] = pack_pts<V>(pk2[0]);
+    L.xch[cur][1][wid][lane] = pack_pts<V>(pk2[TY - 1]);
     L.xh[cur][wid][lane] = inner(hk2);
     const bool in2 = k + 2 >= kb && k + 2 < ke, in1 = k + 1 >= kb && k + 1 < ke,
                in0 = k >= kb && k < ke;
@@ -226,7 +247,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       const auto rs = plane_rsrc(p_new, k + 2);
 #pragma unroll
       for (int q = 0; q < TY; ++q)
-        store_pair(rs, in2 && (row_ok >> q & 1u) ? roff[q] : kOob, pk2[q]);
+        store_pts<V>(rs, in2 && (row_ok >> q & 1u) ? roff[q] : kOob, pk2[q]);
     }
     // w(k+1) = A p, r' = r - alpha w, t = dinv r' - mu: the halo lanes' inner points first
     const double hc = inner(hk1);
@@ -247,26 +268,26 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       constexpr int q = decltype(qc)::value;
       const double lo = x_lo(pk1[q], hc, qc);
       const double hi = x_hi(pk1[q], hc, qc);
-      double rv[2];
+      double rv[V];
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const double xm = e == 0 ? lo : pk1[q][0];
-        const double xp = e == 1 ? hi : pk1[q][1];
-        const double ym = q == 0 ? phl[e] : pk1[q == 0 ? 0 : q - 1][e];
-        const double yp = q == TY - 1 ? phh[e] : pk1[q == TY - 1 ? q : q + 1][e];
+      for (int e = 0; e < V; ++e) {
+        const double xm = e == 0 ? lo : pk1[q][e == 0 ? 0 : e - 1];
+        const double xp = e == V - 1 ? hi : pk1[q][e == V - 1 ? e : e + 1];
+        const double ym = q == 0 ? pt<V>(phl, e) : pk1[q == 0 ? 0 : q - 1][e];
+        const double yp = q == TY - 1 ? pt<V>(phh, e) : pk1[q == TY - 1 ? q : q + 1][e];
         const double w = star7_sum(cx, cy, cz, cc, pk[q][e], ym, xm, pk1[q][e], xp, yp, pk2[q][e]);
         rv[e] = R[Q1][q][e] + (-alpha) * w;
         double z = dinv * rv[e];
         tk1[q][e] = z + shift;
       }
       const bool ok = in1 && (row_ok >> q & 1u);
-      store_pair(rs1, ok ? roff[q] : kOob, rv);
+      store_pts<V>(rs1, ok ? roff[q] : kOob, rv);
       // summands times 1 or 0 (exact; no branch -- selects here became branches and spills):
       // a zero of either sign leaves a sum unchanged. Masked rows hold finite values: real data,
       // zero-initialised registers and the zeroed LDS exchange (a NaN there would survive x 0)
       const double m = ok ? 1.0 : 0.0;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
+      for (int e = 0; e < V; ++e) {
         const double t = tk1[q][e];
         acc[0] += t * m;
         acc[1] += (t * t) * m;
@@ -274,8 +295,8 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
         acc[3] += rv[e] * m;
       }
     });
-    L.xch[cur][2][wid][lane] = dv2{tk1[0][0], tk1[0][1]};
-    L.xch[cur][3][wid][lane] = dv2{tk1[TY - 1][0], tk1[TY - 1][1]};
+    L.xch[cur][2][wid][lane] = pack_pts<V>(tk1[0]);
+    L.xch[cur][3][wid][lane] = pack_pts<V>(tk1[TY - 1]);
     // s(k) = A t, delta sum t.s
     unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
       constexpr int q = decltype(qc)::value;
@@ -283,11 +304,11 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       const double hi = x_hi(tk[q], TH[Q1], qc);
       const double m = in0 && (row_ok >> q & 1u) ? 1.0 : 0.0;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const double xm = e == 0 ? lo : tk[q][0];
-        const double xp = e == 1 ? hi : tk[q][1];
-        const double ym = q == 0 ? thl[e] : tk[q == 0 ? 0 : q - 1][e];
-        const double yp = q == TY - 1 ? thh[e] : tk[q == TY - 1 ? q : q + 1][e];
+      for (int e = 0; e < V; ++e) {
+        const double xm = e == 0 ? lo : tk[q][e == 0 ? 0 : e - 1];
+        const double xp = e == V - 1 ? hi : tk[q][e == V - 1 ? e : e + 1];
+        const double ym = q == 0 ? pt<V>(thl, e) : tk[q == 0 ? 0 : q - 1][e];
+        const double yp = q == TY - 1 ? pt<V>(thh, e) : tk[q == TY - 1 ? q : q + 1][e];
         const double sv = star7_sum(cx, cy, cz, cc, tkm[q][e], ym, xm, tk[q][e], xp, yp, tk1[q][e]);
         acc[4] += (tk[q][e] * sv) * m;
       }
@@ -300,14 +321,14 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
                  [&](auto Qc) { body(Qc, k + decltype(Qc)::value); });
 }
 
-template <int NW, int TY>
+template <int NW, int TY, int V>
 __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, double cy, double cz,
                                                          double cc, const double* __restrict__ r,
                                                          const double* __restrict__ p_old,
                                                          double* __restrict__ p_new,
                                                          double* __restrict__ r_out,
                                                          double* parts, Fold fold) {
-  __shared__ SrLds<NW, TY> lds;
+  __shared__ SrLds<NW, TY, V> lds;
   CgState st;
   fold_prologue(fold, st);  // every wave: the previous residual-sum stage + this iteration's top
   if (st.done) return;      // (uniform: every wave computed the same state)
@@ -315,7 +336,7 @@ __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, dou
      // kernels, possibly NaN, which the masked sums' factor 0 would not cancel); the first step's
      // barrier orders these stores before every read
     double* z = reinterpret_cast<double*>(&lds);
-    constexpr int nd = (int)(sizeof(SrLds<NW, TY>) / sizeof(double));
+    constexpr int nd = (int)(sizeof(SrLds<NW, TY, V>) / sizeof(double));
     for (int i = threadIdx.x; i < nd; i += 64 * NW) z[i] = 0.0;
   }
   const double dinv = st.dinv, shift = -st.mu, bb = st.bbp, alpha = st.alpha;
@@ -323,7 +344,7 @@ __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, dou
   const int bid = xcd_block(g.remap);
   const int ncol = g.nseg * g.ntile, W = g.W, T = g.nzl / W;
   auto run = [&](int col, int kb, int ke) {
-    sr1_range<NW, TY>(g, cx, cy, cz, cc, r, p_old, p_new, r_out, dinv, shift, bb, alpha,
+    sr1_range<NW, TY, V>(g, cx, cy, cz, cc, r, p_old, p_new, r_out, dinv, shift, bb, alpha,
                       col % g.nseg, col / g.nseg, kb, ke, lds, acc);
   };
   if (bid < T * ncol) {  // bands of W planes of every column
@@ -357,7 +378,12 @@ bool cg_sr1_supported(const pb_grid* g) {
 int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_old,
                   double* p_new, double* r_out, const SrFold& sf, const double* parts_in,
                   double* parts_out, int64_t host_iter, int* nblocks) {
-  constexpr int NW = 8, TY = 2;  // 8 waves of 2 rows: two waves per SIMD, one block per CU
+#ifndef PB_SR_TY
+#define PB_SR_TY 2
+#endif
+  // 8 waves (two per SIMD, one block per CU) of TY rows of 64 V points (TY V = 4: the register
+  // budget)
+  constexpr int NW = 8, TY = PB_SR_TY, V = 4 / TY;
   pb_ctx* ctx = g->ctx;
   ScopedTimer tm(ctx, "cg_sr1");
   SrGeo geo;
@@ -365,7 +391,7 @@ int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_ol
   geo.ny = (int)g->n[1];
   geo.nzl = (int)g->nzl;
   geo.plane = g->plane;
-  geo.nseg = (geo.nx + kSrSeg - 1) / kSrSeg;
+  geo.nseg = (geo.nx + 64 * V - 1) / (64 * V);
   geo.ntile = (geo.ny + NW * TY - 5) / (NW * TY - 4);
   geo.remap = 1;
   const int64_t work = (int64_t)geo.nseg * geo.ntile * geo.nzl;  // column-planes
@@ -384,7 +410,7 @@ int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_ol
   f.hist = sf.hist;
   f.h_done = sf.h_done;
   f.host_iter = host_iter - 1;
-  hipLaunchKernelGGL((cg_sr1_kernel<NW, TY>), dim3((unsigned)nb), dim3(64 * NW), 0, ctx->stream,
+  hipLaunchKernelGGL((cg_sr1_kernel<NW, TY, V>), dim3((unsigned)nb), dim3(64 * NW), 0, ctx->stream,
                      geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out, parts_out, f);
   PB_HIP(hipGetLastError());
   *nblocks = (int)nb;
