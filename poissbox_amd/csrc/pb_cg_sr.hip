@@ -17,8 +17,8 @@
 // use, double buffered by step parity, one block barrier per step); each stage loses a row at the
 // block's ends, so blocks store rows 2 .. NW TY - 3 and advance by NW TY - 4 rows.
 // Columns: a wave owns 64 V points (V = 2, the default: 64 lanes x one 16-B pair, whole 128-B
-// lines, segments that tile a 512-point row exactly; V = 1 with 4-row waves, PB_SR_TY=4, measured
-// slower). The two points either side of each row are a "halo pair", all of a wave's halo pairs
+// lines, segments that tile a 512-point row exactly; V = 1 with 3- or 4-row waves, PB_SR_TY /
+// PB_SR_V, measured slower). The two points either side of each row are a "halo pair", all of a wave's halo pairs
 // in ONE more register set: lane q holds row q's left pair (x0 - 2, x0 - 1), lane 64 - TY + q row
 // q's right pair (x0 + 64 V, x0 + 64 V + 1). The halo's inner point gets
 // p, w, r', t like any other point: its x-neighbours are its outer point and the segment's edge
@@ -383,7 +383,10 @@ int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_ol
 #endif
   // 8 waves (two per SIMD, one block per CU) of TY rows of 64 V points (TY V = 4: the register
   // budget)
-  constexpr int NW = 8, TY = PB_SR_TY, V = 4 / TY;
+#ifndef PB_SR_V
+#define PB_SR_V (4 / PB_SR_TY)
+#endif
+  constexpr int NW = 8, TY = PB_SR_TY, V = PB_SR_V;
   pb_ctx* ctx = g->ctx;
   ScopedTimer tm(ctx, "cg_sr1");
   SrGeo geo;
