@@ -47,22 +47,6 @@ struct SrGeo {
   int remap;
 };
 
-static constexpr unsigned kOob = 0x80000000u;  // a store offset past every plane: dropped
-
-typedef unsigned u4 __attribute__((ext_vector_type(4)));
-typedef unsigned u2 __attribute__((ext_vector_type(2)));
-// a lane's V points of a row (V = 2: one 16-B store, V = 1: 8 B)
-template <int V>
-__device__ __forceinline__ void store_pts(__amdgpu_buffer_rsrc_t rs, unsigned off,
-                                          const double (&v)[V]) {
-  if constexpr (V == 2) {
-    const dv2 d{v[0], v[1]};
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, d), rs, (int)off, 0, 0);
-  } else {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v[0]), rs, (int)off, 0, 0);
-  }
-}
-
 template <int V>
 using lane_pts = std::conditional_t<V == 2, dv2, double>;
 template <int V>
@@ -129,15 +113,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
 #pragma unroll
   for (int q = 0; q < TY; ++q) roff[q] = (unsigned)(ro[q] * 8) + boff;
   const int pbytes = (int)(g.plane * 8);
-  auto plane_rsrc = [&](double* base, int kk) {
-    // (inputs readfirstlane'd: a descriptor the compiler cannot prove uniform is waterfall'd)
-    const uint64_t a = (uint64_t)(base + pl(kk));
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a),
-                   hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-    void* pa = (void*)(((uint64_t)hi << 32) | lo);
-    return __builtin_amdgcn_make_buffer_rsrc(pa, (short)0, __builtin_amdgcn_readfirstlane(pbytes),
-                                             0x00020000);
-  };
+  auto plane_rsrc = [&](double* base, int kk) { return buf_rsrc(base + pl(kk), pbytes); };
   unsigned hoff = 0;  // the halo lane's byte offset in a plane
 #pragma unroll
   for (int q = 0; q < TY; ++q)

@@ -97,6 +97,34 @@ __device__ __forceinline__ void store_row(double* p, RowIx ix, const double (&v)
   }
 }
 
+// Stores through a buffer descriptor of one plane (base and size wave-uniform): an offset at or
+// past the size is dropped by the range check, so a masked store needs no branch -- control flow
+// in a z-march step makes the compiler merge its wait counts at the join (vmcnt(0): the prefetch
+// drains; gfx9 counts stores in vmcnt too)
+static constexpr unsigned kOob = 0x80000000u;  // a store offset past every plane: dropped
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int bytes) {
+  // (inputs readfirstlane'd: a descriptor the compiler cannot prove uniform is waterfall'd)
+  const uint64_t a = (uint64_t)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a),
+                 hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* pa = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pa, (short)0, __builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
+}
+// V consecutive doubles of a lane (V = 2: one 16-B store, V = 1: 8 B); AUX 2: non-temporal
+template <int V, int AUX = 0>
+__device__ __forceinline__ void store_pts(__amdgpu_buffer_rsrc_t rs, unsigned off,
+                                          const double (&v)[V]) {
+  if constexpr (V == 2) {
+    const dv2 d{v[0], v[1]};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, d), rs, (int)off, 0, AUX);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v[0]), rs, (int)off, 0, AUX);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Cross-lane helpers (DPP wave shifts: VALU only, no LDS traffic; bound_ctrl: the end lane
 // with no source reads 0, no old-value operand to initialise)
