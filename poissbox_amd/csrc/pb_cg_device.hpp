@@ -256,7 +256,7 @@ __device__ __forceinline__ void fold_prologue(const Fold& f, CgState& st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// z-march helpers of the ring-buffered CG kernels (pb_cg_sr.hip, pb_cg_pa.hip)
+// z-march helpers of the ring-buffered CG kernel (pb_cg_sr.hip)
 // ---------------------------------------------------------------------------------------------
 template <int... Qs, class F>
 __device__ __forceinline__ void unroll_steps(std::integer_sequence<int, Qs...>, F&& f) {

@@ -345,11 +345,6 @@ int launch_cg_boundary(pb_grid* g, const double* r, const double* p_old, CgState
 int launch_cg_pass_a_fold(pb_grid* g, const Star& s, const double* r, const double* p_old,
                           double* p_new, const StencilPlanes& gp, const Fold& fold, int mode,
                           int part_off, int* nblocks, bool store);
-// one rank, read-only pass A (PB_CG_PSTORE_B) as a ring-buffered z-march (pb_cg_pa.hip): the
-// partials of p.w at d_partials (width 1); fold.stage 2 (folded) or st (fold.stage 0)
-bool cg_pa_supported(const pb_grid* g);
-int launch_cg_pa(pb_grid* g, const Star& s, const double* r, const double* p_old,
-                 const CgState* st, const Fold& fold, int* nblocks);
 // split grids, folded iteration: a pass's partials reduced and allreduced into ctx->d_scalars
 int cg_reduce_allreduce(pb_ctx* ctx, int nparts, int width, bool b_region);
 int cg_reduce_allreduce(pb_ctx* ctx, const double* parts, int nparts, int width);

@@ -1065,8 +1065,6 @@ int launch_cg_pass_a(pb_grid* g, const Star& s, const double* r, const double* p
   ScopedTimer tm(g->ctx,
                  timer_name(mode, "cg_pass_a", "cg_pass_a_interior", "cg_pass_a_boundary"));
   const CombineLoad ld{r, p_old, st, 0.0, 0.0, 0.0};
-  if (!store && mode == PLANES_ALL && gp.wrap && part_off == 0 && cg_pa_supported(g))
-    return launch_cg_pa(g, s, r, p_old, st, Fold{}, nblocks);  // one rank: the ring z-march
   if (!store)
     return launch_any(g, s, ld, gp, PassAT<false>{p_new}, &st->done, mode, part_off, nblocks);
   return launch_any(g, s, ld, gp, PassA{p_new}, &st->done, mode, part_off, nblocks);
@@ -1093,8 +1091,6 @@ int launch_cg_pass_a_folded(pb_grid* g, const Star& s, const double* r, const do
   f.h_done = h_done;
   f.host_iter = host_iter - 1;  // stage 2 of the previous iteration
   const CombineLoad ld{r, p_old, nullptr, 0.0, 0.0, 0.0};
-  if (!store && gp.wrap && cg_pa_supported(g))
-    return launch_cg_pa(g, s, r, p_old, nullptr, f, nblocks);
   if (!store)
     return launch_any(g, s, ld, gp, PassAT<false>{p_new}, nullptr, PLANES_ALL, 0, nblocks, 0,
                       0, f);

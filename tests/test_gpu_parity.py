@@ -298,44 +298,6 @@ def test_cg_folded_finalize_bit_identical(ctx, case, tune):
     check_history(h1, ho)
 
 
-@pytest.mark.parametrize("n3", [(64, 32, 16), (130, 6, 33), (4, 3, 3), (6, 3, 5), (128, 15, 3),
-                                (256, 17, 3), (24, 3, 40), (512, 512, 4)])
-def test_cg_ring_pass_a_vs_engine(ctx, n3, tune):
-    """One-rank pass A (read-only, PB_CG_PSTORE_B) as the ring-buffered z-march (pb_cg_pa.hip,
-    tuning cg_pa_ring = 1) against the stencil engine's pass A (the default): p.w differs only in
-    which points each partial sums, so reason and its are equal and the histories agree to
-    rounding (1e-12 relative here, 1e-14 of the first norm at round-off level); both against the oracle. Shapes: x not a multiple of the
-    128-point segment, 3 rows, 3 planes, tiles of 14 rows with ragged last tiles, work split
-    into bands and pieces (512^2 planes over 4 z-planes: pieces cross columns)."""
-    N = int(np.prod(n3))
-    h = tuple(1.0 / m for m in n3)
-    b = O.stencil(O.fill_random(N, SEED), n3, h)
-    # (a few dozen unknowns: CG ends in exact convergence, the last norm is rounding noise)
-    rtol = 1e-8 if N >= 1000 else 1e-3
-    out = {}
-    for ring in (1, 0):
-        tune.set("cg_pa_ring", ring)
-        for fold in ("1", "0"):
-            tune.setenv("PB_CG_FOLD", fold)
-            da = pb.DA(ctx, n3)
-            P, A, x, bv = pb.initialise_linear_system(da, h)
-            bv.set_values(b)
-            reason, its, hist = pb.solve(P, A, x, bv, ["-ksp_rtol", str(rtol)])
-            out[ring, fold] = (reason, its, np.asarray(hist), x.get_values())
-    # folded and unfolded ring: the same partials in the same order, bit for bit
-    (r1, i1, h1, x1), (r0, i0, h0, x0) = out[1, "1"], out[1, "0"]
-    assert (r1, i1) == (r0, i0)
-    assert np.array_equal(h1, h0) and np.array_equal(x1, x0)
-    re, ie, he, xe = out[0, "1"]
-    assert (r1, i1) == (re, ie)
-    # (to rounding: 1e-12 relative, or 1e-14 of the initial norm once at round-off level)
-    np.testing.assert_allclose(h1, he, rtol=1e-12, atol=1e-14 * he[0])
-    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=rtol)
-    assert (r1, i1) == (ro, itso)
-    check_history(h1, ho)
-    check_x(x1, xo)
-
-
 def test_cg_zero_rhs_converges_immediately(ctx):
     n3 = (8, 8, 8)
     da = pb.DA(ctx, n3)
