@@ -47,6 +47,12 @@ struct SrGeo {
   int remap;
 };
 
+// p, r' stores non-temporal (buffer-store aux 2), like the stencil engine's outputs: 0.874-0.904
+// against 0.937-0.949 ms for cached stores at 512^3, and the next x-update pass P 0.193 against
+// 0.207-0.213 ms at 256^3 (profiles/r05/sr/sr_store_nt_ab.txt); 0: cached
+#ifndef PB_SR_STORE_AUX
+#define PB_SR_STORE_AUX 2
+#endif
 template <int V>
 using lane_pts = std::conditional_t<V == 2, dv2, double>;
 template <int V>
@@ -223,7 +229,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       const auto rs = plane_rsrc(p_new, k + 2);
 #pragma unroll
       for (int q = 0; q < TY; ++q)
-        store_pts<V>(rs, in2 && (row_ok >> q & 1u) ? roff[q] : kOob, pk2[q]);
+        store_pts<V, PB_SR_STORE_AUX>(rs, in2 && (row_ok >> q & 1u) ? roff[q] : kOob, pk2[q]);
     }
     // w(k+1) = A p, r' = r - alpha w, t = dinv r' - mu: the halo lanes' inner points first
     const double hc = inner(hk1);
@@ -257,7 +263,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
         tk1[q][e] = z + shift;
       }
       const bool ok = in1 && (row_ok >> q & 1u);
-      store_pts<V>(rs1, ok ? roff[q] : kOob, rv);
+      store_pts<V, PB_SR_STORE_AUX>(rs1, ok ? roff[q] : kOob, rv);
       // summands times 1 or 0 (exact; no branch -- selects here became branches and spills):
       // a zero of either sign leaves a sum unchanged. Masked rows hold finite values: real data,
       // zero-initialised registers and the zeroed LDS exchange (a NaN there would survive x 0)
