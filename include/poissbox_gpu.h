@@ -27,7 +27,7 @@ extern "C" {
 #endif
 
 #define PB_VERSION_MAJOR 0
-#define PB_VERSION_MINOR 1
+#define PB_VERSION_MINOR 2
 
 enum pb_error {
   PB_OK = 0,

@@ -3,7 +3,11 @@
 ! Our own driver program (not reference source). It is linked against the reference's own
 ! modules compiled where they lie (/root/reference/src/{constants,tridsol,compact_schemes}.f90,
 ! see oracle/Makefile target `ref`) and evaluates them on inputs written by
-! tests/golden/make_golden.py, so the committed fixtures are outputs of the real reference.
+! tests/golden/make_golden.py, so the committed fixtures are outputs of the real reference. The
+! 7-point operator (`star`) calls the reference's evaluate_laplacian_pointwise
+! (src/poissbox.f90:128-148) with lapl_star_coeffs (src/coefficients.f90:22-48), cut out of those
+! PETSc-dependent files by the Makefile, on each point's periodic 3x3x3 neighbourhood -- the loop
+! of compute_lapl_pointwise (src/poissbox.f90:112-119) on a one-rank periodic DMDA.
 !
 ! Manifest (text, one case per line):  op nx ny nz dx dy dz infile outfile
 !   tdma | tdma_periodic | fwd_sweep : in = [a, b, c, d] (4*nx), out = [b', d'] (2*nx)
@@ -14,11 +18,13 @@
 !   div                              : in = f (3N), out = df (N)
 !   interp | interp_div              : in = f (N),  out = fi (N)
 !   lapl                             : in = f (N),  out = d2f (N)
+!   star                             : in = f (N),  out = A f (N), uses dx, dy, dz
 program gen_fixtures
 
   use constants
   use tridsol
   use compact_schemes
+  use ref_pointwise, only: evaluate_laplacian_pointwise
 
   implicit none
 
@@ -113,10 +119,42 @@ contains
        if (op == 'interp_div') call interp_div(f3, g3)
        if (op == 'lapl') call lapl(f3, h, g3)
        call write_vec(outfile, reshape(g3, [nx * ny * nz]))
+    case ('star')
+       allocate(f3(nx, ny, nz), g3(nx, ny, nz), buf(nx * ny * nz))
+       call read_vec(infile, buf)
+       f3 = reshape(buf, [nx, ny, nz])
+       call star_apply(f3, h, g3)
+       call write_vec(outfile, reshape(g3, [nx * ny * nz]))
     case default
        print *, "unknown op ", op
        stop 2
     end select
   end subroutine run_case
+
+  ! b(i,j,k) = evaluate_laplacian_pointwise(x(i-1:i+1, j-1:j+1, k-1:k+1)) with periodic wrap (the
+  ! ghosted local vector DMGlobalToLocal fills on one rank)
+  subroutine star_apply(x, h, b)
+    real(pb_dp), dimension(:, :, :), intent(in) :: x
+    real(pb_dp), dimension(3), intent(in) :: h
+    real(pb_dp), dimension(:, :, :), intent(out) :: b
+    real(pb_dp) :: nb(3, 3, 3)
+    integer :: i, j, k, di, dj, dk, nx, ny, nz
+    nx = size(x, 1); ny = size(x, 2); nz = size(x, 3)
+    do k = 1, nz
+       do j = 1, ny
+          do i = 1, nx
+             do dk = -1, 1
+                do dj = -1, 1
+                   do di = -1, 1
+                      nb(di + 2, dj + 2, dk + 2) = x(modulo(i + di - 1, nx) + 1, &
+                           modulo(j + dj - 1, ny) + 1, modulo(k + dk - 1, nz) + 1)
+                   end do
+                end do
+             end do
+             b(i, j, k) = evaluate_laplacian_pointwise(nb, h)
+          end do
+       end do
+    end do
+  end subroutine star_apply
 
 end program gen_fixtures

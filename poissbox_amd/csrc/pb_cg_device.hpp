@@ -15,6 +15,10 @@ namespace pb {
 // the folded pass prologues
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ bool finite(double v) { return v == v && v - v == 0.0; }
+// ||z|| from the shifted sum of squares: a rounding-negative sum clamps to 0, a NaN stays NaN (so
+// the norm test below reports DIVERGED_NANORINF like PETSc's KSPCheckNorm; a clamp written as
+// zz > 0 ? zz : 0 turned a NaN into CONVERGED_ATOL)
+__device__ __forceinline__ double norm_from_sq(double zz) { return sqrt(zz < 0.0 ? 0.0 : zz); }
 // timing-only ablation builds (wrong results): every exit but the iteration limit is ignored
 template <class S>
 __device__ __forceinline__ void ablate_keep_going(S& st) {
@@ -56,7 +60,7 @@ __device__ __forceinline__ void cg_stage0(CgState& st, const double* S, double* 
     zz = S[1] - N * delta * delta;
     zr = S[2] - delta * S[3];
   }
-  const double dp = sqrt(zz > 0.0 ? zz : 0.0);
+  const double dp = norm_from_sq(zz);
   st.mu = mu;
   st.dp = dp;
   st.rnorm0 = dp;
@@ -97,12 +101,14 @@ __device__ __forceinline__ void cg_stage0(CgState& st, const double* S, double* 
   if (h_done) h_done[0] = st.done;
 }
 
-// stage 1 (after pass A): dpi = p.w -> alpha, or an INDEFINITE_MAT / NaN exit
-__device__ __forceinline__ void cg_stage1(CgState& st, double dpi) {
+// stage 1 (after pass A): dpi = p.w -> alpha, or an INDEFINITE_MAT / NaN exit. check_dot:
+// KSPSolve_CG's KSPCheckDot on p.w; PETSc's single-reduction iteration checks only beta, so a
+// non-finite recurrence dpi runs one more pass and ends at the next norm test (oracle alike)
+__device__ __forceinline__ void cg_stage1(CgState& st, double dpi, bool check_dot = true) {
   if (st.done) return;
   const int64_t i = st.it;
   const double sp = (double)((dpi > 0) - (dpi < 0)), so = (double)((st.dpi > 0) - (st.dpi < 0));
-  if (!finite(dpi)) {
+  if (check_dot && !finite(dpi)) {
     st.its = i + 1;
     st.reason = PB_KSP_DIVERGED_NANORINF;
     st.done = 1;
@@ -153,7 +159,7 @@ __device__ __forceinline__ void cg_stage2(CgState& st, const double* S, double* 
       zz = S[1] - N * delta * delta;
       zr = S[2] - delta * S[3];
     }
-    const double dp = sqrt(zz > 0.0 ? zz : 0.0);
+    const double dp = norm_from_sq(zz);
     // (single reduction: alpha_i was booked by cg_sr_top, before pass P applied it)
     if (!st.sr) cg_pend(st);
     st.dp = dp;
@@ -207,7 +213,7 @@ __device__ __forceinline__ void cg_sr_top(CgState& st) {
   if (st.done) return;
   const double dpi = st.it == 0 ? st.delta
                                 : st.delta - st.beta * st.beta * st.dpi / (st.betaold * st.betaold);
-  cg_stage1(st, dpi);
+  cg_stage1(st, dpi, false);
   if (!st.done) cg_pend(st);
 }
 

@@ -66,6 +66,11 @@ __device__ __forceinline__ double pt(const lane_pts<V>& x, int e) {
   else return x;
 }
 
+// v, or +0 where the mask is 0 (bitwise, exact; +0 leaves a sum that started at +0 bit-identical)
+__device__ __forceinline__ double keep_if(double v, long long mk) {
+  return __builtin_bit_cast(double, __builtin_bit_cast(long long, v) & mk);
+}
+
 template <int NW, int TY, int V>
 struct SrLds {
   // [step parity][p row 0, p row TY-1, t row 0, t row TY-1][wave][lane]
@@ -264,17 +269,16 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       }
       const bool ok = in1 && (row_ok >> q & 1u);
       store_pts<V, PB_SR_STORE_AUX>(rs1, ok ? roff[q] : kOob, rv);
-      // summands times 1 or 0 (exact; no branch -- selects here became branches and spills):
-      // a zero of either sign leaves a sum unchanged. Masked rows hold finite values: real data,
-      // zero-initialised registers and the zeroed LDS exchange (a NaN there would survive x 0)
-      const double m = ok ? 1.0 : 0.0;
+      // summands of masked rows become +0 by a bit mask (no branch -- selects here became
+      // branches and spills; a multiply by 0 would let a NaN / Inf of a masked row through)
+      const long long mk = ok ? -1LL : 0LL;
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         const double t = tk1[q][e];
-        acc[0] += t * m;
-        acc[1] += (t * t) * m;
-        acc[2] += (t * rv[e]) * m;
-        acc[3] += rv[e] * m;
+        acc[0] += keep_if(t, mk);
+        acc[1] += keep_if(t * t, mk);
+        acc[2] += keep_if(t * rv[e], mk);
+        acc[3] += keep_if(rv[e], mk);
       }
     });
     L.xch[cur][2][wid][lane] = pack_pts<V>(tk1[0]);
@@ -284,7 +288,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       constexpr int q = decltype(qc)::value;
       const double lo = x_lo(tk[q], TH[Q1], qc);
       const double hi = x_hi(tk[q], TH[Q1], qc);
-      const double m = in0 && (row_ok >> q & 1u) ? 1.0 : 0.0;
+      const long long mk = in0 && (row_ok >> q & 1u) ? -1LL : 0LL;
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         const double xm = e == 0 ? lo : tk[q][e == 0 ? 0 : e - 1];
@@ -292,7 +296,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
         const double ym = q == 0 ? pt<V>(thl, e) : tk[q == 0 ? 0 : q - 1][e];
         const double yp = q == TY - 1 ? pt<V>(thh, e) : tk[q == TY - 1 ? q : q + 1][e];
         const double sv = star7_sum(cx, cy, cz, cc, tkm[q][e], ym, xm, tk[q][e], xp, yp, tk1[q][e]);
-        acc[4] += (tk[q][e] * sv) * m;
+        acc[4] += keep_if(tk[q][e] * sv, mk);
       }
     });
   };

@@ -148,10 +148,10 @@ int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p) {
     p->yc[q] = p->nzl[q] * nx * p->ny_me;
   }
   p->nb = (int)std::min<int64_t>((g->nlocal + 255) / 256, (int64_t)ctx->num_cus * 16);
-  // the self block stays on the rank: RCCL contexts skip its copy (host staging moves whole
-  // buffers and keeps it)
+  // the self block stays on the rank: the pack / unpack kernels read and write it in the y-slab
+  // buffer directly and the all-to-all skips it (RCCL and, for the tests, the host transport)
   p->me = ctx->rank;
-  p->self_direct = ctx->comm != nullptr && !tune("a2a_copy_self", 0);
+  p->self_direct = (ctx->comm != nullptr || P > 1) && !tune("a2a_copy_self", 0);
   int64_t zo = 0, yo = 0;
   for (int q = 0; q < ctx->rank; ++q) {
     zo += p->zc[q];

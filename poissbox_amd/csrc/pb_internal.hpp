@@ -406,7 +406,8 @@ int launch_cg_sr_pass_p(pb_grid* g, const Star& s, const double* r, const double
                         double* p_new, double* x, double* r_out, const StencilPlanes& gp,
                         const SrFold& f, int mode, int64_t host_iter, int defer);
 int launch_cg_sr_pass_s(pb_grid* g, const Star& s, const double* r, const StencilPlanes& gp,
-                        const CgState* st, int mode, int part_off, int* nblocks);
+                        const CgState* st, int mode, int part_off, int part_end,
+                        int* nblocks);
 // after pass S (unfolded): reduce its partials `parts` (+ allreduce on split grids) and run the
 // residual-sum stage on st in place (stage_delta0: the setup's delta = z0'A z0 only)
 int cg_sr_finalize(pb_ctx* ctx, const double* parts, int nparts, CgState* st, double* hist,

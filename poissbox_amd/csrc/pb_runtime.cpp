@@ -456,8 +456,6 @@ int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, dou
                             hipMemcpyDeviceToDevice, ctx->stream));
     return PB_OK;
   }
-  if (skip_self)  // (host staging moves whole buffers: the plan never elides there)
-    return set_error(PB_ERR_ARG, "all-to-all: self-block elision needs an RCCL context");
   if (!ctx->h_alltoallv)
     return set_error(PB_ERR_COMM, "host transport without an alltoallv callback");
   const size_t need = (size_t)(so[P] + ro[P]);
@@ -473,7 +471,21 @@ int alltoallv_device(pb_ctx* ctx, const double* send, const int64_t* scount, dou
   PB_SYNC(ctx, "all-to-all staging");
   if (ctx->h_alltoallv(ctx->h_a2a_user, hs, scount, hr, rcount) != 0)
     return comm_fail(ctx, "host alltoallv callback failed");
-  PB_HIP(hipMemcpyAsync(recv, hr, ro[P] * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if (!skip_self) {
+    PB_HIP(hipMemcpyAsync(recv, hr, ro[P] * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  } else {
+    // the self block is already in place (the pack wrote it there): the staged buffers carried
+    // a stale copy through the callback, which is not brought back -- the same offsets
+    // (YSlabPlan::self_shift) as the RCCL path, on a transport the one-GPU tests can run
+    const int me = ctx->rank;
+    if (ro[me])
+      PB_HIP(hipMemcpyAsync(recv, hr, ro[me] * sizeof(double), hipMemcpyHostToDevice,
+                            ctx->stream));
+    if (ro[P] > ro[me + 1])
+      PB_HIP(hipMemcpyAsync(recv + ro[me + 1], hr + ro[me + 1],
+                            (ro[P] - ro[me + 1]) * sizeof(double), hipMemcpyHostToDevice,
+                            ctx->stream));
+  }
   PB_SYNC(ctx, "all-to-all staging");
   return PB_OK;
 }

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <strings.h>
 #include <string>
 #include <vector>
 
@@ -256,9 +257,11 @@ int pb_ksp_opts_parse(pb_ksp_opts* o, int argc, const char* const* argv) {
     } else if (!strcmp(a, "-ksp_cg_single_reduction")) {
       // PetscOptionsBool: a bare flag is true; an explicit value may follow
       o->cg_single_reduction = 1;
-      if (v && (!strcmp(v, "true") || !strcmp(v, "1") || !strcmp(v, "yes"))) {
+      // (PetscOptionsStringToBool: case-insensitive true/yes/on/1 and false/no/off/0)
+      auto is = [&](const char* w) { return v && !strcasecmp(v, w); };
+      if (is("true") || is("yes") || is("on") || is("1")) {
         ++i;
-      } else if (v && (!strcmp(v, "false") || !strcmp(v, "0") || !strcmp(v, "no"))) {
+      } else if (is("false") || is("no") || is("off") || is("0")) {
         o->cg_single_reduction = 0;
         ++i;
       }
@@ -528,8 +531,6 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   return cg_finalize_stage2(ctx, np, k->d_st, k->d_hist, k->h_done_dev, k->host_iter);
 }
 
-// pass S over r (t = dinv r - mu of state st): split grids exchange r's boundary planes (raw;
-// the loader transforms ghosts too) under the interior planes
 // the single-reduction iteration's two partial-sum regions (5 wide): iteration n of a batch
 // writes region n & 1 and its folded prologue reduces region (n - 1) & 1, so a launch never
 // overwrites the partials its own blocks may still be reading (part_off in 5-wide blocks)
@@ -540,30 +541,35 @@ static const double* sr_region(const pb_ctx* ctx, int64_t n) {
   return ctx->d_partials + sr_region_off(ctx, n) * 5;
 }
 
+// pass S over r (t = dinv r - mu of state st): split grids exchange r's boundary planes (raw;
+// the loader transforms ghosts too) under the interior planes. Every launch is bounded by the
+// end of region n & 1 (a grid that does not fit is PB_ERR_UNSUPPORTED, not a spill into the
+// region the next prologue reads)
 static int sr_pass_s(pb_ksp* k, const double* r, const CgState* st, int* nparts, int64_t n) {
   pb_grid* g = k->A->grid;
   pb_ctx* ctx = g->ctx;
   Star s{k->A->cx, k->A->cy, k->A->cz, k->A->cc};
   StencilPlanes gp;
   const int off = (int)sr_region_off(ctx, n);
+  const int end = off + (int)(ctx->partials_cap / 10);
   if (!ctx->split) {
     gp.ghost_lo = gp.ghost_hi = nullptr;
     gp.wrap = true;
-    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, off, nparts);
+    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, off, end, nparts);
   }
   gp.ghost_lo = g->ghost_lo;
   gp.ghost_hi = g->ghost_hi;
   const double* hi = r + (g->nzl - 1) * g->plane;
   if (g->nzl < 3) {
     PB_TRY(halo_exchange(g, r, hi));
-    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, off, nparts);
+    return launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_ALL, off, end, nparts);
   }
   int nb1 = 0, nb2 = 0;
   ScopedTimer tm(ctx, "cg_sr_s");
   PB_TRY(halo_begin(g, r, hi));
-  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_INTERIOR, off, &nb1));
+  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_INTERIOR, off, end, &nb1));
   PB_TRY(halo_end(g));
-  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_BOUNDARY, off + nb1, &nb2));
+  PB_TRY(launch_cg_sr_pass_s(g, s, r, gp, st, PLANES_BOUNDARY, off + nb1, end, &nb2));
   *nparts = nb1 + nb2;
   return PB_OK;
 }

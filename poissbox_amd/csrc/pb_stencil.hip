@@ -655,12 +655,14 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                     const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev,
-                    int wgcu, const Fold& fold) {
+                    int wgcu, const Fold& fold, int64_t part_end) {
   Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU);
   geo.wrap = gp.wrap && !g->ctx->split ? 1 : 0;
   const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
   constexpr int NS = Epi::NS > 0 ? Epi::NS : 1;
-  if ((part_off + nblocks) * NS > g->ctx->partials_cap)
+  // part_end (in blocks, 0: the whole buffer): the end of the caller's partial-sum region
+  const int64_t end = part_end > 0 ? part_end * NS : g->ctx->partials_cap;
+  if ((part_off + nblocks) * NS > std::min(end, g->ctx->partials_cap))
     return set_error(PB_ERR_UNSUPPORTED, "stencil grid of %lld blocks exceeds partials capacity",
                      (long long)nblocks);
   // Residency cap (Epi::CAP, the CG passes): a grid with more columns than the epilogue's WGCU
@@ -712,31 +714,31 @@ template <class Load, class Epi>
 static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                       const Epi& ep, const int* skip, int mode = PLANES_ALL, int part_off = 0,
                       int* nb_out = nullptr, int rev = 0, int wgcu = 0,
-                      const Fold& fold = Fold{}) {
+                      const Fold& fold = Fold{}, int64_t part_end = 0) {
   const bool vec2 = (g->n[0] % 2) == 0;
   const int ty = pick_ty((int)g->n[1]);
   if constexpr (Wide8Of<Epi>::v) {
     const int64_t cols4 = ((g->n[0] + 127) / 128) * ((g->n[1] + kWaves * 4 - 1) / (kWaves * 4));
     const int w = wgcu > 0 ? wgcu : Epi::WGCU;
     if (vec2 && ty == 4 && g->n[1] % 8 == 0 && cols4 > (int64_t)w * g->ctx->num_cus)
-      return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
+      return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
   }
   if constexpr (TallOf<Epi>::v) {
     if (vec2 && ty == 4 && g->n[1] % 8 == 0 && g->plane >= 512 * 512)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev,
-                            wgcu > 0 ? wgcu : 1, fold);
+                            wgcu > 0 ? wgcu : 1, fold, part_end);
   }
   if (vec2) {
     switch (ty) {
-      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
-      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
-      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
+      case 4: return launch_t<2, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
+      case 2: return launch_t<2, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
+      default: return launch_t<2, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
     }
   }
   switch (ty) {
-    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
-    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
-    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold);
+    case 4: return launch_t<1, 4>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
+    case 2: return launch_t<1, 2>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
+    default: return launch_t<1, 1>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
   }
 }
 
@@ -1288,12 +1290,13 @@ int launch_cg_sr_pass_p(pb_grid* g, const Star& s, const double* r, const double
 }
 
 int launch_cg_sr_pass_s(pb_grid* g, const Star& s, const double* r, const StencilPlanes& gp,
-                        const CgState* st, int mode, int part_off, int* nblocks) {
+                        const CgState* st, int mode, int part_off, int part_end, int* nblocks) {
   ScopedTimer tm(g->ctx, timer_name(mode, "cg_sr_s", "cg_sr_s_interior", "cg_sr_s_boundary"));
   // (marches upwards after pass P marched downwards: it starts on the planes P wrote last)
   // 4-row tiles, two workgroups per CU (a single read-only stream: 0.218-0.221 ms at 512^3 against
   // 0.247 with one per CU, 0.223-0.228 with three, 0.224 with 8-row tiles; gpurun_out sr2/sr3)
-  return launch_any(g, s, ZLoad{r, st}, gp, SrSums{}, &st->done, mode, part_off, nblocks, 0, 2);
+  return launch_any(g, s, ZLoad{r, st}, gp, SrSums{}, &st->done, mode, part_off, nblocks, 0, 2,
+                    Fold{}, part_end);
 }
 
 int cg_sr_finalize(pb_ctx* ctx, const double* parts, int nparts, CgState* st, double* hist,

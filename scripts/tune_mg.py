@@ -1,7 +1,7 @@
 """A/B the V-cycle kernel knobs at 512^3 on one GPU: PC applies (-pc_type mg) with per-phase
 HIP-event timing, interleaved rounds in ONE process.
 
-PB_TUNE_CONFIGS: JSON list of tuning dicts (pb_tune_set names, e.g. {"mg_tail": 0}). Prints one JSON line per config (median over rounds).
+PB_TUNE_CONFIGS: JSON list of tuning dicts (pb_tune_set names, e.g. {"mg_sweep2": 0}). Prints one JSON line per config (median over rounds).
 """
 import json
 import os

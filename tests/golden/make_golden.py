@@ -10,6 +10,9 @@ using the same recipes as the reference tests:
     multiplied by 10 until |b| >= |a| + |c|; a(1) = c(n) = 0 unless periodic; d = A x)
   * 1-D compact fields: sin on a 2*pi periodic line (tests/grad/test_grad_1d.f90:89-96) + random
   * 3-D compact fields: random and sum-of-sines (tests/lapl/test_lapl.f90:87-100)
+  * 7-point operator fields: random on periodic grids with uniform and non-uniform spacing
+    (src/poissbox.f90:128-148 evaluate_laplacian_pointwise + src/coefficients.f90:22-48, cut out
+    of those PETSc-dependent files by oracle/Makefile)
 The Fortran program oracle/_ref/gen_fixtures evaluates the reference routines on these inputs.
 """
 import os
@@ -94,6 +97,19 @@ def main():
             cases.append((f"{op}__{tag}_rnd", op, n3, h3, f, None))
         cases.append((f"div__{tag}_rnd", "div", n3, h3, v, None))
         cases.append((f"lapl__{tag}_sin", "lapl", n3, h3, sines3(n3, h3, 0.5), None))
+
+    # 7-point operator (SURVEY.md §8(c) golden vector 4): the reference's own
+    # evaluate_laplacian_pointwise + lapl_star_coeffs on periodic grids, unit-cube and non-uniform
+    # spacings (drawn after every case above, so those fixtures are unchanged)
+    for n3, L in (((16, 16, 16), (1.0, 1.0, 1.0)), ((17, 12, 9), (1.0, 2.0, 0.5)),
+                  ((24, 20, 10), (2.4, 0.74, 2.9)), ((32, 32, 32), (1.0, 1.0, 1.0)),
+                  ((9, 7, 5), (3.0, 1.0, 7.0))):
+        h3 = tuple(Lq / m for Lq, m in zip(L, n3))
+        N = int(np.prod(n3))
+        tag = "x".join(map(str, n3))
+        cases.append((f"star__{tag}_rnd", "star", n3, h3, rng.random(N) * 2 - 1, None))
+        if n3 == (16, 16, 16):
+            cases.append((f"star__{tag}_sin", "star", n3, h3, sines3(n3, h3, 0.0), None))
 
     out = {}
     with tempfile.TemporaryDirectory() as td:

@@ -32,7 +32,7 @@ def test_version_and_error_string():
     assert isinstance(lib.pb_last_error(), bytes)
     import ctypes as C
     a, b = C.c_int(), C.c_int()
-    assert lib.pb_version(C.byref(a), C.byref(b)) == 0 and (a.value, b.value) == (0, 1)
+    assert lib.pb_version(C.byref(a), C.byref(b)) == 0 and (a.value, b.value) == (0, 2)
 
 
 @pytest.mark.parametrize("nz,nranks", [(64, 3), (7, 3), (1024, 8), (5, 5), (512, 1), (13, 4)])
@@ -73,9 +73,37 @@ def test_options_parse_single_reduction():
     assert pb.ksp_options(["-ksp_cg_single_reduction"]).cg_single_reduction == 1
     o = pb.ksp_options(["-ksp_cg_single_reduction", "-ksp_rtol", "1e-9"])
     assert o.cg_single_reduction == 1 and o.rtol == 1e-9
-    for v, want in (("true", 1), ("1", 1), ("yes", 1), ("false", 0), ("0", 0), ("no", 0)):
+    # PetscOptionsStringToBool: case-insensitive, on/off too (FALSE turned it on)
+    for v, want in (("true", 1), ("1", 1), ("yes", 1), ("false", 0), ("0", 0), ("no", 0),
+                    ("FALSE", 0), ("True", 1), ("on", 1), ("OFF", 0), ("No", 0), ("YES", 1)):
         o = pb.ksp_options(["-ksp_cg_single_reduction", v, "-ksp_max_it", "5"])
         assert o.cg_single_reduction == want and o.max_it == 5
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors of the header's structs have the C sizes and field offsets (gcc on
+    include/poissbox_gpu.h): a stale mirror would let pb_ksp_opts_default write past it."""
+    import ctypes as C
+    import subprocess
+    structs = {"pb_ksp_opts": _lib.KspOpts, "pb_ksp_result": _lib.KspResult}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "poissbox_gpu.h"',
+             'int main(void) {']
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'  printf("{cname}.{f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append('  return 0; }')
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                 text=True).stdout.splitlines())
+    for cname, py in structs.items():
+        assert int(got[cname]) == C.sizeof(py), cname
+        for f in py._fields_:
+            assert int(got[f"{cname}.{f[0]}"]) == getattr(py, f[0]).offset, (cname, f[0])
 
 
 def test_tuning_table_round_trip():

@@ -86,6 +86,36 @@ def test_stencil_bit_exact(ctx, n):
     da.destroy()
 
 
+def test_stencil_matches_reference_fixtures(ctx, golden):
+    """SURVEY.md §8(c) golden vector 4, pinned to the reference's own arithmetic: A x (the
+    matvec kernel, MatMult through the shell operator) and compute_lapl_pointwise equal the
+    outputs of the reference's evaluate_laplacian_pointwise + lapl_star_coeffs (flang-built,
+    tests/golden/make_golden.py) bit for bit, uniform and non-uniform spacings; the assembled
+    P's rows away from the seams as well (its seam rows sum in AIJ order: test_stencil_bit_exact)."""
+    names = [n for n in sorted({k.rsplit("__", 1)[0] for k in golden.files})
+             if n.startswith("star__")]
+    assert len(names) >= 6
+    for name in names:
+        m = golden[name + "__meta"]
+        n3, h = tuple(int(v) for v in m[:3]), tuple(float(v) for v in m[3:])
+        x, ref = golden[name + "__in"], golden[name + "__out"]
+        da, xv = grid_vec(ctx, n3, x)
+        yv = pb.Vec(da)
+        A = pb.Mat(da, pb.STAR7, h)
+        A.mult(xv, yv)
+        assert np.array_equal(yv.get_values(), ref), name
+        yv.set(0.0)
+        pb.compute_lapl_pointwise(da, h, xv, yv)
+        assert np.array_equal(yv.get_values(), ref), name
+        P = pb.Mat(da, pb.ASSEMBLED27, h)
+        P.mult(xv, yv)
+        yp, r3 = yv.get_values().reshape(n3[::-1]), ref.reshape(n3[::-1])
+        assert np.array_equal(yp[1:-1, 1:-1, 1:-1], r3[1:-1, 1:-1, 1:-1]), name
+        for o in (A, P, xv, yv):
+            o.destroy()
+        da.destroy()
+
+
 def test_stencil_nonuniform_spacing(ctx):
     n = (24, 20, 10)
     L = (1.0, 2.5, 0.3)
@@ -1637,3 +1667,41 @@ def test_multirank_cg_folded_bit_identical(nranks, n, sr):
         assert np.array_equal(h8, h1) and np.array_equal(x8, x1)
         check_history(h8, ho)
         check_x(x8, xo.reshape(n[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
+
+
+@pytest.mark.parametrize("nranks,n3", [(2, (64, 64, 64)), (4, (64, 64, 64)), (3, (64, 40, 32)),
+                                       (2, (64, 40, 32))])
+def test_multirank_self_block_elision_bit_identical(tune, nranks, n3):
+    """ADVICE r05: the all-to-all's self-block elision (YSlabPlan::self_direct, the producer
+    writes the rank's own block at ybuf + self_shift) had run only on a one-rank communicator,
+    where self_shift is 0. The host transport now elides it the same way, so ranks > 0 use their
+    real offsets here: the compact operator and the spectral PC on 2 - 4 ranks (2^k rows per rank:
+    the blocked Y passes; 40 rows: the pack / unpack kernels), bit-identical to the copying form
+    (a2a_copy_self = 1) and to one rank."""
+    N = int(np.prod(n3))
+    hc = tuple(2 * np.pi / m for m in n3)
+    f = O.fill_random(N, 11)
+
+    def run(ctx, rank=0):
+        da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        xv, y = pb.Vec(da), pb.Vec(da)
+        xv.set_values(f.reshape(n3[2], -1)[k0:k0 + nk])
+        pb.compact_lapl_fast(da, hc, xv, y)
+        P = pb.Mat(da, pb.COMPACT, hc)
+        k = pb.KSP(P, P, pb.ksp_options(["-pc_type", "fft"]))
+        z = pb.Vec(da)
+        k.pc_apply(xv, z)
+        out = (k0, nk, y.get_values(), z.get_values())
+        k.destroy()
+        return out
+
+    _, _, y1, z1 = run(ctx_one := pb.Context(0))
+    ctx_one.destroy()
+    plane = n3[0] * n3[1]
+    for copy in (0, 1):
+        tune.set("a2a_copy_self", copy)
+        for k0, nk, y, z in run_ranks(nranks, run):
+            assert np.array_equal(y, y1[k0 * plane:(k0 + nk) * plane]), (copy, k0)
+            assert np.array_equal(z, z1[k0 * plane:(k0 + nk) * plane]), (copy, k0)
+    tune.set("a2a_copy_self", 0)

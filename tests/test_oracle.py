@@ -2,8 +2,10 @@
 
 * tests/golden/ref_fixtures.npz holds outputs of the flang-built reference routines
   (src/tridsol.f90, src/compact_schemes.f90) on stored inputs -> bit-exact equality.
-* The 7-point operator (src/poissbox.f90:128-148 + src/coefficients.f90:22-48) cannot be built
-  here (PETSc); it is pinned by the reference's own known-answer tests
+* The 7-point operator: evaluate_laplacian_pointwise (src/poissbox.f90:128-148) and
+  lapl_star_coeffs (src/coefficients.f90:22-48) are cut out of their PETSc-dependent files and
+  built by oracle/Makefile; the `star__*` fixtures are their outputs on periodic grids (uniform and
+  non-uniform spacing) -> bit-exact equality; plus the reference's own known-answer tests
   (tests/coefficients/test_star.f90, test_d2dx2.f90) restated below.
 * KSPCG is pinned by properties (convergence, residual, iteration counts of SURVEY.md §6).
 """
@@ -115,6 +117,21 @@ def test_star_coefficients_known_answers():
         val = float(np.dot(f.reshape(-1), coef.reshape(-1))) * dx ** 2
         ref = expect * dx ** 2
         assert abs(val - ref) <= tol * abs(ref) or abs(val - ref) <= tol
+
+
+def test_stencil_matches_reference_pointwise(golden):
+    """SURVEY.md §8(c) golden vector 4: the oracle's 7-term stencil and its 27-term faithful form
+    equal the reference's own evaluate_laplacian_pointwise bit for bit; the assembled P's rows
+    away from the seams (AIJ column order = the reference's order there) too."""
+    names = _cases(golden, "star")
+    assert len(names) >= 6
+    for name in names:
+        n3, h = _meta(golden, name)
+        x, ref = golden[name + "__in"], golden[name + "__out"]
+        assert np.array_equal(O.stencil(x, n3, h), ref), name
+        assert np.array_equal(O.stencil(x, n3, h, faithful=True), ref), name
+        ya = O.assembled(x, n3, h).reshape(n3[::-1])
+        assert np.array_equal(ya[1:-1, 1:-1, 1:-1], ref.reshape(n3[::-1])[1:-1, 1:-1, 1:-1]), name
 
 
 def test_stencil_fast_equals_faithful():
