@@ -133,6 +133,10 @@ int pb_ctx_reset_timing(pb_ctx* ctx);
  * standalone matvec's access mix without its stencil -- `reps` timed launches after two warm-ups;
  * GB/s counted as 16 B per element. Allocates and frees its own 2 x n doubles. */
 int pb_ctx_copy_probe(pb_ctx* ctx, int64_t n, int reps, double* best_gbps, double* median_gbps);
+/* The same copy from x into y (both of one grid; y is overwritten): the matvec's own buffers,
+ * so a placement-dependent rate shows up beside the matvec x -> y. */
+int pb_vec_copy_probe(const pb_vec* x, pb_vec* y, int reps, double* best_gbps,
+                      double* median_gbps);
 
 /* ---- tuning (kernel selection and launch shapes; no reference counterpart) ----
  * Process-wide table of the launchers' parameters (INTEGRATION.md lists the names: z-march

@@ -68,6 +68,7 @@ _SIGS = {
     "pb_ctx_get_timing_samples": [c_p, C.c_char_p, C.POINTER(C.c_float), c_i64, P_i64],
     "pb_ctx_reset_timing": [c_p],
     "pb_ctx_copy_probe": [c_p, c_i64, C.c_int, P_d, P_d],
+    "pb_vec_copy_probe": [c_p, c_p, C.c_int, P_d, P_d],
     "pb_slab_partition": [c_i64, C.c_int, C.c_int, P_i64, P_i64],
     "pb_grid_create": [c_p, P_i64, P_d, C.POINTER(c_p)],
     "pb_grid_get_corners": [c_p, P_i64, P_i64],

@@ -304,6 +304,13 @@ class Vec:
     def set_random(self, seed):
         L.call("pb_vec_set_random", self.h, C.c_uint64(int(seed)))
 
+    def copy_probe(self, y, reps=10):
+        """HBM calibration over this vector's and y's own buffers (y is overwritten): flat copy
+        self -> y, the matvec's access mix. Returns (best, median) GB/s."""
+        best, med = C.c_double(), C.c_double()
+        L.call("pb_vec_copy_probe", self.h, y.h, int(reps), C.byref(best), C.byref(med))
+        return best.value, med.value
+
     def device_ptr(self):
         p, n = C.c_void_p(), C.c_int64()
         L.call("pb_vec_device_ptr", self.h, C.byref(p), C.byref(n))

@@ -538,7 +538,8 @@ int vec_random(pb_ctx* ctx, double* d, int64_t n, uint64_t seed, int64_t g0);
 // reduce kind: 0 = sum(x), 1 = dot(x, y); result into *out (global over ranks)
 int vec_reduce(pb_ctx* ctx, int kind, const double* x, const double* y, int64_t n, double* out);
 // flat fp64 copy of n doubles (HBM calibration): per-launch ms of `reps` timed launches
-int copy_probe(pb_ctx* ctx, int64_t n, int reps, std::vector<float>& ms);
+int copy_probe(pb_ctx* ctx, int64_t n, int reps, std::vector<float>& ms,
+               const double* src = nullptr, double* dst = nullptr);
 
 // ---- grid with an explicit slab (multigrid levels) ----
 int grid_create_part(pb_ctx* ctx, const int64_t n[3], const double L[3], int64_t k0, int64_t nzl,

@@ -896,6 +896,24 @@ int pb_ctx_copy_probe(pb_ctx* ctx, int64_t n, int reps, double* best_gbps, doubl
   return PB_OK;
 }
 
+int pb_vec_copy_probe(const pb_vec* x, pb_vec* y, int reps, double* best_gbps,
+                      double* median_gbps) {
+  PB_CHECK_ARG(x && y && x != y && reps >= 1 && best_gbps && median_gbps,
+               "bad copy probe args");
+  PB_CHECK_ARG(x->grid == y->grid && x->nlocal == y->nlocal, "vectors of different grids");
+  pb_ctx* ctx = x->grid->ctx;
+  PB_HIP(hipSetDevice(ctx->device));
+  const int64_t n = x->nlocal / 2 * 2;
+  PB_CHECK_ARG(n >= 2, "vector too short for the copy probe");
+  std::vector<float> ms;
+  PB_TRY(copy_probe(ctx, n, reps, ms, x->d, y->d));
+  std::sort(ms.begin(), ms.end());
+  const double bytes = 16.0 * (double)n;
+  *best_gbps = bytes / (ms.front() * 1e-3) / 1e9;
+  *median_gbps = bytes / (ms[ms.size() / 2] * 1e-3) / 1e9;
+  return PB_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Grid
 // ---------------------------------------------------------------------------------------------

@@ -137,19 +137,23 @@ __global__ __launch_bounds__(256) void copy_probe_kernel(const dv2* __restrict__
     __builtin_nontemporal_store(x[i], y + i);
 }
 
-int copy_probe(pb_ctx* ctx, int64_t n, int reps, std::vector<float>& ms) {
+// src / dst given: copy between those buffers (the matvec's own x and y, pb_vec_copy_probe);
+// otherwise two fresh buffers, zero-filled
+int copy_probe(pb_ctx* ctx, int64_t n, int reps, std::vector<float>& ms, const double* src,
+               double* dst) {
   const int64_t n2 = n / 2;
-  dv2 *x = nullptr, *y = nullptr;
-  if (hipMalloc(&x, n2 * sizeof(dv2)) != hipSuccess)
+  const bool own = !src || !dst;
+  dv2 *x = own ? nullptr : (dv2*)src, *y = own ? nullptr : (dv2*)dst;
+  if (own && hipMalloc(&x, n2 * sizeof(dv2)) != hipSuccess)
     return set_error(PB_ERR_ALLOC, "copy probe: out of device memory");
-  if (hipMalloc(&y, n2 * sizeof(dv2)) != hipSuccess) {
+  if (own && hipMalloc(&y, n2 * sizeof(dv2)) != hipSuccess) {
     (void)hipFree(x);
     return set_error(PB_ERR_ALLOC, "copy probe: out of device memory");
   }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = PB_OK;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
-      hipMemsetAsync(x, 0, n2 * sizeof(dv2), ctx->stream) != hipSuccess) {
+      (own && hipMemsetAsync(x, 0, n2 * sizeof(dv2), ctx->stream) != hipSuccess)) {
     rc = set_error(PB_ERR_HIP, "copy probe: setup failed");
   }
   // grids of 4 .. 32 workgroups per CU; the samples of the fastest (by median) are returned
@@ -178,8 +182,10 @@ int copy_probe(pb_ctx* ctx, int64_t n, int reps, std::vector<float>& ms) {
   (void)hipStreamSynchronize(ctx->stream);
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
-  (void)hipFree(x);
-  (void)hipFree(y);
+  if (own) {
+    (void)hipFree(x);
+    (void)hipFree(y);
+  }
   return rc;
 }
 
