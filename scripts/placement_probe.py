@@ -40,7 +40,7 @@ def main():
             for _ in range(reps):
                 A.mult(x, y)
             ctx.sync()
-            smp = sorted(ctx.timing_samples("stencil"))
+            smp = sorted(float(v) for v in ctx.timing_samples("stencil"))
             ctx.set_timing(False)
             cb, cm = x.copy_probe(y, reps=6)
             px, py = x.device_ptr()[0], y.device_ptr()[0]

@@ -48,6 +48,12 @@ def _check(reason, its, hist, ro, itso, ho, pc, tag):
         assert rel < bar, (tag, rel)
 
 
+def _oracle_sr(pc, sr):
+    # the single-reduction iteration runs with the Jacobi / no PC; with a stored-z PC (mg, fft)
+    # the library runs KSPSolve_CG (include/poissbox_gpu.h), so that is the oracle's form there
+    return sr if pc in ("jacobi", "none") else 0
+
+
 def _opts(pc, sr):
     return ["-pc_type", pc, "-ksp_rtol", "1e-8"] + (["-ksp_cg_single_reduction"] if sr else [])
 
@@ -65,7 +71,7 @@ def _mats(da, h, pc):
 @pytest.mark.parametrize("kind", KINDS)
 def test_nonfinite_rhs_one_rank(ctx, pc, sr, kind):
     n3, h, b = _rhs(pc, kind)
-    _, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-8, pc=pc, single_reduction=sr)
+    _, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-8, pc=pc, single_reduction=_oracle_sr(pc, sr))
     if kind != "big":
         assert (ro, itso) == (-9, 0)
     da = pb.DA(ctx, n3)
@@ -82,7 +88,8 @@ def test_nonfinite_rhs_one_rank(ctx, pc, sr, kind):
 def test_nonfinite_rhs_two_ranks(pc, sr, kind):
     from test_gpu_parity import run_ranks
     n3, h, b = _rhs(pc, kind)
-    _, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-8, pc=pc, single_reduction=sr, nranks=2)
+    _, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-8, pc=pc, single_reduction=_oracle_sr(pc, sr),
+                                 nranks=2)
 
     def body(ctx, rank):
         da = pb.DA(ctx, n3)
