@@ -658,6 +658,7 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
                     int wgcu, const Fold& fold, int64_t part_end) {
   Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU);
   geo.wrap = gp.wrap && !g->ctx->split ? 1 : 0;
+  if constexpr (std::is_same_v<Epi, StoreY>) geo.nt = tune("stencil_nt", 1);  // (A/B runs)
   const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
   constexpr int NS = Epi::NS > 0 ? Epi::NS : 1;
   // part_end (in blocks, 0: the whole buffer): the end of the caller's partial-sum region
@@ -724,7 +725,8 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
   }
   if constexpr (TallOf<Epi>::v) {
-    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && g->plane >= 512 * 512)
+    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && g->plane >= 512 * 512 &&
+        tune("stencil_tall", 1) != 0)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev,
                             wgcu > 0 ? wgcu : 1, fold, part_end);
   }
@@ -758,7 +760,8 @@ int launch_star7_apply(pb_grid* g, const Star& s, const double* x, double* y,
   // plane per chunk, direction-free, and does not flip it)
   const int rev = g->ctx->zflip;
   if (mode != PLANES_BOUNDARY) g->ctx->zflip ^= 1;
-  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, g->ctx->op_skip, mode, 0, nullptr, rev);
+  return launch_any(g, s, PlainLoad{x}, gp, StoreY{y}, g->ctx->op_skip, mode, 0, nullptr, rev,
+                    tune("stencil_wgcu", 0));
 }
 
 // ---------------------------------------------------------------------------------------------
