@@ -449,6 +449,22 @@ def run_solve_workload(args, pb, ctx, workload, scaling, steps, warmup, rank, wo
             comm[f"{nm}_ms_per_solve"] = ms_
             comm[f"{nm}_calls"] = cnt_
     ctx.set_timing(False)
+    if workload == "compact-fft" and "pc_fft_x" in kern:
+        # the spectral PC's X passes carry CG's work, so their bytes differ by role, but each
+        # solve's are fixed: per PC apply a forward X pass (16 B/DoF: r in,
+        # z out) and an inverse one taking the residual sums (24: z, r in, z out); on the
+        # iterations' applies (x / r update fused, pb_solver.cpp enqueue_pc_iteration, planes
+        # 512 / 1024 wide) the forward pass also reads w, p and x (not on the first) and stores
+        # r and x: 48 (first iteration, x0 = 0) or 56
+        its_d = int(its_seen[-1]) if its_seen else 0
+        fused = n[0] in (512, 1024) and n[1] % 2 == 0 and pb.tune_get("fft_rupd") != 0
+        bpd_it = [(48 if i == 0 else 56) if fused else 16 for i in range(its_d)]
+        bpd_solve = 16 + 24 + sum(b_ + 24 for b_ in bpd_it)
+        row = kern["pc_fft_x"]
+        if row["launches_per_solve"] == 2 + 2 * its_d:
+            t_ = row["avg_ms"] * row["launches_per_solve"] / 1e3
+            row.update(bytes_per_dof_per_solve=bpd_solve, GBps=bpd_solve * nloc / t_ / 1e9,
+                       frac=bpd_solve * nloc / t_ / 1e9 / HBM_PEAK_GBS)
     # true residual of the last solve: ||b - A x|| / ||b||
     r = pb.Vec(da)
     A.mult(x, r)

@@ -630,6 +630,13 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   if (nchunk > nk) nchunk = nk;
   if (nchunk < 1) nchunk = 1;
   geo.kc = (nk + nchunk - 1) / nchunk;
+  // chunk skew (A/B, in 64ths of a chunk): longer chunks and a shorter last one, so that the
+  // planes the chunks march through together are not a power-of-two number of planes apart
+  const int skew = tune("engine_kc_skew", 0);
+  if (nchunk > 1 && skew > 0) {
+    const int kc = geo.kc + std::max(1, geo.kc * skew / 64);
+    if ((int64_t)kc * (nchunk - 1) < nk) geo.kc = kc;
+  }
   geo.kstride = geo.kc;
   geo.nchunk = (nk + geo.kc - 1) / geo.kc;
   return geo;
@@ -658,7 +665,16 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
                     int wgcu, const Fold& fold, int64_t part_end) {
   Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU);
   geo.wrap = gp.wrap && !g->ctx->split ? 1 : 0;
-  if constexpr (std::is_same_v<Epi, StoreY>) geo.nt = tune("stencil_nt", 1);  // (A/B runs)
+  if constexpr (std::is_same_v<Epi, StoreY>) {  // (A/B runs)
+    geo.nt = tune("stencil_nt", 1);
+    const int kc = tune("stencil_kc", 0);
+    if (kc > 0 && mode != PLANES_BOUNDARY) {
+      const int nk = geo.k_hi - geo.k_lo;
+      geo.kc = std::min(kc, nk);
+      geo.kstride = geo.kc;
+      geo.nchunk = (nk + geo.kc - 1) / geo.kc;
+    }
+  }
   const int64_t nblocks = (int64_t)geo.nsegx * geo.ntile * geo.nchunk;
   constexpr int NS = Epi::NS > 0 ? Epi::NS : 1;
   // part_end (in blocks, 0: the whole buffer): the end of the caller's partial-sum region
