@@ -588,7 +588,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
 // Plane sets: PLANES_ALL = [0, nzl); PLANES_INTERIOR = [1, nzl-1) (no ghost plane is read);
 // PLANES_BOUNDARY = {0, nzl-1} (the two planes that read ghosts) -- the split lets the halo
 // exchange of a multi-rank step overlap the interior.
-static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
+static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu, int skew) {
   Geo geo;
   geo.rev = rev;
   geo.k0 = (int)g->k0;
@@ -630,9 +630,12 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu) {
   if (nchunk > nk) nchunk = nk;
   if (nchunk < 1) nchunk = 1;
   geo.kc = (nk + nchunk - 1) / nchunk;
-  // chunk skew (A/B, in 64ths of a chunk): longer chunks and a shorter last one, so that the
-  // planes the chunks march through together are not a power-of-two number of planes apart
-  const int skew = tune("engine_kc_skew", 0);
+  // chunk skew (in 64ths of a chunk): longer chunks and a shorter last one, so that the planes
+  // the chunks march through together are not a power-of-two number of planes apart. The
+  // standalone matvec's four 128-plane chunks at 512^3 ran 0.37-0.42 ms depending on where its x
+  // and y sat (pairs of buffers: one slow, one fast group); chunks of 136 planes ran 0.36-0.38
+  // over the same pairs (profiles/r06/placement/). The CG passes' two 256-plane chunks gained
+  // nothing from it (skew 2: within noise, 4 / 8: slower) and keep 0.
   if (nchunk > 1 && skew > 0) {
     const int kc = geo.kc + std::max(1, geo.kc * skew / 64);
     if ((int64_t)kc * (nchunk - 1) < nk) geo.kc = kc;
@@ -663,7 +666,9 @@ template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                     const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev,
                     int wgcu, const Fold& fold, int64_t part_end) {
-  Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU);
+  Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU,
+                     std::is_same_v<Epi, StoreY> ? tune("stencil_kc_skew", 4)
+                                                 : tune("engine_kc_skew", 0));
   geo.wrap = gp.wrap && !g->ctx->split ? 1 : 0;
   if constexpr (std::is_same_v<Epi, StoreY>) {  // (A/B runs)
     geo.nt = tune("stencil_nt", 1);
