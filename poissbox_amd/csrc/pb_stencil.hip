@@ -742,7 +742,10 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
   if constexpr (Wide8Of<Epi>::v) {
     const int64_t cols4 = ((g->n[0] + 127) / 128) * ((g->n[1] + kWaves * 4 - 1) / (kWaves * 4));
     const int w = wgcu > 0 ? wgcu : Epi::WGCU;
-    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && cols4 > (int64_t)w * g->ctx->num_cus)
+    // (cg_tall, A/B: 8-row tiles on 512^2 planes too)
+    if (vec2 && ty == 4 && g->n[1] % 8 == 0 &&
+        (cols4 > (int64_t)w * g->ctx->num_cus ||
+         (g->plane >= 512 * 512 && tune("cg_tall", 0) != 0)))
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
   }
   if constexpr (TallOf<Epi>::v) {
