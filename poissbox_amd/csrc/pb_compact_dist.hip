@@ -43,10 +43,25 @@ __global__ __launch_bounds__(256) void slab_transpose_kernel(double* zs, double*
 // doubles in its rank's block, so a thread moves 16-byte pairs of a row and the rank lookup and
 // index arithmetic are done once per row instead of once per element (force_comm 512^3 pack /
 // unpack: the per-element kernel moved ~3.4 TB/s).
+// cz (pack only, CG on a split grid, CgFuse::z): the packed field is CG's direction formed on the
+// way, p = (dinv z - mu) + beta/beta_old p_old with p_old = zs (cg_gen_p_kernel's arithmetic, bit
+// for bit), and it is also stored back into zs; with the state's done flag set zs is packed as is
+struct PackP {
+  const double* cz = nullptr;
+  const CgState* st = nullptr;
+  int first = 0;
+};
 __global__ __launch_bounds__(256) void slab_rows_kernel(double* zs, double* buf, int nx, int ny,
                                                         int nzl, const int* jrank, const int* j0,
                                                         const int* nyl, int dir, int me,
-                                                        double* self) {
+                                                        double* self, PackP pp) {
+  const bool form_p = pp.cz && !pp.st->done;  // (uniform)
+  double dinv = 1.0, shift = 0.0, bbp = 0.0;
+  if (form_p) {
+    dinv = pp.st->dinv;
+    shift = -pp.st->mu;
+    bbp = pp.st->it == 0 ? 0.0 : pp.st->beta / pp.st->betaold;
+  }
   const int hp = nx >> 1;                              // pairs per row
   const int step = hp < 256 ? hp : 256;                // pair stride of a thread within its row
   const int rpb = hp < 256 ? 256 / hp : 1;             // rows per block step
@@ -61,7 +76,18 @@ __global__ __launch_bounds__(256) void slab_rows_kernel(double* zs, double* buf,
     const int64_t a = row * nx;
     double* bb = self && r == me ? self : buf;  // the self block: straight to / from the y-slab
     for (int q = p0; q < hp; q += step) {
-      if (dir == 0)
+      if (dir == 0 && form_p) {
+        const dv2 zv = *reinterpret_cast<const dv2*>(pp.cz + a + 2 * q);
+        const dv2 po = *reinterpret_cast<const dv2*>(zs + a + 2 * q);
+        dv2 pv;
+        double z0 = dinv * zv.x, z1 = dinv * zv.y;
+        z0 = z0 + shift;
+        z1 = z1 + shift;
+        pv.x = pp.first ? z0 : z0 + bbp * po.x;
+        pv.y = pp.first ? z1 : z1 + bbp * po.y;
+        *reinterpret_cast<dv2*>(zs + a + 2 * q) = pv;
+        *reinterpret_cast<dv2*>(bb + b + 2 * q) = pv;
+      } else if (dir == 0)
         *reinterpret_cast<dv2*>(bb + b + 2 * q) = *reinterpret_cast<const dv2*>(zs + a + 2 * q);
       else
         *reinterpret_cast<dv2*>(zs + a + 2 * q) = *reinterpret_cast<const dv2*>(bb + b + 2 * q);
@@ -71,8 +97,9 @@ __global__ __launch_bounds__(256) void slab_rows_kernel(double* zs, double* buf,
 
 // ybuf: the y-slab buffer on the other side of the all-to-all (its self block is read / written
 // here directly when p.self_direct)
+// pp.cz: the pack forms CG's p on the way (even nx only; the caller checks)
 static void launch_slab_transpose(pb_grid* g, const YSlabPlan& p, double* zs, int dir,
-                                  const double* ybuf) {
+                                  const double* ybuf, const PackP& pp = PackP{}) {
   pb_ctx* ctx = g->ctx;
   double* self = p.self_direct ? const_cast<double*>(ybuf) + p.self_shift : nullptr;
   const int64_t ny = g->n[1];
@@ -83,7 +110,7 @@ static void launch_slab_transpose(pb_grid* g, const YSlabPlan& p, double* zs, in
     const int nb = (int)std::min<int64_t>((rows + rpb - 1) / rpb, (int64_t)ctx->num_cus * 16);
     hipLaunchKernelGGL(slab_rows_kernel, dim3(nb), dim3(256), 0, ctx->stream, zs, p.stage,
                        (int)g->n[0], (int)ny, (int)g->nzl, p.tab, p.tab + ny, p.tab + ny + P, dir,
-                       p.me, self);
+                       p.me, self, pp);
     return;
   }
   hipLaunchKernelGGL(slab_transpose_kernel, dim3(p.nb), dim3(256), 0, ctx->stream, zs, p.stage,
@@ -169,12 +196,19 @@ bool yslab_blocked(const YSlabPlan& p) {
   return true;
 }
 
-int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy) {
+int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy, CgFuse* cf) {
   pb_ctx* ctx = g->ctx;
   {
     ScopedTimer tm(ctx, "slab_pack");
-    launch_slab_transpose(g, p, const_cast<double*>(f), 0, fy);
+    PackP pp;
+    if (cf && cf->z && g->n[0] % 2 == 0 && cf->p_old == f && cf->p_out == f) {
+      pp.cz = cf->z;
+      pp.st = cf->st;
+      pp.first = cf->first;
+    }
+    launch_slab_transpose(g, p, const_cast<double*>(f), 0, fy, pp);
     PB_HIP(hipGetLastError());
+    if (pp.cz) cf->fused_z = true;
   }
   return alltoallv_device(ctx, p.stage, p.zc.data(), fy, p.yc.data(), p.self_direct);
 }
@@ -199,7 +233,17 @@ int compact_dist_pass_z(pb_grid* g, double h, const double* f, double* u, double
   double* vy = uy + ny_slab;
   YSlabPlan p;
   PB_TRY(yslab_begin(g, vy + ny_slab, &p));
-  PB_TRY(yslab_to(g, p, f, fy));
+  // CG on a split grid (CgFuse): p is formed by the pack; the y-slab Z pass must not form it
+  // again, so the fusion is hidden from the passes until the transposes are done (the X pass
+  // takes p . w)
+  CgFuse* cf = g->ctx->cg_fuse;
+  struct Hide {
+    pb_ctx* c;
+    CgFuse* f;
+    ~Hide() { c->cg_fuse = f; }
+  } hide{g->ctx, cf};
+  g->ctx->cg_fuse = nullptr;
+  PB_TRY(yslab_to(g, p, f, fy, cf));
   const int64_t dy[3] = {g->n[0], p.ny_me, g->n[2]};
   PB_TRY(compact_pass_z(g->ctx, dy, h, fy, uy, vy));
   if (blocked) *blocked = false;

@@ -734,6 +734,14 @@ bool compact_cg_fusable(const pb_grid* g) {
          tune("cg_fuse", 1);
 }
 
+// split grids (z-slab <-> y-slab transposes, r06): p is formed by the pack of the transpose
+// (pb_compact_dist.hip, even nx) and p . w taken by the X pass (register line solves in x);
+// a pass that does not fuse is reported and the solver runs the separate kernels for it
+bool compact_cg_fusable_split(const pb_grid* g) {
+  return g->ctx->split && tune("compact_lines", 1) && compact_lines_supported(g->n[0]) &&
+         g->n[0] % 2 == 0 && tune("cg_fuse", 1);
+}
+
 bool compact_lines_supported(int64_t n) {
   if (n % 64) return false;
   const int64_t C = n / 64;

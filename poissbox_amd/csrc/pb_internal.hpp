@@ -453,6 +453,7 @@ inline hipError_t field_alloc(T** p, size_t bytes) {
 // ---- register-resident line solves (pb_compact_lines.hip) ----
 bool compact_lines_supported(int64_t n);
 bool compact_cg_fusable(const pb_grid* g);  // CgFuse applies to the compact operator on g
+bool compact_cg_fusable_split(const pb_grid* g);  // ... on a split grid (pack + X pass)
 struct YSlabPlan;
 // blk_in (Y pass of a decomposed grid): in0 / in1 are the all-to-all receive buffers in their
 // blocked layout (yslab_blocked), not z-slab fields
@@ -498,7 +499,10 @@ struct YSlabPlan {
 int64_t yslab_len(const pb_grid* g);
 int64_t yslab_aux_len(const pb_grid* g);
 int yslab_begin(pb_grid* g, double* aux, YSlabPlan* p);  // aux: yslab_aux_len doubles
-int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy);
+struct CgFuse;
+// cf (CG on a split grid): the pack forms CG's p from cf->z and p_old = f in place (sets
+// cf->fused_z)
+int yslab_to(pb_grid* g, const YSlabPlan& p, const double* f, double* fy, CgFuse* cf = nullptr);
 // equal y-slabs of 2^k rows: a z-slab row (kl, j) sits in the all-to-all buffer at block j >> k,
 // row kl * nyl + (j & (nyl - 1)) -- producers / consumers may address it directly
 bool yslab_blocked(const YSlabPlan& p);

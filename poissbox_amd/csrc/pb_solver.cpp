@@ -492,9 +492,10 @@ static int enqueue_pc_iteration(pb_ksp* k) {
   double* p = k->pb[0];
   int np = 0;
   const int first = k->lazy0 && k->host_iter == 0;  // r0 = b, x0 = 0, p0 = 0 implicit
-  if (k->A->kind == PB_OP_COMPACT && compact_cg_fusable(g)) {
-    // the compact operator forms p in its Z pass and takes p . w in its X pass (CgFuse):
-    // two vector passes fewer (cg_gen_p, cg_gen_dot), 16 B/DoF less per iteration
+  if (k->A->kind == PB_OP_COMPACT && (compact_cg_fusable(g) || compact_cg_fusable_split(g))) {
+    // the compact operator forms p in its Z pass (split grids: in the pack of the z -> y
+    // transpose) and takes p . w in its X pass (CgFuse): two vector passes fewer (cg_gen_p,
+    // cg_gen_dot), 16 B/DoF less per iteration
     CgFuse cf;
     cf.z = k->z;
     cf.p_old = p;

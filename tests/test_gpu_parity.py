@@ -1705,3 +1705,43 @@ def test_multirank_self_block_elision_bit_identical(tune, nranks, n3):
             assert np.array_equal(y, y1[k0 * plane:(k0 + nk) * plane]), (copy, k0)
             assert np.array_equal(z, z1[k0 * plane:(k0 + nk) * plane]), (copy, k0)
     tune.set("a2a_copy_self", 0)
+
+
+@pytest.mark.parametrize("nranks,n3,pc", [(2, (64, 32, 32), "fft"), (3, (64, 48, 32), "fft"),
+                                          (2, (64, 32, 16), "mg")])
+def test_multirank_compact_cg_fused(tune, nranks, n3, pc):
+    """Split grids, compact A (r06): the transpose's pack forms CG's p = (z - mu) + b/b0 p_old
+    (cg_gen_p_kernel's arithmetic) and the X pass takes p . w (CgFuse), against the separate
+    kernels (cg_fuse = 0): same reason and iterations, histories within 1e-12 of each other (p . w
+    summed in another order), both on the oracle's history; x alike. Fixed iterations with the
+    7-point symbol's spectral PC / the 7-point MG (long histories)."""
+    its = 12
+    h = tuple(2 * np.pi / m for m in n3)
+    b = O.lapl(O.fill_random(int(np.prod(n3)), SEED), n3, h)
+    opts = ["-pc_type", pc, "-ksp_rtol", "0", "-ksp_atol", "0", "-ksp_max_it", str(its),
+            "-ksp_divtol", "1e300"]
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=0.0, atol=0.0, dtol=1e300, max_it=its, pc=pc,
+                                  op="compact", pc_compact=False, nthreads=8, nranks=nranks)
+
+    def body(ctx, rank):
+        da = pb.DA(ctx, n3, (2 * np.pi,) * 3)
+        (_, _, k0), (_, _, nk) = da.get_corners()
+        A = pb.Mat(da, pb.COMPACT, h)
+        P = pb.Mat(da, pb.STAR7 if pc == "fft" else pb.ASSEMBLED27, h)
+        x, bv = pb.Vec(da), pb.Vec(da)
+        bv.set_values(b.reshape(n3[2], -1)[k0:k0 + nk])
+        reason, its_g, hist = pb.solve(P, A, x, bv, opts)
+        return k0, nk, reason, its_g, np.asarray(hist), x.get_values()
+
+    res = {}
+    for fuse in (1, 0):
+        tune.set("cg_fuse", fuse)
+        res[fuse] = run_ranks(nranks, body)
+    tune.set("cg_fuse", 1)
+    for (k0, nk, r1, i1, h1, x1), (_, _, r0, i0, h0, x0) in zip(res[1], res[0]):
+        assert (r1, i1) == (r0, i0) == (ro, itso)
+        assert np.max(np.abs(h1 - h0) / h0) < 1e-12
+        check_history(h1, ho, bar=HIST_RTOL_PC)
+        xs = np.max(np.abs(xo))
+        assert np.max(np.abs(x1 - x0)) <= 1e-12 * xs
+        check_x(x1, xo.reshape(n3[2], -1)[k0:k0 + nk].reshape(-1), scale=xs)
