@@ -625,7 +625,10 @@ template <int C>
 static int launch_x_direct(pb_ctx* ctx, LinePass& p, int64_t nlines) {
   CgFuse* cf = ctx->cg_fuse;
   if (cf && cf->dot_p) {  // p . w partial sums: a fixed grid of at most 16 blocks per CU
-    const int64_t nb = std::min<int64_t>((nlines + 3) / 4, (int64_t)ctx->num_cus * 16);
+    // (x_dot_cu, A/B: blocks per CU of that grid; 0: one line per wave like the plain X pass)
+    const int per_cu = tune("x_dot_cu", 16);
+    const int64_t nb = per_cu > 0 ? std::min<int64_t>((nlines + 3) / 4, (int64_t)ctx->num_cus * per_cu)
+                                   : (nlines + 3) / 4;
     if (nb > ctx->partials_cap) return set_error(PB_ERR_UNSUPPORTED, "x pass: partials");
     p.dot_p = cf->dot_p;
     p.parts = ctx->d_partials;
