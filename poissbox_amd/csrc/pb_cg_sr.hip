@@ -15,7 +15,8 @@
 // Rows: a block stacks NW waves of TY rows, each wave forms every stage on its own rows only, and
 // the values one row out come from the neighbouring waves through LDS (published one step before
 // use, double buffered by step parity, one block barrier per step); each stage loses a row at the
-// block's ends, so blocks store rows 2 .. NW TY - 3 and advance by NW TY - 4 rows.
+// block's ends, so blocks store rows 2 .. NW TY - 3 and advance by NW TY - 4 rows (with delta in
+// the difference form, below: rows 1 .. NW TY - 3, advancing by NW TY - 3).
 // Columns: a wave owns 64 V points (V = 2, the default: 64 lanes x one 16-B pair, whole 128-B
 // lines, segments that tile a 512-point row exactly; V = 1 with 3- or 4-row waves, PB_SR_TY /
 // PB_SR_V, measured slower). The two points either side of each row are a "halo pair", all of a wave's halo pairs
@@ -42,10 +43,21 @@ namespace pb {
 struct SrGeo {
   int nx, ny, nzl;
   int64_t plane;
-  int nseg, ntile;  // x segments of 64 V points, y tiles of NW TY - 4 rows
+  int nseg, ntile;  // x segments of 64 V points, y tiles of NW TY - kSrHalo rows
   int W;            // planes of work per workgroup
   int remap;
 };
+
+// delta = t'A t in the difference form (r06, default): -sum (cx dx^2 + cy dy^2 + cz dz^2) over
+// forward differences of t, plus (cc + 2 cx + 2 cy + 2 cz) sum t^2 (~0), equal to t'A t in exact
+// arithmetic on the periodic grid. It needs t one row further on one side only, so a block stores
+// NW TY - 3 of its NW TY rows instead of NW TY - 4 (fewer rows fetched twice by neighbouring
+// tiles). 0: delta = t . (A t) with the stencil, two rows of halo each side (r05).
+#ifndef PB_SR_DDIFF
+#define PB_SR_DDIFF 1
+#endif
+static constexpr int kSrHalo = PB_SR_DDIFF ? 3 : 4;  // block rows not stored (both sides)
+static constexpr int kSrLead = PB_SR_DDIFF ? 1 : 2;  // block rows below the first stored one
 
 // p, r' stores non-temporal (buffer-store aux 2), like the stencil engine's outputs: 0.874-0.904
 // against 0.937-0.949 ms for cached stores at 512^3, and the next x-update pass P 0.193 against
@@ -87,8 +99,9 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
                                           int seg, int tile, int kb, int ke, SrLds<NW, TY, V>& L,
                                           double (&acc)[5]) {
   constexpr int RB = NW * TY;
-  constexpr int SB = RB - 4;
+  constexpr int SB = RB - kSrHalo;
   constexpr int SEG = 64 * V;  // points per wave segment
+  const double ce = ((cc + 2.0 * cx) + 2.0 * cy) + 2.0 * cz;  // (difference form: ~0)
   // register ring slots: plane loads D = U - 2 steps ahead of the step that forms p from them.
   // U = 3 (one step ahead) fits the 256-register budget; at U = 4 the x-halo registers spill
   // (two-step prefetch measured within noise before the halo lanes: 0.86-0.93 vs 0.87-0.90 ms)
@@ -96,7 +109,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
   constexpr int D = U - 2;
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nx = g.nx, ny = g.ny, nz = g.nzl;
-  const int g0 = tile * SB - 2;  // global row of block row 0
+  const int g0 = tile * SB - kSrLead;  // global row of block row 0
   const int br0 = wid * TY;
   const int j0 = g0 + br0;
   auto wrap = [](int v, int n) { v %= n; return v < 0 ? v + n : v; };
@@ -113,7 +126,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
   for (int q = 0; q < TY; ++q) {
     ro[q] = (int64_t)wrap(j0 + q, ny) * nx;
     const int brow = br0 + q;
-    if (out_ok && brow >= 2 && brow < RB - 2 && g0 + brow < ny) row_ok |= 1u << q;
+    if (out_ok && brow >= kSrLead && brow < kSrLead + SB && g0 + brow < ny) row_ok |= 1u << q;
   }
   const unsigned boff = (unsigned)ip * 8u;
   auto pl = [&](int kk) -> int64_t { return (int64_t)wrap(kk, nz) * g.plane; };
@@ -223,7 +236,12 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
     // rows -1 / TY of p(k+1) and t(k): published by the neighbouring waves at step k-1
     const int rp = (k + 1) & 1, cur = k & 1;
     const lane_pts<V> phl = L.xch[rp][1][wm][lane], phh = L.xch[rp][0][wp][lane];
+#if PB_SR_DDIFF
+    const lane_pts<V> thh = L.xch[rp][2][wp][lane];
+    const int thl = 0;
+#else
     const lane_pts<V> thl = L.xch[rp][3][wm][lane], thh = L.xch[rp][2][wp][lane];
+#endif
     const double hhl = L.xh[rp][wm][hl_lo], hhh = L.xh[rp][wp][hl_hi];
     L.xch[cur][0][wid][lane] = pack_pts<V>(pk2[0]);
     L.xch[cur][1][wid][lane] = pack_pts<V>(pk2[TY - 1]);
@@ -282,6 +300,29 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       }
     });
     L.xch[cur][2][wid][lane] = pack_pts<V>(tk1[0]);
+#if PB_SR_DDIFF
+    // delta of plane k in the difference form: forward differences of t in x (past lane 63: the
+    // halo lanes), y (past the wave's top row: the wave above's row 0, thh) and z (t(k+1))
+    unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const double hi = x_hi(tk[q], TH[Q1], qc);
+      const long long mk = in0 && (row_ok >> q & 1u) ? -1LL : 0LL;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const double tc = tk[q][e];
+        const double xp = e == V - 1 ? hi : tk[q][e == V - 1 ? e : e + 1];
+        const double yp = q == TY - 1 ? pt<V>(thh, e) : tk[q == TY - 1 ? q : q + 1][e];
+        const double dxv = xp - tc, dyv = yp - tc, dzv = tk1[q][e] - tc;
+        double v = ce * (tc * tc);
+        v = v - cx * (dxv * dxv);
+        v = v - cy * (dyv * dyv);
+        v = v - cz * (dzv * dzv);
+        acc[4] += keep_if(v, mk);
+      }
+    });
+    (void)thl;
+    (void)tkm;
+#else
     L.xch[cur][3][wid][lane] = pack_pts<V>(tk1[TY - 1]);
     // s(k) = A t, delta sum t.s
     unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
@@ -299,6 +340,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
         acc[4] += keep_if(tk[q][e] * sv, mk);
       }
     });
+#endif
   };
   // steps kb-4 .. ke-1 (padded to whole rounds of U steps: the spare steps store and sum nothing)
 #pragma unroll 1
@@ -381,7 +423,7 @@ int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_ol
   geo.nzl = (int)g->nzl;
   geo.plane = g->plane;
   geo.nseg = (geo.nx + 64 * V - 1) / (64 * V);
-  geo.ntile = (geo.ny + NW * TY - 5) / (NW * TY - 4);
+  geo.ntile = (geo.ny + NW * TY - kSrHalo - 1) / (NW * TY - kSrHalo);
   geo.remap = 1;
   const int64_t work = (int64_t)geo.nseg * geo.ntile * geo.nzl;  // column-planes
   const int64_t want = (int64_t)(ctx->num_cus);
