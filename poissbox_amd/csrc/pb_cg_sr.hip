@@ -43,21 +43,22 @@ namespace pb {
 struct SrGeo {
   int nx, ny, nzl;
   int64_t plane;
-  int nseg, ntile;  // x segments of 64 V points, y tiles of NW TY - kSrHalo rows
+  int nseg, ntile;  // x segments of 64 V points, y tiles of NW TY - SrRows::kHalo rows
   int W;            // planes of work per workgroup
   int remap;
 };
 
-// delta = t'A t in the difference form (r06, default): -sum (cx dx^2 + cy dy^2 + cz dz^2) over
+// delta = t'A t in the difference form (r06): -sum (cx dx^2 + cy dy^2 + cz dz^2) over
 // forward differences of t, plus (cc + 2 cx + 2 cy + 2 cz) sum t^2 (~0), equal to t'A t in exact
 // arithmetic on the periodic grid. It needs t one row further on one side only, so a block stores
 // NW TY - 3 of its NW TY rows instead of NW TY - 4 (fewer rows fetched twice by neighbouring
 // tiles). 0: delta = t . (A t) with the stencil, two rows of halo each side (r05).
-#ifndef PB_SR_DDIFF
-#define PB_SR_DDIFF 1
-#endif
-static constexpr int kSrHalo = PB_SR_DDIFF ? 3 : 4;  // block rows not stored (both sides)
-static constexpr int kSrLead = PB_SR_DDIFF ? 1 : 2;  // block rows below the first stored one
+// (template flag DD; tuning sr_ddiff, default: see launch_cg_sr1)
+template <bool DD>
+struct SrRows {
+  static constexpr int kHalo = DD ? 3 : 4;  // block rows not stored (both sides)
+  static constexpr int kLead = DD ? 1 : 2;  // block rows below the first stored one
+};
 
 // p, r' stores non-temporal (buffer-store aux 2), like the stencil engine's outputs: 0.874-0.904
 // against 0.937-0.949 ms for cached stores at 512^3, and the next x-update pass P 0.193 against
@@ -90,7 +91,7 @@ struct SrLds {
   double xh[2][NW][64];  // [step parity][wave][lane]: the halo lanes' p
 };
 
-template <int NW, int TY, int V>
+template <int NW, int TY, int V, bool DD>
 __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, double cz,
                                           double cc, const double* __restrict__ r,
                                           const double* __restrict__ p_old,
@@ -99,7 +100,8 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
                                           int seg, int tile, int kb, int ke, SrLds<NW, TY, V>& L,
                                           double (&acc)[5]) {
   constexpr int RB = NW * TY;
-  constexpr int SB = RB - kSrHalo;
+  constexpr int SB = RB - SrRows<DD>::kHalo;
+  constexpr int kSrLead = SrRows<DD>::kLead;
   constexpr int SEG = 64 * V;  // points per wave segment
   const double ce = ((cc + 2.0 * cx) + 2.0 * cy) + 2.0 * cz;  // (difference form: ~0)
   // register ring slots: plane loads D = U - 2 steps ahead of the step that forms p from them.
@@ -236,12 +238,8 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
     // rows -1 / TY of p(k+1) and t(k): published by the neighbouring waves at step k-1
     const int rp = (k + 1) & 1, cur = k & 1;
     const lane_pts<V> phl = L.xch[rp][1][wm][lane], phh = L.xch[rp][0][wp][lane];
-#if PB_SR_DDIFF
     const lane_pts<V> thh = L.xch[rp][2][wp][lane];
-    const int thl = 0;
-#else
-    const lane_pts<V> thl = L.xch[rp][3][wm][lane], thh = L.xch[rp][2][wp][lane];
-#endif
+    const lane_pts<V> thl = DD ? thh : L.xch[rp][3][wm][lane];  // (DD: unused)
     const double hhl = L.xh[rp][wm][hl_lo], hhh = L.xh[rp][wp][hl_hi];
     L.xch[cur][0][wid][lane] = pack_pts<V>(pk2[0]);
     L.xch[cur][1][wid][lane] = pack_pts<V>(pk2[TY - 1]);
@@ -300,7 +298,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
       }
     });
     L.xch[cur][2][wid][lane] = pack_pts<V>(tk1[0]);
-#if PB_SR_DDIFF
+    if constexpr (DD) {
     // delta of plane k in the difference form: forward differences of t in x (past lane 63: the
     // halo lanes), y (past the wave's top row: the wave above's row 0, thh) and z (t(k+1))
     unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
@@ -322,7 +320,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
     });
     (void)thl;
     (void)tkm;
-#else
+    } else {
     L.xch[cur][3][wid][lane] = pack_pts<V>(tk1[TY - 1]);
     // s(k) = A t, delta sum t.s
     unroll_steps(std::make_integer_sequence<int, TY>{}, [&](auto qc) {
@@ -340,7 +338,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
         acc[4] += keep_if(tk[q][e] * sv, mk);
       }
     });
-#endif
+    }
   };
   // steps kb-4 .. ke-1 (padded to whole rounds of U steps: the spare steps store and sum nothing)
 #pragma unroll 1
@@ -349,7 +347,7 @@ __device__ __forceinline__ void sr1_range(const SrGeo& g, double cx, double cy, 
                  [&](auto Qc) { body(Qc, k + decltype(Qc)::value); });
 }
 
-template <int NW, int TY, int V>
+template <int NW, int TY, int V, bool DD>
 __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, double cy, double cz,
                                                          double cc, const double* __restrict__ r,
                                                          const double* __restrict__ p_old,
@@ -372,7 +370,7 @@ __global__ __launch_bounds__(64 * NW) void cg_sr1_kernel(SrGeo g, double cx, dou
   const int bid = xcd_block(g.remap);
   const int ncol = g.nseg * g.ntile, W = g.W, T = g.nzl / W;
   auto run = [&](int col, int kb, int ke) {
-    sr1_range<NW, TY, V>(g, cx, cy, cz, cc, r, p_old, p_new, r_out, dinv, shift, bb, alpha,
+    sr1_range<NW, TY, V, DD>(g, cx, cy, cz, cc, r, p_old, p_new, r_out, dinv, shift, bb, alpha,
                       col % g.nseg, col / g.nseg, kb, ke, lds, acc);
   };
   if (bid < T * ncol) {  // bands of W planes of every column
@@ -423,7 +421,13 @@ int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_ol
   geo.nzl = (int)g->nzl;
   geo.plane = g->plane;
   geo.nseg = (geo.nx + 64 * V - 1) / (64 * V);
-  geo.ntile = (geo.ny + NW * TY - kSrHalo - 1) / (NW * TY - kSrHalo);
+  // delta in the difference form: 256^3 0.1518-0.1525 against 0.1581-0.1599 ms/iteration, but
+  // 512^3 1.107-1.115 against 1.096-1.097 (profiles/r06/sr_ddiff_ab.txt): by default on planes
+  // below 512^2 points
+  const int ddt = tune("sr_ddiff", -1);
+  const bool dd = ddt < 0 ? g->plane < 512 * 512 : ddt != 0;
+  const int halo = dd ? SrRows<true>::kHalo : SrRows<false>::kHalo;
+  geo.ntile = (geo.ny + NW * TY - halo - 1) / (NW * TY - halo);
   geo.remap = 1;
   const int64_t work = (int64_t)geo.nseg * geo.ntile * geo.nzl;  // column-planes
   const int64_t want = (int64_t)(ctx->num_cus);
@@ -441,8 +445,14 @@ int launch_cg_sr1(pb_grid* g, const Star& s, const double* r, const double* p_ol
   f.hist = sf.hist;
   f.h_done = sf.h_done;
   f.host_iter = host_iter - 1;
-  hipLaunchKernelGGL((cg_sr1_kernel<NW, TY, V>), dim3((unsigned)nb), dim3(64 * NW), 0, ctx->stream,
-                     geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out, parts_out, f);
+  if (dd)
+    hipLaunchKernelGGL((cg_sr1_kernel<NW, TY, V, true>), dim3((unsigned)nb), dim3(64 * NW), 0,
+                       ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out, parts_out,
+                       f);
+  else
+    hipLaunchKernelGGL((cg_sr1_kernel<NW, TY, V, false>), dim3((unsigned)nb), dim3(64 * NW), 0,
+                       ctx->stream, geo, s.cx, s.cy, s.cz, s.cc, r, p_old, p_new, r_out, parts_out,
+                       f);
   PB_HIP(hipGetLastError());
   *nblocks = (int)nb;
   return PB_OK;

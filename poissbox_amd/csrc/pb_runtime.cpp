@@ -65,7 +65,7 @@ const char* const kTuneNames[] = {
     "a2a_copy_self", "cg_defer_x", "cg_tall", "engine_kc_skew", "field_stagger_kib", "cg_fold", "cg_fuse", "cg_sr_fused", "comm_mark_every",
     "comm_stall_test_ms", "compact_lines", "fft_rupd", "fft_zpad", "fft_zpad_min_plane",
     "force_comm", "ksp_lazy0", "ksp_pool_pad_kib", "mg_agglomerate", "mg_engine_min_plane", "mg_restrict_z_min_cols",
-    "mg_split_fused", "mg_sweep2", "mg_tail_max", "mg_u4_split", "pcr_lines", "sor_omega_any",
+    "mg_split_fused", "mg_sweep2", "mg_tail_max", "mg_u4_split", "pcr_lines", "sor_omega_any", "sr_ddiff",
     "stencil_kc", "stencil_kc_skew", "stencil_nt", "stencil_tall", "stencil_wgcu", "x_dot_cu"};
 constexpr int kNumTune = (int)(sizeof(kTuneNames) / sizeof(kTuneNames[0]));
 // lock-free table (tune() runs several times per CG iteration / V-cycle): a value and

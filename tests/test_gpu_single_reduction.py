@@ -223,3 +223,19 @@ def test_multirank_single_reduction(nranks, n):
         assert (reason, its) == (ro, itso)
         check_history(hist, ho)
         check_x(xs, xo.reshape(n[2], -1)[k0:k0 + nk].reshape(-1), scale=np.max(np.abs(xo)))
+
+
+@pytest.mark.parametrize("ddiff", [0, 1])
+@pytest.mark.parametrize("n3", [(32, 32, 32), (24, 20, 12), (17, 18, 9), (130, 6, 33),
+                                (512, 512, 4), (64, 13, 16)])
+def test_single_reduction_delta_forms(ctx, tune, n3, ddiff):
+    """The one-pass kernel's delta = z'A z as t.(A t) (two halo rows per block side) or in the
+    difference form (-sum c (forward difference)^2, one row fewer to fetch twice; r06): both on
+    the oracle's reason, iterations and history (PETSc's single-reduction form)."""
+    tune.set("sr_ddiff", ddiff)
+    h, b = _case(n3)
+    xo, ro, itso, ho = O.cg_solve(b, n3, h, rtol=1e-9, single_reduction=1)
+    reason, its, hist, xs = _solve(ctx, n3, h, b, SR + ["-ksp_rtol", "1e-9"])
+    assert (reason, its) == (ro, itso)
+    check_history(hist, ho, tag=f"sr_ddiff{ddiff}")
+    check_x(xs, xo)
