@@ -20,41 +20,12 @@
 namespace pb {
 
 // ---- field allocations (pb_internal.hpp) ----
-// field_stagger_kib (tuning, A/B of the placement sensitivity): the k-th field
-// allocation starts (k mod 16) * n KiB into an allocation that much larger, so that fields are
-// not all at the same offset from a 2 MiB boundary
-namespace {
-std::mutex g_field_mu;
-std::unordered_map<void*, void*> g_field_base;  // staggered pointer -> hipMalloc'd base
-unsigned g_field_count = 0;
-}  // namespace
-
-hipError_t field_alloc(void** p, size_t bytes) {
-  const int kib = tune("field_stagger_kib", 0);
-  if (kib <= 0) return hipMalloc(p, bytes);
-  std::lock_guard<std::mutex> lk(g_field_mu);
-  const size_t off = (size_t)(g_field_count++ % 16) * (size_t)kib * 1024;
-  void* base = nullptr;
-  const hipError_t e = hipMalloc(&base, bytes + off);
-  if (e != hipSuccess) return e;
-  *p = static_cast<char*>(base) + off;
-  g_field_base[*p] = base;
-  return hipSuccess;
-}
+// (r06 measured a stagger of every allocation by 4-260 KiB and the KSP vectors pooled in one
+// allocation: neither controls pass B's placement-dependent rate; code in commit 8e8b21f)
+hipError_t field_alloc(void** p, size_t bytes) { return hipMalloc(p, bytes); }
 
 void field_free(void* p) {
-  if (!p) return;
-  {
-    std::lock_guard<std::mutex> lk(g_field_mu);
-    auto it = g_field_base.find(p);
-    if (it != g_field_base.end()) {
-      void* base = it->second;
-      g_field_base.erase(it);
-      (void)hipFree(base);
-      return;
-    }
-  }
-  (void)hipFree(p);
+  if (p) (void)hipFree(p);
 }
 
 // ---- tuning table (pb_tune_set; pb_internal.hpp tune()) ----
@@ -62,9 +33,9 @@ namespace {
 // every name a kernel launcher consults; the defaults live at the call sites (the measured
 // choices), the table only holds values a caller set
 const char* const kTuneNames[] = {
-    "a2a_copy_self", "cg_defer_x", "cg_pass_a_ty", "cg_tall", "engine_kc_skew", "field_stagger_kib", "cg_fold", "cg_fuse", "cg_sr_fused", "comm_mark_every",
+    "a2a_copy_self", "cg_defer_x", "engine_kc_skew", "cg_fold", "cg_fuse", "cg_sr_fused", "comm_mark_every",
     "comm_stall_test_ms", "compact_lines", "fft_rupd", "fft_zpad", "fft_zpad_min_plane",
-    "force_comm", "ksp_lazy0", "ksp_pool_pad_kib", "mg_agglomerate", "mg_engine_min_plane", "mg_restrict_z_min_cols",
+    "force_comm", "ksp_lazy0", "mg_agglomerate", "mg_engine_min_plane", "mg_restrict_z_min_cols",
     "mg_split_fused", "mg_sweep2", "mg_tail_max", "mg_u4_split", "pcr_lines", "sor_omega_any", "sr_ddiff",
     "stencil_kc", "stencil_kc_skew", "stencil_nt", "stencil_tall", "stencil_wgcu", "x_dot_cu"};
 constexpr int kNumTune = (int)(sizeof(kTuneNames) / sizeof(kTuneNames[0]));

@@ -40,7 +40,6 @@ struct pb_ksp {
   double* pb[4] = {nullptr, nullptr, nullptr, nullptr};
   double* w = nullptr;   // generic (unfused) path only
   double* z = nullptr;   // generic path only
-  void* pool = nullptr;  // r, r2, pb[0..3] in one allocation (ksp_pool_pad_kib >= 0)
   pb::Mg* mg = nullptr;  // SOR / multigrid preconditioner (PB_PC_SOR, PB_PC_MG)
   pb::FftPc* fft = nullptr;  // spectral preconditioner (PB_PC_FFT)
   int fold_nparts_b = 0;     // partial-sum blocks of the last folded pass B
@@ -323,22 +322,9 @@ int pb_ksp_create(pb_op* A, pb_op* P, const pb_ksp_opts* opts, pb_ksp** out) {
     const int rc = fftpc_create(g, P->deltas, P->kind == PB_OP_COMPACT, &k->fft);
     if (rc != PB_OK) return fail(rc);
   }
-  // ksp_pool_pad_kib >= 0 (A/B of the placement sensitivity): the fused iteration's
-  // six streamed vectors (r, r2, the four directions) in ONE allocation, vector i at
-  // i * (size + pad), so their relative placement is the same in every process
-  const int pad = tune("ksp_pool_pad_kib", -1);
-  if (pad >= 0 && fused_kind(A->kind) && !k->stored_z()) {
-    const size_t stride = (vb + (size_t)pad * 1024 + 255) / 256 * 256;
-    if (hipMalloc(&k->pool, 6 * stride) != hipSuccess)
-      return fail(set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory"));
-    char* base = static_cast<char*>(k->pool);
-    k->r = reinterpret_cast<double*>(base);
-    k->r2 = reinterpret_cast<double*>(base + stride);
-    for (int q = 0; q < 4; ++q) k->pb[q] = reinterpret_cast<double*>(base + (2 + q) * stride);
-  } else if (field_alloc(&k->r, vb) != hipSuccess || field_alloc(&k->pb[0], vb) != hipSuccess ||
-             field_alloc(&k->pb[1], vb) != hipSuccess) {
+  if (field_alloc(&k->r, vb) != hipSuccess || field_alloc(&k->pb[0], vb) != hipSuccess ||
+      field_alloc(&k->pb[1], vb) != hipSuccess)
     return fail(set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory"));
-  }
   if (!fused_kind(A->kind) || k->stored_z()) {
     if (field_alloc(&k->w, vb) != hipSuccess || field_alloc(&k->z, vb) != hipSuccess)
       return fail(set_error(PB_ERR_ALLOC, "KSP work vectors: out of device memory"));
@@ -959,11 +945,6 @@ int pb_ksp_solve(pb_ksp* k, const pb_vec* b, pb_vec* x, pb_ksp_result* res, doub
 int pb_ksp_destroy(pb_ksp* k) {
   if (!k) return PB_OK;
   (void)wait_stream(k->A->grid->ctx, k->A->grid->ctx->stream, "pb_ksp_destroy");
-  if (k->pool) {
-    (void)hipFree(k->pool);
-    k->r = k->r2 = nullptr;
-    for (double*& p : k->pb) p = nullptr;
-  }
   field_free(k->r);
   field_free(k->r2);
   for (double* p : k->pb) field_free(p);

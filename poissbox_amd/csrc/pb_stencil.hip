@@ -738,17 +738,11 @@ static int launch_any(pb_grid* g, const Star& s, const Load& ld, const StencilPl
                       int* nb_out = nullptr, int rev = 0, int wgcu = 0,
                       const Fold& fold = Fold{}, int64_t part_end = 0) {
   const bool vec2 = (g->n[0] % 2) == 0;
-  int ty = pick_ty((int)g->n[1]);
-  if constexpr (std::is_same_v<Epi, PassAT<false>>) {  // (cg_pass_a_ty, A/B: 2-row tiles)
-    if (tune("cg_pass_a_ty", 0) == 2 && g->n[1] % 2 == 0) ty = 2;
-  }
+  const int ty = pick_ty((int)g->n[1]);
   if constexpr (Wide8Of<Epi>::v) {
     const int64_t cols4 = ((g->n[0] + 127) / 128) * ((g->n[1] + kWaves * 4 - 1) / (kWaves * 4));
     const int w = wgcu > 0 ? wgcu : Epi::WGCU;
-    // (cg_tall, A/B: 8-row tiles on 512^2 planes too)
-    if (vec2 && ty == 4 && g->n[1] % 8 == 0 &&
-        (cols4 > (int64_t)w * g->ctx->num_cus ||
-         (g->plane >= 512 * 512 && tune("cg_tall", 0) != 0)))
+    if (vec2 && ty == 4 && g->n[1] % 8 == 0 && cols4 > (int64_t)w * g->ctx->num_cus)
       return launch_t<2, 8>(g, s, ld, gp, ep, skip, mode, part_off, nb_out, rev, wgcu, fold, part_end);
   }
   if constexpr (TallOf<Epi>::v) {
