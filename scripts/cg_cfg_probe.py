@@ -3,7 +3,7 @@ R solver instances at n^3, each with fresh vectors (the earlier instances stay a
 gets other memory); every instance runs every configuration interleaved: `its` fixed CG + Jacobi
 iterations (ms/iteration, per-pass HIP-event averages) and `mv` matvecs x -> y of its own vectors.
 Prints per configuration min / median / max over instances.
-Usage: python scripts/cg_cfg_probe.py [n] [R] [configs-json]"""
+Usage: python scripts/cg_cfg_probe.py [n | nxXnyXnz] [R] [configs-json] [alloc]"""
 import json
 import os
 import sys
@@ -16,7 +16,8 @@ PASSES = ("cg_pass_a", "cg_pass_b_even", "cg_pass_b_x4", "stencil")
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+    a1 = sys.argv[1] if len(sys.argv) > 1 else "512"
+    n3 = tuple(int(v) for v in a1.split("x")) if "x" in a1 else (int(a1),) * 3
     R = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     configs = json.loads(sys.argv[3]) if len(sys.argv) > 3 else [{}, {"engine_kc_skew": 4}]
     # alloc mode: every configuration gets its own instances (settings that act at allocation,
@@ -24,7 +25,7 @@ def main():
     alloc_mode = len(sys.argv) > 4 and sys.argv[4] == "alloc"
     its, warm, mv = 32, 8, 10
     ctx = pb.Context(0)
-    da = pb.initialise_grid(ctx, (n, n, n))
+    da = pb.initialise_grid(ctx, n3)
     P, A = pb.Mat(da, pb.ASSEMBLED27, da.spacing), pb.Mat(da, pb.STAR7, da.spacing)
     keep = []
     res = {}
