@@ -34,7 +34,8 @@ ROLES = {
         # single-reduction iteration (bench.py's variant line)
         "cg_sr_p": r"star7_kernel<.*PassB<0, true, false>",
         "cg_sr_p_x4": r"star7_kernel<.*PassB<3, true, false>",
-        "cg_sr_s": r"star7_kernel<.*ZLoad, pb::SrSumsT",
+        "cg_sr_s": r"star7_kernel<.*ZLoad, pb::SrSums",
+        "cg_sr1": r"cg_sr1_kernel<",
     },
 }
 
