@@ -921,11 +921,6 @@ int launch_dht_n(pb_ctx* ctx, DhtPass& p, const int* skip) {
     return set_error(PB_ERR_UNSUPPORTED, "fft pc: %d lines (even counts only)", p.ninner);
   if constexpr (RegPlan<N>::OK && LAYOUT == 1) return launch_dht_reg_x<N>(ctx, p, skip);
   if (p.ru_st) return set_error(PB_ERR_STATE, "fft pc: r update on the register-edge X pass only");
-  if constexpr (N == 512 && LAYOUT == 0) {
-    // (fft_tl8, A/B: 8-line tiles for the strided passes, 1 = Z, 2 = Y: 41 KB of LDS, three
-    // tiles per CU instead of two)
-    if (tune("fft_tl8", 0) & (MODE == 1 ? 1 : 2)) return launch_dht_k<N, 8, LAYOUT, MODE>(ctx, p, skip);
-  }
   return launch_dht_k<N, tile_lines<N>(), LAYOUT, MODE>(ctx, p, skip);
 }
 
