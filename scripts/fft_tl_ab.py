@@ -11,7 +11,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import poissbox_amd as pb  # noqa: E402
 
-VARIANTS = [{}, {"fft_tl8": 1}, {"fft_tl8": 3}]
+VARIANTS = [{}, {"fft_persist": 1}]
 
 
 def main():
