@@ -70,7 +70,6 @@ struct DhtPass {
   const CgState* st;
   int nparts_out;     // (host) partial blocks written
   int ncu;
-  int persist;        // (fft_persist, A/B) strided passes: one resident round of blocks walking the tiles
   // CG's x / r update on the first X pass (register-edge kernel): the line input is
   // r = ru_in + (-alpha) ru_w, also stored to ru_out; ru_x = ru_x + alpha ru_p (ru_first: alpha p)
   const double* ru_in;
@@ -566,7 +565,7 @@ __global__ __launch_bounds__(32 * TL_, N <= 512 ? 4 : 1) void dht_lines_kernel(D
   const double mu = SUMS ? p.st->mu : 0.0;
   // PF: prefetch the next tile into registers (lines of <= 512 points; longer lines have no
   // registers to spare: their tile is loaded where it is needed)
-  const int G = (PF || p.persist) ? (int)gridDim.x : ntiles;
+  const int G = PF ? (int)gridDim.x : ntiles;
   int t = PF ? (int)blockIdx.x : xcd_block(p.remap);
   if (PF && t < ntiles) fetch(t);
   for (; t < ntiles; t += G) {
@@ -896,8 +895,7 @@ int launch_dht_k(pb_ctx* ctx, DhtPass& p, const int* skip) {
   }
   // persistent passes: one resident round of blocks; the others one tile per block
   int64_t nblocks = (int64_t)occ * ctx->num_cus;
-  p.persist = LAYOUT == 0 && tune("fft_persist", 0) != 0;
-  const bool persist = (N <= 512 && LAYOUT == 1) || p.persist;
+  const bool persist = N <= 512 && LAYOUT == 1;
   if (!persist || nblocks > ntiles) nblocks = ntiles;
   if (p.parts) {
     if (!SUMS) return set_error(PB_ERR_STATE, "fft pc: residual sums on the X pass only");

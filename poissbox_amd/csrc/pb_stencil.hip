@@ -662,24 +662,10 @@ struct CapOf<E, std::void_t<decltype(E::CAP)>> {
 };
 constexpr size_t kLdsPerCu = 160 * 1024;
 
-// the KSPSolve_CG passes of the default iteration (pass A read-only, pass B re-forming p)
-template <class E>
-struct IsCgPass {
-  static constexpr bool v = std::is_same_v<E, PassAT<false>>;
-};
-template <int XU, bool SUMS>
-struct IsCgPass<PassB<XU, true, SUMS>> {
-  static constexpr bool v = true;
-};
-
 template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                     const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev,
                     int wgcu, const Fold& fold, int64_t part_end) {
-  if constexpr (IsCgPass<Epi>::v) {  // (cg_wgcu, A/B: workgroups per CU of the CG passes)
-    const int o = tune("cg_wgcu", 0);
-    if (o > 0) wgcu = o;
-  }
   Geo geo = make_geo(g, V, TY, mode, rev, wgcu > 0 ? wgcu : Epi::WGCU,
                      std::is_same_v<Epi, StoreY> ? tune("stencil_kc_skew", 4)
                                                  : tune("engine_kc_skew", 0));
