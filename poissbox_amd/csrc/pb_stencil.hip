@@ -635,8 +635,10 @@ static Geo make_geo(pb_grid* g, int V, int TY, int mode, int rev, int wgcu, int 
   // standalone matvec's four 128-plane chunks at 512^3 ran 0.37-0.42 ms depending on where its x
   // and y sat (pairs of buffers: one slow, one fast group); chunks of 136 planes ran 0.36-0.38
   // over the same pairs (profiles/r06/placement/). The CG passes' two 256-plane chunks gained
-  // nothing from it (skew 2: within noise, 4 / 8: slower) and keep 0.
-  if (nchunk > 1 && skew > 0) {
+  // nothing from it (skew 2: within noise, 4 / 8: slower) and keep 0. Only for chunks at least
+  // 128 MiB of planes apart: 256^3's matvec (eight 32-plane chunks, 16 MiB apart) ran 0.0439
+  // against 0.0414 ms with the skew (profiles/r06/placement/cgcfg256.jsonl)
+  if (nchunk > 1 && skew > 0 && (int64_t)geo.kc * g->plane * 8 >= ((int64_t)128 << 20)) {
     const int kc = geo.kc + std::max(1, geo.kc * skew / 64);
     if ((int64_t)kc * (nchunk - 1) < nk) geo.kc = kc;
   }
