@@ -1394,7 +1394,10 @@ def test_fft_pc_rejects_bad_extents(ctx):
 # compact Laplacian / compact CG on a split grid (z-slab <-> y-slab all-to-all transposes)
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("op", ["grad", "div", "interp", "interp_div", "lapl"])
-@pytest.mark.parametrize("nranks,n", [(2, (16, 12, 10)), (3, (12, 9, 7)), (4, (8, 8, 13))])
+@pytest.mark.parametrize("nranks,n", [(2, (16, 12, 10)), (3, (12, 9, 7)), (4, (8, 8, 13)),
+                                       # odd x extent: the per-element transpose kernel, whose
+                                       # rank-own block is written in place (r06 host transport)
+                                       (3, (9, 8, 6))])
 def test_multirank_compact_reference_order(nranks, n, op):
     """src/compact_schemes.f90:17-257 in the reference's operation order on a split grid: the Z
     steps run on y-slabs (complete z-lines), so every rank's slab is bit-identical to the
