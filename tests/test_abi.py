@@ -137,3 +137,19 @@ def test_library_reads_only_the_documented_environment():
     assert names <= documented, names - documented
     integ = open(os.path.join(REPO, "INTEGRATION.md")).read()
     assert all(f"`{n}" in integ for n in documented)
+
+
+def test_every_tuning_name_is_documented():
+    """Every name of the library's tuning table (pb_runtime.cpp kTuneNames) has a row in
+    INTEGRATION.md's tuning table, and the table lists no name the library does not know."""
+    src = open(os.path.join(REPO, "poissbox_amd", "csrc", "pb_runtime.cpp")).read()
+    i = src.index("kTuneNames[] = {")
+    names = set(re.findall(r'"([a-z0-9_]+)"', src[i:src.index("};", i)]))
+    assert len(names) >= 20
+    integ = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    table = integ[integ.index("## Tuning table"):]
+    missing = sorted(n for n in names if f"`{n}`" not in table)
+    assert not missing, missing
+    for n in names:
+        pb.tune_set(n, pb.tune_get(n) or 0)  # known to the library
+    pb.tune_reset()
