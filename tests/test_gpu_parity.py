@@ -1748,3 +1748,37 @@ def test_multirank_compact_cg_fused(tune, nranks, n3, pc):
         xs = np.max(np.abs(xo))
         assert np.max(np.abs(x1 - x0)) <= 1e-12 * xs
         check_x(x1, xo.reshape(n3[2], -1)[k0:k0 + nk].reshape(-1), scale=xs)
+
+
+@pytest.mark.parametrize("pc", ["fft", "mg"])
+def test_rccl_compact_cg_fused_split(tune, pc):
+    """The split-grid compact CG fusions (the transpose's pack forms p, the X pass takes p . w;
+    r06) on a one-rank RCCL communicator (force_comm: the RCCL all-to-all path, self block
+    elided) against the one-rank context: same reason and iterations, histories within 1e-12,
+    x alike; 12 fixed iterations with the 7-point symbol's spectral PC / the 7-point MG."""
+    n3 = (64, 32, 32)
+    its = 12
+    h = tuple(2 * np.pi / m for m in n3)
+    b = O.lapl(O.fill_random(int(np.prod(n3)), SEED), n3, h)
+    opts = ["-pc_type", pc, "-ksp_rtol", "0", "-ksp_atol", "0", "-ksp_max_it", str(its),
+            "-ksp_divtol", "1e300"]
+    res = {}
+    for fc in (0, 1):
+        tune.set("force_comm", fc)
+        c = pb.Context(0)
+        tune.set("force_comm", 0)
+        da = pb.DA(c, n3, (2 * np.pi,) * 3)
+        A = pb.Mat(da, pb.COMPACT, h)
+        P = pb.Mat(da, pb.STAR7 if pc == "fft" else pb.ASSEMBLED27, h)
+        x, bv = pb.Vec(da), pb.Vec(da)
+        bv.set_values(b)
+        reason, its_g, hist = pb.solve(P, A, x, bv, opts)
+        res[fc] = (reason, its_g, np.asarray(hist), x.get_values())
+        for o in (A, P, x, bv):
+            o.destroy()
+        da.destroy()
+        c.destroy()
+    (r0, i0, h0, x0), (r1, i1, h1, x1) = res[0], res[1]
+    assert (r0, i0) == (r1, i1) == (-3, its)
+    assert np.max(np.abs(h1 - h0) / h0) < 1e-12
+    assert np.max(np.abs(x1 - x0)) <= 1e-12 * np.max(np.abs(x0))
