@@ -449,6 +449,11 @@ def run_solve_workload(args, pb, ctx, workload, scaling, steps, warmup, rank, wo
             comm[f"{nm}_ms_per_solve"] = ms_
             comm[f"{nm}_calls"] = cnt_
     ctx.set_timing(False)
+    if roof in kern and "frac" not in kern[roof]:  # the roofline kernel's fixed bytes
+        t_ = kern[roof]["avg_ms"] / 1e3
+        roof_bpd = roof_bytes_np[0] if world == 1 else roof_bytes_np[1]
+        kern[roof].update(GBps=roof_bpd * nloc / t_ / 1e9,
+                          frac=roof_bpd * nloc / t_ / 1e9 / HBM_PEAK_GBS, bytes_per_dof=roof_bpd)
     if workload == "compact-fft" and "pc_fft_x" in kern:
         # the spectral PC's X passes carry CG's work, so their bytes differ by role, but each
         # solve's are fixed: per PC apply a forward X pass (16 B/DoF: r in,
