@@ -14,7 +14,7 @@ import pytest
 
 import poissbox_amd as pb
 from oracle import oracle as O
-from parity_bars import check_history, check_x
+from parity_bars import HIST_RTOL, check_history, check_x
 
 pytestmark = pytest.mark.gpu
 
@@ -157,7 +157,11 @@ def test_single_reduction_nonzero_mean_rhs(ctx):
     relative to a vector far larger than z: the oracle's own three forms (KSPSolve_CG, PETSc's
     single reduction, w recomputed) agree to 1e-12 while ||z_k|| > 1e-4 ||z_0|| and drift apart to
     2.4e-2 at ||z_k|| ~ 1e-9 ||z_0|| (same reason and its). Bars: same reason / its; history
-    within HIST_RTOL down to 1e-4 ||z_0||, within 0.1 below; x (mean removed) within 1e-8."""
+    within HIST_RTOL down to 1e-4 ||z_0||, and at every entry within HIST_RTOL plus three times
+    the spread, at that entry, of 14 equivalent runs of the oracle (its three forms, each with its
+    sums in 1, 2, 3, 4 and 8 thread orders): the rounding the reference algorithm itself leaves
+    undetermined there. Leave-one-out over those runs, a single-reduction run in another sum
+    order stays within 0.9 of twice the others' spread. x (mean removed) within 1e-8."""
     n3 = (32, 16, 16)
     h, b = _case(n3)
     b = b + 3.0
@@ -166,7 +170,18 @@ def test_single_reduction_nonzero_mean_rhs(ctx):
     assert (reason, its) == (ro, itso)
     head = ho > 1e-4 * ho[0]
     check_history(hist[head], ho[head])
-    assert np.max(np.abs(hist - ho) / ho) < 0.1
+    ho = np.asarray(ho)
+    spread = np.zeros_like(ho)
+    for form in (0, 1, 2):  # KSPSolve_CG, PETSc's single reduction, w recomputed
+        for nt in (1, 2, 3, 4, 8):
+            if (form, nt) == (1, 1):
+                continue
+            _, rf, itf, hf = O.cg_solve(b, n3, h, rtol=1e-9, single_reduction=form, nthreads=nt)
+            assert (rf, itf) == (ro, itso), (form, nt)
+            spread = np.maximum(spread, np.abs(np.asarray(hf) - ho))
+    bar = HIST_RTOL * ho + 3.0 * spread
+    dev = np.abs(np.asarray(hist) - ho)
+    assert np.all(dev <= bar), np.max(dev / bar)
     xm, xom = xs - xs.mean(), xo - xo.mean()
     assert np.max(np.abs(xm - xom)) < 1e-8 * np.max(np.abs(xom))
 
