@@ -33,7 +33,7 @@ namespace {
 // every name a kernel launcher consults; the defaults live at the call sites (the measured
 // choices), the table only holds values a caller set
 const char* const kTuneNames[] = {
-    "a2a_copy_self", "cg_defer_x", "engine_depth", "engine_kc_skew", "cg_fold", "cg_fuse", "cg_sr_fused", "comm_mark_every",
+    "a2a_copy_self", "cg_defer_x", "engine_kc_skew", "cg_fold", "cg_fuse", "cg_sr_fused", "comm_mark_every",
     "comm_stall_test_ms", "compact_lines", "fft_rupd", "fft_zpad", "fft_zpad_min_plane",
     "force_comm", "ksp_lazy0", "mg_agglomerate", "mg_engine_min_plane", "mg_restrict_z_min_cols",
     "mg_split_fused", "mg_sweep2", "mg_tail_max", "mg_u4_split", "pcr_lines", "sor_omega_any", "sr_ddiff",

@@ -114,7 +114,7 @@ struct PassAT {
   static constexpr int NS = 1, NE = 0;
   static constexpr bool RAW = false, TALL = STORE || PB_PASSA_TALL;  // put() takes the Laplacian; 8-row tiles
   static constexpr int WGCU = STORE ? 3 : 1;        // (4-row tiles; 1 with 8 rows)
-  static constexpr bool CAP = !STORE, WIDE8 = !STORE, DEEP = !STORE;
+  static constexpr bool CAP = !STORE, WIDE8 = !STORE;
   static constexpr bool PREFETCH = true;
   // (p stores non-temporal like every engine output: cached stores, which pass B could re-read
   // from the Infinity Cache, measured within noise, profiles/r01/ab_passa_nt.txt)
@@ -314,12 +314,7 @@ __device__ __forceinline__ void prepare_state(T& t, const CgState&, long) {
 // ---------------------------------------------------------------------------------------------
 // The stencil engine
 // ---------------------------------------------------------------------------------------------
-// DEPTH: planes of look-ahead of the z-queue (1: plane k+2 in flight while plane k is computed;
-// 2: plane k+3 as well, two register sets alternating between the steps of a 2-unrolled march --
-// Epi::DEEP, engine_depth). The halo / edge / operand rows of plane k+1 (mostly L2 hits: the
-// neighbouring waves' own rows) stay one plane ahead and are issued before the queue plane, so
-// waiting for them leaves the queue loads in flight.
-template <int V, int TY, class Load, class Epi, int DEPTH = 1>
+template <int V, int TY, class Load, class Epi>
 __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, double cy, double cz,
                                                          double cc, Load ld0,
                                                          const double* __restrict__ ghost_lo,
@@ -387,14 +382,12 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
   if (wave_on) {
     // combined z-queue (planes k-1, k, k+1) and raw prefetch of plane k+2
     double q0[TY][V], q1[TY][V], q2[TY][V];
-    double zr[DEPTH][NR][TY][V];
-    bool zr_ghost[DEPTH];
+    double zr[NR][TY][V];
+    bool zr_ghost = false;
     // plane-k operands (combined) and their plane-(k+1) prefetch (raw)
     double hdn[V], hup[V], edge = 0.0;
     double hdn_r[NR][V], hup_r[NR][V], edge_r[NR];
     double opc[TY][NE][V], opn[Epi::PREFETCH ? TY : 1][NE][V];
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) zr_ghost[d] = false;
 
     // Every load below is issued unconditionally (ghost planes by a uniform pointer select, the
     // chunk's last step re-loading valid planes): no branch around a load, so the compiler keeps
@@ -424,6 +417,8 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
           q[t][e] = (ghost && !Load::GHOST_RAW) ? src[0][t][e] : ld.value(raw);
         }
     };
+    auto issue_zrow = [&](int kk) { issue_rows(kk, zr, zr_ghost); };
+    auto take_zrow = [&](double (&q)[TY][V]) { take_rows(zr, zr_ghost, q); };
     auto issue_plane_ops = [&](int kk) {  // halo rows, edges, epilogue operands of own plane kk
       const int64_t base = (int64_t)kk * g.plane;
 #pragma unroll
@@ -493,8 +488,6 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
             for (int e = 0; e < V; ++e) opc[t][a][e] = opn[t][a][e];
       }
     };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, DEPTH - 1>;  // (DEPTH 1: slot 0 again)
 
     // prologue: planes kf-dir, kf combined; raw plane kf+dir and plane kf's operands in flight.
     // Marching downwards (g.rev) lets a kernel start on the planes its predecessor touched last
@@ -512,7 +505,7 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
       issue_rows(kf, r1, g1);
       if constexpr (NR == 1) {
         issue_plane_ops(kf);
-        issue_rows(kf + dir, zr[0], zr_ghost[0]);
+        issue_zrow(kf + dir);
       }
       if (fold.stage && !do_fold()) return;
       take_rows(r0, g0, q0);
@@ -520,33 +513,17 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
       take_queue_ops(r1);  // plane kf (owned, never a ghost)
       if constexpr (NR != 1) {
         issue_plane_ops(kf);
-        issue_rows(kf + dir, zr[0], zr_ghost[0]);
-      }
-      if constexpr (DEPTH == 2) {  // slot 1: queue plane kf+2dir, issued after slot 0's loads
-        __builtin_amdgcn_sched_barrier(0);
-        issue_rows(nk >= 2 ? kf + 2 * dir : kf + dir, zr[1], zr_ghost[1]);
+        issue_zrow(kf + dir);
       }
     }
-    // step m (plane k = kf + m dir) with queue slot s: the queue plane k+dir was issued DEPTH steps
-    // earlier into slot s, which then receives plane k+(1+DEPTH)dir; plane k+1's rows go out first
-    // (the last steps re-load valid planes, unused)
-    auto step = [&](auto sc, int m) {
-      constexpr int s = decltype(sc)::value;
+    for (int m = 0; m < nk; ++m) {
       const int k = kf + m * dir;
-      take_rows(zr[s], zr_ghost[s], q2);  // plane k+dir
-      take_plane_ops();                     // halo/edges/operands of plane k
-      take_queue_ops(zr[s]);                // queue-sourced operands of plane k+dir
+      take_zrow(q2);                    // plane k+dir (in flight since the previous step)
+      take_plane_ops();                 // halo/edges/operands of plane k
+      take_queue_ops(zr);               // queue-sourced operands of plane k+dir
       issue_ops_now(k);
-      if constexpr (DEPTH == 1) {
-        issue_rows(m + 2 <= nk ? k + 2 * dir : k + dir, zr[s], zr_ghost[s]);
-        issue_plane_ops(m + 1 < nk ? k + dir : k);
-      } else {
-        // slot s is consumed before it is re-loaded (no scheduling across this point), so its
-        // registers carry over the loop edge in place
-        __builtin_amdgcn_sched_barrier(0);
-        issue_plane_ops(m + 1 < nk ? k + dir : k);
-        issue_rows(m + 1 + DEPTH <= nk ? k + (1 + DEPTH) * dir : k + dir, zr[s], zr_ghost[s]);
-      }
+      issue_zrow(m + 2 <= nk ? k + 2 * dir : k + dir);  // (last step: a valid plane, unused)
+      issue_plane_ops(m + 1 < nk ? k + dir : k);
       const int64_t base = (int64_t)k * g.plane;
 #pragma unroll
       for (int t = 0; t < TY; ++t) {
@@ -600,20 +577,6 @@ __global__ __launch_bounds__(kThreads) void star7_kernel(Geo g, double cx, doubl
           q0[t][e] = q1[t][e];
           q1[t][e] = q2[t][e];
         }
-    };
-    if constexpr (DEPTH == 1) {
-      for (int m = 0; m < nk; ++m) step(S0{}, m);
-    } else {  // two steps per trip: the slots' roles stay compile-time (no register copies)
-      // the prologue's loads retire before the loop, so the loop head sees only the back edge's
-      // pending loads (merging the prologue's order with the back edge's made the compiler wait
-      // vmcnt(1) there, draining the look-ahead every trip)
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      int m = 0;
-      for (; m + 1 < nk; m += 2) {
-        step(S0{}, m);
-        step(S1{}, m + 1);
-      }
-      if (m < nk) step(S0{}, m);
     }
   }
   block_partials<NS>(acc, parts);
@@ -701,17 +664,6 @@ struct CapOf<E, std::void_t<decltype(E::CAP)>> {
 };
 constexpr size_t kLdsPerCu = 160 * 1024;
 
-// Epi::DEEP (optional trait): the epilogue is also built with two planes of look-ahead
-// (star7_kernel DEPTH 2), selected at launch by the tuning value engine_depth
-template <class E, class = void>
-struct DeepOf {
-  static constexpr bool v = false;
-};
-template <class E>
-struct DeepOf<E, std::void_t<decltype(E::DEEP)>> {
-  static constexpr bool v = E::DEEP;
-};
-
 template <int V, int TY, class Load, class Epi>
 static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlanes& gp,
                     const Epi& ep, const int* skip, int mode, int part_off, int* nb_out, int rev,
@@ -747,18 +699,10 @@ static int launch_t(pb_grid* g, const Star& s, const Load& ld, const StencilPlan
     const int w = wgcu > 0 ? wgcu : Epi::WGCU;
     if (nblocks > (int64_t)w * g->ctx->num_cus) lds = kLdsPerCu / (size_t)(w + 1) + 4096;
   }
-  hipStream_t sm = g->ctx->engine_stream ? g->ctx->engine_stream : g->ctx->stream;
-  double* parts = g->ctx->d_partials + (int64_t)part_off * NS;
-  bool deep = false;
-  if constexpr (DeepOf<Epi>::v) deep = tune("engine_depth", 1) == 2;
-  if (deep)
-    hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi, DeepOf<Epi>::v ? 2 : 1>),
-                       dim3((unsigned)nblocks), dim3(kThreads), lds, sm, geo, s.cx, s.cy, s.cz,
-                       s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep, parts, skip, fold);
-  else
-    hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads),
-                       lds, sm, geo, s.cx, s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
-                       parts, skip, fold);
+  hipLaunchKernelGGL((star7_kernel<V, TY, Load, Epi>), dim3((unsigned)nblocks), dim3(kThreads),
+                     lds, g->ctx->engine_stream ? g->ctx->engine_stream : g->ctx->stream, geo, s.cx,
+                     s.cy, s.cz, s.cc, ld, gp.ghost_lo, gp.ghost_hi, ep,
+                     g->ctx->d_partials + (int64_t)part_off * NS, skip, fold);
   PB_HIP(hipGetLastError());
   if (nb_out) *nb_out = (int)nblocks;
   return PB_OK;
