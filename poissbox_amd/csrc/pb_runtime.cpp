@@ -71,6 +71,9 @@ int set_error(int code, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+  // a failed HIP call reported here is consumed: without this, HIP's per-thread last error (e.g.
+  // a refused hipMalloc) would resurface at the next, unrelated kernel-launch check
+  if (code == PB_ERR_ALLOC || code == PB_ERR_HIP) (void)hipGetLastError();
   return code;
 }
 
@@ -563,7 +566,12 @@ int grid_create_part(pb_ctx* ctx, const int64_t n[3], const double L[3], int64_t
   g->ghost_hi = ghosts + g->plane;
   g->bnd_lo = ghosts + 2 * g->plane;
   g->bnd_hi = ghosts + 3 * g->plane;
-  if (ctx->h_sendrecv) PB_HIP(hipHostMalloc(&g->h_stage, 4 * pb, hipHostMallocDefault));
+  if (ctx->h_sendrecv && hipHostMalloc(&g->h_stage, 4 * pb, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(ghosts);
+    delete g;
+    return set_error(PB_ERR_ALLOC, "host staging planes: out of pinned memory");
+  }
   *out = g;
   return PB_OK;
 }
@@ -686,17 +694,21 @@ int pb_ctx_create(int device, int rank, int nranks, const unsigned char* uid, pb
     ctx->num_cus = cus;
   ctx->roctx = env_int("PB_ROCTX", 0) != 0;
   ctx->comm_timeout_ms = std::max(1, env_int("PB_COMM_TIMEOUT_MS", 180000));
-  PB_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-  PB_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
-  PB_HIP(hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming));
-  PB_HIP(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
   ctx->partials_cap = (int64_t)1 << 20;  // doubles: room for 131072 blocks x 8 sums
-  PB_HIP(hipMalloc(&ctx->d_partials, ctx->partials_cap * sizeof(double)));
-  PB_HIP(hipMalloc(&ctx->d_scalars, 64 * sizeof(double)));
-  PB_HIP(hipMemsetAsync(ctx->d_scalars, 0, 64 * sizeof(double), ctx->stream));
-  PB_HIP(hipHostMalloc(&ctx->h_scalars, 64 * sizeof(double), hipHostMallocDefault));
-  int rc = PB_OK;
-  if (nranks > 1 && uid) {
+  // streams, events and the scalar buffers; a failure tears the partial context down below
+  auto resources = [&]() -> int {
+    PB_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    PB_HIP(hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+    PB_HIP(hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming));
+    PB_HIP(hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming));
+    PB_HIP(hipMalloc(&ctx->d_partials, ctx->partials_cap * sizeof(double)));
+    PB_HIP(hipMalloc(&ctx->d_scalars, 64 * sizeof(double)));
+    PB_HIP(hipMemsetAsync(ctx->d_scalars, 0, 64 * sizeof(double), ctx->stream));
+    PB_HIP(hipHostMalloc(&ctx->h_scalars, 64 * sizeof(double), hipHostMallocDefault));
+    return PB_OK;
+  };
+  int rc = resources();
+  if (rc == PB_OK && nranks > 1 && uid) {
     ncclUniqueId id;
     memcpy(&id, uid, 128);
     rc = comm_init_bounded(ctx, nranks, id, rank);
@@ -784,8 +796,8 @@ int pb_ctx_comm_status(const pb_ctx* ctx, int* failed) {
 int pb_ctx_destroy(pb_ctx* ctx) {
   if (!ctx) return PB_OK;
   (void)hipSetDevice(ctx->device);
-  (void)wait_stream(ctx, ctx->stream, "pb_ctx_destroy");
-  (void)wait_stream(ctx, ctx->comm_stream, "pb_ctx_destroy");
+  if (ctx->stream) (void)wait_stream(ctx, ctx->stream, "pb_ctx_destroy");
+  if (ctx->comm_stream) (void)wait_stream(ctx, ctx->comm_stream, "pb_ctx_destroy");
   if (!ctx->comm_failed) timers_collect(ctx);
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   for (hipEvent_t e : ctx->comm_marks) (void)hipEventDestroy(e);
@@ -797,12 +809,13 @@ int pb_ctx_destroy(pb_ctx* ctx) {
   transport_destroy(ctx);
   (void)hipFree(ctx->d_partials);
   (void)hipFree(ctx->d_scalars);
-  (void)hipHostFree(ctx->h_scalars);
-  (void)hipEventDestroy(ctx->ev_ready);
-  (void)hipEventDestroy(ctx->ev_done);
-  (void)hipStreamDestroy(ctx->comm_stream);
-  (void)hipStreamDestroy(ctx->stream);
+  if (ctx->h_scalars) (void)hipHostFree(ctx->h_scalars);
+  if (ctx->ev_ready) (void)hipEventDestroy(ctx->ev_ready);
+  if (ctx->ev_done) (void)hipEventDestroy(ctx->ev_done);
+  if (ctx->comm_stream) (void)hipStreamDestroy(ctx->comm_stream);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+  (void)hipGetLastError();  // a teardown error is not the next launch's error
   return PB_OK;
 }
 
@@ -992,8 +1005,12 @@ int pb_vec_create(pb_grid* g, pb_vec** out) {
     return set_error(PB_ERR_ALLOC, "vector of %lld doubles: out of device memory",
                      (long long)g->nlocal);
   }
-  int rc = vec_fill(g->ctx, v->d, v->nlocal, 0.0);  // PETSc vectors start zeroed
-  if (rc) return rc;
+  const int rc = vec_fill(g->ctx, v->d, v->nlocal, 0.0);  // PETSc vectors start zeroed
+  if (rc) {
+    const std::string msg = pb_last_error();
+    (void)pb_vec_destroy(v);
+    return set_error(rc, "%s", msg.c_str());
+  }
   *out = v;
   return PB_OK;
 }

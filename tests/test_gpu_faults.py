@@ -113,3 +113,29 @@ def test_stalled_peer_times_out(monkeypatch, tune, forced):
         assert not c2.comm_failed
     finally:
         c2.destroy()
+
+
+@pytest.mark.gpu
+def test_out_of_memory_is_an_error_and_the_context_goes_on():
+    """A vector that cannot be allocated (8192^3 doubles, 4 TiB) is PB_ERR_ALLOC (4), with nothing
+    left behind; the same context then runs a matvec and a CG solve on a small grid (HIP's
+    last-error state of the refused allocation does not resurface at their launch checks)."""
+    from oracle import oracle as O
+    ctx = pb.Context(0)
+    big = pb.DA(ctx, (8192, 8192, 8192))
+    with pytest.raises(PbError) as e:
+        pb.Vec(big)
+    assert e.value.code == 4
+    big.destroy()
+    n3 = (16, 12, 10)
+    da = pb.DA(ctx, n3)
+    h = tuple(1.0 / m for m in n3)
+    x0 = O.fill_random(int(np.prod(n3)), 7)
+    P, A, x, b = pb.initialise_linear_system(da, h)
+    x.set_values(x0)
+    A.mult(x, b)
+    assert np.array_equal(b.get_values(), O.stencil(x0, n3, h))
+    x.set(0.0)
+    reason, its, hist = pb.solve(P, A, x, b, ["-ksp_rtol", "1e-8"])
+    assert reason == 2 and its > 0
+    ctx.destroy()
